@@ -1,0 +1,246 @@
+/*
+ * marlsched.h — C ABI of libmarlsched.so, the MI355X-native hot path of
+ * lr40/marl-scheduling (per-round environment step + policy act + PPO returns).
+ *
+ * The boundary replaces the reference's Python surface (paths relative to
+ * /root/reference/src):
+ *   ms_env_create   <- World.__init__                     world.py:211-254
+ *                      + Env.__init__ (agents/collections) SchedulingEnvironment.py:253-348
+ *   ms_env_reset    <- SchedulingEnv.reset                SchedulingEnvironment.py:85-109
+ *   ms_env_step     <- SchedulingEnv.step                 SchedulingEnvironment.py:32-83
+ *                      (World.step1 world.py:295-334, gatherObservations Agent.py:148-300,
+ *                       gatherDividedAuctioneerObservation Auctioneer.py:20-77,
+ *                       Auctioneer.getAuctioneerAction Auctioneer.py:95-102 +
+ *                       HardcodedAuctioneerAcceptor HardcodedModules.py:48-78,
+ *                       getDividedFixedPricesReward Reward.py:146-212,
+ *                       getDividedFreePricesReward Reward.py:6-89)
+ *   ms_env_randbelow <- random.randint/_randbelow on the env's global stream
+ *                      (Agent.py:718,725; SchedulingEnvironment.py:317-326)
+ *   ms_policy_act   <- PPO.selectAction / ActorCritic.act  PPOmodules.py:53-63,114-125
+ *   ms_discounted_returns <- PPO.update return estimate    PPOmodules.py:128-137
+ *
+ * Conventions: plain pointers and sizes; every device pointer is a HIP device
+ * allocation owned by the caller unless stated; all work is enqueued on the
+ * caller's stream (hipStream_t passed as void*; NULL = default stream); a handle
+ * is not thread-safe; no pointer is retained after a call returns.
+ * Errors are return codes (0 = ok); ms_last_error() gives the message of the
+ * last failing call on the calling thread. No exception crosses the ABI.
+ */
+#ifndef MARLSCHED_H
+#define MARLSCHED_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MS_ABI_VERSION 1
+
+#define MS_MAX_KINDS 16
+#define MS_MAX_AGENTS 64
+#define MS_MAX_CORES 64
+#define MS_MAX_COLLECTION 32
+#define MS_MAX_OFFERS 126 /* O = N*L; acceptor actions [0, O] must fit int8 */
+
+/* return codes */
+#define MS_OK 0
+#define MS_EINVAL 22      /* bad argument / shape / config */
+#define MS_ENOMEM 12      /* device or host allocation failed */
+#define MS_EHIP 1001      /* a HIP runtime call failed */
+#define MS_EOVERFLOW 75   /* a per-env error flag is set (see MS_FLAG_*) */
+
+/* per-env error flags (ORed over envs by ms_env_flags) */
+#define MS_FLAG_LIABILITY_OVERFLOW 0x01u /* a core's liability chain exceeded liability_cap */
+#define MS_FLAG_BAD_ACTION 0x02u         /* acceptor action outside [0, O] (reference asserts, world.py:389,404) */
+#define MS_FLAG_COLLECTION_FULL 0x04u    /* insertJob into a full collection (reference raises, world.py:133) */
+#define MS_FLAG_SPAWN_EDGE 0x08u         /* u >= accProbabilities[-1]; clamped to last kind (Agent.py:53-56) */
+#define MS_FLAG_RNG_WINDOW 0x10u         /* more random words requested in one step than the stream window holds */
+#define MS_FLAG_GUARD 0x20u              /* offer recipient != core owner at execution (world.py:266) */
+
+/* RNG modes */
+#define MS_RNG_CPYTHON_MT19937 0 /* per-env MT19937 with CPython random.seed/random/_randbelow semantics */
+
+typedef struct ms_config {
+    int32_t n_agents;          /* numberOfAgents            world.py:215 */
+    int32_t n_cores;           /* numberOfCores             world.py:216 */
+    int32_t collection_length; /* collectionLength          world.py:225 */
+    int32_t n_kinds;           /* len(possibleJobPriorities) */
+    int32_t job_priority[MS_MAX_KINDS]; /* possibleJobPriorities world.py:218 */
+    int32_t job_length[MS_MAX_KINDS];   /* possibleJobLengths    world.py:217 */
+    /* world.accProbabilities (world.py:220-222): Python left-to-right float sums */
+    double acc_probability[MS_MAX_KINDS];
+    int32_t n_fix_prices;              /* len(fixPricesList); fixed-price mode needs >= n_kinds */
+    int32_t fix_price[MS_MAX_KINDS];   /* listOfFixPrices world.py:214, indexed by job kind */
+    int32_t free_prices;               /* world.freePrices world.py:212 */
+    int32_t commercial_reward;         /* commercialFreePriceReward Reward.py:22,36 */
+    double net_zero_offer_reward;      /* env.netZeroOfferReward SchedulingEnvironment.py:30 */
+    int32_t new_jobs_per_round;        /* newJobsPerRoundPerAgent world.py:236 */
+    int32_t reward_multiplier;         /* rewardMultiplier world.py:246 (integer in every driver) */
+    int32_t episode_length;            /* episodeLength world.py:243 */
+    int32_t liability_cap;             /* entries kept per core liability chain (0 -> 128) */
+    int32_t rng_mode;                  /* MS_RNG_* */
+    int32_t reserved[7];
+} ms_config;
+
+/* Derived shapes of a configuration (all byte strides are multiples of 4). */
+typedef struct ms_shape {
+    int32_t n_agents, n_cores, collection_length;
+    int32_t max_offers;        /* O = N*L (world.py:227-229) */
+    int32_t acc_obs_dim;       /* D_acc = 3 + 2*O (PPOmodules.py:237-238) */
+    int32_t acc_obs_stride;    /* bytes per acceptor/auctioneer obs row (D_acc rounded up to 4) */
+    int32_t off_obs_dim;       /* D_off = 2*C + 2 (PPOmodules.py:257) */
+    int32_t off_obs_stride;    /* bytes per offer obs row (D_off rounded up to 4) */
+    int32_t acc_actions;       /* A_acc = O + 1 (reject index O) */
+    int32_t off_actions;       /* A_off = C + 1 */
+    int32_t price_actions;     /* A_pc = max(priorities) + 1 (PPOmodules.py:295) */
+    int32_t liability_cap;
+    int64_t env_record_bytes;  /* packed per-env state record on the device */
+} ms_shape;
+
+/* Actions for one step of all E envs (device pointers). */
+typedef struct ms_actions {
+    const int8_t* acceptor;    /* [E][N][C] in [0, O]; O = reject (world.py:391-404) */
+    const int8_t* offer_core;  /* [E][N][L] core action a: core a+1 if a < C else no offer (world.py:412,450) */
+    const int8_t* offer_price; /* [E][N][L] free prices only (world.py:452); NULL in fixed-price mode */
+    const int8_t* auctioneer;  /* [E][C] or NULL = in-kernel HardcodedAuctioneerAcceptor on the env RNG */
+} ms_actions;
+
+/* Observation outputs (device pointers; any may be NULL to skip). */
+typedef struct ms_obs_out {
+    int8_t* acceptor;   /* [E][N][C][acc_obs_stride]  Agent.py:167-212 (pad bytes zero) */
+    int8_t* offer;      /* [E][N][L][off_obs_stride]  Agent.py:271-300 */
+    int8_t* auctioneer; /* [E][C][acc_obs_stride]     Auctioneer.py:34-77 */
+} ms_obs_out;
+
+/* Reward outputs (device pointers; any may be NULL to skip). */
+typedef struct ms_reward_out {
+    float* offer;           /* [E][N][L] offerNetRewards (fixed) / coreChooserRewards (free) */
+    float* price;           /* [E][N][L] priceChooserRewards (free prices only) */
+    int32_t* acceptor;      /* [E][N][C] acceptorNetRewards */
+    int32_t* auctioneer;    /* [E][C]    auctioneerReward */
+    int32_t* agent;         /* [E][N]    agentReward */
+} ms_reward_out;
+
+/* One executed offer (world.acceptedOffers entry), stored at its core's index. */
+typedef struct ms_accept_rec {
+    int8_t valid;     /* 1 if an offer was executed on this core this round */
+    int8_t offerer;   /* offererID (1..N) */
+    int8_t recipient; /* recipientID (0 = auctioneer) */
+    int8_t slot;      /* queuePosition */
+    int8_t price;     /* offeredReward */
+    int8_t nec_time;  /* necessaryTime */
+    int8_t prio;      /* prio1 */
+    int8_t kind;      /* jobKind */
+    int8_t order;     /* position in world.acceptedOffers (execution order) */
+    int8_t pad[3];
+    int32_t round;    /* world.round at execution */
+} ms_accept_rec;
+
+/* One job termination (jobTerminationInfo + verweilzeiten entry) at its core's index. */
+typedef struct ms_term_rec {
+    int8_t valid;     /* 1 if the core's job terminated this round */
+    int8_t owner;     /* ownerID */
+    int8_t prio;      /* Prioritaet */
+    int8_t init_len;  /* Bedienzeit */
+    int32_t dwell;    /* Verweilzeit = round - birthDate (world.py:350-357) */
+} ms_term_rec;
+
+typedef struct ms_event_out {
+    ms_accept_rec* accepted; /* [E][C] or NULL */
+    ms_term_rec* terminated; /* [E][C] or NULL */
+} ms_event_out;
+
+/* Host-side canonical state (export/import for parity tests and KAT scenarios).
+ * Arrays are host memory, shaped as noted, int32 unless stated. */
+typedef struct ms_state_host {
+    int32_t* round;        /* [E] world.round */
+    uint32_t* flags;       /* [E] MS_FLAG_* */
+    int32_t* core_owner;   /* [E][C] ownerID (0 = auctioneer) */
+    int32_t* core_kind;    /* [E][C] job kind, -1 = empty job */
+    int32_t* core_rem;     /* [E][C] remainingLength (-1 if empty) */
+    int32_t* core_birth;   /* [E][C] birthDate */
+    int32_t* slot_kind;    /* [E][N][L] -1 = empty */
+    int32_t* slot_rem;     /* [E][N][L] */
+    int32_t* slot_wait;    /* [E][N][L] Job.wait */
+    int32_t* slot_birth;   /* [E][N][L] */
+    int32_t* offer_core;   /* [E][N][L] pending offer of this slot: core index, -1 = none */
+    int32_t* offer_recip;  /* [E][N][L] recipientID */
+    int32_t* offer_price;  /* [E][N][L] offeredReward */
+    int32_t* liab_n;       /* [E][C] chain length */
+    int32_t* liab;         /* [E][C][cap][5] {offerer, recipient, price, nec_time, round}, oldest first */
+    uint32_t* mt;          /* [E][624] MT19937 state words */
+    int32_t* mt_index;     /* [E] mti (0..624) */
+} ms_state_host;
+
+typedef struct ms_env ms_env;
+
+/* Create E independent env replicas in the reference initial state
+ * (world.py:247, Core.__init__ world.py:30-37, JobCollection world.py:118-121),
+ * env e's RNG seeded as CPython random.seed(seed + e). */
+int ms_env_create(const ms_config* cfg, int64_t n_envs, uint64_t seed, ms_env** out);
+void ms_env_destroy(ms_env* env);
+int ms_env_shape(const ms_env* env, ms_shape* out);
+int ms_config_shape(const ms_config* cfg, ms_shape* out);
+
+/* Observations of the current state, no state change (SchedulingEnvironment.py:85-109). */
+int ms_env_reset(ms_env* env, const ms_obs_out* obs, void* stream);
+
+/* One round for all E envs (SchedulingEnvironment.py:32-83). Rewards/events are
+ * fully written (zeros where nothing happened). */
+int ms_env_step(ms_env* env, const ms_actions* act, const ms_obs_out* obs,
+                const ms_reward_out* rew, const ms_event_out* ev, void* stream);
+
+/* Host round counter (all replicas advance together). */
+int64_t ms_env_round(const ms_env* env);
+
+/* Synchronises the stream and returns the OR of all env flags in *flags. */
+int ms_env_flags(ms_env* env, uint32_t* flags, void* stream);
+
+/* CPython random._randbelow(n) drawn on env e's stream (n >= 1); synchronous. */
+int ms_env_randbelow(ms_env* env, int64_t env_index, uint32_t n, uint32_t* out, void* stream);
+
+/* Copy the full state to / from host arrays (synchronous). Import validates
+ * the reference invariants the kernel relies on. */
+int ms_env_export(ms_env* env, const ms_state_host* out, void* stream);
+int ms_env_import(ms_env* env, const ms_state_host* in, void* stream);
+
+/* ---- policy act: fused Linear-tanh-Linear-tanh-Linear-softmax + Categorical ----
+ * Rows: obs[e][u][stride] int8 for e < n_envs, u < n_units. Unit u uses weight
+ * group g = u / units_per_group (units_per_group * n_groups == n_units), i.e.
+ * divided nets (units_per_group = 1), locally shared (= sub-units per agent),
+ * globally shared (n_groups = 1). Weights are torch nn.Linear layouts, stacked
+ * over groups: w1 [G][H][D], b1 [G][H], w2 [G][H][H], b2 [G][H], w3 [G][A][H], b3 [G][A].
+ * Sampling: inverse CDF of the normalised probabilities (torch Categorical,
+ * PPOmodules.py:55-61) with u = uniform (Philox4x32-10 keyed by seed, counter
+ * (offset, row)) or, when uniforms != NULL, the given per-row uniform in [0,1).
+ * Outputs: action[e*n_units+u] int8, logprob f32 (log of clamped normalised prob). */
+typedef struct ms_mlp_params {
+    const float *w1, *b1, *w2, *b2, *w3, *b3;
+    int32_t in_dim;    /* D */
+    int32_t hidden;    /* H (<= 64) */
+    int32_t n_actions; /* A (<= 128) */
+    int32_t n_groups;  /* G */
+} ms_mlp_params;
+
+int ms_policy_act(const ms_mlp_params* p, const int8_t* obs, int32_t obs_stride,
+                  int64_t n_envs, int32_t n_units, int32_t units_per_group,
+                  uint64_t seed, uint64_t offset, const float* uniforms,
+                  int8_t* action, float* logprob, void* stream);
+
+/* Discounted Monte-Carlo returns + per-sequence normalisation (PPOmodules.py:128-137):
+ * rewards [T][M] (f32, as stored per round), for each sequence m:
+ * G_t = r_t + gamma*G_{t+1} in float64, cast to f32, then
+ * (G - mean) / (std_unbiased + 1e-7); out [M][T] f32. */
+int ms_discounted_returns(const float* rewards, int32_t T, int64_t M, int64_t row_stride,
+                          double gamma, float* out, void* stream);
+
+const char* ms_last_error(void);
+int ms_abi_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* MARLSCHED_H */

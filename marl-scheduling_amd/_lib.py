@@ -1,0 +1,87 @@
+"""Loader for libmarlsched.so (the C ABI of include/marlsched.h).
+
+The product has no CPU fallback: if the library is missing or fails to load,
+importing this module raises. torch is imported first so that the HIP runtime
+torch bundles is the one the library binds to (both carry the soname
+libamdhip64.so.7).
+"""
+from __future__ import annotations
+
+import ctypes as ct
+import os
+
+import torch  # noqa: F401  (load torch's HIP runtime before the library)
+
+from . import abi
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libmarlsched.so")
+
+
+class MarlSchedError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__("libmarlsched error %d: %s" % (code, msg))
+        self.code = code
+
+
+def _load():
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(
+            "libmarlsched.so is not built (expected at %s); run `python -c 'import __graft_entry__ as g; g.build()'`"
+            % LIB_PATH
+        )
+    L = ct.CDLL(LIB_PATH)
+    P = ct.c_void_p
+    i32, i64, u32, u64 = ct.c_int32, ct.c_int64, ct.c_uint32, ct.c_uint64
+    sig = {
+        "ms_last_error": (ct.c_char_p, []),
+        "ms_abi_version": (ct.c_int, []),
+        "ms_config_shape": (ct.c_int, [ct.POINTER(abi.MsConfig), ct.POINTER(abi.MsShape)]),
+        "ms_env_create": (ct.c_int, [ct.POINTER(abi.MsConfig), i64, u64, ct.POINTER(P)]),
+        "ms_env_destroy": (None, [P]),
+        "ms_env_shape": (ct.c_int, [P, ct.POINTER(abi.MsShape)]),
+        "ms_env_reset": (ct.c_int, [P, ct.POINTER(abi.MsObsOut), P]),
+        "ms_env_step": (ct.c_int, [P, ct.POINTER(abi.MsActions), ct.POINTER(abi.MsObsOut),
+                                   ct.POINTER(abi.MsRewardOut), ct.POINTER(abi.MsEventOut), P]),
+        "ms_env_round": (i64, [P]),
+        "ms_env_flags": (ct.c_int, [P, ct.POINTER(u32), P]),
+        "ms_env_randbelow": (ct.c_int, [P, i64, u32, ct.POINTER(u32), P]),
+        "ms_env_export": (ct.c_int, [P, ct.POINTER(abi.MsStateHost), P]),
+        "ms_env_import": (ct.c_int, [P, ct.POINTER(abi.MsStateHost), P]),
+        "ms_policy_act": (ct.c_int, [ct.POINTER(abi.MsMlpParams), P, i32, i64, i32, i32, u64, u64, P, P, P, P]),
+        "ms_discounted_returns": (ct.c_int, [P, i32, i64, i64, ct.c_double, P, P]),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(L, name)
+        fn.restype = res
+        fn.argtypes = args
+    if L.ms_abi_version() != 1:
+        raise ImportError("libmarlsched.so ABI version mismatch")
+    return L
+
+
+lib = _load()
+
+# every entry point include/marlsched.h declares (checked by tests)
+EXPORTED = (
+    "ms_last_error", "ms_abi_version", "ms_config_shape", "ms_env_create", "ms_env_destroy", "ms_env_shape",
+    "ms_env_reset", "ms_env_step", "ms_env_round", "ms_env_flags", "ms_env_randbelow", "ms_env_export",
+    "ms_env_import", "ms_policy_act", "ms_discounted_returns",
+)
+
+
+def check(rc: int):
+    if rc != 0:
+        raise MarlSchedError(rc, (lib.ms_last_error() or b"").decode(errors="replace"))
+
+
+def ptr(t) -> ct.c_void_p | None:
+    """Device pointer of a torch tensor (None passes NULL)."""
+    if t is None:
+        return None
+    return ct.c_void_p(t.data_ptr())
+
+
+def stream_ptr(stream=None):
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return ct.c_void_p(s.cuda_stream)

@@ -1,0 +1,25 @@
+#!/usr/bin/env bash
+# Builds libmarlsched.so (gfx950) in-tree: the HIP kernels + the C ABI.
+set -euo pipefail
+HERE="$(cd "$(dirname "${BASH_SOURCE[0]}")" && pwd)"
+OUT="${HERE}/libmarlsched.so"
+HIPCC="${HIPCC:-/opt/rocm/bin/hipcc}"
+ARCH="${MS_OFFLOAD_ARCH:-gfx950}"
+FLAGS=(-O3 -std=c++17 -fPIC --offload-arch="${ARCH}" -ffp-contract=off -Wall -Wno-unused-function
+       -I"${HERE}/../include")
+OBJDIR="${HERE}/build"
+mkdir -p "${OBJDIR}"
+objs=()
+for src in env_kernels.hip policy_kernels.hip capi.cpp; do
+  obj="${OBJDIR}/${src%.*}.o"
+  if [[ ! -f "${obj}" || "${HERE}/csrc/${src}" -nt "${obj}" || "${HERE}/csrc/ms_layout.h" -nt "${obj}" || "${HERE}/../include/marlsched.h" -nt "${obj}" ]]; then
+    if [[ "${src}" == *.cpp ]]; then
+      "${HIPCC}" "${FLAGS[@]}" -x hip -c "${HERE}/csrc/${src}" -o "${obj}"
+    else
+      "${HIPCC}" "${FLAGS[@]}" -c "${HERE}/csrc/${src}" -o "${obj}"
+    fi
+  fi
+  objs+=("${obj}")
+done
+"${HIPCC}" -shared -fPIC --offload-arch="${ARCH}" -o "${OUT}" "${objs[@]}"
+echo "${OUT}"

@@ -1,0 +1,392 @@
+// capi.cpp — extern "C" boundary of libmarlsched.so (include/marlsched.h).
+//
+// Host side of the drop-in: validates configurations, owns the device state of
+// E env replicas, and enqueues the HIP kernels on the caller's stream.
+#include <hip/hip_runtime.h>
+
+#include <stdarg.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <vector>
+
+#include "ms_layout.h"
+
+namespace ms {
+hipError_t launch_env_init(const Params&, int64_t, uint8_t*, uint32_t*, Liab*, uint64_t, hipStream_t);
+hipError_t launch_env_reset(const Params&, int64_t, const uint8_t*, int8_t*, int8_t*, int8_t*, hipStream_t);
+hipError_t launch_env_step(const Params&, int64_t, uint8_t*, uint32_t*, Liab*, const StepIO&, hipStream_t);
+hipError_t launch_env_randbelow(const Params&, uint8_t*, uint32_t*, int64_t, uint32_t, uint32_t*, hipStream_t);
+hipError_t launch_policy_act(const ms_mlp_params*, const int8_t*, int, int64_t, int, int, uint64_t, uint64_t,
+                             const float*, int8_t*, float*, hipStream_t);
+hipError_t launch_returns(const float*, int, int64_t, int64_t, double, float*, hipStream_t);
+}  // namespace ms
+
+struct ms_env {
+    ms_config cfg;
+    ms::Params P;
+    int64_t E;
+    int device;
+    uint8_t* recs;
+    uint32_t* mt;
+    ms::Liab* liab;
+    uint32_t* scratch_u32;  // device word for randbelow
+    int64_t round;
+};
+
+static thread_local char g_err[512] = "";
+
+static int fail(int code, const char* fmt, ...) {
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(g_err, sizeof(g_err), fmt, ap);
+    va_end(ap);
+    return code;
+}
+
+#define HIP_TRY(expr)                                                                          \
+    do {                                                                                       \
+        hipError_t _e = (expr);                                                                \
+        if (_e != hipSuccess) return fail(MS_EHIP, "%s: %s", #expr, hipGetErrorString(_e)); \
+    } while (0)
+
+static bool fits_i8(long v) { return v >= -128 && v <= 127; }
+
+static int validate_config(const ms_config* c) {
+    if (!c) return fail(MS_EINVAL, "config is NULL");
+    if (c->n_agents < 1 || c->n_agents > MS_MAX_AGENTS) return fail(MS_EINVAL, "n_agents must be in [1, %d]", MS_MAX_AGENTS);
+    if (c->n_cores < 1 || c->n_cores > MS_MAX_CORES) return fail(MS_EINVAL, "n_cores must be in [1, %d]", MS_MAX_CORES);
+    if (c->collection_length < 1 || c->collection_length > MS_MAX_COLLECTION)
+        return fail(MS_EINVAL, "collection_length must be in [1, %d]", MS_MAX_COLLECTION);
+    if (c->n_agents * c->collection_length > MS_MAX_OFFERS)
+        return fail(MS_EINVAL, "n_agents * collection_length must be <= %d", MS_MAX_OFFERS);
+    if (c->n_kinds < 1 || c->n_kinds > MS_MAX_KINDS) return fail(MS_EINVAL, "n_kinds must be in [1, %d]", MS_MAX_KINDS);
+    for (int i = 0; i < c->n_kinds; i++) {
+        if (c->job_priority[i] < 0 || c->job_priority[i] > 127) return fail(MS_EINVAL, "job priorities must be in [0, 127]");
+        if (c->job_length[i] < 1 || c->job_length[i] > 127) return fail(MS_EINVAL, "job lengths must be in [1, 127]");
+        if (i > 0 && !(c->acc_probability[i] >= c->acc_probability[i - 1]))
+            return fail(MS_EINVAL, "accumulated probabilities must be non-decreasing");
+    }
+    if (!c->free_prices) {
+        if (c->n_fix_prices < c->n_kinds) return fail(MS_EINVAL, "fixed prices need one price per job kind");
+        for (int i = 0; i < c->n_fix_prices && i < MS_MAX_KINDS; i++)
+            if (!fits_i8(c->fix_price[i])) return fail(MS_EINVAL, "fixed prices must fit int8");
+    }
+    if (c->new_jobs_per_round < 0 || c->new_jobs_per_round > c->collection_length)
+        return fail(MS_EINVAL, "new_jobs_per_round must be in [0, collection_length]");
+    if (c->n_agents * (c->new_jobs_per_round > 0 ? c->new_jobs_per_round : 1) > 256)
+        return fail(MS_EINVAL, "n_agents * new_jobs_per_round must be <= 256");
+    long max_rew = (long)c->reward_multiplier * 127;
+    if (max_rew > (1L << 24) || max_rew < -(1L << 24)) return fail(MS_EINVAL, "reward_multiplier out of range");
+    if (c->episode_length < 1) return fail(MS_EINVAL, "episode_length must be >= 1");
+    if (c->liability_cap < 0 || c->liability_cap > 255) return fail(MS_EINVAL, "liability_cap must be in [0, 255]");
+    if (c->rng_mode != MS_RNG_CPYTHON_MT19937) return fail(MS_EINVAL, "unknown rng_mode");
+    return MS_OK;
+}
+
+static int cap_of(const ms_config* c) { return c->liability_cap > 0 ? c->liability_cap : 128; }
+
+extern "C" {
+
+const char* ms_last_error(void) { return g_err; }
+int ms_abi_version(void) { return MS_ABI_VERSION; }
+
+int ms_config_shape(const ms_config* cfg, ms_shape* s) {
+    int rc = validate_config(cfg);
+    if (rc) return rc;
+    if (!s) return fail(MS_EINVAL, "shape is NULL");
+    ms::Params P = ms::make_params(*cfg, cap_of(cfg));
+    memset(s, 0, sizeof(*s));
+    s->n_agents = P.N;
+    s->n_cores = P.C;
+    s->collection_length = P.L;
+    s->max_offers = P.O;
+    s->acc_obs_dim = P.d_acc;
+    s->acc_obs_stride = P.acc_stride;
+    s->off_obs_dim = P.d_off;
+    s->off_obs_stride = P.off_stride;
+    s->acc_actions = P.O + 1;
+    s->off_actions = P.C + 1;
+    int mp = 0;
+    for (int i = 0; i < cfg->n_kinds; i++) mp = cfg->job_priority[i] > mp ? cfg->job_priority[i] : mp;
+    s->price_actions = mp + 1;
+    s->liability_cap = P.cap;
+    s->env_record_bytes = P.rec_bytes;
+    return MS_OK;
+}
+
+int ms_env_shape(const ms_env* env, ms_shape* out) {
+    if (!env) return fail(MS_EINVAL, "env is NULL");
+    return ms_config_shape(&env->cfg, out);
+}
+
+void ms_env_destroy(ms_env* env) {
+    if (!env) return;
+    int cur = 0;
+    if (hipGetDevice(&cur) == hipSuccess && cur != env->device) (void)hipSetDevice(env->device);
+    if (env->recs) (void)hipFree(env->recs);
+    if (env->mt) (void)hipFree(env->mt);
+    if (env->liab) (void)hipFree(env->liab);
+    if (env->scratch_u32) (void)hipFree(env->scratch_u32);
+    if (cur != env->device) (void)hipSetDevice(cur);
+    delete env;
+}
+
+int ms_env_create(const ms_config* cfg, int64_t n_envs, uint64_t seed, ms_env** out) {
+    if (!out) return fail(MS_EINVAL, "out is NULL");
+    *out = nullptr;
+    int rc = validate_config(cfg);
+    if (rc) return rc;
+    if (n_envs < 1 || n_envs > (1LL << 31) - 1) return fail(MS_EINVAL, "n_envs must be in [1, 2^31)");
+    ms_env* env = new ms_env();
+    env->cfg = *cfg;
+    env->P = ms::make_params(*cfg, cap_of(cfg));
+    env->E = n_envs;
+    env->round = 0;
+    HIP_TRY(hipGetDevice(&env->device));
+    size_t rec_b = (size_t)n_envs * env->P.rec_bytes;
+    size_t mt_b = (size_t)n_envs * ms::kMtN * sizeof(uint32_t);
+    size_t liab_b = (size_t)n_envs * env->P.C * env->P.cap * sizeof(ms::Liab);
+    if (hipMalloc(&env->recs, rec_b) != hipSuccess || hipMalloc(&env->mt, mt_b) != hipSuccess ||
+        hipMalloc(&env->liab, liab_b) != hipSuccess || hipMalloc(&env->scratch_u32, 16) != hipSuccess) {
+        ms_env_destroy(env);
+        return fail(MS_ENOMEM, "device allocation of %zu bytes failed", rec_b + mt_b + liab_b);
+    }
+    hipError_t e = ms::launch_env_init(env->P, n_envs, env->recs, env->mt, env->liab, seed, nullptr);
+    if (e == hipSuccess) e = hipDeviceSynchronize();
+    if (e != hipSuccess) {
+        ms_env_destroy(env);
+        return fail(MS_EHIP, "env init: %s", hipGetErrorString(e));
+    }
+    *out = env;
+    return MS_OK;
+}
+
+int64_t ms_env_round(const ms_env* env) { return env ? env->round : -1; }
+
+int ms_env_reset(ms_env* env, const ms_obs_out* obs, void* stream) {
+    if (!env || !obs) return fail(MS_EINVAL, "env/obs is NULL");
+    HIP_TRY(ms::launch_env_reset(env->P, env->E, env->recs, obs->acceptor, obs->offer, obs->auctioneer,
+                                 (hipStream_t)stream));
+    return MS_OK;
+}
+
+int ms_env_step(ms_env* env, const ms_actions* act, const ms_obs_out* obs, const ms_reward_out* rew,
+                const ms_event_out* ev, void* stream) {
+    if (!env || !act) return fail(MS_EINVAL, "env/actions is NULL");
+    if (!act->acceptor || !act->offer_core) return fail(MS_EINVAL, "acceptor and offer_core actions are required");
+    if (env->cfg.free_prices && !act->offer_price) return fail(MS_EINVAL, "free prices need offer_price actions");
+    ms::StepIO io{};
+    io.act_acc = act->acceptor;
+    io.act_off = act->offer_core;
+    io.act_price = env->cfg.free_prices ? act->offer_price : nullptr;
+    io.act_auct = act->auctioneer;
+    if (obs) {
+        io.obs_acc = obs->acceptor;
+        io.obs_off = obs->offer;
+        io.obs_auct = obs->auctioneer;
+    }
+    if (rew) {
+        io.rew_offer = rew->offer;
+        io.rew_price = rew->price;
+        io.rew_acc = rew->acceptor;
+        io.rew_auct = rew->auctioneer;
+        io.rew_agent = rew->agent;
+    }
+    if (ev) {
+        io.ev_acc = ev->accepted;
+        io.ev_term = ev->terminated;
+    }
+    HIP_TRY(ms::launch_env_step(env->P, env->E, env->recs, env->mt, env->liab, io, (hipStream_t)stream));
+    env->round += 1;
+    return MS_OK;
+}
+
+int ms_env_flags(ms_env* env, uint32_t* flags, void* stream) {
+    if (!env || !flags) return fail(MS_EINVAL, "env/flags is NULL");
+    HIP_TRY(hipStreamSynchronize((hipStream_t)stream));
+    std::vector<uint8_t> h((size_t)env->E * env->P.rec_bytes);
+    HIP_TRY(hipMemcpy(h.data(), env->recs, h.size(), hipMemcpyDeviceToHost));
+    uint32_t f = 0;
+    for (int64_t e = 0; e < env->E; e++) {
+        uint32_t v;
+        memcpy(&v, h.data() + e * env->P.rec_bytes + 4, 4);
+        f |= v;
+    }
+    *flags = f;
+    return MS_OK;
+}
+
+int ms_env_randbelow(ms_env* env, int64_t e, uint32_t n, uint32_t* out, void* stream) {
+    if (!env || !out) return fail(MS_EINVAL, "env/out is NULL");
+    if (e < 0 || e >= env->E) return fail(MS_EINVAL, "env index out of range");
+    if (n < 1) return fail(MS_EINVAL, "n must be >= 1");
+    HIP_TRY(ms::launch_env_randbelow(env->P, env->recs, env->mt, e, n, env->scratch_u32, (hipStream_t)stream));
+    HIP_TRY(hipMemcpyAsync(out, env->scratch_u32, 4, hipMemcpyDeviceToHost, (hipStream_t)stream));
+    HIP_TRY(hipStreamSynchronize((hipStream_t)stream));
+    return MS_OK;
+}
+
+#define REC_I8(base, off, i) (*(int8_t*)((base) + (off) + (i)))
+#define REC_U8(base, off, i) (*(uint8_t*)((base) + (off) + (i)))
+#define REC_I32(base, off, i) (*(int32_t*)((base) + (off) + 4 * (i)))
+
+int ms_env_export(ms_env* env, const ms_state_host* o, void* stream) {
+    if (!env || !o) return fail(MS_EINVAL, "env/out is NULL");
+    const ms::Params& P = env->P;
+    HIP_TRY(hipStreamSynchronize((hipStream_t)stream));
+    std::vector<uint8_t> rec((size_t)env->E * P.rec_bytes);
+    std::vector<uint32_t> mt((size_t)env->E * ms::kMtN);
+    std::vector<ms::Liab> lb((size_t)env->E * P.C * P.cap);
+    HIP_TRY(hipMemcpy(rec.data(), env->recs, rec.size(), hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(mt.data(), env->mt, mt.size() * 4, hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(lb.data(), env->liab, lb.size() * sizeof(ms::Liab), hipMemcpyDeviceToHost));
+    const int C = P.C, NL = P.NL, cap = P.cap;
+    for (int64_t e = 0; e < env->E; e++) {
+        const uint8_t* b = rec.data() + e * P.rec_bytes;
+        if (o->round) o->round[e] = REC_I32(b, 0, 0);
+        if (o->flags) o->flags[e] = (uint32_t)REC_I32(b, 4, 0);
+        if (o->mt_index) o->mt_index[e] = REC_I32(b, 8, 0);
+        for (int c = 0; c < C; c++) {
+            if (o->core_owner) o->core_owner[e * C + c] = REC_I8(b, P.o_core_owner, c);
+            if (o->core_kind) o->core_kind[e * C + c] = REC_I8(b, P.o_core_kind, c);
+            if (o->core_rem) o->core_rem[e * C + c] = REC_I8(b, P.o_core_rem, c);
+            if (o->core_birth) o->core_birth[e * C + c] = REC_I32(b, P.o_core_birth, c);
+            int n = REC_U8(b, P.o_liab_n, c);
+            if (o->liab_n) o->liab_n[e * C + c] = n;
+            if (o->liab)
+                for (int k = 0; k < cap; k++) {
+                    int32_t* d = o->liab + (((size_t)e * C + c) * cap + k) * 5;
+                    if (k < n) {
+                        const ms::Liab& le = lb[((size_t)e * C + c) * cap + k];
+                        d[0] = le.offerer;
+                        d[1] = le.recipient;
+                        d[2] = le.price;
+                        d[3] = le.nec;
+                        d[4] = le.round;
+                    } else {
+                        d[0] = d[1] = d[2] = d[3] = d[4] = 0;
+                    }
+                }
+        }
+        for (int i = 0; i < NL; i++) {
+            size_t j = (size_t)e * NL + i;
+            if (o->slot_kind) o->slot_kind[j] = REC_I8(b, P.o_slot_kind, i);
+            if (o->slot_rem) o->slot_rem[j] = REC_I8(b, P.o_slot_rem, i);
+            if (o->slot_wait) o->slot_wait[j] = REC_I8(b, P.o_slot_wait, i);
+            if (o->slot_birth) o->slot_birth[j] = REC_I32(b, P.o_slot_birth, i);
+            if (o->offer_core) o->offer_core[j] = REC_I8(b, P.o_offer_core, i);
+            if (o->offer_recip) o->offer_recip[j] = REC_I8(b, P.o_offer_recip, i);
+            if (o->offer_price) o->offer_price[j] = REC_I8(b, P.o_offer_price, i);
+        }
+        if (o->mt) memcpy(o->mt + e * ms::kMtN, mt.data() + e * ms::kMtN, ms::kMtN * 4);
+    }
+    return MS_OK;
+}
+
+int ms_env_import(ms_env* env, const ms_state_host* in, void* stream) {
+    if (!env || !in) return fail(MS_EINVAL, "env/in is NULL");
+    const ms::Params& P = env->P;
+    const int N = P.N, C = P.C, L = P.L, NL = P.NL, cap = P.cap;
+    std::vector<uint8_t> rec((size_t)env->E * P.rec_bytes, 0);
+    std::vector<ms::Liab> lb((size_t)env->E * C * cap);
+    memset(lb.data(), 0, lb.size() * sizeof(ms::Liab));
+    for (int64_t e = 0; e < env->E; e++) {
+        uint8_t* b = rec.data() + e * P.rec_bytes;
+        REC_I32(b, 0, 0) = in->round[e];
+        REC_I32(b, 4, 0) = in->flags ? (int32_t)in->flags[e] : 0;
+        int mti = in->mt_index[e];
+        if (mti < 0 || mti > ms::kMtN) return fail(MS_EINVAL, "env %lld: mt_index out of range", (long long)e);
+        REC_I32(b, 8, 0) = mti;
+        std::vector<int> owned(N + 1, 0), empty(N, 0);
+        for (int c = 0; c < C; c++) {
+            int k = in->core_kind[e * C + c], own = in->core_owner[e * C + c];
+            if (k < -1 || k >= env->cfg.n_kinds) return fail(MS_EINVAL, "env %lld core %d: bad kind", (long long)e, c);
+            if (own < 0 || own > N) return fail(MS_EINVAL, "env %lld core %d: bad owner", (long long)e, c);
+            if ((k < 0) != (own == 0)) return fail(MS_EINVAL, "env %lld core %d: owner 0 <=> empty job violated", (long long)e, c);
+            int rem = in->core_rem[e * C + c];
+            if (k >= 0 && (rem < 1 || rem > 127)) return fail(MS_EINVAL, "env %lld core %d: bad remaining length", (long long)e, c);
+            REC_I8(b, P.o_core_owner, c) = (int8_t)own;
+            REC_I8(b, P.o_core_kind, c) = (int8_t)k;
+            REC_I8(b, P.o_core_rem, c) = (int8_t)(k < 0 ? -1 : rem);
+            REC_I32(b, P.o_core_birth, c) = k < 0 ? -1 : in->core_birth[e * C + c];
+            int n = in->liab_n[e * C + c];
+            if (n < 0 || n > cap) return fail(MS_EINVAL, "env %lld core %d: liability chain too long", (long long)e, c);
+            REC_U8(b, P.o_liab_n, c) = (uint8_t)n;
+            for (int q = 0; q < n; q++) {
+                const int32_t* d = in->liab + (((size_t)e * C + c) * cap + q) * 5;
+                if (d[0] < 1 || d[0] > N || d[1] < 0 || d[1] > N || !fits_i8(d[2]) || d[3] < 1 || d[3] > 127)
+                    return fail(MS_EINVAL, "env %lld core %d: bad liability entry", (long long)e, c);
+                ms::Liab& le = lb[((size_t)e * C + c) * cap + q];
+                le.offerer = (int8_t)d[0];
+                le.recipient = (int8_t)d[1];
+                le.price = (int8_t)d[2];
+                le.nec = (int8_t)d[3];
+                le.round = d[4];
+            }
+            owned[own]++;
+        }
+        for (int i = 0; i < NL; i++) {
+            size_t j = (size_t)e * NL + i;
+            int k = in->slot_kind[j];
+            if (k < -1 || k >= env->cfg.n_kinds) return fail(MS_EINVAL, "env %lld slot %d: bad kind", (long long)e, i);
+            int rem = in->slot_rem[j];
+            if (k >= 0 && (rem < 1 || rem > 127)) return fail(MS_EINVAL, "env %lld slot %d: bad remaining length", (long long)e, i);
+            REC_I8(b, P.o_slot_kind, i) = (int8_t)k;
+            REC_I8(b, P.o_slot_rem, i) = (int8_t)(k < 0 ? -1 : rem);
+            REC_I8(b, P.o_slot_wait, i) = (int8_t)(k < 0 ? 0 : (in->slot_wait[j] != 0));
+            REC_I32(b, P.o_slot_birth, i) = k < 0 ? -1 : in->slot_birth[j];
+            if (k < 0) empty[i / L]++;
+            int oc = in->offer_core[j];
+            if (oc >= 0) {
+                if (oc >= C || k < 0) return fail(MS_EINVAL, "env %lld slot %d: bad pending offer", (long long)e, i);
+                // offers to a core are addressed to its owner (world.py:428 runs after the tick)
+                if (in->offer_recip[j] != in->core_owner[e * C + oc])
+                    return fail(MS_EINVAL, "env %lld slot %d: offer recipient is not the core owner", (long long)e, i);
+                if (!fits_i8(in->offer_price[j])) return fail(MS_EINVAL, "env %lld slot %d: price must fit int8", (long long)e, i);
+                REC_I8(b, P.o_offer_core, i) = (int8_t)oc;
+                REC_I8(b, P.o_offer_recip, i) = (int8_t)in->offer_recip[j];
+                REC_I8(b, P.o_offer_price, i) = (int8_t)in->offer_price[j];
+            } else {
+                REC_I8(b, P.o_offer_core, i) = -1;
+                REC_I8(b, P.o_offer_recip, i) = 0;
+                REC_I8(b, P.o_offer_price, i) = 0;
+            }
+        }
+        for (int a = 0; a < N; a++)  // numberOfFreeSlots >= len(ownedCores) (world.py:371-373 keeps it)
+            if (empty[a] < owned[a + 1])
+                return fail(MS_EINVAL, "env %lld agent %d: fewer free slots than owned cores", (long long)e, a + 1);
+    }
+    HIP_TRY(hipStreamSynchronize((hipStream_t)stream));
+    HIP_TRY(hipMemcpy(env->recs, rec.data(), rec.size(), hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(env->mt, in->mt, (size_t)env->E * ms::kMtN * 4, hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(env->liab, lb.data(), lb.size() * sizeof(ms::Liab), hipMemcpyHostToDevice));
+    env->round = in->round[0];
+    return MS_OK;
+}
+
+int ms_policy_act(const ms_mlp_params* p, const int8_t* obs, int32_t obs_stride, int64_t n_envs, int32_t n_units,
+                  int32_t units_per_group, uint64_t seed, uint64_t offset, const float* uniforms, int8_t* action,
+                  float* logprob, void* stream) {
+    if (!p || !obs || !action || !logprob) return fail(MS_EINVAL, "NULL argument");
+    if (!p->w1 || !p->b1 || !p->w2 || !p->b2 || !p->w3 || !p->b3) return fail(MS_EINVAL, "NULL weight");
+    if (p->hidden != 16) return fail(MS_EINVAL, "hidden width %d not built (16 only)", p->hidden);
+    if (p->n_actions < 1 || p->n_actions > 127) return fail(MS_EINVAL, "n_actions must be in [1, 127]");
+    if (p->in_dim < 1 || obs_stride < p->in_dim || (obs_stride & 3)) return fail(MS_EINVAL, "bad obs stride");
+    if (units_per_group < 1 || p->n_groups < 1 || units_per_group * p->n_groups != n_units)
+        return fail(MS_EINVAL, "units_per_group * n_groups must equal n_units");
+    if (n_envs < 1) return fail(MS_EINVAL, "n_envs must be >= 1");
+    HIP_TRY(ms::launch_policy_act(p, obs, obs_stride, n_envs, n_units, units_per_group, seed, offset, uniforms, action,
+                                  logprob, (hipStream_t)stream));
+    return MS_OK;
+}
+
+int ms_discounted_returns(const float* rewards, int32_t T, int64_t M, int64_t row_stride, double gamma, float* out,
+                          void* stream) {
+    if (!rewards || !out) return fail(MS_EINVAL, "NULL argument");
+    if (T < 1 || M < 0 || row_stride < M) return fail(MS_EINVAL, "bad shape");
+    HIP_TRY(ms::launch_returns(rewards, T, M, row_stride, gamma, out, (hipStream_t)stream));
+    return MS_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,138 @@
+// ms_layout.h — per-env state record layout and launch parameters shared by
+// the host ABI (capi.cpp) and the HIP kernels.
+//
+// One env replica's state lives in one contiguous record in HBM (the
+// [env][field][agent/core/slot] layout: env-major so that the one wave that
+// steps an env reads and writes it with a few coalesced dword accesses):
+//
+//   int32  round, flags, mti, pad                       16 B
+//   int8   core_owner[C], core_kind[C], core_rem[C], liab_n[C]   (each padded to 4)
+//   int32  core_birth[C]
+//   int8   slot_kind[NL], slot_rem[NL], slot_wait[NL],
+//          offer_core[NL], offer_recip[NL], offer_price[NL]        (each padded to 4)
+//   int32  slot_birth[NL]
+//
+// Beside it: liability chains [E][C][cap] of 8-byte entries and the MT19937
+// state words [E][624].
+#pragma once
+
+#include <stdint.h>
+
+#include "../../include/marlsched.h"
+
+namespace ms {
+
+constexpr int kWave = 64;
+constexpr int kMtN = 624;
+constexpr int kMtM = 397;
+constexpr int kObsChunk = 4096;  // LDS staging bytes for observation rows
+
+struct Liab {  // one liabilityList entry (world.py:285-289)
+    int8_t offerer, recipient, price, nec;
+    int32_t round;
+};
+
+struct Params {
+    // shapes
+    int32_t N, C, L, NL, O, K, cap;
+    int32_t d_acc, acc_stride, d_off, off_stride;
+    // record byte offsets
+    int32_t o_core_owner, o_core_kind, o_core_rem, o_liab_n, o_core_birth;
+    int32_t o_slot_kind, o_slot_rem, o_slot_wait, o_offer_core, o_offer_recip, o_offer_price,
+        o_slot_birth;
+    int32_t rec_bytes;
+    // config (world.py:211-246, Reward.py)
+    int32_t prio[MS_MAX_KINDS];
+    int32_t len[MS_MAX_KINDS];
+    double acc[MS_MAX_KINDS];
+    int32_t fix[MS_MAX_KINDS];
+    int32_t n_fix;
+    int32_t free_prices, commercial, new_jobs, mult;
+    float net_zero;
+    // LDS carve-up (byte offsets into dynamic shared memory)
+    int32_t s_rec, s_act_acc, s_act_off, s_act_price, s_act_auct, s_accr, s_offr, s_pricer,
+        s_spawn_kind, s_scratch, s_total;
+};
+
+// device pointers of one ms_env_step call
+struct StepIO {
+    const int8_t* act_acc;
+    const int8_t* act_off;
+    const int8_t* act_price;
+    const int8_t* act_auct;
+    int8_t* obs_acc;
+    int8_t* obs_off;
+    int8_t* obs_auct;
+    float* rew_offer;
+    float* rew_price;
+    int32_t* rew_acc;
+    int32_t* rew_auct;
+    int32_t* rew_agent;
+    ms_accept_rec* ev_acc;
+    ms_term_rec* ev_term;
+};
+
+inline int32_t align4(int32_t x) { return (x + 3) & ~3; }
+inline int32_t align16(int32_t x) { return (x + 15) & ~15; }
+
+// Build the record layout and LDS plan for a validated config.
+inline Params make_params(const ms_config& c, int32_t cap) {
+    Params p{};
+    p.N = c.n_agents;
+    p.C = c.n_cores;
+    p.L = c.collection_length;
+    p.NL = p.N * p.L;
+    p.O = p.NL;
+    p.K = c.n_kinds;
+    p.cap = cap;
+    p.d_acc = 3 + 2 * p.O;
+    p.acc_stride = align4(p.d_acc);
+    p.d_off = 2 * p.C + 2;
+    p.off_stride = align4(p.d_off);
+    int32_t o = 16;
+    p.o_core_owner = o; o += align4(p.C);
+    p.o_core_kind = o; o += align4(p.C);
+    p.o_core_rem = o; o += align4(p.C);
+    p.o_liab_n = o; o += align4(p.C);
+    p.o_core_birth = o; o += 4 * p.C;
+    p.o_slot_kind = o; o += align4(p.NL);
+    p.o_slot_rem = o; o += align4(p.NL);
+    p.o_slot_wait = o; o += align4(p.NL);
+    p.o_offer_core = o; o += align4(p.NL);
+    p.o_offer_recip = o; o += align4(p.NL);
+    p.o_offer_price = o; o += align4(p.NL);
+    p.o_slot_birth = o; o += 4 * p.NL;
+    p.rec_bytes = align16(o);
+    for (int i = 0; i < MS_MAX_KINDS; i++) {
+        p.prio[i] = c.job_priority[i];
+        p.len[i] = c.job_length[i];
+        p.acc[i] = c.acc_probability[i];
+        p.fix[i] = c.fix_price[i];
+    }
+    p.n_fix = c.n_fix_prices;
+    p.free_prices = c.free_prices;
+    p.commercial = c.commercial_reward;
+    p.new_jobs = c.new_jobs_per_round;
+    p.mult = c.reward_multiplier;
+    p.net_zero = (float)c.net_zero_offer_reward;
+    // LDS plan
+    int32_t s = 0;
+    p.s_rec = s; s += p.rec_bytes;
+    p.s_act_acc = s; s += align4(p.N * p.C);
+    p.s_act_off = s; s += align4(p.NL);
+    p.s_act_price = s; s += align4(p.NL);
+    p.s_act_auct = s; s += align4(p.C);
+    p.s_accr = s; s += 4 * p.N * p.C;          // acceptorNetRewards int32
+    p.s_offr = s; s += 4 * p.NL;               // offer / coreChooser rewards f32
+    p.s_pricer = s; s += 4 * p.NL;             // priceChooser rewards f32
+    p.s_spawn_kind = s; s += align4(p.N * (p.new_jobs > 0 ? p.new_jobs : 1));
+    s = align16(s);
+    p.s_scratch = s;
+    int32_t scratch = 4 * kMtN;  // MT twist buffer
+    if (scratch < kObsChunk) scratch = kObsChunk;
+    s += scratch;
+    p.s_total = s;
+    return p;
+}
+
+}  // namespace ms

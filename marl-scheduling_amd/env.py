@@ -1,0 +1,170 @@
+"""Batched env replicas on the device (torch tensors in, torch tensors out).
+
+``BatchedEnv`` is the E-replica counterpart of the reference's
+``SchedulingEnv.step()/reset()`` (SchedulingEnvironment.py:32-109): E
+independent worlds advance one round per ``step`` with one HIP kernel launch
+(ms_env_step). Observations are int8 rows, rewards f32/int32, all resident in
+HBM; optional ``out=`` tensors let a trainer write straight into its rollout
+buffers.
+"""
+from __future__ import annotations
+
+import ctypes as ct
+
+import numpy as np
+import torch
+
+from . import abi
+from ._lib import check, lib, ptr, stream_ptr
+
+
+class BatchedEnv:
+    def __init__(self, cfg: abi.MsConfig, n_envs: int, seed: int = 0, device=None):
+        if not torch.cuda.is_available():
+            raise RuntimeError("BatchedEnv needs a HIP device (no CPU fallback)")
+        self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+        self.cfg = cfg
+        self.E = int(n_envs)
+        self.seed = int(seed)
+        self._h = ct.c_void_p()
+        with torch.cuda.device(self.device):
+            check(lib.ms_env_create(ct.byref(cfg), self.E, ct.c_uint64(self.seed), ct.byref(self._h)))
+        sh = abi.MsShape()
+        check(lib.ms_env_shape(self._h, ct.byref(sh)))
+        self.shape = sh
+        self.N, self.C, self.L, self.O = sh.n_agents, sh.n_cores, sh.collection_length, sh.max_offers
+        self.free_prices = bool(cfg.free_prices)
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib.ms_env_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ---- buffers
+    def obs_buffers(self, auctioneer=False):
+        s, E, d = self.shape, self.E, self.device
+        acc = torch.empty((E, self.N, self.C, s.acc_obs_stride), dtype=torch.int8, device=d)
+        off = torch.empty((E, self.N, self.L, s.off_obs_stride), dtype=torch.int8, device=d)
+        auct = torch.empty((E, self.C, s.acc_obs_stride), dtype=torch.int8, device=d) if auctioneer else None
+        return dict(acceptor=acc, offer=off, auctioneer=auct)
+
+    def reward_buffers(self):
+        E, d = self.E, self.device
+        return dict(
+            offer=torch.empty((E, self.N, self.L), dtype=torch.float32, device=d),
+            price=torch.empty((E, self.N, self.L), dtype=torch.float32, device=d) if self.free_prices else None,
+            acceptor=torch.empty((E, self.N, self.C), dtype=torch.int32, device=d),
+            auctioneer=torch.empty((E, self.C), dtype=torch.int32, device=d),
+            agent=torch.empty((E, self.N), dtype=torch.int32, device=d),
+        )
+
+    def event_buffers(self):
+        E, d = self.E, self.device
+        return dict(
+            accepted=torch.empty((E, self.C, abi.ACCEPT_REC_BYTES), dtype=torch.int8, device=d),
+            terminated=torch.empty((E, self.C, abi.TERM_REC_BYTES), dtype=torch.int8, device=d),
+        )
+
+    # ---- API
+    @property
+    def round(self) -> int:
+        return int(lib.ms_env_round(self._h))
+
+    def reset(self, obs=None, stream=None):
+        """SchedulingEnv.reset (SchedulingEnvironment.py:85-109): observations only."""
+        obs = obs or self.obs_buffers()
+        o = abi.MsObsOut(ptr(obs.get("acceptor")), ptr(obs.get("offer")), ptr(obs.get("auctioneer")))
+        check(lib.ms_env_reset(self._h, ct.byref(o), stream_ptr(stream)))
+        return obs
+
+    def step(self, acceptor, offer_core, offer_price=None, auctioneer=None, obs=None, rewards=None, events=None,
+             stream=None):
+        """One round of SchedulingEnv.step (SchedulingEnvironment.py:32-83) for all replicas.
+
+        acceptor [E,N,C] int8, offer_core [E,N,L] int8, offer_price [E,N,L] int8
+        (free prices), auctioneer [E,C] int8 or None for the in-kernel
+        HardcodedAuctioneerAcceptor. Returns (obs, rewards, events) dicts.
+        """
+        for t in (acceptor, offer_core, offer_price, auctioneer):
+            if t is not None:
+                assert t.dtype == torch.int8 and t.is_contiguous() and t.device == self.device
+        assert acceptor.numel() == self.E * self.N * self.C and offer_core.numel() == self.E * self.N * self.L
+        if self.free_prices:
+            assert offer_price is not None and offer_price.numel() == self.E * self.N * self.L
+        if auctioneer is not None:
+            assert auctioneer.numel() == self.E * self.C
+        obs = self.obs_buffers() if obs is None else obs
+        rewards = self.reward_buffers() if rewards is None else rewards
+        a = abi.MsActions(ptr(acceptor), ptr(offer_core), ptr(offer_price if self.free_prices else None),
+                          ptr(auctioneer))
+        o = abi.MsObsOut(ptr(obs.get("acceptor")), ptr(obs.get("offer")), ptr(obs.get("auctioneer")))
+        r = abi.MsRewardOut(ptr(rewards.get("offer")), ptr(rewards.get("price")), ptr(rewards.get("acceptor")),
+                            ptr(rewards.get("auctioneer")), ptr(rewards.get("agent")))
+        ev = abi.MsEventOut(ptr(events.get("accepted")), ptr(events.get("terminated"))) if events else None
+        check(lib.ms_env_step(self._h, ct.byref(a), ct.byref(o), ct.byref(r), ct.byref(ev) if ev else None,
+                              stream_ptr(stream)))
+        return obs, rewards, events
+
+    def flags(self, stream=None) -> int:
+        f = ct.c_uint32()
+        check(lib.ms_env_flags(self._h, ct.byref(f), stream_ptr(stream)))
+        return int(f.value)
+
+    def randbelow(self, n: int, env_index: int = 0, stream=None) -> int:
+        """random._randbelow(n) on replica env_index's stream (random.randint(a, b) = a + randbelow(b-a+1))."""
+        out = ct.c_uint32()
+        check(lib.ms_env_randbelow(self._h, int(env_index), int(n), ct.byref(out), stream_ptr(stream)))
+        return int(out.value)
+
+    # ---- state export / import (canonical ms_state_host layout)
+    def _state_arrays(self):
+        E, N, C, L, cap = self.E, self.N, self.C, self.L, self.shape.liability_cap
+        return dict(
+            round=np.zeros(E, np.int32), flags=np.zeros(E, np.uint32),
+            core_owner=np.zeros((E, C), np.int32), core_kind=np.zeros((E, C), np.int32),
+            core_rem=np.zeros((E, C), np.int32), core_birth=np.zeros((E, C), np.int32),
+            slot_kind=np.zeros((E, N, L), np.int32), slot_rem=np.zeros((E, N, L), np.int32),
+            slot_wait=np.zeros((E, N, L), np.int32), slot_birth=np.zeros((E, N, L), np.int32),
+            offer_core=np.zeros((E, N, L), np.int32), offer_recip=np.zeros((E, N, L), np.int32),
+            offer_price=np.zeros((E, N, L), np.int32), liab_n=np.zeros((E, C), np.int32),
+            liab=np.zeros((E, C, cap, 5), np.int32), mt=np.zeros((E, 624), np.uint32),
+            mt_index=np.zeros(E, np.int32),
+        )
+
+    @staticmethod
+    def _struct(arrs):
+        st = abi.MsStateHost()
+        for name, _ in abi.MsStateHost._fields_:
+            setattr(st, name, arrs[name].ctypes.data)
+        return st
+
+    def export_state(self, stream=None) -> dict:
+        arrs = self._state_arrays()
+        check(lib.ms_env_export(self._h, ct.byref(self._struct(arrs)), stream_ptr(stream)))
+        return arrs
+
+    def import_state(self, state: dict, stream=None):
+        arrs = self._state_arrays()
+        for k, v in arrs.items():
+            if k in state:
+                v[...] = np.asarray(state[k]).reshape(v.shape).astype(v.dtype)
+        check(lib.ms_env_import(self._h, ct.byref(self._struct(arrs)), stream_ptr(stream)))
+
+
+def decode_accepted(raw: torch.Tensor) -> np.ndarray:
+    """[E,C,16] int8 ms_accept_rec bytes -> numpy structured array."""
+    dt = np.dtype([("valid", "i1"), ("offerer", "i1"), ("recipient", "i1"), ("slot", "i1"), ("price", "i1"),
+                   ("nec_time", "i1"), ("prio", "i1"), ("kind", "i1"), ("order", "i1"), ("pad", "i1", 3),
+                   ("round", "<i4")])
+    return raw.cpu().numpy().view(dt)[..., 0]
+
+
+def decode_terminated(raw: torch.Tensor) -> np.ndarray:
+    dt = np.dtype([("valid", "i1"), ("owner", "i1"), ("prio", "i1"), ("init_len", "i1"), ("dwell", "<i4")])
+    return raw.cpu().numpy().view(dt)[..., 0]
