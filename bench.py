@@ -1,0 +1,263 @@
+#!/usr/bin/env python3
+"""Headline benchmark: agent-env-steps/s of the marl-scheduling PPO loop (BASELINE.json cfg3).
+
+One benchmark step = one PPO iteration of the batched trainer: UPDATE_STEP (200)
+rounds of policy act (HIP) -> env step (HIP) -> buffer writes, followed by the
+full PPO update of every unit type (returns on HIP, K epochs of Adam in
+PyTorch-ROCm). Workload per GPU: 16384 env replicas x 8 agents x 8 cores,
+collectionLength 3, free prices + commercial reward, locally shared PPO
+(SURVEY.md §8(d) cfg3). value = agents x replicas x rounds over all ranks /
+max-over-ranks wall time of the timed steps (weak scaling: replicas per GPU fixed).
+
+Run: python bench.py [--gpus N --steps K --warmup W]; N > 1 under
+torch.distributed.run (one rank per GPU, RCCL all-reduce of the shared nets' gradients).
+"""
+from __future__ import annotations
+
+import argparse
+import importlib
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+if REPO not in sys.path:
+    sys.path.insert(0, REPO)
+
+METRIC = "agent-env-steps/sec (whole node), 8 agents×8 cores×16384 envs, 1/2/4/8 MI355X"
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
+
+
+def env_round_bytes(shape, k_new_jobs: int, free: bool) -> int:
+    """Algorithmic HBM bytes of one env replica's round in k_env_step:
+    state record read+write, actions read, observations written, rewards written,
+    and the MT19937 words the spawn draws consume (tie-break words and liability
+    entries are data dependent and not counted: this is a lower bound)."""
+    N, C, L = shape.n_agents, shape.n_cores, shape.collection_length
+    rec = shape.env_record_bytes
+    acts = N * C + N * L * (2 if free else 1)
+    obs = N * C * shape.acc_obs_stride + N * L * shape.off_obs_stride
+    rew = 4 * (N * C + N * L * (2 if free else 1) + N + C)
+    rng = 4 * 2 * k_new_jobs * N
+    return 2 * rec + acts + obs + rew + rng
+
+
+def cpu_baseline(seconds_budget: float = 20.0):
+    """The CPU restatement timed on this host: oracle env step (C, OpenMP) + torch-CPU
+    policy act / PPO update of the same cfg3 loop, on a bounded sample of replicas."""
+    import numpy as np
+    import torch
+
+    from oracle import pyoracle
+    from oracle.ppo_ref import RefActorCritic
+
+    # the box's CPU share is OMP_NUM_THREADS (os.sched_getaffinity shows the whole machine)
+    cores = min(len(os.sched_getaffinity(0)), int(os.environ.get("OMP_NUM_THREADS", "0") or 10**6))
+    torch.set_num_threads(cores)
+    cfg = pyoracle.abi.named_config("cfg3")
+    s = pyoracle.abi.config_shape(cfg)
+    N, C, L = s["N"], s["C"], s["L"]
+    E, T = 64, 200
+    batch = pyoracle.OracleBatch(cfg, E, seed=1)
+    torch.manual_seed(0)
+    nets = dict(acc=[RefActorCritic(s["acc_obs_dim"], s["acc_actions"]) for _ in range(N)],
+                off=[RefActorCritic(s["off_obs_dim"], s["off_actions"]) for _ in range(N)],
+                price=[RefActorCritic(4, s["price_actions"]) for _ in range(N)])
+    opt = {k: [torch.optim.Adam([{"params": n.actor.parameters(), "lr": 3e-3},
+                                 {"params": n.critic.parameters(), "lr": 1e-2}]) for n in v] for k, v in nets.items()}
+    acc_obs = np.zeros((E, N, C, s["acc_obs_stride"]), np.int8)
+    off_obs = np.zeros((E, N, L, s["off_obs_stride"]), np.int8)
+    buf = dict(acc=[], off=[], price=[])
+
+    def act(group, x):  # x [E, N, U, D] float -> actions [E, N, U]
+        out = torch.empty(x.shape[:3], dtype=torch.long)
+        lps = torch.empty(x.shape[:3])
+        with torch.no_grad():
+            for a in range(N):
+                probs = group[a].actor(x[:, a])
+                d = torch.distributions.Categorical(probs)
+                act_ = d.sample()
+                out[:, a], lps[:, a] = act_, d.log_prob(act_)
+        return out, lps
+
+    t0 = time.perf_counter()
+    rounds = 0
+    for t in range(T):
+        xa = torch.from_numpy(acc_obs[..., : s["acc_obs_dim"]]).float()
+        xo = torch.from_numpy(off_obs[..., : s["off_obs_dim"]]).float()
+        ao, lpo = act(nets["off"], xo)
+        idx = (2 * ao).unsqueeze(-1) + torch.arange(2)
+        pin = torch.cat((torch.gather(xo, 3, idx), xo[..., 2 * C:2 * C + 2]), -1)
+        pin = torch.where((ao == 0).unsqueeze(-1), torch.full_like(pin, -5.0), pin)
+        ap, lpp = act(nets["price"], pin)
+        aa, lpa = act(nets["acc"], xa)
+        price = torch.where(ao == 0, torch.full_like(ap, -5), ap)
+        res = batch.step(aa.numpy().astype(np.int8), ao.numpy().astype(np.int8), price.numpy().astype(np.int8),
+                         threads=cores)
+        acc_obs, off_obs = res["acc_obs"], res["off_obs"]
+        buf["acc"].append((xa, aa, lpa, torch.from_numpy(res["acceptor"]).float()))
+        buf["off"].append((xo, ao, lpo, torch.from_numpy(res["offer"])))
+        buf["price"].append((pin, ap, lpp, torch.from_numpy(res["price"])))
+        rounds += 1
+        if rounds >= 8 and time.perf_counter() - t0 > seconds_budget:
+            break
+    # one PPO update on 2 sub-units per agent and unit type (locally shared, K = 1)
+    for kind, units in (("acc", C), ("off", L), ("price", L)):
+        xs = torch.stack([b[0] for b in buf[kind]], 1)        # [E, R, N, U, D]
+        as_ = torch.stack([b[1] for b in buf[kind]], 1)
+        lp = torch.stack([b[2] for b in buf[kind]], 1)
+        rw = torch.stack([b[3] for b in buf[kind]], 1)
+        for a in range(N):
+            for sub in range(2):
+                u = sub % units
+                x = xs[:, :, a, u].reshape(-1, xs.shape[-1])
+                g = torch.zeros_like(rw[:, :, a, u])
+                run = torch.zeros(E)
+                for r in range(rw.shape[1] - 1, -1, -1):
+                    run = rw[:, r, a, u] + 0.95 * run
+                    g[:, r] = run
+                g = ((g - g.mean(1, keepdim=True)) / (g.std(1, keepdim=True) + 1e-7)).reshape(-1)
+                logp, v, ent = nets[kind][a].evaluate(x, as_[:, :, a, u].reshape(-1))
+                ratio = torch.exp(logp - lp[:, :, a, u].reshape(-1))
+                adv = g - v.detach()
+                loss = (-torch.min(ratio * adv, ratio.clamp(0.8, 1.2) * adv) + 0.5 * ((v - g) ** 2).mean()
+                        - 0.01 * ent).mean()
+                opt[kind][a].zero_grad()
+                loss.backward()
+                opt[kind][a].step()
+    dt = time.perf_counter() - t0
+    return {"value": E * N * rounds / dt, "unit": "agent-env-steps/s", "cores": cores, "kind": "port",
+            "sample": "%d replicas x %d rounds of cfg3 (oracle C env step, OpenMP %d threads) + torch-CPU act and "
+                      "one locally-shared PPO update (K=1, 2 sub-units per agent and unit type)" % (E, rounds, cores)}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=2)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--envs", type=int, default=16384, help="env replicas per GPU")
+    ap.add_argument("--update-step", type=int, default=200)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    device = torch.device("cuda", local_rank)
+    torch.cuda.set_device(device)
+    ms = importlib.import_module("marl-scheduling_amd")
+    trainer_mod = importlib.import_module("marl-scheduling_amd.trainer")
+    tr = trainer_mod.Trainer.from_named("cfg3", n_envs=args.envs, update_step=args.update_step, seed=0,
+                                        device=device, rank=rank, world_size=world)
+    shape = tr.env.shape
+
+    # per-launch timing of the env-step kernel on its stream (HIP events) inside the timed region
+    stream = torch.cuda.current_stream(device)
+    step_events = []
+    orig_step = tr.env.step
+
+    def timed_step(*a, **kw):
+        if timing[0]:
+            s_ev, e_ev = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            s_ev.record(stream)
+            out = orig_step(*a, **kw)
+            e_ev.record(stream)
+            step_events.append((s_ev, e_ev))
+            return out
+        return orig_step(*a, **kw)
+
+    timing = [False]
+    tr.env.step = timed_step
+
+    for _ in range(args.warmup):
+        tr.iteration()
+    torch.cuda.synchronize(device)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(device)
+    tr.timings = dict(rollout=0.0, update=0.0)
+    timing[0] = True
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        tr.iteration()
+    torch.cuda.synchronize(device)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(device)
+    elapsed = time.perf_counter() - t0
+    timing[0] = False
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    flags = tr.flags()
+    if flags:
+        raise SystemExit("env error flags set: 0x%x" % flags)
+
+    rounds = args.update_step * args.steps
+    agent_steps = world * args.envs * shape.n_agents * rounds
+    value = agent_steps / elapsed
+    step_ms = [s.elapsed_time(e) for s, e in step_events]
+    avg_step_s = sum(step_ms) / len(step_ms) / 1e3
+    b_round = env_round_bytes(shape, tr.cfg.new_jobs_per_round, tr.free)
+    achieved = b_round * args.envs / avg_step_s / 1e9
+    result = {
+        "metric": METRIC,
+        "value": value,
+        "unit": "agent-env-steps/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": elapsed / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "int8/f32",
+        "data": "synthetic (env job stream from the reference spawn sampler, random-init nets)",
+        "config": {
+            "workload": "cfg3: %d env replicas/GPU x 8 agents x 8 cores, collectionLength 3, freePrices + "
+                        "commercialFreePriceReward, PPO locallySharedParameters, UPDATE_STEP %d; one step = one PPO "
+                        "iteration (%d rounds + update)" % (args.envs, args.update_step, args.update_step),
+            "replicas_per_gpu": args.envs,
+            "rounds_per_step": args.update_step,
+            "parallelism": "replicas sharded over %d rank(s), RCCL grad all-reduce" % world,
+        },
+        "roofline": {
+            "kernel": "ms::k_env_step",
+            "bound": "hbm",
+            "achieved": achieved,
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBS,
+            "traffic": None,
+            "bytes_per_env_round": b_round,
+            "avg_launch_us": avg_step_s * 1e6,
+        },
+        "breakdown_ms_per_step": {
+            "rollout": tr.timings["rollout"] / args.steps * 1e3,
+            "update": tr.timings["update"] / args.steps * 1e3,
+            "env_step_kernels": sum(step_ms) / args.steps,
+        },
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        try:
+            result["cpu_baseline"] = cpu_baseline()
+        except Exception as exc:  # reported, never fatal for the GPU number
+            result["cpu_baseline"] = {"error": repr(exc)}
+    if rank == 0:
+        print(json.dumps(result))
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,175 @@
+"""PPO for groups of tiny actor-critics (PPOmodules.py, batched over units and replicas).
+
+The reference keeps one ``ActorCritic`` per unit (PPOmodules.py:25-72) and
+updates each with its own ``PPO.update`` (PPOmodules.py:127-174). Here the
+nets of one unit type are stacked into groups ``[G, ...]``:
+
+* divided agents   — one group per unit (``AcceptorPPO``/``OfferPPO``/``FreePriceOfferPPO``),
+* locally shared   — one group per agent (``LocallySharedPPO``, PPOmodules.py:490-597),
+* globally shared  — one group (``GloballySharedPPO``, PPOmodules.py:335-449).
+
+Action selection runs in the fused HIP kernel (``ms_policy_act``); the
+update runs as batched torch ops (bmm over groups) with ``torch.optim.Adam``
+on two parameter groups (actor / critic learning rates, PPOmodules.py:100-105).
+All groups step in lockstep, which equals independent per-net optimizers
+because Adam is elementwise. With E replicas a sub-unit's batch holds its
+E*T transitions; returns are normalised per replica over T so that E = 1 is
+exactly the reference.
+"""
+from __future__ import annotations
+
+import ctypes as ct
+
+import torch
+import torch.nn as nn
+from torch.distributions import Categorical
+
+from . import abi
+from ._lib import check, lib, ptr, stream_ptr
+
+HIDDEN = 16  # numberOfNeurons of every divided / shared net (PPOmodules.py:241,259,276,456,475,604,623)
+
+
+def reference_actor_critic_params(in_dim: int, n_actions: int, hidden: int = HIDDEN):
+    """One ActorCritic initialised exactly like the reference constructor:
+    actor Linear x3 then critic Linear x3 with nn.Linear's default init on the
+    current torch CPU generator (PPOmodules.py:32-48). Returns a flat dict."""
+    a1, a2, a3 = nn.Linear(in_dim, hidden), nn.Linear(hidden, hidden), nn.Linear(hidden, n_actions)
+    c1, c2, c3 = nn.Linear(in_dim, hidden), nn.Linear(hidden, hidden), nn.Linear(hidden, 1)
+    return dict(w1=a1.weight, b1=a1.bias, w2=a2.weight, b2=a2.bias, w3=a3.weight, b3=a3.bias,
+                cw1=c1.weight, cb1=c1.bias, cw2=c2.weight, cb2=c2.bias, cw3=c3.weight, cb3=c3.bias)
+
+
+ACTOR_KEYS = ("w1", "b1", "w2", "b2", "w3", "b3")
+CRITIC_KEYS = ("cw1", "cb1", "cw2", "cb2", "cw3", "cb3")
+
+
+class GroupedActorCritic(nn.Module):
+    """G ActorCritic nets of identical shape, parameters stacked along dim 0."""
+
+    def __init__(self, n_groups: int, in_dim: int, n_actions: int, hidden: int = HIDDEN, init: bool = True):
+        super().__init__()
+        self.G, self.D, self.A, self.H = n_groups, in_dim, n_actions, hidden
+        if not init:
+            shapes = dict(w1=(hidden, in_dim), b1=(hidden,), w2=(hidden, hidden), b2=(hidden,), w3=(n_actions, hidden),
+                          b3=(n_actions,), cw1=(hidden, in_dim), cb1=(hidden,), cw2=(hidden, hidden), cb2=(hidden,),
+                          cw3=(1, hidden), cb3=(1,))
+            for k in ACTOR_KEYS + CRITIC_KEYS:
+                self.register_parameter(k, nn.Parameter(torch.zeros((n_groups,) + shapes[k])))
+            return
+        nets = []
+        for _ in range(n_groups):
+            # the reference builds policy then policy_old (PPOmodules.py:99,107): both draw
+            # from torch's generator, so construct both to keep the same init stream.
+            p = reference_actor_critic_params(in_dim, n_actions, hidden)
+            reference_actor_critic_params(in_dim, n_actions, hidden)
+            nets.append(p)
+        for k in ACTOR_KEYS + CRITIC_KEYS:
+            self.register_parameter(k, nn.Parameter(torch.stack([n[k].detach() for n in nets]).contiguous()))
+
+    def actor_parameters(self):
+        return [getattr(self, k) for k in ACTOR_KEYS]
+
+    def critic_parameters(self):
+        return [getattr(self, k) for k in CRITIC_KEYS]
+
+    @staticmethod
+    def _mlp(x, w1, b1, w2, b2, w3, b3):
+        h = torch.tanh(torch.baddbmm(b1.unsqueeze(1), x, w1.transpose(1, 2)))
+        h = torch.tanh(torch.baddbmm(b2.unsqueeze(1), h, w2.transpose(1, 2)))
+        return torch.baddbmm(b3.unsqueeze(1), h, w3.transpose(1, 2))
+
+    def actor_probs(self, x):
+        """x [G, R, D] float -> action probabilities [G, R, A] (nn.Softmax(dim=-1))."""
+        return torch.softmax(self._mlp(x, self.w1, self.b1, self.w2, self.b2, self.w3, self.b3), dim=-1)
+
+    def critic(self, x):
+        return self._mlp(x, self.cw1, self.cb1, self.cw2, self.cb2, self.cw3, self.cb3).squeeze(-1)
+
+    def evaluate(self, x, actions):
+        """ActorCritic.evaluate (PPOmodules.py:65-72) batched over groups."""
+        dist = Categorical(self.actor_probs(x))
+        return dist.log_prob(actions), self.critic(x), dist.entropy()
+
+    def mlp_params(self) -> abi.MsMlpParams:
+        for k in ACTOR_KEYS:
+            t = getattr(self, k)
+            assert t.is_cuda and t.is_contiguous() and t.dtype == torch.float32
+        return abi.MsMlpParams(ptr(self.w1), ptr(self.b1), ptr(self.w2), ptr(self.b2), ptr(self.w3), ptr(self.b3),
+                               self.D, self.H, self.A, self.G)
+
+    @torch.no_grad()
+    def act(self, obs_i8, n_units: int, seed: int, offset: int, uniforms=None, action=None, logprob=None, stream=None):
+        """ActorCritic.act (PPOmodules.py:53-63) for obs [E, n_units, stride] int8 on the HIP kernel.
+        Unit u uses group u // (n_units // G). Returns (action int8 [E, U], logprob f32 [E, U])."""
+        E, U, stride = obs_i8.shape
+        assert U == n_units and U % self.G == 0 and obs_i8.dtype == torch.int8 and obs_i8.is_contiguous()
+        dev = obs_i8.device
+        if action is None:
+            action = torch.empty((E, U), dtype=torch.int8, device=dev)
+        if logprob is None:
+            logprob = torch.empty((E, U), dtype=torch.float32, device=dev)
+        p = self.mlp_params()
+        check(lib.ms_policy_act(ct.byref(p), ptr(obs_i8), stride, E, U, U // self.G, ct.c_uint64(seed),
+                                ct.c_uint64(offset), ptr(uniforms), ptr(action), ptr(logprob), stream_ptr(stream)))
+        return action, logprob
+
+
+def discounted_returns(rewards_tm: torch.Tensor, gamma: float, stream=None) -> torch.Tensor:
+    """PPO.update's return estimate (PPOmodules.py:128-137) on the HIP kernel.
+    rewards_tm [T, M] f32 (time-major, M independent sequences) -> [M, T] f32 normalised per sequence."""
+    rewards_tm = rewards_tm.contiguous().float()
+    T, M = rewards_tm.shape
+    out = torch.empty((M, T), dtype=torch.float32, device=rewards_tm.device)
+    check(lib.ms_discounted_returns(ptr(rewards_tm), T, M, M, ct.c_double(gamma), ptr(out), stream_ptr(stream)))
+    return out
+
+
+class PPOGroup:
+    """Policy / policy_old pair + Adam for one unit type (PPOmodules.py:75-174)."""
+
+    def __init__(self, n_groups, in_dim, n_actions, lr_actor, lr_critic, gamma, eps_clip, k_epochs, device,
+                 allreduce=None):
+        self.policy = GroupedActorCritic(n_groups, in_dim, n_actions).to(device)
+        self.policy_old = GroupedActorCritic(n_groups, in_dim, n_actions, init=False).to(device)
+        self.policy_old.requires_grad_(False)
+        self.sync_old()
+        self.optimizer = torch.optim.Adam([
+            {"params": self.policy.actor_parameters(), "lr": lr_actor},
+            {"params": self.policy.critic_parameters(), "lr": lr_critic},
+        ])
+        self.gamma, self.eps_clip, self.K = gamma, eps_clip, k_epochs
+        self.allreduce = allreduce
+        self.last_losses = []
+
+    @torch.no_grad()
+    def sync_old(self):
+        """policy_old.load_state_dict(policy.state_dict()) (PPOmodules.py:171)."""
+        for k in ACTOR_KEYS + CRITIC_KEYS:
+            getattr(self.policy_old, k).copy_(getattr(self.policy, k))
+
+    def update(self, states, actions, old_logprobs, returns):
+        """K epochs of full-batch clipped-surrogate PPO (PPOmodules.py:144-168).
+
+        states [G, R, D] float, actions [G, R] int64, old_logprobs [G, R], returns [G, R]
+        (already normalised). Each group's loss is the mean over its R rows; the
+        groups' losses are summed, so every group receives exactly its own gradient.
+        """
+        losses = []
+        for _ in range(self.K):
+            logprobs, values, entropy = self.policy.evaluate(states, actions)
+            ratios = torch.exp(logprobs - old_logprobs)
+            adv = returns - values.detach()
+            surr1 = ratios * adv
+            surr2 = torch.clamp(ratios, 1 - self.eps_clip, 1 + self.eps_clip) * adv
+            mse = ((values - returns) ** 2).mean(dim=1, keepdim=True)  # nn.MSELoss() per group, broadcast
+            loss = -torch.min(surr1, surr2) + 0.5 * mse - 0.01 * entropy
+            per_group = loss.mean(dim=1)
+            self.optimizer.zero_grad()
+            per_group.sum().backward()
+            if self.allreduce is not None:
+                self.allreduce(self.policy.parameters())
+            self.optimizer.step()
+            losses.append(per_group.detach())
+        self.last_losses = losses
+        return losses

@@ -1,0 +1,262 @@
+"""Batched PPO training loop over E env replicas (the trainPPO.py loop, trainPPO.py:133-227).
+
+One ``iteration`` = UPDATE_STEP rounds of (policy act -> env step -> buffer
+writes) followed by the PPO update of every unit type, the cadence of
+``trainPPO.py:169`` (update when ``world.round % UPDATE_STEP == 0``).
+Everything stays on the device: observations are written by the env kernel
+straight into the rollout buffers, actions/log-probs by the act kernel.
+
+Architectures (SchedulingEnvironment.py:253-348):
+  ``divided`` — PPODividedFixedPriceEnv / PPODividedFreePriceEnv: one net per unit,
+  ``local``   — LocallySharedParamsDividedFixedPriceEnv (+ the free-price variant
+                BASELINE cfg3 names): one net per agent and unit type,
+                CENTRALISATION_SAMPLE sub-units drawn per agent (Agent.py:708-728),
+  ``global``  — GloballySharedParamsDividedFixedPriceEnv: one net per unit type,
+                CENTRALISATION_SAMPLE (agent, sub-unit) pairs (SchedulingEnvironment.py:314-329).
+
+Multi-GPU: replicas shard across ranks (weak scaling); the nets are shared, so
+each optimizer step all-reduces one flattened gradient buffer (RCCL).
+"""
+from __future__ import annotations
+
+import random
+import time
+from dataclasses import dataclass, field
+
+import torch
+
+from . import abi
+from .env import BatchedEnv
+from .ppo import PPOGroup, discounted_returns
+
+
+@dataclass
+class Hyper:
+    """RL hyper-parameters of trainPPO.py:66-84 (defaults: trainPPO.py)."""
+    lr_actor: float = 0.003
+    lr_critic: float = 0.01
+    eps_clip: float = 0.2
+    acceptor_gamma: float | None = None   # default -((1-maxLen)/maxLen) + 0.04 (trainPPO.py:72)
+    offer_gamma: float = 0.5
+    raw_k_epochs: int = 3
+    centralisation_sample: int = 2
+    update_step: int = 200
+    extra: dict = field(default_factory=dict)
+
+
+def _k_epochs(raw, factor):
+    return max(round(raw / factor), 1)  # trainPPO.py:76-77 (Python round: half-even)
+
+
+class _Unit:
+    """Rollout buffers + PPO group of one unit type (acceptor / offer / price chooser)."""
+
+    def __init__(self, name, E, T, n_units, per_group, in_dim, stride, n_actions, group: PPOGroup, device,
+                 reward_dtype):
+        self.name, self.E, self.T, self.U, self.S = name, E, T, n_units, per_group
+        self.D, self.stride = in_dim, stride
+        self.group = group
+        self.actions = torch.zeros((T, E, n_units), dtype=torch.int8, device=device)
+        self.logprobs = torch.zeros((T, E, n_units), dtype=torch.float32, device=device)
+        self.rewards = torch.zeros((T, E, n_units), dtype=reward_dtype, device=device)
+
+    def batch(self, states_i8, u_sel):
+        """Gather the update batch of the selected unit per group (u_sel [G] long)."""
+        T, E, G = self.T, self.E, u_sel.numel()
+        x = states_i8.index_select(2, u_sel)[..., : self.D]               # [T, E, G, D]
+        x = x.permute(2, 0, 1, 3).reshape(G, T * E, self.D).float()
+        a = self.actions.index_select(2, u_sel).permute(2, 0, 1).reshape(G, T * E).long()
+        lp = self.logprobs.index_select(2, u_sel).permute(2, 0, 1).reshape(G, T * E)
+        r = self.rewards.index_select(2, u_sel).float().reshape(T, E * G)
+        ret = discounted_returns(r, self.group.gamma)                     # [E*G, T]
+        ret = ret.view(E, G, T).permute(1, 2, 0).reshape(G, T * E)
+        return x, a, lp, ret
+
+
+class Trainer:
+    def __init__(self, cfg: abi.MsConfig, n_envs: int, arch: str = "local", hyper: Hyper | None = None, seed: int = 0,
+                 device=None, rank: int = 0, world_size: int = 1, process_group=None):
+        assert arch in ("divided", "local", "global")
+        self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+        torch.cuda.set_device(self.device)
+        self.cfg, self.arch, self.E = cfg, arch, int(n_envs)
+        self.hp = hyper or Hyper()
+        self.rank, self.world_size, self.pg = rank, world_size, process_group
+        self.seed = seed
+        self.env = BatchedEnv(cfg, self.E, seed=seed * 1_000_003 + rank * self.E, device=self.device)
+        s = self.env.shape
+        N, C, L = s.n_agents, s.n_cores, s.collection_length
+        self.N, self.C, self.L = N, C, L
+        self.free = bool(cfg.free_prices)
+        T = self.T = self.hp.update_step
+        hp = self.hp
+        max_len = max(cfg.job_length[: cfg.n_kinds])
+        acc_gamma = hp.acceptor_gamma if hp.acceptor_gamma is not None else -((1 - max_len) / max_len) + 0.04
+        # K epochs and groups per architecture (trainPPO.py:54-55,76-77; PPOmodules.py:289,304)
+        if arch == "divided":
+            ga, go, k_acc, k_off = N * C, N * L, _k_epochs(hp.raw_k_epochs, 1), _k_epochs(hp.raw_k_epochs, 1)
+            if self.free:
+                k_off = hp.raw_k_epochs  # FreePriceOfferPPO uses env.RAW_K_EPOCHS
+        elif arch == "local":
+            ga, go, k_acc, k_off = N, N, _k_epochs(hp.raw_k_epochs, C), _k_epochs(hp.raw_k_epochs, L)
+        else:
+            ga, go, k_acc, k_off = 1, 1, _k_epochs(hp.raw_k_epochs, N * C), _k_epochs(hp.raw_k_epochs, N * L)
+        self.k_acc, self.k_off = k_acc, k_off
+        allreduce = self._allreduce if world_size > 1 else None
+        torch.manual_seed(seed)  # same initial weights on every rank
+        dev = self.device
+        mk = lambda G, D, A, gamma, K: PPOGroup(G, D, A, hp.lr_actor, hp.lr_critic, gamma, hp.eps_clip, K, dev,
+                                                allreduce)
+        self.acc = _Unit("acceptor", self.E, T, N * C, (N * C) // ga, s.acc_obs_dim, s.acc_obs_stride, s.acc_actions,
+                         mk(ga, s.acc_obs_dim, s.acc_actions, acc_gamma, k_acc), dev, torch.int32)
+        self.off = _Unit("offer", self.E, T, N * L, (N * L) // go, s.off_obs_dim, s.off_obs_stride, s.off_actions,
+                         mk(go, s.off_obs_dim, s.off_actions, hp.offer_gamma, k_off), dev, torch.float32)
+        self.price = None
+        if self.free:
+            self.price = _Unit("price", self.E, T, N * L, (N * L) // go, 4, 4, s.price_actions,
+                               mk(go, 4, s.price_actions, hp.offer_gamma, k_off), dev, torch.float32)
+        if world_size > 1:
+            self._broadcast_params()
+        # observation ring: slot t holds the state acted on at round t; slot T the next state
+        self.acc_obs = torch.zeros((T + 1, self.E, N * C, s.acc_obs_stride), dtype=torch.int8, device=dev)
+        self.off_obs = torch.zeros((T + 1, self.E, N * L, s.off_obs_stride), dtype=torch.int8, device=dev)
+        self.price_obs = torch.zeros((T, self.E, N * L, 4), dtype=torch.int8, device=dev) if self.free else None
+        self.env_price = torch.zeros((self.E, N * L), dtype=torch.int8, device=dev)
+        self.agent_reward = torch.zeros((self.E, N), dtype=torch.int32, device=dev)
+        self.auct_reward = torch.zeros((self.E, C), dtype=torch.int32, device=dev)
+        self.rng = random.Random(seed)  # sub-unit draws (random.randint), identical on every rank
+        self.act_offset = 0
+        self.iterations = 0
+        self.env.reset(dict(acceptor=self.acc_obs[0], offer=self.off_obs[0]))
+        self.timings = dict(rollout=0.0, update=0.0)
+
+    @classmethod
+    def from_named(cls, name: str, n_envs=None, update_step=200, seed=0, device=None, **kw):
+        cfg = abi.named_config(name)
+        arch = {"cfg1": "divided", "cfg2": "global", "cfg3": "local", "cfg4": "divided", "cfg5": "divided"}[name]
+        hp = Hyper(update_step=update_step)
+        if name == "cfg3":  # trainPPOExperiment4.py:96-98 (free prices): RAW_K 2, ACCEPTOR_GAMMA 0.95
+            hp.raw_k_epochs = 2
+            hp.acceptor_gamma = -((1 - 5) / 5) + 0.15
+        return cls(cfg, n_envs or abi.NAMED_ENVS[name], arch=kw.pop("arch", arch), hyper=hp, seed=seed, device=device,
+                   **kw)
+
+    # ---- distributed helpers
+    def _allreduce(self, params):
+        import torch.distributed as dist
+        grads = [p.grad for p in params if p.grad is not None]
+        flat = torch._utils._flatten_dense_tensors(grads)
+        dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=self.pg)
+        flat.div_(self.world_size)
+        for g, f in zip(grads, torch._utils._unflatten_dense_tensors(flat, grads)):
+            g.copy_(f)
+
+    def _broadcast_params(self):
+        import torch.distributed as dist
+        for u in self.units():
+            for p in u.group.policy.parameters():
+                dist.broadcast(p.data, src=0, group=self.pg)
+            u.group.sync_old()
+
+    def units(self):
+        return [u for u in (self.acc, self.off, self.price) if u is not None]
+
+    # ---- rollout
+    def round(self, t: int):
+        """getActionForAllAgents + env.step + saveRewards for round t of the iteration
+        (trainPPO.py:160-167)."""
+        E, N, C, L = self.E, self.N, self.C, self.L
+        seed = self.seed * 7919 + self.rank
+        # per agent: offer units then acceptors (Agent.py:504-515); separate streams per unit type
+        self.off.group.policy_old.act(self.off_obs[t], N * L, seed, self.act_offset + 1,
+                                      action=self.off.actions[t], logprob=self.off.logprobs[t])
+        if self.free:
+            # FreePriceOfferPPO.selectAction (PPOmodules.py:312-332): price chooser input
+            # [obs[2a:2a+2], obs[-2:]] or the dummy [-5,-5,-5,-5] when the core chooser picked 0
+            a = self.off.actions[t].long()                                   # [E, NL]
+            obs = self.off_obs[t]
+            idx = (2 * a).unsqueeze(-1) + torch.arange(2, device=obs.device)
+            core_part = torch.gather(obs, 2, idx)
+            slot_part = obs[..., 2 * C: 2 * C + 2]
+            pin = torch.cat((core_part, slot_part), dim=-1)
+            pin = torch.where((a == 0).unsqueeze(-1), torch.full_like(pin, -5), pin)
+            self.price_obs[t].copy_(pin)
+            self.price.group.policy_old.act(self.price_obs[t], N * L, seed, self.act_offset + 2,
+                                            action=self.price.actions[t], logprob=self.price.logprobs[t])
+            torch.where(a == 0, torch.full_like(self.price.actions[t], -5), self.price.actions[t], out=self.env_price)
+        self.acc.group.policy_old.act(self.acc_obs[t], N * C, seed, self.act_offset + 3,
+                                      action=self.acc.actions[t], logprob=self.acc.logprobs[t])
+        self.act_offset += 4
+        obs = dict(acceptor=self.acc_obs[t + 1], offer=self.off_obs[t + 1])
+        rew = dict(offer=self.off.rewards[t].view(E, N, L), acceptor=self.acc.rewards[t].view(E, N, C),
+                   agent=self.agent_reward, auctioneer=self.auct_reward,
+                   price=self.price.rewards[t].view(E, N, L) if self.free else None)
+        self.env.step(self.acc.actions[t].view(E, N, C), self.off.actions[t].view(E, N, L),
+                      self.env_price.view(E, N, L) if self.free else None, obs=obs, rewards=rew)
+
+    def rollout(self):
+        for t in range(self.T):
+            self.round(t)
+
+    # ---- update
+    def _draws(self):
+        """Sub-unit selections, in the reference's random.randint order."""
+        N, C, L, CS = self.N, self.C, self.L, self.hp.centralisation_sample
+        dev = self.device
+        if self.arch == "divided":
+            sel = dict(acceptor=[torch.arange(N * C, device=dev)], offer=[torch.arange(N * L, device=dev)])
+        elif self.arch == "local":
+            acc = [[0] * N for _ in range(CS)]
+            off = [[0] * N for _ in range(CS)]
+            for a in range(N):  # per agent: acceptor draws then offer draws (Agent.py:716-728)
+                for i in range(CS):
+                    acc[i][a] = a * C + self.rng.randint(0, C - 1)
+                for j in range(CS):
+                    off[j][a] = a * L + self.rng.randint(0, L - 1)
+            sel = dict(acceptor=[torch.tensor(r, device=dev) for r in acc],
+                       offer=[torch.tensor(r, device=dev) for r in off])
+        else:
+            acc, off = [], []
+            for _ in range(CS):  # SchedulingEnvironment.py:315-321
+                a = self.rng.randint(0, N - 1)
+                c = self.rng.randint(0, C - 1)
+                acc.append(torch.tensor([a * C + c], device=dev))
+            for _ in range(CS):  # SchedulingEnvironment.py:323-329
+                a = self.rng.randint(0, N - 1)
+                l = self.rng.randint(0, L - 1)
+                off.append(torch.tensor([a * L + l], device=dev))
+            sel = dict(acceptor=acc, offer=off)
+        sel["price"] = sel["offer"]
+        return sel
+
+    def update(self):
+        """env.updateAgents() (SchedulingEnvironment.py:208-210 / 314-329, Agent.py:524-529,708-728)."""
+        sel = self._draws()
+        losses = {}
+        for u in self.units():
+            states = self.acc_obs if u is self.acc else (self.off_obs if u is self.off else self.price_obs)
+            states = states[: self.T]
+            ls = []
+            for u_sel in sel[u.name]:
+                x, a, lp, ret = u.batch(states, u_sel)
+                ls += u.group.update(x, a, lp, ret)
+            u.group.sync_old()
+            losses[u.name] = torch.stack(ls)
+        # next iteration starts from the last observation
+        self.acc_obs[0].copy_(self.acc_obs[self.T])
+        self.off_obs[0].copy_(self.off_obs[self.T])
+        return losses
+
+    def iteration(self):
+        t0 = time.perf_counter()
+        self.rollout()
+        t1 = time.perf_counter()
+        losses = self.update()
+        t2 = time.perf_counter()
+        self.timings["rollout"] += t1 - t0
+        self.timings["update"] += t2 - t1
+        self.iterations += 1
+        return losses
+
+    def flags(self):
+        return self.env.flags()
