@@ -1,0 +1,18 @@
+#!/usr/bin/env bash
+# Profile the bench on a GPU box: kernel trace + stats, then separate PMC passes
+# (FETCH_SIZE / WRITE_SIZE, one counter block per pass) for the env-step kernel.
+# Usage (via gpurun): bash profiles/run_profile.sh <tag>
+set -euo pipefail
+TAG="${1:-r1}"
+R="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
+OUT="$R/gpurun_out/prof_${TAG}"
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+cd /tmp
+timeout -k 10 600 rocprofv3 --kernel-trace --stats -f csv -d "$OUT/trace" -o run -- \
+  python3 "$R/bench.py" --steps 1 --warmup 1 --no-cpu-baseline > "$OUT/bench.json" 2> "$OUT/trace.err"
+timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex k_env_step -f csv -d "$OUT/pmc_fetch" -o run -- \
+  python3 "$R/bench.py" --steps 1 --warmup 0 --update-step 20 --no-cpu-baseline > "$OUT/pmc_fetch.json" 2> "$OUT/pmc_fetch.err"
+timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex k_env_step -f csv -d "$OUT/pmc_write" -o run -- \
+  python3 "$R/bench.py" --steps 1 --warmup 0 --update-step 20 --no-cpu-baseline > "$OUT/pmc_write.json" 2> "$OUT/pmc_write.err"
+echo "profile done: $OUT"
