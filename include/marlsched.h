@@ -236,6 +236,32 @@ int ms_policy_act(const ms_mlp_params* p, const int8_t* obs, int32_t obs_stride,
 int ms_discounted_returns(const float* rewards, int32_t T, int64_t M, int64_t row_stride,
                           double gamma, float* out, void* stream);
 
+/* ---- fused PPO loss gradient (one K-epoch step of PPO.update, PPOmodules.py:144-168) ----
+ * For every group g: d/dθ_g of
+ *   mean_r[-min(ratio*adv, clamp(ratio, 1-eps, 1+eps)*adv)] + 0.5*mean_r[(V-G)^2] - 0.01*mean_r[entropy]
+ * over the R = T*E transitions of sub-unit unit_of_group[g], read straight from the
+ * int8 rollout buffer (row r = t*E + e). Gradients are written (not accumulated) in
+ * torch .grad layouts; the optimizer step stays with the caller. Deterministic. */
+typedef struct ms_ppo_batch {
+    const int8_t* states;          /* [R][U][stride] observation rows */
+    const int8_t* actions;         /* [R][U] */
+    const float* old_logprobs;     /* [R][U] */
+    const float* returns;          /* [E][G][T] normalised (ms_discounted_returns output) */
+    const int32_t* unit_of_group;  /* [G] device array */
+    int32_t stride, T, U;
+    int64_t E;
+} ms_ppo_batch;
+
+typedef struct ms_ppo_grads {  /* device outputs, [G][...] like the weights */
+    float *w1, *b1, *w2, *b2, *w3, *b3;       /* actor */
+    float *cw1, *cb1, *cw2, *cb2, *cw3, *cb3; /* critic (output width 1) */
+    float* loss;                              /* [G][3]: mean(-min(surr)), mean((V-G)^2), mean(entropy) */
+} ms_ppo_grads;
+
+size_t ms_ppo_workspace_bytes(const ms_mlp_params* actor, int64_t rows);
+int ms_ppo_grad(const ms_mlp_params* actor, const ms_mlp_params* critic, const ms_ppo_batch* batch, float eps_clip,
+                void* workspace, size_t workspace_bytes, const ms_ppo_grads* grads, void* stream);
+
 const char* ms_last_error(void);
 int ms_abi_version(void);
 

@@ -50,6 +50,10 @@ def _load():
         "ms_env_import": (ct.c_int, [P, ct.POINTER(abi.MsStateHost), P]),
         "ms_policy_act": (ct.c_int, [ct.POINTER(abi.MsMlpParams), P, i32, i64, i32, i32, u64, u64, P, P, P, P]),
         "ms_discounted_returns": (ct.c_int, [P, i32, i64, i64, ct.c_double, P, P]),
+        "ms_ppo_workspace_bytes": (ct.c_size_t, [ct.POINTER(abi.MsMlpParams), i64]),
+        "ms_ppo_grad": (ct.c_int, [ct.POINTER(abi.MsMlpParams), ct.POINTER(abi.MsMlpParams),
+                                   ct.POINTER(abi.MsPpoBatch), ct.c_float, P, ct.c_size_t,
+                                   ct.POINTER(abi.MsPpoGrads), P]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)
@@ -66,7 +70,7 @@ lib = _load()
 EXPORTED = (
     "ms_last_error", "ms_abi_version", "ms_config_shape", "ms_env_create", "ms_env_destroy", "ms_env_shape",
     "ms_env_reset", "ms_env_step", "ms_env_round", "ms_env_flags", "ms_env_randbelow", "ms_env_export",
-    "ms_env_import", "ms_policy_act", "ms_discounted_returns",
+    "ms_env_import", "ms_policy_act", "ms_discounted_returns", "ms_ppo_workspace_bytes", "ms_ppo_grad",
 )
 
 

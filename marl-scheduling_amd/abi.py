@@ -150,6 +150,25 @@ class MsMlpParams(ct.Structure):
     ]
 
 
+class MsPpoBatch(ct.Structure):
+    _fields_ = [
+        ("states", ct.c_void_p),
+        ("actions", ct.c_void_p),
+        ("old_logprobs", ct.c_void_p),
+        ("returns", ct.c_void_p),
+        ("unit_of_group", ct.c_void_p),
+        ("stride", ct.c_int32),
+        ("T", ct.c_int32),
+        ("U", ct.c_int32),
+        ("E", ct.c_int64),
+    ]
+
+
+class MsPpoGrads(ct.Structure):
+    _fields_ = [(name, ct.c_void_p) for name in (
+        "w1", "b1", "w2", "b2", "w3", "b3", "cw1", "cb1", "cw2", "cb2", "cw3", "cb3", "loss")]
+
+
 ACCEPT_REC_BYTES = ct.sizeof(MsAcceptRec)
 TERM_REC_BYTES = ct.sizeof(MsTermRec)
 assert ACCEPT_REC_BYTES == 16 and TERM_REC_BYTES == 8

@@ -10,9 +10,9 @@ FLAGS=(-O3 -std=c++17 -fPIC --offload-arch="${ARCH}" -ffp-contract=off -Wall -Wn
 OBJDIR="${HERE}/build"
 mkdir -p "${OBJDIR}"
 objs=()
-for src in env_kernels.hip policy_kernels.hip capi.cpp; do
+for src in env_kernels.hip policy_kernels.hip ppo_kernels.hip capi.cpp; do
   obj="${OBJDIR}/${src%.*}.o"
-  if [[ ! -f "${obj}" || "${HERE}/csrc/${src}" -nt "${obj}" || "${HERE}/csrc/ms_layout.h" -nt "${obj}" || "${HERE}/../include/marlsched.h" -nt "${obj}" ]]; then
+  if [[ ! -f "${obj}" || "${HERE}/csrc/${src}" -nt "${obj}" || "${HERE}/csrc/ms_layout.h" -nt "${obj}" || "${HERE}/csrc/ms_ppo.h" -nt "${obj}" || "${HERE}/../include/marlsched.h" -nt "${obj}" ]]; then
     if [[ "${src}" == *.cpp ]]; then
       "${HIPCC}" "${FLAGS[@]}" -x hip -c "${HERE}/csrc/${src}" -o "${obj}"
     else

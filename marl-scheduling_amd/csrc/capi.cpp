@@ -11,6 +11,7 @@
 #include <vector>
 
 #include "ms_layout.h"
+#include "ms_ppo.h"
 
 namespace ms {
 hipError_t launch_env_init(const Params&, int64_t, uint8_t*, uint32_t*, Liab*, uint64_t, hipStream_t);
@@ -20,7 +21,18 @@ hipError_t launch_env_randbelow(const Params&, uint8_t*, uint32_t*, int64_t, uin
 hipError_t launch_policy_act(const ms_mlp_params*, const int8_t*, int, int64_t, int, int, uint64_t, uint64_t,
                              const float*, int8_t*, float*, hipStream_t);
 hipError_t launch_returns(const float*, int, int64_t, int64_t, double, float*, hipStream_t);
+hipError_t launch_ppo_grad(const PpoArgs&, const GradOut&, hipStream_t);
+int ppo_param_count(int D, int A);
 }  // namespace ms
+
+// work split of k_ppo_grad: ~4096 one-wave blocks over all groups, >= 8 tiles of 16 rows each
+static void ppo_split(int64_t rows, int G, int* chunk_tiles, int* n_chunks) {
+    int64_t tiles = (rows + 15) / 16;
+    int64_t ct = (tiles * G + 4095) / 4096;
+    if (ct < 8) ct = 8;
+    *chunk_tiles = (int)ct;
+    *n_chunks = (int)((tiles + ct - 1) / ct);
+}
 
 struct ms_env {
     ms_config cfg;
@@ -378,6 +390,53 @@ int ms_policy_act(const ms_mlp_params* p, const int8_t* obs, int32_t obs_stride,
     if (n_envs < 1) return fail(MS_EINVAL, "n_envs must be >= 1");
     HIP_TRY(ms::launch_policy_act(p, obs, obs_stride, n_envs, n_units, units_per_group, seed, offset, uniforms, action,
                                   logprob, (hipStream_t)stream));
+    return MS_OK;
+}
+
+size_t ms_ppo_workspace_bytes(const ms_mlp_params* a, int64_t rows) {
+    if (!a || rows < 1 || a->n_groups < 1) return 0;
+    int ct, nc;
+    ppo_split(rows, a->n_groups, &ct, &nc);
+    return (size_t)a->n_groups * nc * ms::ppo_param_count(a->in_dim, a->n_actions) * sizeof(float);
+}
+
+int ms_ppo_grad(const ms_mlp_params* a, const ms_mlp_params* c, const ms_ppo_batch* b, float eps_clip, void* ws,
+                size_t ws_bytes, const ms_ppo_grads* g, void* stream) {
+    if (!a || !c || !b || !g || !ws) return fail(MS_EINVAL, "NULL argument");
+    if (a->hidden != 16 || c->hidden != 16) return fail(MS_EINVAL, "hidden width must be 16");
+    if (c->n_actions != 1 || c->in_dim != a->in_dim || c->n_groups != a->n_groups)
+        return fail(MS_EINVAL, "critic must be [D -> 16 -> 16 -> 1] with the actor's groups");
+    if (a->in_dim < 1 || a->in_dim > 256 || a->n_actions < 1 || a->n_actions > 128)
+        return fail(MS_EINVAL, "in_dim must be in [1, 256] and n_actions in [1, 128]");
+    if (b->stride < a->in_dim || (b->stride & 3) || b->T < 1 || b->E < 1 || b->U < 1)
+        return fail(MS_EINVAL, "bad batch shape");
+    if (!b->states || !b->actions || !b->old_logprobs || !b->returns || !b->unit_of_group)
+        return fail(MS_EINVAL, "NULL batch pointer");
+    const int64_t R = (int64_t)b->T * b->E;
+    if (ws_bytes < ms_ppo_workspace_bytes(a, R)) return fail(MS_EINVAL, "workspace too small");
+    ms::PpoArgs p{};
+    p.w1 = a->w1; p.b1 = a->b1; p.w2 = a->w2; p.b2 = a->b2; p.w3 = a->w3; p.b3 = a->b3;
+    p.cw1 = c->w1; p.cb1 = c->b1; p.cw2 = c->w2; p.cb2 = c->b2; p.cw3 = c->w3; p.cb3 = c->b3;
+    p.states = b->states;
+    p.actions = b->actions;
+    p.old_lp = b->old_logprobs;
+    p.ret = b->returns;
+    p.unit_of_group = b->unit_of_group;
+    p.partials = (float*)ws;
+    p.D = a->in_dim;
+    p.A = a->n_actions;
+    p.stride = b->stride;
+    p.T = b->T;
+    p.U = b->U;
+    p.G = a->n_groups;
+    p.E = b->E;
+    p.R = R;
+    ppo_split(R, p.G, &p.chunk_tiles, &p.n_chunks);
+    p.P = ms::ppo_param_count(p.D, p.A);
+    p.eps_clip = eps_clip;
+    p.inv_R = 1.0f / (float)R;
+    ms::GradOut go{g->w1, g->b1, g->w2, g->b2, g->w3, g->b3, g->cw1, g->cb1, g->cw2, g->cb2, g->cw3, g->cb3, g->loss};
+    HIP_TRY(ms::launch_ppo_grad(p, go, (hipStream_t)stream));
     return MS_OK;
 }
 

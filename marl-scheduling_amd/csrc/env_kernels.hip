@@ -318,8 +318,6 @@ __global__ void __launch_bounds__(64) k_env_step(Params P, uint8_t* recs, uint32
     __shared__ int32_t s_agent_r[64];   // agentReward
     __shared__ int32_t s_auct_r[64];    // auctioneerReward
     __shared__ int8_t s_term[64];       // core terminated this round
-    __shared__ int8_t s_term_owner[64];
-    __shared__ int32_t s_term_rew[64];
     __shared__ uint32_t s_flags;
     __shared__ int s_n_exec;
 

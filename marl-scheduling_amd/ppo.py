@@ -98,6 +98,10 @@ class GroupedActorCritic(nn.Module):
         return abi.MsMlpParams(ptr(self.w1), ptr(self.b1), ptr(self.w2), ptr(self.b2), ptr(self.w3), ptr(self.b3),
                                self.D, self.H, self.A, self.G)
 
+    def critic_mlp_params(self) -> abi.MsMlpParams:
+        return abi.MsMlpParams(ptr(self.cw1), ptr(self.cb1), ptr(self.cw2), ptr(self.cb2), ptr(self.cw3),
+                               ptr(self.cb3), self.D, self.H, 1, self.G)
+
     @torch.no_grad()
     def act(self, obs_i8, n_units: int, seed: int, offset: int, uniforms=None, action=None, logprob=None, stream=None):
         """ActorCritic.act (PPOmodules.py:53-63) for obs [E, n_units, stride] int8 on the HIP kernel.
@@ -171,5 +175,38 @@ class PPOGroup:
                 self.allreduce(self.policy.parameters())
             self.optimizer.step()
             losses.append(per_group.detach())
+        self.last_losses = losses
+        return losses
+
+    def update_fused(self, states_i8, actions_i8, old_logprobs, returns_egt, unit_of_group, T: int, E: int,
+                     stream=None):
+        """The same K epochs with the gradient from the fused HIP kernel (ms_ppo_grad).
+
+        states_i8 [R, U, stride] int8 rollout rows (R = T*E, row r = t*E + e), actions_i8 [R, U],
+        old_logprobs [R, U] f32, returns_egt [E, G, T] f32 normalised, unit_of_group [G] int32
+        (device). Adam (torch) applies the gradient; with several ranks the gradient is
+        all-reduced first."""
+        pol = self.policy
+        R, U, stride = states_i8.shape
+        assert R == T * E and states_i8.is_contiguous() and actions_i8.is_contiguous()
+        for prm in pol.parameters():
+            if prm.grad is None:
+                prm.grad = torch.zeros_like(prm)
+        loss_buf = torch.empty((pol.G, 3), dtype=torch.float32, device=states_i8.device)
+        a = pol.mlp_params()
+        c = pol.critic_mlp_params()
+        ws_bytes = lib.ms_ppo_workspace_bytes(ct.byref(a), R)
+        ws = torch.empty(((ws_bytes + 3) // 4,), dtype=torch.float32, device=states_i8.device)
+        batch = abi.MsPpoBatch(ptr(states_i8), ptr(actions_i8), ptr(old_logprobs), ptr(returns_egt),
+                               ptr(unit_of_group), stride, T, U, E)
+        grads = abi.MsPpoGrads(*[ptr(getattr(pol, k).grad) for k in ACTOR_KEYS + CRITIC_KEYS], ptr(loss_buf))
+        losses = []
+        for _ in range(self.K):
+            check(lib.ms_ppo_grad(ct.byref(a), ct.byref(c), ct.byref(batch), ct.c_float(self.eps_clip), ptr(ws),
+                                  ws_bytes, ct.byref(grads), stream_ptr(stream)))
+            if self.allreduce is not None:
+                self.allreduce(pol.parameters())
+            self.optimizer.step()
+            losses.append(loss_buf[:, 0] + 0.5 * loss_buf[:, 1] - 0.01 * loss_buf[:, 2])
         self.last_losses = losses
         return losses

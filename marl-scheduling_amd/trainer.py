@@ -75,8 +75,9 @@ class _Unit:
 
 class Trainer:
     def __init__(self, cfg: abi.MsConfig, n_envs: int, arch: str = "local", hyper: Hyper | None = None, seed: int = 0,
-                 device=None, rank: int = 0, world_size: int = 1, process_group=None):
+                 device=None, rank: int = 0, world_size: int = 1, process_group=None, fused: bool = True):
         assert arch in ("divided", "local", "global")
+        self.fused = fused  # fused HIP gradient (ms_ppo_grad) vs torch autograd
         self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
         torch.cuda.set_device(self.device)
         self.cfg, self.arch, self.E = cfg, arch, int(n_envs)
@@ -233,13 +234,21 @@ class Trainer:
         """env.updateAgents() (SchedulingEnvironment.py:208-210 / 314-329, Agent.py:524-529,708-728)."""
         sel = self._draws()
         losses = {}
+        T, E = self.T, self.E
         for u in self.units():
             states = self.acc_obs if u is self.acc else (self.off_obs if u is self.off else self.price_obs)
-            states = states[: self.T]
+            states = states[:T]
             ls = []
             for u_sel in sel[u.name]:
-                x, a, lp, ret = u.batch(states, u_sel)
-                ls += u.group.update(x, a, lp, ret)
+                if self.fused:
+                    G = u_sel.numel()
+                    r = u.rewards.index_select(2, u_sel).float().reshape(T, E * G)
+                    ret = discounted_returns(r, u.group.gamma)  # [E*G, T] = [E][G][T]
+                    ls += u.group.update_fused(states.reshape(T * E, u.U, u.stride), u.actions.view(T * E, u.U),
+                                               u.logprobs.view(T * E, u.U), ret, u_sel.to(torch.int32), T, E)
+                else:
+                    x, a, lp, ret = u.batch(states, u_sel)
+                    ls += u.group.update(x, a, lp, ret)
             u.group.sync_old()
             losses[u.name] = torch.stack(ls)
         # next iteration starts from the last observation
