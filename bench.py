@@ -140,6 +140,7 @@ def main():
     ap.add_argument("--envs", type=int, default=16384, help="env replicas per GPU")
     ap.add_argument("--update-step", type=int, default=200)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-graph", action="store_true", help="eager rollout instead of HIP-graph replay")
     args = ap.parse_args()
 
     import torch
@@ -160,32 +161,15 @@ def main():
                                         device=device, rank=rank, world_size=world)
     shape = tr.env.shape
 
-    # per-launch timing of the env-step kernel on its stream (HIP events) inside the timed region
+    tr.use_graph = not args.no_graph
     stream = torch.cuda.current_stream(device)
-    step_events = []
-    orig_step = tr.env.step
-
-    def timed_step(*a, **kw):
-        if timing[0]:
-            s_ev, e_ev = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            s_ev.record(stream)
-            out = orig_step(*a, **kw)
-            e_ev.record(stream)
-            step_events.append((s_ev, e_ev))
-            return out
-        return orig_step(*a, **kw)
-
-    timing = [False]
-    tr.env.step = timed_step
-
-    for _ in range(args.warmup):
-        tr.iteration()
+    for _ in range(max(args.warmup, 1 if tr.use_graph else 0)):
+        tr.iteration()  # the first rollout also captures the HIP graph
     torch.cuda.synchronize(device)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(device)
     tr.timings = dict(rollout=0.0, update=0.0)
-    timing[0] = True
     t0 = time.perf_counter()
     for _ in range(args.steps):
         tr.iteration()
@@ -194,7 +178,28 @@ def main():
         dist.barrier()
     torch.cuda.synchronize(device)
     elapsed = time.perf_counter() - t0
-    timing[0] = False
+    timings = dict(tr.timings)
+
+    # Per-launch duration of the env-step kernel with HIP events on its stream. Timing
+    # events cannot be captured into a HIP graph on ROCm 7.2 (hipErrorInvalidHandle,
+    # tools/graph_event_probe.py), so this is one eager rollout right after the timed
+    # region on the same buffers and evolving state; rocprofv3 cross-checks it (profiles/).
+    step_events = []
+    orig_step = tr.env.step
+
+    def timed_step(*a, **kw):
+        s_ev, e_ev = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s_ev.record(stream)
+        out = orig_step(*a, **kw)
+        e_ev.record(stream)
+        step_events.append((s_ev, e_ev))
+        return out
+
+    tr.env.step = timed_step
+    graph_mode, tr.use_graph = tr.use_graph, False
+    tr.iteration()
+    torch.cuda.synchronize(device)
+    tr.env.step, tr.use_graph = orig_step, graph_mode
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=device)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -243,9 +248,10 @@ def main():
             "avg_launch_us": avg_step_s * 1e6,
         },
         "breakdown_ms_per_step": {
-            "rollout": tr.timings["rollout"] / args.steps * 1e3,
-            "update": tr.timings["update"] / args.steps * 1e3,
-            "env_step_kernels": sum(step_ms) / args.steps,
+            "rollout": timings["rollout"] / args.steps * 1e3,
+            "update": timings["update"] / args.steps * 1e3,
+            "rollout_mode": "hip-graph replay" if not args.no_graph else "eager",
+            "env_step_kernels": sum(step_ms),
         },
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

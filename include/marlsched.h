@@ -224,10 +224,24 @@ typedef struct ms_mlp_params {
     int32_t n_groups;  /* G */
 } ms_mlp_params;
 
+/* The Philox counter offset is offset + *offset_dev (offset_dev may be NULL); a
+ * device-resident offset lets a captured HIP graph draw fresh numbers per replay. */
 int ms_policy_act(const ms_mlp_params* p, const int8_t* obs, int32_t obs_stride,
                   int64_t n_envs, int32_t n_units, int32_t units_per_group,
-                  uint64_t seed, uint64_t offset, const float* uniforms,
+                  uint64_t seed, uint64_t offset, const uint64_t* offset_dev, const float* uniforms,
                   int8_t* action, float* logprob, void* stream);
+
+/* FreePriceOfferPPO.selectAction (PPOmodules.py:312-332) in one launch: the core
+ * chooser acts on the offer observation (D_off = 2C+2); the price chooser acts on
+ * price_state = [obs[2a], obs[2a+1], obs[2C], obs[2C+1]] or [-5,-5,-5,-5] when a == 0
+ * (written to price_state [E][U][4]); env_price = -5 if a == 0 else the price action
+ * (the offer price world.py:452 sees). uniforms: [2][E*U] (core, price) or NULL. */
+int ms_offer_act_free(const ms_mlp_params* core_chooser, const ms_mlp_params* price_chooser,
+                      const int8_t* obs, int32_t obs_stride, int64_t n_envs, int32_t n_units,
+                      int32_t units_per_group, int32_t n_cores, uint64_t seed, uint64_t offset,
+                      const uint64_t* offset_dev, const float* uniforms, int8_t* core_action,
+                      float* core_logprob, int8_t* price_state, int8_t* price_action,
+                      float* price_logprob, int8_t* env_price, void* stream);
 
 /* Discounted Monte-Carlo returns + per-sequence normalisation (PPOmodules.py:128-137):
  * rewards [T][M] (f32, as stored per round), for each sequence m:

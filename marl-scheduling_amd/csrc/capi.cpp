@@ -19,7 +19,10 @@ hipError_t launch_env_reset(const Params&, int64_t, const uint8_t*, int8_t*, int
 hipError_t launch_env_step(const Params&, int64_t, uint8_t*, uint32_t*, Liab*, const StepIO&, hipStream_t);
 hipError_t launch_env_randbelow(const Params&, uint8_t*, uint32_t*, int64_t, uint32_t, uint32_t*, hipStream_t);
 hipError_t launch_policy_act(const ms_mlp_params*, const int8_t*, int, int64_t, int, int, uint64_t, uint64_t,
-                             const float*, int8_t*, float*, hipStream_t);
+                             const uint64_t*, const float*, int8_t*, float*, hipStream_t);
+hipError_t launch_offer_act_free(const ms_mlp_params*, const ms_mlp_params*, const int8_t*, int, int64_t, int, int, int,
+                                 uint64_t, uint64_t, const uint64_t*, const float*, int8_t*, float*, int8_t*, int8_t*,
+                                 float*, int8_t*, hipStream_t);
 hipError_t launch_returns(const float*, int, int64_t, int64_t, double, float*, hipStream_t);
 hipError_t launch_ppo_grad(const PpoArgs&, const GradOut&, hipStream_t);
 int ppo_param_count(int D, int A);
@@ -174,7 +177,15 @@ int ms_env_create(const ms_config* cfg, int64_t n_envs, uint64_t seed, ms_env** 
     return MS_OK;
 }
 
-int64_t ms_env_round(const ms_env* env) { return env ? env->round : -1; }
+// world.round of replica 0 as stored on the device (authoritative also when the
+// steps were replayed from a captured HIP graph); synchronises the device.
+int64_t ms_env_round(const ms_env* env) {
+    if (!env) return -1;
+    int32_t r = -1;
+    if (hipDeviceSynchronize() != hipSuccess || hipMemcpy(&r, env->recs, 4, hipMemcpyDeviceToHost) != hipSuccess)
+        return -1;
+    return r;
+}
 
 int ms_env_reset(ms_env* env, const ms_obs_out* obs, void* stream) {
     if (!env || !obs) return fail(MS_EINVAL, "env/obs is NULL");
@@ -377,19 +388,48 @@ int ms_env_import(ms_env* env, const ms_state_host* in, void* stream) {
     return MS_OK;
 }
 
-int ms_policy_act(const ms_mlp_params* p, const int8_t* obs, int32_t obs_stride, int64_t n_envs, int32_t n_units,
-                  int32_t units_per_group, uint64_t seed, uint64_t offset, const float* uniforms, int8_t* action,
-                  float* logprob, void* stream) {
-    if (!p || !obs || !action || !logprob) return fail(MS_EINVAL, "NULL argument");
+static int check_mlp(const ms_mlp_params* p, int32_t obs_stride, int32_t n_units, int32_t units_per_group) {
+    if (!p) return fail(MS_EINVAL, "NULL params");
     if (!p->w1 || !p->b1 || !p->w2 || !p->b2 || !p->w3 || !p->b3) return fail(MS_EINVAL, "NULL weight");
     if (p->hidden != 16) return fail(MS_EINVAL, "hidden width %d not built (16 only)", p->hidden);
     if (p->n_actions < 1 || p->n_actions > 127) return fail(MS_EINVAL, "n_actions must be in [1, 127]");
-    if (p->in_dim < 1 || obs_stride < p->in_dim || (obs_stride & 3)) return fail(MS_EINVAL, "bad obs stride");
+    if (p->in_dim < 1 || p->in_dim > 256 || obs_stride < p->in_dim || obs_stride > 256 || (obs_stride & 3))
+        return fail(MS_EINVAL, "bad in_dim / obs stride (<= 256, multiple of 4)");
     if (units_per_group < 1 || p->n_groups < 1 || units_per_group * p->n_groups != n_units)
         return fail(MS_EINVAL, "units_per_group * n_groups must equal n_units");
+    return MS_OK;
+}
+
+int ms_policy_act(const ms_mlp_params* p, const int8_t* obs, int32_t obs_stride, int64_t n_envs, int32_t n_units,
+                  int32_t units_per_group, uint64_t seed, uint64_t offset, const uint64_t* offset_dev,
+                  const float* uniforms, int8_t* action, float* logprob, void* stream) {
+    if (!obs || !action || !logprob) return fail(MS_EINVAL, "NULL argument");
+    int rc = check_mlp(p, obs_stride, n_units, units_per_group);
+    if (rc) return rc;
     if (n_envs < 1) return fail(MS_EINVAL, "n_envs must be >= 1");
-    HIP_TRY(ms::launch_policy_act(p, obs, obs_stride, n_envs, n_units, units_per_group, seed, offset, uniforms, action,
-                                  logprob, (hipStream_t)stream));
+    HIP_TRY(ms::launch_policy_act(p, obs, obs_stride, n_envs, n_units, units_per_group, seed, offset, offset_dev,
+                                  uniforms, action, logprob, (hipStream_t)stream));
+    return MS_OK;
+}
+
+int ms_offer_act_free(const ms_mlp_params* core, const ms_mlp_params* price, const int8_t* obs, int32_t obs_stride,
+                      int64_t n_envs, int32_t n_units, int32_t units_per_group, int32_t n_cores, uint64_t seed,
+                      uint64_t offset, const uint64_t* offset_dev, const float* uniforms, int8_t* core_action,
+                      float* core_logprob, int8_t* price_state, int8_t* price_action, float* price_logprob,
+                      int8_t* env_price, void* stream) {
+    if (!obs || !core_action || !core_logprob || !price_state || !price_action || !price_logprob || !env_price)
+        return fail(MS_EINVAL, "NULL argument");
+    int rc = check_mlp(core, obs_stride, n_units, units_per_group);
+    if (rc) return rc;
+    rc = check_mlp(price, 4, n_units, units_per_group);
+    if (rc) return rc;
+    if (price->in_dim != 4 || price->n_groups != core->n_groups) return fail(MS_EINVAL, "price chooser must be 4 -> A");
+    if (core->in_dim != 2 * n_cores + 2 || core->n_actions != n_cores + 1)
+        return fail(MS_EINVAL, "core chooser must be (2C+2) -> (C+1)");
+    if (n_envs < 1) return fail(MS_EINVAL, "n_envs must be >= 1");
+    HIP_TRY(ms::launch_offer_act_free(core, price, obs, obs_stride, n_envs, n_units, units_per_group, n_cores, seed,
+                                      offset, offset_dev, uniforms, core_action, core_logprob, price_state,
+                                      price_action, price_logprob, env_price, (hipStream_t)stream));
     return MS_OK;
 }
 

@@ -120,28 +120,42 @@ __global__ void __launch_bounds__(64) k_ppo_grad(PpoArgs p) {
     const float eps = 1.1920928955078125e-07f;
 
     const int stride4 = p.stride >> 2;
-    const long long tile0 = (long long)chunk * p.chunk_tiles;
-    for (int it = 0; it < p.chunk_tiles; it++) {
-        const long long r0 = (tile0 + it) * 16;
-        if (r0 >= p.R) break;
-        // ---- stage the tile's 16 observation rows (int8) in LDS
-        for (int i = lane; i < 16 * stride4; i += 64) {
-            int rr = i / stride4, cc = i % stride4;
-            long long r = r0 + rr;
-            uint32_t w = 0;
-            if (r < p.R) w = reinterpret_cast<const uint32_t*>(p.states + ((size_t)r * p.U + u) * p.stride)[cc];
-            reinterpret_cast<uint32_t*>(sX)[rr * stride4 + cc] = w;
+    const int R = (int)p.R, E = (int)p.E;
+    const int tile0 = chunk * p.chunk_tiles;
+    const int tile_end = min(tile0 + p.chunk_tiles, (R + 15) >> 4);
+    // lane (j, g4) copies dwords g4 + 4m of tile row j and owns row j's scalars; the next
+    // tile's loads are issued before the current tile is processed (register prefetch)
+    constexpr int kPreW = 16;  // 16 rows x 256 B / 64 lanes
+    uint32_t pre[kPreW];
+    int pre_act = 0;
+    float pre_olp = 0.f, pre_G = 0.f;
+    auto prefetch = [&](int tile) {
+        const int r = tile * 16 + j;
+        const bool ok = r < R;
+        const size_t ru = (size_t)(ok ? r : 0) * p.U + u;
+        const uint32_t* src = reinterpret_cast<const uint32_t*>(p.states + ru * p.stride);
+#pragma unroll
+        for (int m = 0; m < kPreW; m++) {
+            const int cc = g4 + 4 * m;
+            pre[m] = (ok && cc < stride4) ? src[cc] : 0u;
         }
-        const long long r = r0 + j;
-        const bool valid = r < p.R;
-        int act = 0;
-        float olp = 0.f, G = 0.f;
-        if (valid) {
-            act = p.actions[(size_t)r * p.U + u];
-            olp = p.old_lp[(size_t)r * p.U + u];
-            long long t = r / p.E, e = r % p.E;
-            G = p.ret[((size_t)e * p.G + grp) * p.T + t];
+        pre_act = ok ? p.actions[ru] : 0;
+        pre_olp = ok ? p.old_lp[ru] : 0.f;
+        const int t = ok ? r / E : 0;
+        pre_G = ok ? p.ret[((size_t)(r - t * E) * p.G + grp) * p.T + t] : 0.f;
+    };
+    if (tile0 < tile_end) prefetch(tile0);
+    for (int tile = tile0; tile < tile_end; tile++) {
+        // ---- stage the tile's 16 observation rows (int8) in LDS, then start the next tile's loads
+#pragma unroll
+        for (int m = 0; m < kPreW; m++) {
+            const int cc = g4 + 4 * m;
+            if (cc < stride4) reinterpret_cast<uint32_t*>(sX)[j * stride4 + cc] = pre[m];
         }
+        const bool valid = tile * 16 + j < R;
+        const int act = pre_act;
+        const float olp = pre_olp, G = pre_G;
+        if (tile + 1 < tile_end) prefetch(tile + 1);
         __syncthreads();
 
         // ---- forward, layer 1 (actor + critic share the X operand)
@@ -202,23 +216,23 @@ __global__ void __launch_bounds__(64) k_ppo_grad(PpoArgs p) {
                 pe[t][q] = (16 * t + 4 * g4 + q < A) ? expf(z[t][q] - m) : 0.f;
                 s0 += pe[t][q];
             }
-        s0 = xsum4g(s0);
+        const float inv0 = 1.f / xsum4g(s0);
         float s1 = 0.f;
 #pragma unroll
         for (int t = 0; t < NT; t++)
 #pragma unroll
             for (int q = 0; q < 4; q++) {
-                pe[t][q] = pe[t][q] / s0;  // softmax output
+                pe[t][q] *= inv0;  // softmax output (same arithmetic as k_act)
                 s1 += pe[t][q];
             }
-        s1 = xsum4g(s1);
+        const float inv1 = 1.f / xsum4g(s1);
         float pn[NT][4], cl[NT][4], lp = 0.f, ent = 0.f;
 #pragma unroll
         for (int t = 0; t < NT; t++)
 #pragma unroll
             for (int q = 0; q < 4; q++) {
                 int a = 16 * t + 4 * g4 + q;
-                pn[t][q] = pe[t][q] / s1;
+                pn[t][q] = pe[t][q] * inv1;
                 float pc = fminf(fmaxf(pn[t][q], eps), 1.f - eps);
                 cl[t][q] = logf(pc);
                 if (a < A) {
@@ -263,7 +277,7 @@ __global__ void __launch_bounds__(64) k_ppo_grad(PpoArgs p) {
                 if (a < A) {
                     float dc = (a == act ? g_lp : 0.f) - g_h * pn[t][q];
                     float in = (pn[t][q] >= eps && pn[t][q] <= 1.f - eps) ? 1.f : 0.f;
-                    v = dc * in / fminf(fmaxf(pn[t][q], eps), 1.f - eps) - g_h * cl[t][q];
+                    v = dc * in * __builtin_amdgcn_rcpf(fminf(fmaxf(pn[t][q], eps), 1.f - eps)) - g_h * cl[t][q];
                 }
                 dpn[t][q] = v;
                 x1 += v * pe[t][q];
@@ -274,7 +288,7 @@ __global__ void __launch_bounds__(64) k_ppo_grad(PpoArgs p) {
         for (int t = 0; t < NT; t++)
 #pragma unroll
             for (int q = 0; q < 4; q++) {
-                float dp = dpn[t][q] / s1 - x1 / (s1 * s1);
+                float dp = (dpn[t][q] - x1 * inv1) * inv1;
                 gz[t][q] = dp;
                 x2 += dp * pe[t][q];
             }

@@ -103,7 +103,8 @@ class GroupedActorCritic(nn.Module):
                                ptr(self.cb3), self.D, self.H, 1, self.G)
 
     @torch.no_grad()
-    def act(self, obs_i8, n_units: int, seed: int, offset: int, uniforms=None, action=None, logprob=None, stream=None):
+    def act(self, obs_i8, n_units: int, seed: int, offset: int, uniforms=None, action=None, logprob=None, stream=None,
+            offset_dev=None):
         """ActorCritic.act (PPOmodules.py:53-63) for obs [E, n_units, stride] int8 on the HIP kernel.
         Unit u uses group u // (n_units // G). Returns (action int8 [E, U], logprob f32 [E, U])."""
         E, U, stride = obs_i8.shape
@@ -115,8 +116,26 @@ class GroupedActorCritic(nn.Module):
             logprob = torch.empty((E, U), dtype=torch.float32, device=dev)
         p = self.mlp_params()
         check(lib.ms_policy_act(ct.byref(p), ptr(obs_i8), stride, E, U, U // self.G, ct.c_uint64(seed),
-                                ct.c_uint64(offset), ptr(uniforms), ptr(action), ptr(logprob), stream_ptr(stream)))
+                                ct.c_uint64(offset), ptr(offset_dev), ptr(uniforms), ptr(action), ptr(logprob),
+                                stream_ptr(stream)))
         return action, logprob
+
+
+@torch.no_grad()
+def offer_act_free(core: GroupedActorCritic, price: GroupedActorCritic, obs_i8, n_cores: int, seed: int, offset: int,
+                   out: dict, uniforms=None, offset_dev=None, stream=None):
+    """FreePriceOfferPPO.selectAction (PPOmodules.py:312-332) for obs [E, U, stride] int8 in one launch.
+    out: core_action/price_action/env_price int8 [E, U], core_logprob/price_logprob f32 [E, U],
+    price_state int8 [E, U, 4]."""
+    E, U, stride = obs_i8.shape
+    assert obs_i8.dtype == torch.int8 and obs_i8.is_contiguous() and U % core.G == 0
+    pc, pp = core.mlp_params(), price.mlp_params()
+    check(lib.ms_offer_act_free(ct.byref(pc), ct.byref(pp), ptr(obs_i8), stride, E, U, U // core.G, n_cores,
+                                ct.c_uint64(seed), ct.c_uint64(offset), ptr(offset_dev), ptr(uniforms),
+                                ptr(out["core_action"]), ptr(out["core_logprob"]), ptr(out["price_state"]),
+                                ptr(out["price_action"]), ptr(out["price_logprob"]), ptr(out["env_price"]),
+                                stream_ptr(stream)))
+    return out
 
 
 def discounted_returns(rewards_tm: torch.Tensor, gamma: float, stream=None) -> torch.Tensor:

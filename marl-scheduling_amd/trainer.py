@@ -27,7 +27,7 @@ import torch
 
 from . import abi
 from .env import BatchedEnv
-from .ppo import PPOGroup, discounted_returns
+from .ppo import PPOGroup, discounted_returns, offer_act_free
 
 
 @dataclass
@@ -75,7 +75,8 @@ class _Unit:
 
 class Trainer:
     def __init__(self, cfg: abi.MsConfig, n_envs: int, arch: str = "local", hyper: Hyper | None = None, seed: int = 0,
-                 device=None, rank: int = 0, world_size: int = 1, process_group=None, fused: bool = True):
+                 device=None, rank: int = 0, world_size: int = 1, process_group=None, fused: bool = True,
+                 use_graph: bool = True):
         assert arch in ("divided", "local", "global")
         self.fused = fused  # fused HIP gradient (ms_ppo_grad) vs torch autograd
         self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
@@ -126,7 +127,10 @@ class Trainer:
         self.agent_reward = torch.zeros((self.E, N), dtype=torch.int32, device=dev)
         self.auct_reward = torch.zeros((self.E, C), dtype=torch.int32, device=dev)
         self.rng = random.Random(seed)  # sub-unit draws (random.randint), identical on every rank
-        self.act_offset = 0
+        self.rng_ctr = torch.zeros(1, dtype=torch.int64, device=dev)  # device Philox offset base
+        self.use_graph = use_graph
+        self.graph = None
+        self.rounds_done = 0
         self.iterations = 0
         self.env.reset(dict(acceptor=self.acc_obs[0], offer=self.off_obs[0]))
         self.timings = dict(rollout=0.0, update=0.0)
@@ -168,26 +172,21 @@ class Trainer:
         (trainPPO.py:160-167)."""
         E, N, C, L = self.E, self.N, self.C, self.L
         seed = self.seed * 7919 + self.rank
+        base = 8 * t  # Philox offsets: static per round + the device counter (advanced per rollout)
         # per agent: offer units then acceptors (Agent.py:504-515); separate streams per unit type
-        self.off.group.policy_old.act(self.off_obs[t], N * L, seed, self.act_offset + 1,
-                                      action=self.off.actions[t], logprob=self.off.logprobs[t])
         if self.free:
-            # FreePriceOfferPPO.selectAction (PPOmodules.py:312-332): price chooser input
-            # [obs[2a:2a+2], obs[-2:]] or the dummy [-5,-5,-5,-5] when the core chooser picked 0
-            a = self.off.actions[t].long()                                   # [E, NL]
-            obs = self.off_obs[t]
-            idx = (2 * a).unsqueeze(-1) + torch.arange(2, device=obs.device)
-            core_part = torch.gather(obs, 2, idx)
-            slot_part = obs[..., 2 * C: 2 * C + 2]
-            pin = torch.cat((core_part, slot_part), dim=-1)
-            pin = torch.where((a == 0).unsqueeze(-1), torch.full_like(pin, -5), pin)
-            self.price_obs[t].copy_(pin)
-            self.price.group.policy_old.act(self.price_obs[t], N * L, seed, self.act_offset + 2,
-                                            action=self.price.actions[t], logprob=self.price.logprobs[t])
-            torch.where(a == 0, torch.full_like(self.price.actions[t], -5), self.price.actions[t], out=self.env_price)
-        self.acc.group.policy_old.act(self.acc_obs[t], N * C, seed, self.act_offset + 3,
-                                      action=self.acc.actions[t], logprob=self.acc.logprobs[t])
-        self.act_offset += 4
+            # FreePriceOfferPPO.selectAction (PPOmodules.py:312-332): core chooser, then the price
+            # chooser on [obs[2a:2a+2], obs[-2:]] or the dummy [-5,-5,-5,-5] when a == 0, one launch
+            out = dict(core_action=self.off.actions[t], core_logprob=self.off.logprobs[t],
+                       price_state=self.price_obs[t], price_action=self.price.actions[t],
+                       price_logprob=self.price.logprobs[t], env_price=self.env_price)
+            offer_act_free(self.off.group.policy_old, self.price.group.policy_old, self.off_obs[t], C, seed, base + 1,
+                           out, offset_dev=self.rng_ctr)
+        else:
+            self.off.group.policy_old.act(self.off_obs[t], N * L, seed, base + 1, action=self.off.actions[t],
+                                          logprob=self.off.logprobs[t], offset_dev=self.rng_ctr)
+        self.acc.group.policy_old.act(self.acc_obs[t], N * C, seed, base + 3, action=self.acc.actions[t],
+                                      logprob=self.acc.logprobs[t], offset_dev=self.rng_ctr)
         obs = dict(acceptor=self.acc_obs[t + 1], offer=self.off_obs[t + 1])
         rew = dict(offer=self.off.rewards[t].view(E, N, L), acceptor=self.acc.rewards[t].view(E, N, C),
                    agent=self.agent_reward, auctioneer=self.auct_reward,
@@ -195,9 +194,26 @@ class Trainer:
         self.env.step(self.acc.actions[t].view(E, N, C), self.off.actions[t].view(E, N, L),
                       self.env_price.view(E, N, L) if self.free else None, obs=obs, rewards=rew)
 
-    def rollout(self):
+    def _rollout_body(self):
         for t in range(self.T):
             self.round(t)
+        self.rng_ctr.add_(8 * self.T)
+
+    def rollout(self):
+        """UPDATE_STEP rounds. With use_graph the first rollout runs eagerly and is then
+        captured once into a HIP graph (every pointer is static); later rollouts replay it."""
+        if not self.use_graph:
+            self._rollout_body()
+        elif self.graph is None:
+            self._rollout_body()
+            torch.cuda.synchronize(self.device)
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                self._rollout_body()
+            self.graph = g
+        else:
+            self.graph.replay()
+        self.rounds_done += self.T
 
     # ---- update
     def _draws(self):
@@ -257,15 +273,30 @@ class Trainer:
         return losses
 
     def iteration(self):
-        t0 = time.perf_counter()
+        """One PPO iteration; device time of rollout / update accumulates in self.timings (s)."""
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+        ev[0].record()
         self.rollout()
-        t1 = time.perf_counter()
+        ev[1].record()
         losses = self.update()
-        t2 = time.perf_counter()
-        self.timings["rollout"] += t1 - t0
-        self.timings["update"] += t2 - t1
+        ev[2].record()
+        self._pending_events.append(ev)
         self.iterations += 1
         return losses
+
+    @property
+    def timings(self):
+        for ev in self._pending_events:
+            ev[2].synchronize()
+            self._timings["rollout"] += ev[0].elapsed_time(ev[1]) / 1e3
+            self._timings["update"] += ev[1].elapsed_time(ev[2]) / 1e3
+        self._pending_events = []
+        return self._timings
+
+    @timings.setter
+    def timings(self, value):
+        self._pending_events = []
+        self._timings = dict(value)
 
     def flags(self):
         return self.env.flags()
