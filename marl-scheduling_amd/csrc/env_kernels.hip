@@ -1,12 +1,19 @@
 // env_kernels.hip — the batched marl-scheduling round as one HIP kernel for gfx950.
 //
-// One 64-lane wave steps one env replica per round: the env's packed state
-// record (ms_layout.h) is staged in LDS, the round runs as wave-parallel
-// phases (per core / per slot / per agent lanes, ballots for the ordered
-// selections), and observations are assembled in LDS and streamed out with
-// coalesced dword stores. Reference semantics (paths relative to
-// /root/reference/src) are cited per phase; the CPU restatement that checks
-// this kernel bit-for-bit is oracle/ms_oracle.c.
+// One 64-lane wave steps one env replica per round. The env's packed state
+// record (ms_layout.h) is staged in LDS and the round runs as wave-parallel
+// phases. The offer set of a round (at most N*L <= 126 offers, one per slot,
+// offer-ID order = slot order) is indexed by 128-bit masks, one per core and
+// one per recipient, built with LDS atomic ORs: every ordered selection of the
+// reference — the idx-th offer of (recipient, core) behind an acceptor action,
+// the auctioneer's tied maxima, the offers listed in an acceptor observation —
+// is a walk over the set bits of mask(core) & mask(recipient). The loads the
+// round depends on (MT19937 window, liability chains of cores that may
+// terminate) are issued right after staging so their latency overlaps the
+// selection phases. Observations are assembled in LDS (prefilled with the -2
+// pad by dword stores) and streamed out with dword stores. Reference semantics
+// (paths relative to /root/reference/src) are cited per phase; the CPU
+// restatement that checks this kernel bit-for-bit is oracle/ms_oracle.c.
 #include <hip/hip_runtime.h>
 
 #include "ms_layout.h"
@@ -63,9 +70,11 @@ struct MtStream {
     bool twisted;
     uint32_t v;       // this lane's tempered word (position wb + lane)
 
+    // Window at stream position pos. need = words the caller is about to
+    // consume; need == 0 only peeks (never twists; the window may be empty).
     __device__ void load(int pos, int need, int lane) {
         int limit = twisted ? 0x3fffffff : (kMtN - mti0);  // old words end here
-        if (!twisted && pos + need > limit) {
+        if (!twisted && need > 0 && pos + need > limit) {
             // read the old words of this window before the state is replaced
             int g = mti0 + pos + lane;
             uint32_t old = (g < kMtN) ? gmt[g] : 0u;
@@ -154,77 +163,168 @@ __device__ __forceinline__ void ratio_of(int p, int n, int& num, int& den) {
 }
 
 // ---------------------------------------------------------------------------
+// offer-set masks (bit i = the offer of slot i; slot order is offer-ID order)
+
+struct M128 {
+    uint64_t lo, hi;
+};
+
+__device__ __forceinline__ M128 mand(const M128& a, const M128& b) { return M128{a.lo & b.lo, a.hi & b.hi}; }
+
+// index of the k-th (k >= 0) set bit of m, -1 if m has fewer bits
+__device__ __forceinline__ int kth_bit(const M128& m, int k) {
+    uint64_t w = m.lo;
+    int base = 0;
+    const int c = __popcll(m.lo);
+    if (k >= c) {
+        k -= c;
+        w = m.hi;
+        base = 64;
+        if (k >= __popcll(w)) return -1;
+    }
+    for (; k > 0; k--) w &= w - 1;
+    return base + __ffsll((unsigned long long)w) - 1;
+}
+
+// Iterate the set bits of m in increasing order: for (MaskIter it(m); it.more(); ) { int i = it.next(); ... }
+struct MaskIter {
+    uint64_t lo, hi;
+    __device__ __forceinline__ explicit MaskIter(const M128& m) : lo(m.lo), hi(m.hi) {}
+    __device__ __forceinline__ bool more() const { return (lo | hi) != 0; }
+    __device__ __forceinline__ int next() {
+        if (lo) {
+            const int i = __ffsll((unsigned long long)lo) - 1;
+            lo &= lo - 1;
+            return i;
+        }
+        const int i = __ffsll((unsigned long long)hi) - 1;
+        hi &= hi - 1;
+        return 64 + i;
+    }
+};
+
+__device__ __forceinline__ void mask_set(M128* m, int i) {
+    unsigned long long* w = reinterpret_cast<unsigned long long*>(m) + (i >> 6);
+    atomicOr(w, 1ull << (i & 63));
+}
+
+// Masks of the current offers: mc[c] = offers to core c, mr[r] = offers to
+// recipient r (0 = auctioneer). Ends with a barrier.
+__device__ void build_masks(Rec& R, const Params& P, M128* mc, M128* mr, int lane) {
+    for (int i = lane; i < P.C; i += kWave) mc[i] = M128{0, 0};
+    for (int i = lane; i <= P.N; i += kWave) mr[i] = M128{0, 0};
+    __syncthreads();
+    const int8_t* oc = R.offer_core();
+    const int8_t* orc = R.offer_recip();
+    for (int i = lane; i < P.NL; i += kWave) {
+        const int c = oc[i];
+        if (c >= 0) {
+            mask_set(&mc[c], i);
+            mask_set(&mr[orc[i]], i);
+        }
+    }
+    __syncthreads();
+}
+
+// ---------------------------------------------------------------------------
 // observations of the current (LDS) state: Agent.py:167-212 (acceptor),
 // Agent.py:271-300 (offer), Auctioneer.py:34-77 (auctioneer)
 
-__device__ void write_acceptor_row(Rec& R, const Params& P, int recipient, int c, int8_t* row) {
-    int8_t* own_core = R.core_owner();
-    bool own = own_core[c] == recipient;
-    int kind = R.core_kind()[c];
+// One acceptor/auctioneer row over a scratch row prefilled with -2 bytes.
+__device__ __forceinline__ void acceptor_row(Rec& R, const Params& P, const M128* mc, const M128* mr, int recipient,
+                                             int c, int8_t* row) {
+    const bool own = R.core_owner()[c] == recipient;
+    const int kind = R.core_kind()[c];
     row[0] = own ? 1 : 0;
     row[1] = (int8_t)(own ? (kind >= 0 ? P.prio[kind] : -1) : -1);
     row[2] = (int8_t)(own ? R.core_rem()[c] : -1);
-    int w = 3;
-    const int8_t* oc = R.offer_core();
-    const int8_t* orc = R.offer_recip();
     const int8_t* op = R.offer_price();
     const int8_t* sr = R.slot_rem();
-    for (int i = 0; i < P.NL; i++) {
-        if (oc[i] == c && orc[i] == recipient) {
-            row[w] = op[i];
-            row[w + 1] = sr[i];
-            w += 2;
-        }
+    int w = 3;
+    for (MaskIter it(mand(mc[c], mr[recipient])); it.more();) {  // (price, necT) in offer-ID order
+        const int i = it.next();
+        row[w] = op[i];
+        row[w + 1] = sr[i];
+        w += 2;
     }
-    for (; w < P.d_acc; w++) row[w] = -2;
-    for (; w < P.acc_stride; w++) row[w] = 0;
+    for (int z = P.d_acc; z < P.acc_stride; z++) row[z] = 0;
 }
 
-__device__ void write_offer_row(Rec& R, const Params& P, int slot, int8_t* row) {
+// Acceptor rows (KIND 0, row g = agent g / C, core g % C) or auctioneer rows
+// (KIND 2, row g = core g), staged in LDS chunks and streamed to dst.
+template <int KIND>
+__device__ void emit_acc_rows(Rec& R, const Params& P, const M128* mc, const M128* mr, uint8_t* scratch, int8_t* dst,
+                              int n_rows, int lane) {
+    if (!dst) return;
+    const int stride = P.acc_stride;
+    const int per_chunk = kObsChunk / stride;
+    uint32_t* sw = reinterpret_cast<uint32_t*>(scratch);
+    for (int r0 = 0; r0 < n_rows; r0 += per_chunk) {
+        const int nr = min(per_chunk, n_rows - r0);
+        const int nd = nr * stride / 4;
+        for (int i = lane; i < nd; i += kWave) sw[i] = 0xFEFEFEFEu;  // -2 pads
+        __syncthreads();
+        for (int r = lane; r < nr; r += kWave) {
+            const int g = r0 + r;
+            int8_t* row = reinterpret_cast<int8_t*>(scratch) + r * stride;
+            if (KIND == 0)
+                acceptor_row(R, P, mc, mr, g / P.C + 1, g - (g / P.C) * P.C, row);
+            else
+                acceptor_row(R, P, mc, mr, 0, g, row);
+        }
+        __syncthreads();
+        copy_dwords(reinterpret_cast<uint32_t*>(dst + (size_t)r0 * stride), sw, nd, lane);
+        __syncthreads();
+    }
+}
+
+// Offer rows: the (prio, rem) pairs of all cores — the same for every row of
+// the env — then the slot's own pair, zero padded to the stride. Built one
+// dword per lane (strides are multiples of 4, so a dword never spans rows).
+__device__ void emit_off_rows(Rec& R, const Params& P, uint8_t* scratch, int8_t* dst, int lane) {
+    if (!dst) return;
+    const int stride = P.off_stride;
+    const int per_chunk = kObsChunk / stride;
     const int8_t* ck = R.core_kind();
     const int8_t* cr = R.core_rem();
-    for (int c = 0; c < P.C; c++) {
-        int k = ck[c];
-        row[2 * c] = (int8_t)(k >= 0 ? P.prio[k] : -1);
-        row[2 * c + 1] = (int8_t)(k >= 0 ? cr[c] : -1);
-    }
-    int k = R.slot_kind()[slot];
-    row[2 * P.C] = (int8_t)(k >= 0 ? P.prio[k] : -1);
-    row[2 * P.C + 1] = (int8_t)(k >= 0 ? R.slot_rem()[slot] : -1);
-    for (int w = P.d_off; w < P.off_stride; w++) row[w] = 0;
-}
-
-// Build rows [0, n_rows) of one kind in LDS chunks and stream them to dst.
-template <int KIND>  // 0 acceptor, 1 offer, 2 auctioneer
-__device__ void emit_rows(Rec& R, const Params& P, uint8_t* scratch, int8_t* dst, int n_rows, int stride,
-                          int lane) {
-    if (!dst) return;
-    int per_chunk = kObsChunk / stride;
-    for (int r0 = 0; r0 < n_rows; r0 += per_chunk) {
-        int nr = min(per_chunk, n_rows - r0);
-        for (int r = lane; r < nr; r += kWave) {
-            int8_t* row = reinterpret_cast<int8_t*>(scratch) + r * stride;
-            int g = r0 + r;
-            if (KIND == 0)
-                write_acceptor_row(R, P, g / P.C + 1, g % P.C, row);
-            else if (KIND == 1)
-                write_offer_row(R, P, g, row);
-            else
-                write_acceptor_row(R, P, 0, g, row);
+    const int8_t* sk = R.slot_kind();
+    const int8_t* srem = R.slot_rem();
+    uint32_t* sw = reinterpret_cast<uint32_t*>(scratch);
+    for (int r0 = 0; r0 < P.NL; r0 += per_chunk) {
+        const int nr = min(per_chunk, P.NL - r0);
+        const int nd = nr * stride / 4;
+        for (int d = lane; d < nd; d += kWave) {
+            const int r = (4 * d) / stride;
+            const int col0 = 4 * d - r * stride;
+            const int s = r0 + r;
+            uint32_t word = 0;
+#pragma unroll
+            for (int b = 0; b < 4; b++) {
+                const int col = col0 + b;
+                int v = 0;
+                if (col < 2 * P.C) {
+                    const int c = col >> 1, k = ck[c];
+                    v = k < 0 ? -1 : ((col & 1) ? cr[c] : P.prio[k]);
+                } else if (col < P.d_off) {
+                    const int k = sk[s];
+                    v = k < 0 ? -1 : ((col & 1) ? srem[s] : P.prio[k]);
+                }
+                word |= (uint32_t)(uint8_t)v << (8 * b);
+            }
+            sw[d] = word;
         }
         __syncthreads();
-        copy_dwords(reinterpret_cast<uint32_t*>(dst + (size_t)r0 * stride), reinterpret_cast<const uint32_t*>(scratch),
-                    nr * stride / 4, lane);
+        copy_dwords(reinterpret_cast<uint32_t*>(dst + (size_t)r0 * stride), sw, nd, lane);
         __syncthreads();
     }
 }
 
-__device__ void emit_obs(Rec& R, const Params& P, uint8_t* scratch, int8_t* acc, int8_t* off, int8_t* auct,
-                         int64_t e, int lane) {
-    emit_rows<0>(R, P, scratch, acc ? acc + e * (int64_t)P.N * P.C * P.acc_stride : nullptr, P.N * P.C,
-                 P.acc_stride, lane);
-    emit_rows<1>(R, P, scratch, off ? off + e * (int64_t)P.NL * P.off_stride : nullptr, P.NL, P.off_stride, lane);
-    emit_rows<2>(R, P, scratch, auct ? auct + e * (int64_t)P.C * P.acc_stride : nullptr, P.C, P.acc_stride, lane);
+__device__ void emit_obs(Rec& R, const Params& P, const M128* mc, const M128* mr, uint8_t* scratch, int8_t* acc,
+                         int8_t* off, int8_t* auct, int64_t e, int lane) {
+    emit_acc_rows<0>(R, P, mc, mr, scratch, acc ? acc + e * (int64_t)P.N * P.C * P.acc_stride : nullptr, P.N * P.C,
+                     lane);
+    emit_off_rows(R, P, scratch, off ? off + e * (int64_t)P.NL * P.off_stride : nullptr, lane);
+    emit_acc_rows<2>(R, P, mc, mr, scratch, auct ? auct + e * (int64_t)P.C * P.acc_stride : nullptr, P.C, lane);
 }
 
 // ---------------------------------------------------------------------------
@@ -297,6 +397,8 @@ __global__ void __launch_bounds__(64) k_env_init(Params P, uint8_t* recs, uint32
 __global__ void __launch_bounds__(64) k_env_reset(Params P, const uint8_t* recs, int8_t* obs_acc, int8_t* obs_off,
                                                   int8_t* obs_auct) {
     extern __shared__ __align__(16) uint8_t smem[];
+    __shared__ M128 s_mc[MS_MAX_CORES];
+    __shared__ M128 s_mr[MS_MAX_AGENTS + 1];
     const int lane = threadIdx.x;
     const int64_t e = blockIdx.x;
     uint8_t* rec = smem + P.s_rec;
@@ -304,20 +406,27 @@ __global__ void __launch_bounds__(64) k_env_reset(Params P, const uint8_t* recs,
                 P.rec_bytes / 4, lane);
     __syncthreads();
     Rec R{rec, &P};
-    emit_obs(R, P, smem + P.s_scratch, obs_acc, obs_off, obs_auct, e, lane);
+    build_masks(R, P, s_mc, s_mr, lane);
+    emit_obs(R, P, s_mc, s_mr, smem + P.s_scratch, obs_acc, obs_off, obs_auct, e, lane);
 }
+
+constexpr int kLiabPrefetch = 4;  // newest chain entries loaded ahead per core that may terminate
 
 // One round of SchedulingEnv.step (SchedulingEnvironment.py:32-83) for env blockIdx.x.
 __global__ void __launch_bounds__(64) k_env_step(Params P, uint8_t* recs, uint32_t* mt, Liab* liab, StepIO io) {
     extern __shared__ __align__(16) uint8_t smem[];
-    __shared__ int16_t s_exec[64];      // per core: executed offer's slot index, -1 none
-    __shared__ int16_t s_key[64];       // execution order key
-    __shared__ int8_t s_by_rank[64];    // cores in execution order
-    __shared__ int16_t s_auct[64];      // auctioneer action per core
-    __shared__ int16_t s_tie_n[64];     // tied maxima count (auctioneer)
-    __shared__ int32_t s_agent_r[64];   // agentReward
-    __shared__ int32_t s_auct_r[64];    // auctioneerReward
-    __shared__ int8_t s_term[64];       // core terminated this round
+    __shared__ M128 s_mc[MS_MAX_CORES];             // offers per core
+    __shared__ M128 s_mr[MS_MAX_AGENTS + 1];        // offers per recipient (0 = auctioneer)
+    __shared__ Liab s_newle[MS_MAX_CORES];          // liability entry appended this round per core
+    __shared__ int16_t s_exec[MS_MAX_CORES];        // per core: executed offer's slot index, -1 none
+    __shared__ int16_t s_key[MS_MAX_CORES];         // execution order key
+    __shared__ int8_t s_by_rank[MS_MAX_CORES];      // cores in execution order
+    __shared__ int8_t s_fresh[MS_MAX_CORES];        // s_newle[c] is the chain's newest entry
+    __shared__ int16_t s_auct[MS_MAX_CORES];        // auctioneer action per core
+    __shared__ int16_t s_tie_n[MS_MAX_CORES];       // tied maxima count (auctioneer)
+    __shared__ int16_t s_pick[MS_MAX_CORES];        // tie-break draw per core
+    __shared__ int32_t s_agent_r[MS_MAX_AGENTS];    // agentReward
+    __shared__ int32_t s_auct_r[MS_MAX_CORES];      // auctioneerReward
     __shared__ uint32_t s_flags;
     __shared__ int s_n_exec;
 
@@ -350,12 +459,12 @@ __global__ void __launch_bounds__(64) k_env_step(Params P, uint8_t* recs, uint32
         off_r[i] = 0.f;
         price_r[i] = 0.f;
     }
-    for (int i = lane; i < 64; i += kWave) {
-        s_agent_r[i] = 0;
+    for (int i = lane; i < MS_MAX_CORES; i += kWave) {
         s_auct_r[i] = 0;
         s_exec[i] = -1;
-        s_term[i] = 0;
+        s_fresh[i] = 0;
     }
+    for (int i = lane; i < MS_MAX_AGENTS; i += kWave) s_agent_r[i] = 0;
     if (lane == 0) {
         s_flags = 0;
         s_n_exec = 0;
@@ -377,87 +486,96 @@ __global__ void __launch_bounds__(64) k_env_step(Params P, uint8_t* recs, uint32
     int8_t* o_price = R.offer_price();
     Liab* my_liab = liab + e * (int64_t)C * P.cap;
 
+    // ---- issue the dependent loads early: the MT window at mti (a peek: no twist
+    //      yet) and the newest liability entries of every core that may terminate
+    //      this round, i.e. whose current job or one of the jobs offered to it has
+    //      one round left (its chain is settled in the tick below)
     MtStream rs;
     rs.gmt = mt + e * kMtN;
     rs.lds = reinterpret_cast<uint32_t*>(scratch);
     rs.mti0 = R.mti();
-    rs.wb = 0;
-    rs.wend = 0;
     rs.p = 0;
     rs.twisted = false;
-    rs.v = 0;
+    rs.load(0, 0, lane);
+    build_masks(R, P, s_mc, s_mr, lane);
+    Liab pf[kLiabPrefetch];
+    int pf_n = 0;
+    if (lane < C) {
+        bool maybe = c_kind[lane] >= 0 && c_rem[lane] == 1;
+        for (MaskIter it(s_mc[lane]); it.more() && !maybe;) maybe = s_rem[it.next()] == 1;
+        if (maybe) {
+            const int n = l_n[lane];
+            pf_n = min(n, kLiabPrefetch);
+            const Liab* chain = my_liab + lane * P.cap;
+#pragma unroll
+            for (int q = 0; q < kLiabPrefetch; q++)
+                if (q < pf_n) pf[q] = chain[n - 1 - q];
+        }
+    }
 
     // ---- auctioneer actions: HardcodedAuctioneerAcceptor (HardcodedModules.py:54-78), asked by the
     //      driver before env.step (trainPPO.py:162); ties broken with random.sample -> _randbelow
-    bool need_tie = false;
     if (!io.act_auct) {
-        for (int c = lane; c < C; c += kWave) {
-            int16_t act = (int16_t)O;
-            int16_t nt = 0;
-            if (c_owner[c] == 0) {
-                int mn = -1, md = 1, cnt = 0;  // max over the padded list starts at the pad ratio -1
-                for (int i = 0; i < NL; i++) {
-                    if (o_core[i] == c && o_recip[i] == 0) {
-                        int num, den;
-                        ratio_of(o_price[i], s_rem[i], num, den);
-                        if (num * md > mn * den) {
-                            mn = num;
-                            md = den;
-                        }
-                        cnt++;
+        // per core: the max ratio over the auctioneer's offers (the padded list's -1 entries and the
+        // own empty job bound it from below) and how many offers attain it
+        int mn = -1, md = 1;
+        if (lane < C) {
+            int nt = 0;
+            if (c_owner[lane] == 0) {
+                const M128 cand = mand(s_mc[lane], s_mr[0]);
+                for (MaskIter it(cand); it.more();) {
+                    const int i = it.next();
+                    int num, den;
+                    ratio_of(o_price[i], s_rem[i], num, den);
+                    if (num * md > mn * den) {
+                        mn = num;
+                        md = den;
                     }
                 }
-                if (mn * 1 > -1 * md) {  // max(ratios) > own ratio (-1, the auctioneer's empty job)
-                    for (int i = 0; i < NL; i++)
-                        if (o_core[i] == c && o_recip[i] == 0) {
-                            int num, den;
-                            ratio_of(o_price[i], s_rem[i], num, den);
-                            nt += (num * md == mn * den);
-                        }
+                if (mn > -md) {  // max(ratios) > own ratio (-1, the auctioneer's empty job)
+                    for (MaskIter it(cand); it.more();) {
+                        const int i = it.next();
+                        int num, den;
+                        ratio_of(o_price[i], s_rem[i], num, den);
+                        nt += (num * md == mn * den);
+                    }
                 }
-                (void)cnt;
             }
-            s_auct[c] = act;
-            s_tie_n[c] = nt;
+            s_auct[lane] = (int16_t)O;
+            s_tie_n[lane] = (int16_t)nt;
         }
         __syncthreads();
-        // tie-breaks in core order on the env stream (Auctioneer.getAuctioneerAction Auctioneer.py:95-102)
+        // tie-break draws in core order on the env stream (Auctioneer.getAuctioneerAction
+        // Auctioneer.py:95-102)
+        bool any = false;
         for (int c = 0; c < C; c++) {
-            int nt = s_tie_n[c];
+            const int nt = s_tie_n[c];
             if (nt > 0) {
-                need_tie = true;
-                uint32_t pick = rs.randbelow((uint32_t)nt, lane);
-                // map the pick-th tied candidate back to its index in the padded list
-                if (lane == 0) {
-                    int mn = -1, md = 1;
-                    for (int i = 0; i < NL; i++)
-                        if (o_core[i] == c && o_recip[i] == 0) {
-                            int num, den;
-                            ratio_of(o_price[i], s_rem[i], num, den);
-                            if (num * md > mn * den) {
-                                mn = num;
-                                md = den;
-                            }
-                        }
-                    int k = 0, t = 0;
-                    for (int i = 0; i < NL; i++)
-                        if (o_core[i] == c && o_recip[i] == 0) {
-                            int num, den;
-                            ratio_of(o_price[i], s_rem[i], num, den);
-                            if (num * md == mn * den) {
-                                if ((uint32_t)t == pick) s_auct[c] = (int16_t)k;
-                                t++;
-                            }
-                            k++;
-                        }
+                const uint32_t pick = rs.randbelow((uint32_t)nt, lane);
+                if (lane == 0) s_pick[c] = (int16_t)pick;
+                any = true;
+            }
+        }
+        if (any) {
+            __syncthreads();
+            // the pick-th maximal candidate's position in the padded list
+            if (lane < C && s_tie_n[lane] > 0) {
+                const int pick = s_pick[lane];
+                int k = 0, t = 0;
+                for (MaskIter it(mand(s_mc[lane], s_mr[0])); it.more(); k++) {
+                    const int i = it.next();
+                    int num, den;
+                    ratio_of(o_price[i], s_rem[i], num, den);
+                    if (num * md == mn * den) {
+                        if (t == pick) s_auct[lane] = (int16_t)k;
+                        t++;
+                    }
                 }
-                __syncthreads();
             }
         }
     } else {
         for (int c = lane; c < C; c += kWave) s_auct[c] = a_auct[c];
     }
-    (void)need_tie;
     __syncthreads();
 
     // ---- which offer each core executes (executeAgentAcceptions1 world.py:391-404,
@@ -473,17 +591,7 @@ __global__ void __launch_bounds__(64) k_env_step(Params P, uint8_t* recs, uint32
         int idx = owner > 0 ? a_acc[(owner - 1) * C + c] : s_auct[c];
         if (owner == 0 && (idx < 0 || idx > O)) atomicOr(&s_flags, MS_FLAG_BAD_ACTION);
         int slot = -1;
-        if (idx >= 0 && idx < O) {
-            int k = 0;
-            for (int i = 0; i < NL; i++)
-                if (o_core[i] == c && o_recip[i] == owner) {
-                    if (k == idx) {
-                        slot = i;
-                        break;
-                    }
-                    k++;
-                }
-        }
+        if (idx >= 0 && idx < O) slot = kth_bit(mand(s_mc[c], s_mr[owner]), idx);
         s_exec[c] = (int16_t)slot;
         s_key[c] = (int16_t)(owner > 0 ? (owner - 1) * C + c : N * C + c);
     }
@@ -542,6 +650,8 @@ __global__ void __launch_bounds__(64) k_env_step(Params P, uint8_t* recs, uint32
                 le.nec = (int8_t)nrem;
                 le.round = round;
                 my_liab[c * P.cap + n] = le;
+                s_newle[c] = le;
+                s_fresh[c] = 1;
                 l_n[c] = (uint8_t)(n + 1);
             } else {
                 s_flags |= MS_FLAG_LIABILITY_OVERFLOW;
@@ -601,13 +711,26 @@ __global__ void __launch_bounds__(64) k_env_step(Params P, uint8_t* recs, uint32
                 c_rem[c] = -1;
                 c_birth[c] = -1;
                 c_owner[c] = 0;
-                // settlement, newest entry first
+                // settlement, newest entry first: this round's entry from LDS, the next
+                // kLiabPrefetch from the registers loaded at staging, older ones from HBM
                 acc_r[(owner - 1) * C + c] = gen;
                 if (!P.free_prices) atomicAdd(&s_agent_r[owner - 1], gen);
-                int n = l_n[c];
+                const int n = l_n[c];
+                const int fresh = s_fresh[c];
                 int last = ts, tm = 0;
                 for (int k = n - 1; k >= 0; k--) {
-                    Liab le = my_liab[c * P.cap + k];
+                    const int q = n - 1 - k - fresh;  // index among the entries older than this round's
+                    Liab le;
+                    if (q < 0) {
+                        le = s_newle[c];
+                    } else if (q < pf_n) {
+                        le = pf[0];
+#pragma unroll
+                        for (int j = 1; j < kLiabPrefetch; j++)
+                            if (q == j) le = pf[j];
+                    } else {
+                        le = my_liab[c * P.cap + k];
+                    }
                     tm += last - le.round;
                     last = le.round;
                     double ratio = (double)le.price / (double)le.nec;  // Python true division
@@ -724,10 +847,9 @@ __global__ void __launch_bounds__(64) k_env_step(Params P, uint8_t* recs, uint32
     }
     __syncthreads();
 
-    // ---- outputs: state record, observations, rewards
+    // ---- outputs: state record, rewards, observations of the new offer set
     copy_dwords(reinterpret_cast<uint32_t*>(recs + e * (int64_t)P.rec_bytes), reinterpret_cast<uint32_t*>(rec),
                 P.rec_bytes / 4, lane);
-    emit_obs(R, P, scratch, io.obs_acc, io.obs_off, io.obs_auct, e, lane);
     if (io.rew_acc) copy_dwords(reinterpret_cast<uint32_t*>(io.rew_acc + e * N * C), reinterpret_cast<uint32_t*>(acc_r), N * C, lane);
     if (io.rew_offer) copy_dwords(reinterpret_cast<uint32_t*>(io.rew_offer + e * NL), reinterpret_cast<uint32_t*>(off_r), NL, lane);
     if (io.rew_price) copy_dwords(reinterpret_cast<uint32_t*>(io.rew_price + e * NL), reinterpret_cast<uint32_t*>(price_r), NL, lane);
@@ -735,6 +857,8 @@ __global__ void __launch_bounds__(64) k_env_step(Params P, uint8_t* recs, uint32
         for (int a = lane; a < N; a += kWave) io.rew_agent[e * N + a] = s_agent_r[a];
     if (io.rew_auct)
         for (int c = lane; c < C; c += kWave) io.rew_auct[e * C + c] = s_auct_r[c];
+    build_masks(R, P, s_mc, s_mr, lane);
+    emit_obs(R, P, s_mc, s_mr, scratch, io.obs_acc, io.obs_off, io.obs_auct, e, lane);
 }
 
 // random._randbelow(n) on env e's stream (random.randint in the update schedulers,
