@@ -201,6 +201,17 @@ int ms_env_flags(ms_env* env, uint32_t* flags, void* stream);
 /* CPython random._randbelow(n) drawn on env e's stream (n >= 1); synchronous. */
 int ms_env_randbelow(ms_env* env, int64_t env_index, uint32_t n, uint32_t* out, void* stream);
 
+/* Auctioneer.getAuctioneerAction (Auctioneer.py:95-102) for all E envs on the current state, as
+ * trainPPO.py:162 calls it before env.step: writes actions [E][C] (O = reject) and consumes the
+ * tie-break draws of each env's stream; pass the actions to ms_env_step afterwards. */
+int ms_env_auctioneer(ms_env* env, int8_t* actions, void* stream);
+
+/* Env e's CPython random state (random.getstate()/setstate(), Modules/_randommodule.c): the 624
+ * MT19937 words and the index. Synchronous. Lets an E = 1 driver share the global `random`
+ * module with the env as the reference does (world.py spawn, Auctioneer ties, Agent.py:718). */
+int ms_env_get_rng(ms_env* env, int64_t env_index, uint32_t* words, int32_t* index, void* stream);
+int ms_env_set_rng(ms_env* env, int64_t env_index, const uint32_t* words, int32_t index, void* stream);
+
 /* Copy the full state to / from host arrays (synchronous). Import validates
  * the reference invariants the kernel relies on. */
 int ms_env_export(ms_env* env, const ms_state_host* out, void* stream);

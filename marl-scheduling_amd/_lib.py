@@ -46,6 +46,9 @@ def _load():
         "ms_env_round": (i64, [P]),
         "ms_env_flags": (ct.c_int, [P, ct.POINTER(u32), P]),
         "ms_env_randbelow": (ct.c_int, [P, i64, u32, ct.POINTER(u32), P]),
+        "ms_env_auctioneer": (ct.c_int, [P, P, P]),
+        "ms_env_get_rng": (ct.c_int, [P, i64, ct.POINTER(u32), ct.POINTER(i32), P]),
+        "ms_env_set_rng": (ct.c_int, [P, i64, ct.POINTER(u32), i32, P]),
         "ms_env_export": (ct.c_int, [P, ct.POINTER(abi.MsStateHost), P]),
         "ms_env_import": (ct.c_int, [P, ct.POINTER(abi.MsStateHost), P]),
         "ms_policy_act": (ct.c_int, [ct.POINTER(abi.MsMlpParams), P, i32, i64, i32, i32, u64, u64, P, P, P, P, P]),
@@ -71,7 +74,8 @@ lib = _load()
 # every entry point include/marlsched.h declares (checked by tests)
 EXPORTED = (
     "ms_last_error", "ms_abi_version", "ms_config_shape", "ms_env_create", "ms_env_destroy", "ms_env_shape",
-    "ms_env_reset", "ms_env_step", "ms_env_round", "ms_env_flags", "ms_env_randbelow", "ms_env_export",
+    "ms_env_reset", "ms_env_step", "ms_env_round", "ms_env_flags", "ms_env_randbelow", "ms_env_auctioneer",
+    "ms_env_get_rng", "ms_env_set_rng", "ms_env_export",
     "ms_env_import", "ms_policy_act", "ms_offer_act_free", "ms_discounted_returns", "ms_ppo_workspace_bytes", "ms_ppo_grad",
 )
 

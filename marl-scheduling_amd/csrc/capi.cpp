@@ -18,6 +18,7 @@ hipError_t launch_env_init(const Params&, int64_t, uint8_t*, uint32_t*, Liab*, u
 hipError_t launch_env_reset(const Params&, int64_t, const uint8_t*, int8_t*, int8_t*, int8_t*, hipStream_t);
 hipError_t launch_env_step(const Params&, int64_t, uint8_t*, uint32_t*, Liab*, const StepIO&, hipStream_t);
 hipError_t launch_env_randbelow(const Params&, uint8_t*, uint32_t*, int64_t, uint32_t, uint32_t*, hipStream_t);
+hipError_t launch_env_auctioneer(const Params&, int64_t, uint8_t*, uint32_t*, int8_t*, hipStream_t);
 hipError_t launch_policy_act(const ms_mlp_params*, const int8_t*, int, int64_t, int, int, uint64_t, uint64_t,
                              const uint64_t*, const float*, int8_t*, float*, hipStream_t);
 hipError_t launch_offer_act_free(const ms_mlp_params*, const ms_mlp_params*, const int8_t*, int, int64_t, int, int, int,
@@ -247,6 +248,31 @@ int ms_env_randbelow(ms_env* env, int64_t e, uint32_t n, uint32_t* out, void* st
     HIP_TRY(ms::launch_env_randbelow(env->P, env->recs, env->mt, e, n, env->scratch_u32, (hipStream_t)stream));
     HIP_TRY(hipMemcpyAsync(out, env->scratch_u32, 4, hipMemcpyDeviceToHost, (hipStream_t)stream));
     HIP_TRY(hipStreamSynchronize((hipStream_t)stream));
+    return MS_OK;
+}
+
+int ms_env_auctioneer(ms_env* env, int8_t* actions, void* stream) {
+    if (!env || !actions) return fail(MS_EINVAL, "env/actions is NULL");
+    HIP_TRY(ms::launch_env_auctioneer(env->P, env->E, env->recs, env->mt, actions, (hipStream_t)stream));
+    return MS_OK;
+}
+
+int ms_env_get_rng(ms_env* env, int64_t e, uint32_t* words, int32_t* index, void* stream) {
+    if (!env || !words || !index) return fail(MS_EINVAL, "NULL argument");
+    if (e < 0 || e >= env->E) return fail(MS_EINVAL, "env index out of range");
+    HIP_TRY(hipStreamSynchronize((hipStream_t)stream));
+    HIP_TRY(hipMemcpy(words, env->mt + e * ms::kMtN, 4 * ms::kMtN, hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(index, env->recs + e * env->P.rec_bytes + 8, 4, hipMemcpyDeviceToHost));
+    return MS_OK;
+}
+
+int ms_env_set_rng(ms_env* env, int64_t e, const uint32_t* words, int32_t index, void* stream) {
+    if (!env || !words) return fail(MS_EINVAL, "NULL argument");
+    if (e < 0 || e >= env->E) return fail(MS_EINVAL, "env index out of range");
+    if (index < 0 || index > ms::kMtN) return fail(MS_EINVAL, "MT index must be in [0, 624]");
+    HIP_TRY(hipStreamSynchronize((hipStream_t)stream));
+    HIP_TRY(hipMemcpy(env->mt + e * ms::kMtN, words, 4 * ms::kMtN, hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(env->recs + e * env->P.rec_bytes + 8, &index, 4, hipMemcpyHostToDevice));
     return MS_OK;
 }
 

@@ -327,6 +327,75 @@ __device__ void emit_obs(Rec& R, const Params& P, const M128* mc, const M128* mr
     emit_acc_rows<2>(R, P, mc, mr, scratch, auct ? auct + e * (int64_t)P.C * P.acc_stride : nullptr, P.C, lane);
 }
 
+// HardcodedAuctioneerAcceptor.selectAction for every core (HardcodedModules.py:54-78,
+// Auctioneer.getAuctioneerAction Auctioneer.py:95-102) on the staged state: per core the max
+// ratio over the auctioneer's offers and the count of offers attaining it, then one
+// _randbelow(count) per tied core in core order on the env stream. Writes s_auct[c] (O = reject).
+__device__ void hardcoded_auctioneer(Rec& R, const Params& P, const M128* s_mc, const M128* s_mr, MtStream& rs,
+                                     int16_t* s_auct, int16_t* s_tie_n, int16_t* s_pick, int lane) {
+    const int C = P.C, O = P.O;
+    const int8_t* c_owner = R.core_owner();
+    const int8_t* o_price = R.offer_price();
+    const int8_t* s_rem = R.slot_rem();
+    // per core: the max ratio over the auctioneer's offers (the padded list's -1 entries and the
+    // own empty job bound it from below) and how many offers attain it
+    int mn = -1, md = 1;
+    if (lane < C) {
+        int nt = 0;
+        if (c_owner[lane] == 0) {
+            const M128 cand = mand(s_mc[lane], s_mr[0]);
+            for (MaskIter it(cand); it.more();) {
+                const int i = it.next();
+                int num, den;
+                ratio_of(o_price[i], s_rem[i], num, den);
+                if (num * md > mn * den) {
+                    mn = num;
+                    md = den;
+                }
+            }
+            if (mn > -md) {  // max(ratios) > own ratio (-1, the auctioneer's empty job)
+                for (MaskIter it(cand); it.more();) {
+                    const int i = it.next();
+                    int num, den;
+                    ratio_of(o_price[i], s_rem[i], num, den);
+                    nt += (num * md == mn * den);
+                }
+            }
+        }
+        s_auct[lane] = (int16_t)O;
+        s_tie_n[lane] = (int16_t)nt;
+    }
+    __syncthreads();
+    // tie-break draws in core order on the env stream (Auctioneer.getAuctioneerAction
+    // Auctioneer.py:95-102)
+    bool any = false;
+    for (int c = 0; c < C; c++) {
+        const int nt = s_tie_n[c];
+        if (nt > 0) {
+            const uint32_t pick = rs.randbelow((uint32_t)nt, lane);
+            if (lane == 0) s_pick[c] = (int16_t)pick;
+            any = true;
+        }
+    }
+    if (any) {
+        __syncthreads();
+        // the pick-th maximal candidate's position in the padded list
+        if (lane < C && s_tie_n[lane] > 0) {
+            const int pick = s_pick[lane];
+            int k = 0, t = 0;
+            for (MaskIter it(mand(s_mc[lane], s_mr[0])); it.more(); k++) {
+                const int i = it.next();
+                int num, den;
+                ratio_of(o_price[i], s_rem[i], num, den);
+                if (num * md == mn * den) {
+                    if (t == pick) s_auct[lane] = (int16_t)k;
+                    t++;
+                }
+            }
+        }
+    }
+}
+
 // ---------------------------------------------------------------------------
 // kernels
 
@@ -516,63 +585,7 @@ __global__ void __launch_bounds__(64) k_env_step(Params P, uint8_t* recs, uint32
     // ---- auctioneer actions: HardcodedAuctioneerAcceptor (HardcodedModules.py:54-78), asked by the
     //      driver before env.step (trainPPO.py:162); ties broken with random.sample -> _randbelow
     if (!io.act_auct) {
-        // per core: the max ratio over the auctioneer's offers (the padded list's -1 entries and the
-        // own empty job bound it from below) and how many offers attain it
-        int mn = -1, md = 1;
-        if (lane < C) {
-            int nt = 0;
-            if (c_owner[lane] == 0) {
-                const M128 cand = mand(s_mc[lane], s_mr[0]);
-                for (MaskIter it(cand); it.more();) {
-                    const int i = it.next();
-                    int num, den;
-                    ratio_of(o_price[i], s_rem[i], num, den);
-                    if (num * md > mn * den) {
-                        mn = num;
-                        md = den;
-                    }
-                }
-                if (mn > -md) {  // max(ratios) > own ratio (-1, the auctioneer's empty job)
-                    for (MaskIter it(cand); it.more();) {
-                        const int i = it.next();
-                        int num, den;
-                        ratio_of(o_price[i], s_rem[i], num, den);
-                        nt += (num * md == mn * den);
-                    }
-                }
-            }
-            s_auct[lane] = (int16_t)O;
-            s_tie_n[lane] = (int16_t)nt;
-        }
-        __syncthreads();
-        // tie-break draws in core order on the env stream (Auctioneer.getAuctioneerAction
-        // Auctioneer.py:95-102)
-        bool any = false;
-        for (int c = 0; c < C; c++) {
-            const int nt = s_tie_n[c];
-            if (nt > 0) {
-                const uint32_t pick = rs.randbelow((uint32_t)nt, lane);
-                if (lane == 0) s_pick[c] = (int16_t)pick;
-                any = true;
-            }
-        }
-        if (any) {
-            __syncthreads();
-            // the pick-th maximal candidate's position in the padded list
-            if (lane < C && s_tie_n[lane] > 0) {
-                const int pick = s_pick[lane];
-                int k = 0, t = 0;
-                for (MaskIter it(mand(s_mc[lane], s_mr[0])); it.more(); k++) {
-                    const int i = it.next();
-                    int num, den;
-                    ratio_of(o_price[i], s_rem[i], num, den);
-                    if (num * md == mn * den) {
-                        if (t == pick) s_auct[lane] = (int16_t)k;
-                        t++;
-                    }
-                }
-            }
-        }
+        hardcoded_auctioneer(R, P, s_mc, s_mr, rs, s_auct, s_tie_n, s_pick, lane);
     } else {
         for (int c = lane; c < C; c += kWave) s_auct[c] = a_auct[c];
     }
@@ -861,6 +874,37 @@ __global__ void __launch_bounds__(64) k_env_step(Params P, uint8_t* recs, uint32
     emit_obs(R, P, s_mc, s_mr, scratch, io.obs_acc, io.obs_off, io.obs_auct, e, lane);
 }
 
+// Auctioneer.getAuctioneerAction (Auctioneer.py:95-102) on its own, as the driver calls it
+// before env.step (trainPPO.py:162): writes actions [E][C] and advances the env stream by the
+// tie-break draws; a following ms_env_step with these actions then draws only the spawn.
+__global__ void __launch_bounds__(64) k_env_auctioneer(Params P, uint8_t* recs, uint32_t* mt, int8_t* actions) {
+    extern __shared__ __align__(16) uint8_t smem[];
+    __shared__ M128 s_mc[MS_MAX_CORES];
+    __shared__ M128 s_mr[MS_MAX_AGENTS + 1];
+    __shared__ int16_t s_auct[MS_MAX_CORES];
+    __shared__ int16_t s_tie_n[MS_MAX_CORES];
+    __shared__ int16_t s_pick[MS_MAX_CORES];
+    const int lane = threadIdx.x;
+    const int64_t e = blockIdx.x;
+    uint8_t* rec = smem + P.s_rec;
+    copy_dwords(reinterpret_cast<uint32_t*>(rec), reinterpret_cast<const uint32_t*>(recs + e * (int64_t)P.rec_bytes),
+                P.rec_bytes / 4, lane);
+    __syncthreads();
+    Rec R{rec, &P};
+    MtStream rs;
+    rs.gmt = mt + e * kMtN;
+    rs.lds = reinterpret_cast<uint32_t*>(smem + P.s_scratch);
+    rs.mti0 = R.mti();
+    rs.p = 0;
+    rs.twisted = false;
+    rs.load(0, 0, lane);
+    build_masks(R, P, s_mc, s_mr, lane);
+    hardcoded_auctioneer(R, P, s_mc, s_mr, rs, s_auct, s_tie_n, s_pick, lane);
+    __syncthreads();
+    for (int c = lane; c < P.C; c += kWave) actions[e * P.C + c] = (int8_t)s_auct[c];
+    if (lane == 0) *reinterpret_cast<int32_t*>(recs + e * (int64_t)P.rec_bytes + 8) = rs.final_index();
+}
+
 // random._randbelow(n) on env e's stream (random.randint in the update schedulers,
 // Agent.py:718,725, SchedulingEnvironment.py:317-326).
 __global__ void __launch_bounds__(64) k_env_randbelow(Params P, uint8_t* recs, uint32_t* mt, int64_t e, uint32_t n,
@@ -901,6 +945,11 @@ hipError_t launch_env_reset(const Params& P, int64_t E, const uint8_t* recs, int
 hipError_t launch_env_step(const Params& P, int64_t E, uint8_t* recs, uint32_t* mt, Liab* liab, const StepIO& io,
                            hipStream_t s) {
     hipLaunchKernelGGL(k_env_step, dim3((unsigned)E), dim3(kWave), P.s_total, s, P, recs, mt, liab, io);
+    return hipGetLastError();
+}
+hipError_t launch_env_auctioneer(const Params& P, int64_t E, uint8_t* recs, uint32_t* mt, int8_t* actions,
+                                 hipStream_t s) {
+    hipLaunchKernelGGL(k_env_auctioneer, dim3((unsigned)E), dim3(kWave), P.s_total, s, P, recs, mt, actions);
     return hipGetLastError();
 }
 hipError_t launch_env_randbelow(const Params& P, uint8_t* recs, uint32_t* mt, int64_t e, uint32_t n, uint32_t* out,

@@ -1,0 +1,278 @@
+"""E = 1 engine behind the drop-in modules ``world``, ``SchedulingEnvironment`` and ``PPOmodules``.
+
+The reference's driver (``trainPPO.py:133-227``) talks to one ``World``
+through ``SchedulingEnv.reset/step`` (SchedulingEnvironment.py:32-109),
+``getActionForAllAgents`` (:150-172), ``world.auctioneer.getAuctioneerAction``
+(Auctioneer.py:95-102), ``saveRewards`` and ``updateAgents``. The drop-in
+modules keep those names, signatures and return containers, and every round
+runs on the HIP library at E = 1:
+
+* the env round is ``ms_env_step``; the hard-coded auctioneer is ``ms_env_auctioneer``;
+* action selection is ``ms_policy_act`` / ``ms_offer_act_free``, with the experience
+  buffers kept on the device;
+* ``updateAgents`` is ``ms_discounted_returns`` + ``ms_ppo_grad`` + Adam.
+
+Python's global ``random`` stream is the env's stream, as in the reference, where
+world.py, Auctioneer.py and Agent.py all call the ``random`` module. Before a call
+that draws, the module's MT19937 state is copied to the device (ms_env_set_rng)
+and copied back after it (ms_env_get_rng). Seeding ``random`` therefore reproduces
+the reference's job stream, tie-breaks and update draws. Policy sampling uses
+counter-based Philox on the device instead of torch.multinomial, so it matches
+in distribution only.
+
+There is no CPU fallback: without a HIP device the env constructor raises.
+"""
+from __future__ import annotations
+
+import importlib
+import os
+import random
+import statistics
+import sys
+from collections import namedtuple
+
+import numpy as np
+import torch
+
+_ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+if _ROOT not in sys.path:
+    sys.path.insert(0, _ROOT)
+_pkg = importlib.import_module("marl-scheduling_amd")
+abi = importlib.import_module("marl-scheduling_amd.abi")
+envmod = importlib.import_module("marl-scheduling_amd.env")
+ppo = importlib.import_module("marl-scheduling_amd.ppo")
+
+# world.py:15-17
+Verweilzeit = namedtuple("Verweilzeit", ["Prioritaet", "Bedienzeit", "Verweilzeit", "normalisierte_Verweilzeit"])
+
+
+class AcceptedOffer:
+    """The offer copies collected in world.acceptedOffers (world.py:156-196, :285-293)."""
+
+    __slots__ = ("offererID", "recipientID", "coreID", "queuePosition", "jobID", "offeredReward", "necessaryTime",
+                 "prio1", "jobKind", "round")
+
+    def __init__(self, offererID, recipientID, coreID, queuePosition, offeredReward, necessaryTime, prio1, jobKind,
+                 round_):
+        self.offererID, self.recipientID, self.coreID = offererID, recipientID, coreID
+        self.queuePosition, self.offeredReward, self.necessaryTime = queuePosition, offeredReward, necessaryTime
+        self.prio1, self.jobKind, self.round = prio1, jobKind, round_
+        self.jobID = None  # job IDs are not kept on the device (only render() prints them)
+
+    def getOfferState(self):
+        return {k: getattr(self, k) for k in self.__slots__}
+
+
+class JobView:
+    """Read-only Job (world.py:79-114) of an exported state; the empty job is all -1."""
+
+    def __init__(self, priority=-1, remainingLength=-1, initialLength=-1, jobKind=-1, birthDate=-1, ownerID=-1,
+                 wait=False):
+        self.priority, self.remainingLength, self.initialLength = priority, remainingLength, initialLength
+        self.jobKind, self.birthDate, self.ownerID, self.wait = jobKind, birthDate, ownerID, wait
+        self.empty = priority == -1
+        self.jobID = None
+
+
+class CoreView:
+    """Read-only Core (world.py:27-76) of an exported state."""
+
+    def __init__(self, coreID, ownerID, job):
+        self.coreID, self.ownerID, self.job = coreID, ownerID, job
+
+    def getCoreState(self):
+        return {"coreID": self.coreID, "ownerID": self.ownerID, "priority": self.job.priority,
+                "remainingLength": self.job.remainingLength}
+
+
+class RandomLink:
+    """Shares Python's global ``random`` stream with the env's device MT19937 (replica 0)."""
+
+    def __init__(self, env):
+        self.env = env
+        self._last = None  # the internal state last exchanged with the device
+
+    def push(self):
+        st = random.getstate()
+        internal = st[1]
+        if internal != self._last:
+            self.env.set_rng_state(internal[:624], internal[624])
+            self._last = internal
+
+    def pull(self):
+        words, idx = self.env.get_rng_state()
+        internal = tuple(words) + (idx,)
+        st = random.getstate()
+        random.setstate((st[0], internal, st[2]))
+        self._last = internal
+
+
+class Engine:
+    """One world on the device: state, observations, rewards and events of the last step."""
+
+    def __init__(self, world, free_prices: bool, commercial: bool, net_zero_offer_reward: float, device=None):
+        if not torch.cuda.is_available():
+            raise RuntimeError("the drop-in env runs on the HIP device (no CPU fallback)")
+        w = world
+        cfg = abi.make_config(
+            w.numberOfAgents, w.numberOfCores, w.collectionLength, w.possibleJobPriorities, w.possibleJobLengths,
+            w.probabilities, fix_prices=None if free_prices else w.listOfFixPrices, free_prices=free_prices,
+            commercial=commercial, net_zero_offer_reward=net_zero_offer_reward, new_jobs=w.newJobsPerRoundPerAgent,
+            reward_multiplier=w.rewardMultiplier, episode_length=w.episodeLength)
+        self.env = envmod.BatchedEnv(cfg, 1, seed=0, device=device)
+        self.device = self.env.device
+        self.free = bool(free_prices)
+        self.N, self.C, self.L, self.O = self.env.N, self.env.C, self.env.L, self.env.O
+        s = self.env.shape
+        self.d_acc, self.d_off = s.acc_obs_dim, s.off_obs_dim
+        self.mult = int(w.rewardMultiplier)
+        self.rng = RandomLink(self.env)
+        self.obs = self.env.obs_buffers(auctioneer=True)
+        self.rew = self.env.reward_buffers()
+        self.ev = self.env.event_buffers()
+        self.auct_dev = torch.empty((1, self.C), dtype=torch.int8, device=self.device)
+        self.last_obs = None  # host containers of the last reset/step (identity marks "device copy is current")
+
+    @property
+    def round(self) -> int:
+        return self.env.round
+
+    # ---- observations (Agent.gatherObservations Agent.py:148-165, gatherDividedAuctioneerObservation)
+    def _host_obs(self):
+        torch.cuda.synchronize(self.device)
+        acc = torch.from_numpy(self.obs["acceptor"][0, :, :, : self.d_acc].cpu().numpy().astype(np.int64))
+        off = torch.from_numpy(self.obs["offer"][0, :, :, : self.d_off].cpu().numpy().astype(np.int64))
+        auct = torch.from_numpy(self.obs["auctioneer"][0, :, : self.d_acc].cpu().numpy().astype(np.int64))
+        acc_l = [[acc[a, c] for c in range(self.C)] for a in range(self.N)]
+        off_l = [[off[a, j] for j in range(self.L)] for a in range(self.N)]
+        auct_l = [auct[c] for c in range(self.C)]
+        self.last_obs = (acc_l, off_l, auct_l)
+        return self.last_obs
+
+    def reset(self):
+        self.env.reset(self.obs)
+        return self._host_obs()
+
+    def auctioneer_actions(self):
+        self.rng.push()
+        self.env.auctioneer(self.auct_dev)
+        self.rng.pull()
+        return [int(v) for v in self.auct_dev[0].cpu().tolist()]
+
+    # ---- one round (World.step1 world.py:295-334 + rewards)
+    def _actions(self, offer_actions, acceptor_actions, auctioneer_action):
+        N, C, L, O = self.N, self.C, self.L, self.O
+        acc = np.asarray(acceptor_actions, dtype=np.int64).reshape(N, C)
+        if acc.min() < 0 or acc.max() > O:
+            raise ValueError("acceptor actions must be in [0, %d] (world.py:389,404)" % O)
+        if self.free:
+            pairs = np.asarray(offer_actions, dtype=np.int64).reshape(N, L, 2)
+            core, price = pairs[..., 0], pairs[..., 1]
+        else:
+            core, price = np.asarray(offer_actions, dtype=np.int64).reshape(N, L), None
+        # an action outside [0, C) names no core (world.py:412-414, 450-452)
+        core = np.where((core >= 0) & (core < C), core, C)
+        auct = np.asarray(auctioneer_action, dtype=np.int64).reshape(C)
+        if auct.min() < 0 or auct.max() > O:
+            raise ValueError("auctioneer actions must be in [0, %d]" % O)
+        if price is not None and (price.min() < -128 or price.max() > 127):
+            raise ValueError("free prices must fit int8")
+        dev = self.device
+        to = lambda x: torch.from_numpy(np.ascontiguousarray(x.astype(np.int8))).to(dev).unsqueeze(0).contiguous()
+        return to(acc), to(core), (to(price) if price is not None else None), to(auct)
+
+    def step(self, offer_actions, acceptor_actions, auctioneer_action):
+        acc, core, price, auct = self._actions(offer_actions, acceptor_actions, auctioneer_action)
+        self.rng.push()
+        self.env.step(acc, core, price, auct, obs=self.obs, rewards=self.rew, events=self.ev)
+        self.rng.pull()
+        obs = self._host_obs()
+        round_before = self.env.round - 1
+        accepted = envmod.decode_accepted(self.ev["accepted"])[0]
+        terminated = envmod.decode_terminated(self.ev["terminated"])[0]
+        offers = []
+        for c in np.argsort(np.where(accepted["valid"] != 0, accepted["order"], 1 << 20), kind="stable"):
+            r = accepted[c]
+            if not r["valid"]:
+                continue
+            offers.append(AcceptedOffer(int(r["offerer"]), int(r["recipient"]), int(c) + 1, int(r["slot"]),
+                                        int(r["price"]), int(r["nec_time"]), int(r["prio"]), int(r["kind"]),
+                                        int(r["round"])))
+        terms = []
+        for c in range(self.C):
+            t = terminated[c]
+            if t["valid"]:
+                terms.append((c + 1, int(t["owner"]), int(t["prio"]), int(t["init_len"]), int(t["dwell"])))
+        r = {k: (v[0].cpu().numpy() if v is not None else None) for k, v in self.rew.items()}
+        return obs, offers, terms, r, round_before
+
+    def export(self):
+        return self.env.export_state()
+
+
+def acception_quality(accepted_offers, former_prios, former_lengths):
+    """SchedulingEnv.calculateAverageAcceptionQuality (SchedulingEnvironment.py:174-192)."""
+    q = []
+    for offer in accepted_offers:
+        if offer.recipientID == 0:
+            continue
+        fp, fl = former_prios[offer.coreID - 1], former_lengths[offer.coreID - 1]
+        v = (offer.offeredReward / offer.necessaryTime) - ((fp / fl) if fp != -1 else 0)
+        q.append(v * 10)
+    return (statistics.mean(q) if q != [] else None), len(q)
+
+
+# ---------------------------------------------------------------------------
+# PPO side: experience buffers on the device + grouped nets
+
+
+class Units:
+    """ExperienceBuffers (PPOmodules.py:9-22) of U units of one net type, on the device:
+    states [T][U][stride] int8, actions [T][U] int8, logprobs [T][U] f32; rewards [T][U] on the host."""
+
+    def __init__(self, group: "ppo.PPOGroup", n_units: int, stride: int, device, cap: int = 256):
+        self.group, self.U, self.stride, self.device = group, n_units, stride, device
+        self.T = 0
+        self.rewards = []
+        self.states = torch.zeros((cap, n_units, stride), dtype=torch.int8, device=device)
+        self.actions = torch.zeros((cap, n_units), dtype=torch.int8, device=device)
+        self.logprobs = torch.zeros((cap, n_units), dtype=torch.float32, device=device)
+
+    def next_slot(self) -> int:
+        if self.T == self.states.shape[0]:
+            cap = 2 * self.T
+            for k in ("states", "actions", "logprobs"):
+                old = getattr(self, k)
+                new = torch.zeros((cap,) + tuple(old.shape[1:]), dtype=old.dtype, device=old.device)
+                new[: self.T].copy_(old[: self.T])
+                setattr(self, k, new)
+        return self.T
+
+    def clear(self):
+        self.T = 0
+        self.rewards = []
+
+    def update(self, u_sel):
+        """PPO.update of the units u_sel (one per group; PPOmodules.py:127-174) on the fused HIP gradient."""
+        T = self.T
+        if T == 0:
+            return []
+        if len(self.rewards) != T:
+            raise RuntimeError("%d rewards saved for %d actions" % (len(self.rewards), T))
+        sel = torch.as_tensor(u_sel, dtype=torch.long)
+        r = torch.from_numpy(np.stack(self.rewards).astype(np.float32))[:, sel].to(self.device)
+        ret = ppo.discounted_returns(r, self.group.gamma)  # [G, T]
+        return self.group.update_fused(self.states[:T], self.actions[:T], self.logprobs[:T], ret,
+                                       sel.to(torch.int32).to(self.device), T, 1)
+
+
+def reference_nets(order, dims):
+    """Build ActorCritic parameter dicts in the reference's construction order: each PPO object makes
+    policy then policy_old (PPOmodules.py:99,107) on torch's CPU generator. order: list of unit-type
+    names in construction order; dims: name -> (in_dim, n_actions). Returns name -> [dict, ...]."""
+    nets = {k: [] for k in dims}
+    for name in order:
+        D, A = dims[name]
+        nets[name].append(ppo.reference_actor_critic_params(D, A))
+        ppo.reference_actor_critic_params(D, A)  # policy_old: same init stream, then overwritten
+    return nets

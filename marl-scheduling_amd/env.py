@@ -122,6 +122,26 @@ class BatchedEnv:
         check(lib.ms_env_randbelow(self._h, int(env_index), int(n), ct.byref(out), stream_ptr(stream)))
         return int(out.value)
 
+    def auctioneer(self, out: torch.Tensor | None = None, stream=None) -> torch.Tensor:
+        """Auctioneer.getAuctioneerAction (Auctioneer.py:95-102) on the current state of every
+        replica: int8 [E, C] actions (O = reject); consumes the tie-break draws."""
+        if out is None:
+            out = torch.empty((self.E, self.C), dtype=torch.int8, device=self.device)
+        assert out.dtype == torch.int8 and out.is_contiguous() and out.numel() == self.E * self.C
+        check(lib.ms_env_auctioneer(self._h, ptr(out), stream_ptr(stream)))
+        return out
+
+    def get_rng_state(self, env_index: int = 0, stream=None):
+        """(624 MT19937 words as a tuple of ints, index): the random.getstate() internal state."""
+        words = (ct.c_uint32 * 624)()
+        idx = ct.c_int32()
+        check(lib.ms_env_get_rng(self._h, int(env_index), words, ct.byref(idx), stream_ptr(stream)))
+        return tuple(int(w) for w in words), int(idx.value)
+
+    def set_rng_state(self, words, index: int, env_index: int = 0, stream=None):
+        buf = (ct.c_uint32 * 624)(*[int(w) for w in words])
+        check(lib.ms_env_set_rng(self._h, int(env_index), buf, int(index), stream_ptr(stream)))
+
     # ---- state export / import (canonical ms_state_host layout)
     def _state_arrays(self):
         E, N, C, L, cap = self.E, self.N, self.C, self.L, self.shape.liability_cap

@@ -67,6 +67,16 @@ class GroupedActorCritic(nn.Module):
         for k in ACTOR_KEYS + CRITIC_KEYS:
             self.register_parameter(k, nn.Parameter(torch.stack([n[k].detach() for n in nets]).contiguous()))
 
+    @classmethod
+    def from_params(cls, nets: list, in_dim: int, n_actions: int, hidden: int = HIDDEN):
+        """Stack per-net parameter dicts (reference_actor_critic_params) into one grouped module,
+        for callers that build the nets of several unit types in the reference's interleaved order."""
+        m = cls(len(nets), in_dim, n_actions, hidden, init=False)
+        with torch.no_grad():
+            for k in ACTOR_KEYS + CRITIC_KEYS:
+                getattr(m, k).copy_(torch.stack([n[k].detach() for n in nets]))
+        return m
+
     def actor_parameters(self):
         return [getattr(self, k) for k in ACTOR_KEYS]
 
@@ -152,8 +162,12 @@ class PPOGroup:
     """Policy / policy_old pair + Adam for one unit type (PPOmodules.py:75-174)."""
 
     def __init__(self, n_groups, in_dim, n_actions, lr_actor, lr_critic, gamma, eps_clip, k_epochs, device,
-                 allreduce=None):
-        self.policy = GroupedActorCritic(n_groups, in_dim, n_actions).to(device)
+                 allreduce=None, init_nets=None):
+        if init_nets is not None:  # per-group parameter dicts built by the caller, in reference order
+            assert len(init_nets) == n_groups
+            self.policy = GroupedActorCritic.from_params(init_nets, in_dim, n_actions).to(device)
+        else:
+            self.policy = GroupedActorCritic(n_groups, in_dim, n_actions).to(device)
         self.policy_old = GroupedActorCritic(n_groups, in_dim, n_actions, init=False).to(device)
         self.policy_old.requires_grad_(False)
         self.sync_old()

@@ -92,6 +92,45 @@ def test_step_bit_exact_vs_oracle(ms, oracle, name):
     assert genv.round == T
 
 
+def test_separate_auctioneer_call_matches_oracle(ms, oracle):
+    """ms_env_auctioneer (getAuctioneerAction before env.step, trainPPO.py:162) then ms_env_step with
+    those actions: same actions, draws and state as the oracle's separate auctioneer call."""
+    cfg = ms.abi.named_config("cfg3")
+    s = ms.abi.config_shape(cfg)
+    N, C, L, O = s["N"], s["C"], s["L"], s["O"]
+    E, T, seed = 16, 120, 21
+    genv = ms.BatchedEnv(cfg, E, seed=seed)
+    oenvs = [oracle.OracleEnv(cfg, seed + e) for e in range(E)]
+    dev = genv.device
+    genv.reset()
+    oobs = [o.observe() for o in oenvs]
+    rng = np.random.default_rng(5)
+    for t in range(T):
+        acts = [random_actions(rng, offer_counts_from_obs(oobs[e]["acceptor"], O), N, C, L, O, True,
+                               s["price_actions"] - 1, accept_bias=0.7) for e in range(E)]
+        gauct = genv.auctioneer().cpu().numpy()
+        oauct = [o.auctioneer_actions() for o in oenvs]
+        for e in range(E):
+            np.testing.assert_array_equal(gauct[e], oauct[e], err_msg="auct t=%d e=%d" % (t, e))
+        acc = torch.tensor(np.stack([a[0] for a in acts]), dtype=torch.int8, device=dev)
+        off = torch.tensor(np.stack([a[1] for a in acts]), dtype=torch.int8, device=dev)
+        pr = torch.tensor(np.stack([a[2] for a in acts]), dtype=torch.int8, device=dev)
+        genv.step(acc, off, pr, auctioneer=torch.tensor(gauct, dtype=torch.int8, device=dev))
+        for e in range(E):
+            oenvs[e].step(acts[e][0], acts[e][1], acts[e][2], np.asarray(oauct[e]))
+        oobs = [o.observe() for o in oenvs]
+        if t % 30 == 29:
+            _compare_state(genv.export_state(), [o.export_state() for o in oenvs], E)
+    # RNG state round trip (random.getstate()/setstate() words + index)
+    words, idx = genv.get_rng_state(env_index=3)
+    st = genv.export_state()
+    assert list(words) == st["mt"][3].tolist() and idx == st["mt_index"][3]
+    o = oracle.OracleEnv(cfg, 999)
+    ost = o.export_state()
+    genv.set_rng_state(ost["mt"].tolist(), int(ost["mt_index"]), env_index=3)
+    assert [genv.randbelow(n, env_index=3) for n in (5, 9, 1000, 3)] == [o.randbelow(n) for n in (5, 9, 1000, 3)]
+
+
 def test_randbelow_matches_oracle(ms, oracle):
     cfg = ms.abi.named_config("cfg2")
     genv = ms.BatchedEnv(cfg, 3, seed=11)
