@@ -73,6 +73,36 @@ class _Unit:
         return x, a, lp, ret
 
 
+def env_seed(seed: int, rank: int, n_envs: int) -> int:
+    """Base seed of a rank's replicas: replica e of rank r is random.seed(base + e), so the ranks'
+    job streams are disjoint for seeds up to 1000003 / world_size apart."""
+    return seed * 1_000_003 + rank * n_envs
+
+
+def allreduce_mean_grads(params, world_size: int, group=None):
+    """Average the gradients over ranks with one flattened all-reduce (RCCL over xGMI on GPUs,
+    gloo on CPU). Shards are equal, so the mean of the per-rank mean losses' gradients is the
+    gradient of the mean over all replicas."""
+    import torch.distributed as dist
+    grads = [p.grad for p in params if p.grad is not None]
+    if not grads:
+        return
+    flat = torch._utils._flatten_dense_tensors(grads)
+    dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=group)
+    flat.div_(world_size)
+    for g, f in zip(grads, torch._utils._unflatten_dense_tensors(flat, grads)):
+        g.copy_(f)
+
+
+def broadcast_params(groups, group=None):
+    """Rank 0's weights to every rank (identical start), then policy_old <- policy."""
+    import torch.distributed as dist
+    for grp in groups:
+        for p in grp.policy.parameters():
+            dist.broadcast(p.data, src=0, group=group)
+        grp.sync_old()
+
+
 class Trainer:
     def __init__(self, cfg: abi.MsConfig, n_envs: int, arch: str = "local", hyper: Hyper | None = None, seed: int = 0,
                  device=None, rank: int = 0, world_size: int = 1, process_group=None, fused: bool = True,
@@ -85,7 +115,7 @@ class Trainer:
         self.hp = hyper or Hyper()
         self.rank, self.world_size, self.pg = rank, world_size, process_group
         self.seed = seed
-        self.env = BatchedEnv(cfg, self.E, seed=seed * 1_000_003 + rank * self.E, device=self.device)
+        self.env = BatchedEnv(cfg, self.E, seed=env_seed(seed, rank, self.E), device=self.device)
         s = self.env.shape
         N, C, L = s.n_agents, s.n_cores, s.collection_length
         self.N, self.C, self.L = N, C, L
@@ -148,20 +178,10 @@ class Trainer:
 
     # ---- distributed helpers
     def _allreduce(self, params):
-        import torch.distributed as dist
-        grads = [p.grad for p in params if p.grad is not None]
-        flat = torch._utils._flatten_dense_tensors(grads)
-        dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=self.pg)
-        flat.div_(self.world_size)
-        for g, f in zip(grads, torch._utils._unflatten_dense_tensors(flat, grads)):
-            g.copy_(f)
+        allreduce_mean_grads(params, self.world_size, self.pg)
 
     def _broadcast_params(self):
-        import torch.distributed as dist
-        for u in self.units():
-            for p in u.group.policy.parameters():
-                dist.broadcast(p.data, src=0, group=self.pg)
-            u.group.sync_old()
+        broadcast_params([u.group for u in self.units()], self.pg)
 
     def units(self):
         return [u for u in (self.acc, self.off, self.price) if u is not None]

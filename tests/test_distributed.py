@@ -1,0 +1,104 @@
+"""The N > 1 path on CPU: two gloo ranks, each with its own shard of replicas.
+
+The trainer's only collective is the per-epoch gradient all-reduce of the shared nets
+(trainer.allreduce_mean_grads) after a weight broadcast (trainer.broadcast_params). With equal
+shards, two ranks updating on their halves must end with identical weights, equal to one
+process updating on the union."""
+import importlib
+import os
+import socket
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+G, D, A, R, K = 3, 11, 5, 48, 3
+
+
+def _data():
+    g = torch.Generator().manual_seed(123)
+    states = torch.randint(-5, 13, (G, 2 * R, D), generator=g).float()
+    actions = torch.randint(0, A, (G, 2 * R), generator=g)
+    old_lp = -torch.rand((G, 2 * R), generator=g) * 2
+    ret = torch.randn((G, 2 * R), generator=g)
+    return states, actions, old_lp, ret
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _rank_main(rank, world, port, out_dir):
+    import torch.distributed as dist
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    ppo = importlib.import_module("marl-scheduling_amd.ppo")
+    tr = importlib.import_module("marl-scheduling_amd.trainer")
+    torch.manual_seed(0 if rank == 0 else 99)  # rank 1 starts elsewhere: the broadcast must fix that
+    grp = ppo.PPOGroup(G, D, A, 0.003, 0.01, 0.9, 0.2, K, "cpu",
+                       allreduce=lambda ps: tr.allreduce_mean_grads(ps, world))
+    tr.broadcast_params([grp])
+    states, actions, old_lp, ret = _data()
+    sl = slice(rank * R, (rank + 1) * R)
+    losses = grp.update(states[:, sl], actions[:, sl], old_lp[:, sl], ret[:, sl])
+    torch.save({k: v.detach().clone() for k, v in grp.policy.named_parameters()},
+               os.path.join(out_dir, "rank%d.pt" % rank))
+    assert len(losses) == K
+    dist.destroy_process_group()
+
+
+def test_two_rank_update_equals_single_process_on_the_union(tmp_path):
+    ppo = importlib.import_module("marl-scheduling_amd.ppo")
+    mp.spawn(_rank_main, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True)
+    w0 = torch.load(tmp_path / "rank0.pt", weights_only=True)
+    w1 = torch.load(tmp_path / "rank1.pt", weights_only=True)
+    torch.manual_seed(0)
+    single = ppo.PPOGroup(G, D, A, 0.003, 0.01, 0.9, 0.2, K, "cpu")
+    states, actions, old_lp, ret = _data()
+    single.update(states, actions, old_lp, ret)
+    for k, v in single.policy.named_parameters():
+        assert torch.equal(w0[k], w1[k]), k  # ranks stay in lockstep
+        torch.testing.assert_close(w0[k], v.detach(), rtol=1e-5, atol=1e-6)
+
+
+def test_rank_env_seeds_are_disjoint():
+    tr = importlib.import_module("marl-scheduling_amd.trainer")
+    E = 16384
+    bases = [tr.env_seed(0, r, E) for r in range(8)]
+    spans = [(b, b + E) for b in bases]
+    for i in range(8):
+        for j in range(i + 1, 8):
+            assert spans[i][1] <= spans[j][0] or spans[j][1] <= spans[i][0]
+
+
+def _trainer_rank(rank, world, port, out_dir):
+    import torch.distributed as dist
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    tr = importlib.import_module("marl-scheduling_amd.trainer")
+    t = tr.Trainer.from_named("cfg3", n_envs=32, update_step=12, seed=3, rank=rank, world_size=world,
+                              use_graph=False)
+    t.iteration()
+    t.iteration()
+    out = {}
+    for u in t.units():
+        for k, v in u.group.policy.named_parameters():
+            out[u.name + "." + k] = v.detach().cpu().clone()
+    out["flags"] = torch.tensor(t.flags())
+    torch.save(out, os.path.join(out_dir, "trainer%d.pt" % rank))
+    dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_two_rank_trainer_stays_in_lockstep(tmp_path):
+    """Two ranks on one device (gloo carries the all-reduce): different replicas, identical nets."""
+    mp.spawn(_trainer_rank, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True)
+    w0 = torch.load(tmp_path / "trainer0.pt", weights_only=True)
+    w1 = torch.load(tmp_path / "trainer1.pt", weights_only=True)
+    assert int(w0.pop("flags")) == 0 and int(w1.pop("flags")) == 0
+    for k in w0:
+        assert torch.equal(w0[k], w1[k]), k
