@@ -17,7 +17,7 @@
  *   ms_env_randbelow <- random.randint/_randbelow on the env's global stream
  *                      (Agent.py:718,725; SchedulingEnvironment.py:317-326)
  *   ms_policy_act   <- PPO.selectAction / ActorCritic.act  PPOmodules.py:53-63,114-125
- *   ms_discounted_returns <- PPO.update return estimate    PPOmodules.py:128-137
+ *   ms_discounted_returns, ms_unit_returns <- PPO.update return estimate  PPOmodules.py:128-137
  *
  * Conventions: plain pointers and sizes; every device pointer is a HIP device
  * allocation owned by the caller unless stated; all work is enqueued on the
@@ -261,6 +261,12 @@ int ms_offer_act_free(const ms_mlp_params* core_chooser, const ms_mlp_params* pr
 int ms_discounted_returns(const float* rewards, int32_t T, int64_t M, int64_t row_stride,
                           double gamma, float* out, void* stream);
 
+/* The same returns for the sub-unit each group trains on, read straight from the rollout
+ * reward buffer: rewards [T][E][U] (f32, or int32 with rewards_i32 = 1), sequence (e, g) is
+ * unit unit_of_group[g] of replica e; out [T][E][G] f32 (the ms_ppo_batch.returns layout). */
+int ms_unit_returns(const void* rewards, int32_t rewards_i32, int32_t T, int64_t E, int32_t U,
+                    const int32_t* unit_of_group, int32_t G, double gamma, float* out, void* stream);
+
 /* ---- fused PPO loss gradient (one K-epoch step of PPO.update, PPOmodules.py:144-168) ----
  * For every group g: d/dθ_g of
  *   mean_r[-min(ratio*adv, clamp(ratio, 1-eps, 1+eps)*adv)] + 0.5*mean_r[(V-G)^2] - 0.01*mean_r[entropy]
@@ -271,7 +277,7 @@ typedef struct ms_ppo_batch {
     const int8_t* states;          /* [R][U][stride] observation rows */
     const int8_t* actions;         /* [R][U] */
     const float* old_logprobs;     /* [R][U] */
-    const float* returns;          /* [E][G][T] normalised (ms_discounted_returns output) */
+    const float* returns;          /* [T][E][G] normalised (ms_unit_returns output) */
     const int32_t* unit_of_group;  /* [G] device array */
     int32_t stride, T, U;
     int64_t E;

@@ -25,17 +25,19 @@ hipError_t launch_offer_act_free(const ms_mlp_params*, const ms_mlp_params*, con
                                  uint64_t, uint64_t, const uint64_t*, const float*, int8_t*, float*, int8_t*, int8_t*,
                                  float*, int8_t*, hipStream_t);
 hipError_t launch_returns(const float*, int, int64_t, int64_t, double, float*, hipStream_t);
+hipError_t launch_unit_returns(const void*, int, int, int64_t, int, const int32_t*, int, double, float*, hipStream_t);
 hipError_t launch_ppo_grad(const PpoArgs&, const GradOut&, hipStream_t);
 int ppo_param_count(int D, int A);
 }  // namespace ms
 
-// work split of k_ppo_grad: ~4096 one-wave blocks over all groups, >= 8 tiles of 16 rows each
+// work split of k_ppo_grad: ~8192 wave chunks over all groups (4 per block), >= 8 tiles of 16 rows each
 static void ppo_split(int64_t rows, int G, int* chunk_tiles, int* n_chunks) {
     int64_t tiles = (rows + 15) / 16;
-    int64_t ct = (tiles * G + 4095) / 4096;
+    int64_t ct = (tiles * G + 8191) / 8192;
     if (ct < 8) ct = 8;
     *chunk_tiles = (int)ct;
-    *n_chunks = (int)((tiles + ct - 1) / ct);
+    int64_t nc = (tiles + ct - 1) / ct;
+    *n_chunks = (int)((nc + 3) / 4 * 4);
 }
 
 struct ms_env {
@@ -463,7 +465,7 @@ size_t ms_ppo_workspace_bytes(const ms_mlp_params* a, int64_t rows) {
     if (!a || rows < 1 || a->n_groups < 1) return 0;
     int ct, nc;
     ppo_split(rows, a->n_groups, &ct, &nc);
-    return (size_t)a->n_groups * nc * ms::ppo_param_count(a->in_dim, a->n_actions) * sizeof(float);
+    return (size_t)a->n_groups * (nc / 4) * ms::ppo_param_count(a->in_dim, a->n_actions) * sizeof(float);  // per block
 }
 
 int ms_ppo_grad(const ms_mlp_params* a, const ms_mlp_params* c, const ms_ppo_batch* b, float eps_clip, void* ws,
@@ -503,6 +505,15 @@ int ms_ppo_grad(const ms_mlp_params* a, const ms_mlp_params* c, const ms_ppo_bat
     p.inv_R = 1.0f / (float)R;
     ms::GradOut go{g->w1, g->b1, g->w2, g->b2, g->w3, g->b3, g->cw1, g->cb1, g->cw2, g->cb2, g->cw3, g->cb3, g->loss};
     HIP_TRY(ms::launch_ppo_grad(p, go, (hipStream_t)stream));
+    return MS_OK;
+}
+
+int ms_unit_returns(const void* rewards, int32_t rewards_i32, int32_t T, int64_t E, int32_t U,
+                    const int32_t* unit_of_group, int32_t G, double gamma, float* out, void* stream) {
+    if (!rewards || !unit_of_group || !out) return fail(MS_EINVAL, "NULL argument");
+    if (T < 1 || E < 0 || U < 1 || G < 1) return fail(MS_EINVAL, "bad shape");
+    HIP_TRY(ms::launch_unit_returns(rewards, rewards_i32 ? 1 : 0, T, E, U, unit_of_group, G, gamma, out,
+                                    (hipStream_t)stream));
     return MS_OK;
 }
 

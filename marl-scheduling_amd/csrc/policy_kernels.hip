@@ -2,12 +2,15 @@
 //
 // k_act: ActorCritic.act (PPOmodules.py:53-63) for every unit of every env
 // replica. A wave takes 16 observation rows at a time and runs
-// Linear(D,16)-tanh-Linear(16,16)-tanh-Linear(16,A) on the f32 MFMA
-// (v_mfma_f32_16x16x4_f32) with the batch on the lane axis, so each layer's
-// accumulator is the next layer's B operand unchanged (the weights are read
-// with a permuted k order). Softmax, the Categorical renormalisation and the
-// inverse-CDF sample run on the accumulator layout: a row's logits live in 4
-// lanes x 4 registers per 16 actions, reduced with two xor-shuffles.
+// Linear(D,16)-tanh-Linear(16,16)-tanh-Linear(16,A) with the batch on the MFMA
+// column (lane) axis, so each layer's accumulator is the next layer's B operand
+// unchanged. Layer 1 is three v_mfma_f32_16x16x32_bf16 per 32 inputs: the int8
+// observations are exact in bf16 and the f32 weights are split into three bf16
+// terms that sum to them exactly (error of the f32 accumulation only); layers
+// 2-3 run on v_mfma_f32_16x16x4_f32 with the weights read in a permuted k order.
+// All weights live in registers; the kernel uses no LDS. Softmax, the
+// Categorical renormalisation and the inverse-CDF sample run on the accumulator
+// layout: a row's logits live in 4 lanes x 4 registers per 16 actions.
 // With a second (price) net the kernel is FreePriceOfferPPO.selectAction
 // (PPOmodules.py:312-332): core chooser, then the price chooser on
 // [obs[2a:2a+2], obs[-2:]] (or the dummy [-5,-5,-5,-5] for a = 0), in one launch.
@@ -58,143 +61,194 @@ __device__ __forceinline__ float xsum4g(float v) {
     return v;
 }
 
-// One net's weights staged in LDS: W1 [16][D4] (zero padded), W2 [16][16], W3 [16*NT][16] (zero rows >= A), biases.
-struct NetLds {
-    float *w1, *w2, *w3, *b1, *b2, *b3;
-    int D, D4, A;
-};
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef uint32_t u4v __attribute__((ext_vector_type(4)));
 
-template <int NT>
-__device__ float* stage_net(float* s, const ms_mlp_params& p, int g, int tid, int nthreads, NetLds& n) {
-    n.D = p.in_dim;
-    n.D4 = (p.in_dim + 3) & ~3;
-    n.A = p.n_actions;
-    n.w1 = s;
-    n.w2 = n.w1 + 16 * n.D4;
-    n.w3 = n.w2 + 256;
-    n.b1 = n.w3 + 256 * NT;
-    n.b2 = n.b1 + 16;
-    n.b3 = n.b2 + 16;
-    const int D = n.D, D4 = n.D4, A = n.A;
-    for (int i = tid; i < 16 * D4; i += nthreads) {
-        int r = i / D4, c = i % D4;
-        n.w1[i] = c < D ? p.w1[((size_t)g * 16 + r) * D + c] : 0.f;
-    }
-    for (int i = tid; i < 256; i += nthreads) n.w2[i] = p.w2[(size_t)g * 256 + i];
-    for (int i = tid; i < 256 * NT; i += nthreads) {
-        int a = i / 16;
-        n.w3[i] = a < A ? p.w3[((size_t)g * A + a) * 16 + (i % 16)] : 0.f;
-    }
-    for (int i = tid; i < 16; i += nthreads) {
-        n.b1[i] = p.b1[g * 16 + i];
-        n.b2[i] = p.b2[g * 16 + i];
-    }
-    for (int i = tid; i < 16 * NT; i += nthreads) n.b3[i] = i < A ? p.b3[(size_t)g * A + i] : 0.f;
-    return n.b3 + 16 * NT;
+__device__ __forceinline__ f4 mfma_bf16(const u4v& a, const u4v& b, f4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), c, 0, 0,
+                                                   0);
 }
 
-// Layers 2-3, softmax, Categorical renormalisation and inverse-CDF sample for the
-// 16 rows of a tile given layer-1 pre-activations. Returns the action of row
-// (lane & 15) in every lane of that row and its log-probability.
-template <int NT>
-__device__ __forceinline__ void head(const NetLds& n, f4 a1, int j, int g4, float u, int& action, float& logprob) {
-    float h1[4];
+// tanh(x) = sign(x) (1 - t) / (1 + t), t = exp(-2|x|): absolute error ~1e-7 everywhere.
+__device__ __forceinline__ float fast_tanh(float x) {
+    const float t = __builtin_amdgcn_exp2f(-2.8853900817779268f * fabsf(x));
+    const float r = (1.f - t) * __builtin_amdgcn_rcpf(1.f + t);
+    return copysignf(r, x);
+}
+__device__ __forceinline__ float fast_exp(float x) { return __builtin_amdgcn_exp2f(x * 1.4426950408889634f); }
+__device__ __forceinline__ float fast_log(float x) { return __builtin_amdgcn_logf(x) * 0.69314718055994531f; }
+
+// bf16 (upper half of the f32 bits) of elements 2i, 2i+1 packed into one dword
+__device__ __forceinline__ uint32_t pack_hi(float lo, float hi) {
+    return (__float_as_uint(lo) >> 16) | (__float_as_uint(hi) & 0xffff0000u);
+}
+__device__ __forceinline__ float trunc_bf16(float x) { return __uint_as_float(__float_as_uint(x) & 0xffff0000u); }
+
+// Layer-1 weights as three bf16 terms, w = hi + mid + lo exactly (truncation leaves exact residuals),
+// in the A-operand layout of v_mfma_f32_16x16x32_bf16 for k-step s: lane (i, g) holds
+// W1[i][32s + 8g + 0..7].
+template <int S1>
+struct W1Split {
+    u4v hi[S1], mid[S1], lo[S1];
+    __device__ void load(const float* w1 /* [16][D] of this group */, int D, int i, int g) {
 #pragma unroll
-    for (int q = 0; q < 4; q++) h1[q] = tanhf(a1[q] + n.b1[4 * g4 + q]);
-    f4 a2 = {0, 0, 0, 0};
+        for (int s = 0; s < S1; s++) {
+            float h[8], m[8], l[8];
 #pragma unroll
-    for (int s = 0; s < 4; s++) a2 = mfma4(n.w2[j * 16 + 4 * g4 + s], h1[s], a2);
-    float h2[4];
+            for (int e = 0; e < 8; e++) {
+                const int k = 32 * s + 8 * g + e;
+                const float w = k < D ? w1[i * D + k] : 0.f;
+                h[e] = trunc_bf16(w);
+                const float r1 = w - h[e];
+                m[e] = trunc_bf16(r1);
+                l[e] = r1 - m[e];  // <= 8 significant bits: exact in bf16
+            }
 #pragma unroll
-    for (int q = 0; q < 4; q++) h2[q] = tanhf(a2[q] + n.b2[4 * g4 + q]);
-    float z[NT][4];
-    float m = -INFINITY;
-#pragma unroll
-    for (int t = 0; t < NT; t++) {
-        f4 zz = {0, 0, 0, 0};
-#pragma unroll
-        for (int s = 0; s < 4; s++) zz = mfma4(n.w3[(16 * t + j) * 16 + 4 * g4 + s], h2[s], zz);
-#pragma unroll
-        for (int q = 0; q < 4; q++) {
-            z[t][q] = zz[q] + n.b3[16 * t + 4 * g4 + q];
-            if (16 * t + 4 * g4 + q < n.A) m = fmaxf(m, z[t][q]);
-        }
-    }
-    m = fmaxf(m, __shfl_xor(m, 16));
-    m = fmaxf(m, __shfl_xor(m, 32));
-    float s0 = 0.f;
-#pragma unroll
-    for (int t = 0; t < NT; t++)
-#pragma unroll
-        for (int q = 0; q < 4; q++) {
-            z[t][q] = (16 * t + 4 * g4 + q < n.A) ? expf(z[t][q] - m) : 0.f;
-            s0 += z[t][q];
-        }
-    const float inv0 = 1.f / xsum4g(s0);
-    float s1 = 0.f;
-#pragma unroll
-    for (int t = 0; t < NT; t++)
-#pragma unroll
-        for (int q = 0; q < 4; q++) {
-            z[t][q] *= inv0;  // nn.Softmax output
-            s1 += z[t][q];
-        }
-    const float inv1 = 1.f / xsum4g(s1);
-    // Categorical renormalisation, then the inverse CDF over a = 16t + 4*g4 + q in increasing order
-    float cum = 0.f, pc = 0.f;
-    int found = 0x7fff, last_nz = -1;
-#pragma unroll
-    for (int t = 0; t < NT; t++) {
-        float bs = 0.f;
-#pragma unroll
-        for (int q = 0; q < 4; q++) {
-            z[t][q] *= inv1;
-            bs += z[t][q];
-        }
-        const float gs0 = __shfl(bs, j), gs1 = __shfl(bs, j + 16), gs2 = __shfl(bs, j + 32), gs3 = __shfl(bs, j + 48);
-        float c = cum + (g4 > 0 ? gs0 : 0.f) + (g4 > 1 ? gs1 : 0.f) + (g4 > 2 ? gs2 : 0.f);
-#pragma unroll
-        for (int q = 0; q < 4; q++) {
-            const int a = 16 * t + 4 * g4 + q;
-            c += z[t][q];
-            if (a < n.A) {
-                if (z[t][q] > 0.f) last_nz = a;
-                if (u < c && a < found) {
-                    found = a;
-                    pc = z[t][q];
-                }
+            for (int d = 0; d < 4; d++) {
+                hi[s][d] = pack_hi(h[2 * d], h[2 * d + 1]);
+                mid[s][d] = pack_hi(m[2 * d], m[2 * d + 1]);
+                lo[s][d] = pack_hi(l[2 * d], l[2 * d + 1]);
             }
         }
-        cum += gs0 + gs1 + gs2 + gs3;
     }
-    // first crossing over the 4 lanes of the row (each lane found its own first one)
-    int fmin = min(found, __shfl_xor(found, 16));
-    fmin = min(fmin, __shfl_xor(fmin, 32));
-    int lmax = max(last_nz, __shfl_xor(last_nz, 16));
-    lmax = max(lmax, __shfl_xor(lmax, 32));
-    int a_sel = fmin < n.A ? fmin : lmax;
-    float mine = 0.f;
-    if (fmin < n.A) {
-        mine = (found == fmin) ? pc : 0.f;
-    } else {
+};
+
+// int8 observation bytes (two dwords = 8 consecutive inputs) as a bf16 B fragment (exact)
+__device__ __forceinline__ u4v bytes_to_bf16(uint32_t d0, uint32_t d1) {
+    u4v r;
+#pragma unroll
+    for (int d = 0; d < 4; d++) {
+        const uint32_t src = d < 2 ? d0 : d1;
+        const int sh = 16 * (d & 1);
+        const float a = (float)(int8_t)(src >> sh);
+        const float b = (float)(int8_t)(src >> (sh + 8));
+        r[d] = pack_hi(a, b);
+    }
+    return r;
+}
+
+// The 16-wide layers and the head of one net, in registers: lane (j, g4) holds W2[j][4*g4 + s],
+// W3[16t + j][4*g4 + s] (the permuted-k A operands) and the biases of its accumulator rows.
+template <int NT>
+struct Head {
+    float b1[4], w2[4], b2[4], w3[NT][4], b3[NT][4];
+    __device__ void load(const ms_mlp_params& p, int grp, int j, int g4) {
+        const int A = p.n_actions;
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            b1[q] = p.b1[grp * 16 + 4 * g4 + q];
+            w2[q] = p.w2[(size_t)grp * 256 + j * 16 + 4 * g4 + q];
+            b2[q] = p.b2[grp * 16 + 4 * g4 + q];
+#pragma unroll
+            for (int t = 0; t < NT; t++) {
+                const int a = 16 * t + j, ab = 16 * t + 4 * g4 + q;
+                w3[t][q] = a < A ? p.w3[((size_t)grp * A + a) * 16 + 4 * g4 + q] : 0.f;
+                b3[t][q] = ab < A ? p.b3[(size_t)grp * A + ab] : 0.f;
+            }
+        }
+    }
+
+    // Layers 2-3, softmax, Categorical renormalisation and the inverse-CDF sample for the 16 rows of
+    // a tile given layer-1 pre-activations. Every lane of row j returns the row's action and log-prob.
+    __device__ __forceinline__ void run(f4 a1, int A, int j, int g4, float u, int& action, float& logprob) const {
+        float h1[4];
+#pragma unroll
+        for (int q = 0; q < 4; q++) h1[q] = fast_tanh(a1[q] + b1[q]);
+        f4 a2 = {0, 0, 0, 0};
+#pragma unroll
+        for (int s = 0; s < 4; s++) a2 = mfma4(w2[s], h1[s], a2);
+        float h2[4];
+#pragma unroll
+        for (int q = 0; q < 4; q++) h2[q] = fast_tanh(a2[q] + b2[q]);
+        float z[NT][4];
+        float m = -INFINITY;
+#pragma unroll
+        for (int t = 0; t < NT; t++) {
+            f4 zz = {0, 0, 0, 0};
+#pragma unroll
+            for (int s = 0; s < 4; s++) zz = mfma4(w3[t][s], h2[s], zz);
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                z[t][q] = zz[q] + b3[t][q];
+                if (16 * t + 4 * g4 + q < A) m = fmaxf(m, z[t][q]);
+            }
+        }
+        m = fmaxf(m, __shfl_xor(m, 16));
+        m = fmaxf(m, __shfl_xor(m, 32));
+        float s0 = 0.f;
 #pragma unroll
         for (int t = 0; t < NT; t++)
 #pragma unroll
-            for (int q = 0; q < 4; q++)
-                if (16 * t + 4 * g4 + q == a_sel) mine = z[t][q];
+            for (int q = 0; q < 4; q++) {
+                z[t][q] = (16 * t + 4 * g4 + q < A) ? fast_exp(z[t][q] - m) : 0.f;
+                s0 += z[t][q];
+            }
+        const float inv0 = __builtin_amdgcn_rcpf(xsum4g(s0));
+        float s1 = 0.f;
+#pragma unroll
+        for (int t = 0; t < NT; t++)
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                z[t][q] *= inv0;  // nn.Softmax output
+                s1 += z[t][q];
+            }
+        const float inv1 = __builtin_amdgcn_rcpf(xsum4g(s1));
+        // Categorical renormalisation, then the inverse CDF over a = 16t + 4*g4 + q in increasing order
+        float cum = 0.f, pc = 0.f;
+        int found = 0x7fff, last_nz = -1;
+#pragma unroll
+        for (int t = 0; t < NT; t++) {
+            float bs = 0.f;
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                z[t][q] *= inv1;
+                bs += z[t][q];
+            }
+            const float gs0 = __shfl(bs, j), gs1 = __shfl(bs, j + 16), gs2 = __shfl(bs, j + 32), gs3 = __shfl(bs, j + 48);
+            float c = cum + (g4 > 0 ? gs0 : 0.f) + (g4 > 1 ? gs1 : 0.f) + (g4 > 2 ? gs2 : 0.f);
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                const int a = 16 * t + 4 * g4 + q;
+                c += z[t][q];
+                if (a < A) {
+                    if (z[t][q] > 0.f) last_nz = a;
+                    if (u < c && a < found) {
+                        found = a;
+                        pc = z[t][q];
+                    }
+                }
+            }
+            cum += gs0 + gs1 + gs2 + gs3;
+        }
+        // first crossing over the 4 lanes of the row (each lane found its own first one)
+        int fmin = min(found, __shfl_xor(found, 16));
+        fmin = min(fmin, __shfl_xor(fmin, 32));
+        int lmax = max(last_nz, __shfl_xor(last_nz, 16));
+        lmax = max(lmax, __shfl_xor(lmax, 32));
+        const int a_sel = fmin < A ? fmin : lmax;
+        float mine = 0.f;
+        if (fmin < A) {
+            mine = (found == fmin) ? pc : 0.f;
+        } else {
+#pragma unroll
+            for (int t = 0; t < NT; t++)
+#pragma unroll
+                for (int q = 0; q < 4; q++)
+                    if (16 * t + 4 * g4 + q == a_sel) mine = z[t][q];
+        }
+        const float pa = xsum4g(mine);
+        const float eps = 1.1920928955078125e-07f;  // torch.finfo(float32).eps
+        action = a_sel;
+        logprob = fast_log(fminf(fmaxf(pa, eps), 1.f - eps));
     }
-    const float pa = xsum4g(mine);
-    const float eps = 1.1920928955078125e-07f;  // torch.finfo(float32).eps
-    action = a_sel;
-    logprob = logf(fminf(fmaxf(pa, eps), 1.f - eps));
-}
+};
 
 struct ActArgs {
     ms_mlp_params n1, n2;  // n2 used only with a price net (NT2 > 0)
     const int8_t* obs;
     int stride, U, S, n_cores;
     int E, n_items;
-    int tiles_per_wave, blocks_per_group;
+    int tiles_per_wave, waves_per_group;
     uint64_t seed, offset;
     const uint64_t* offset_dev;
     const float* uniforms;  // [2][E*U] or NULL
@@ -206,58 +260,63 @@ struct ActArgs {
     int8_t* env_price;
 };
 
-constexpr int kPreW = 16;  // prefetch dwords per lane: 16 rows x 256 B / 64 lanes
-
-template <int NT, int NT2>
+// One wave = a contiguous range of 16-row tiles of one group; no LDS. Layer 1 runs on the bf16 MFMA
+// with the weights split in three bf16 terms (exact f32 weights; the int8 inputs are exact in bf16):
+// lane (j, g) loads dwords 8s + 2g, 8s + 2g + 1 of tile row j, which are exactly its B fragment of
+// k-step s. S1 = ceil(stride / 32) k-steps.
+template <int S1, int NT, int NT2>
 __global__ void __launch_bounds__(256) k_act(ActArgs a) {
-    extern __shared__ __align__(16) float sm[];
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int gw = blockIdx.x * 4 + (tid >> 6);  // global wave index
+    const int grp = gw / a.waves_per_group;
+    const int wv = gw - grp * a.waves_per_group;
+    if (grp >= a.n1.n_groups) return;
     const int j = lane & 15, g4 = lane >> 4;
-    const int grp = blockIdx.x / a.blocks_per_group;
-    const int blk = blockIdx.x % a.blocks_per_group;
-    NetLds n1, n2;
-    float* s = stage_net<NT>(sm, a.n1, grp, tid, 256, n1);
-    if (NT2 > 0) s = stage_net<(NT2 > 0 ? NT2 : 1)>(s, a.n2, grp, tid, 256, n2);
-    int8_t* sx = reinterpret_cast<int8_t*>(s) + wave * 16 * a.stride;  // this wave's observation tile
-    __syncthreads();
+    W1Split<S1> w1;
+    w1.load(a.n1.w1 + (size_t)grp * 16 * a.n1.in_dim, a.n1.in_dim, j, g4);
+    Head<NT> h1;
+    h1.load(a.n1, grp, j, g4);
+    constexpr int NP = NT2 > 0 ? NT2 : 1;
+    Head<NP> h2;
+    float pw1 = 0.f;  // price chooser layer 1 (K = 4 inputs): lane (j, g4) holds W1p[j][g4]
+    if (NT2 > 0) {
+        h2.load(a.n2, grp, j, g4);
+        pw1 = a.n2.w1[((size_t)grp * 16 + j) * 4 + g4];
+    }
     const uint64_t off = a.offset + (a.offset_dev ? *a.offset_dev : 0ull);
     const int stride4 = a.stride >> 2;
     const int n_rows_total = a.E * a.U;
-    const int S1 = n1.D4 / 4;
-    // this wave's tiles: [t0, t1)
     const int tiles = (a.n_items + 15) >> 4;
-    const int t0 = (blk * 4 + wave) * a.tiles_per_wave;
+    const int t0 = wv * a.tiles_per_wave;
     const int t1 = min(t0 + a.tiles_per_wave, tiles);
-    // lane j copies dwords j-row, columns g4 + 4m; the same lane owns row j's outputs
     auto row_of = [&](int tile) -> int {
-        int i = tile * 16 + j;
+        const int i = tile * 16 + j;
         if (i >= a.n_items) return -1;
-        int e = i / a.S;
+        const int e = i / a.S;
         return e * a.U + grp * a.S + (i - e * a.S);
     };
-    uint32_t pre[kPreW];
-    int row = t0 < t1 ? row_of(t0) : -1;
+    uint32_t pre[S1][2];
     auto prefetch = [&](int r) {
         const uint32_t* src = reinterpret_cast<const uint32_t*>(a.obs + (size_t)(r < 0 ? 0 : r) * a.stride);
 #pragma unroll
-        for (int m = 0; m < kPreW; m++) {
-            int cc = g4 + 4 * m;
-            pre[m] = (r >= 0 && cc < stride4) ? src[cc] : 0u;
-        }
+        for (int s = 0; s < S1; s++)
+#pragma unroll
+            for (int h = 0; h < 2; h++) {
+                const int cc = 8 * s + 2 * g4 + h;
+                pre[s][h] = (r >= 0 && cc < stride4) ? src[cc] : 0u;
+            }
     };
+    int row = t0 < t1 ? row_of(t0) : -1;
     if (t0 < t1) prefetch(row);
     for (int tile = t0; tile < t1; tile++) {
+        uint32_t xd[S1][2];
 #pragma unroll
-        for (int m = 0; m < kPreW; m++) {
-            int cc = g4 + 4 * m;
-            if (cc < stride4) reinterpret_cast<uint32_t*>(sx)[j * stride4 + cc] = pre[m];
-        }
+        for (int s = 0; s < S1; s++) xd[s][0] = pre[s][0], xd[s][1] = pre[s][1];
         const int cur = row;
         if (tile + 1 < t1) {
             row = row_of(tile + 1);
             prefetch(row);
         }
-        __builtin_amdgcn_wave_barrier();
         const bool valid = cur >= 0;
         float u1, u2;
         if (a.uniforms) {
@@ -271,22 +330,35 @@ __global__ void __launch_bounds__(256) k_act(ActArgs a) {
             u2 = u24(r1);
         }
         f4 acc = {0, 0, 0, 0};
-        for (int k = 0; k < S1; k++) acc = mfma4(n1.w1[j * n1.D4 + 4 * k + g4], (float)sx[j * a.stride + 4 * k + g4], acc);
+#pragma unroll
+        for (int s = 0; s < S1; s++) {
+            const u4v x = bytes_to_bf16(xd[s][0], xd[s][1]);
+            acc = mfma_bf16(w1.hi[s], x, acc);
+            acc = mfma_bf16(w1.mid[s], x, acc);
+            acc = mfma_bf16(w1.lo[s], x, acc);
+        }
         int act;
         float lp;
-        head<NT>(n1, acc, j, g4, u1, act, lp);
+        h1.run(acc, a.n1.n_actions, j, g4, u1, act, lp);
         if (NT2 > 0) {
-            // price chooser input (PPOmodules.py:316-327)
-            int8_t pin;
-            if (act == 0)
-                pin = -5;
-            else
-                pin = (g4 < 2) ? sx[j * a.stride + 2 * act + g4] : sx[j * a.stride + 2 * a.n_cores + (g4 - 2)];
+            // price chooser input (PPOmodules.py:316-327): lane g4 takes row byte k of
+            // [obs[2a], obs[2a+1], obs[-2], obs[-1]] (obs[-2:] = the slot's pair at 2C), or -5 for a = 0
+            const int k = g4 < 2 ? 2 * act + g4 : 2 * a.n_cores + (g4 - 2);
+            const int src = j + 16 * ((k >> 3) & 3), ks = k >> 5, kh = (k >> 2) & 1;
+            uint32_t dw = 0;
+#pragma unroll
+            for (int s = 0; s < S1; s++)
+#pragma unroll
+                for (int h = 0; h < 2; h++) {
+                    const uint32_t v = (uint32_t)__shfl((int)xd[s][h], src);
+                    if (s == ks && h == kh) dw = v;
+                }
+            const int8_t pin = act == 0 ? (int8_t)-5 : (int8_t)(dw >> (8 * (k & 3)));
             f4 acc2 = {0, 0, 0, 0};
-            acc2 = mfma4(n2.w1[j * n2.D4 + g4], (float)pin, acc2);
+            acc2 = mfma4(pw1, (float)pin, acc2);
             int pact;
             float plp;
-            head<(NT2 > 0 ? NT2 : 1)>(n2, acc2, j, g4, u2, pact, plp);
+            h2.run(acc2, a.n2.n_actions, j, g4, u2, pact, plp);
             if (valid) {
                 a.price_state[(size_t)cur * 4 + g4] = pin;
                 if (g4 == 0) {
@@ -300,31 +372,28 @@ __global__ void __launch_bounds__(256) k_act(ActArgs a) {
             a.action[cur] = (int8_t)act;
             a.logprob[cur] = lp;
         }
-        __builtin_amdgcn_wave_barrier();
     }
 }
 
-static size_t net_lds_floats(int D, int NT) { return 16 * (size_t)((D + 3) & ~3) + 256 + 256 * NT + 32 + 16 * NT; }
-
-template <int NT, int NT2>
+template <int S1, int NT, int NT2>
 static hipError_t launch_act_t(ActArgs& a, hipStream_t st) {
-    size_t lds = sizeof(float) * (net_lds_floats(a.n1.in_dim, NT) + (NT2 > 0 ? net_lds_floats(a.n2.in_dim, NT2) : 0)) +
-                 4 * 16 * (size_t)a.stride;
     const int G = a.n1.n_groups;
     const int tiles = (a.n_items + 15) / 16;
-    // ~2048 blocks of 4 waves over all groups; each wave walks a contiguous tile range with a prefetch
+    // ~8192 waves over all groups; each wave walks a contiguous tile range with a register prefetch
     int tpw = (int)(((long long)tiles * G + 8191) / 8192);
     a.tiles_per_wave = tpw < 1 ? 1 : tpw;
-    a.blocks_per_group = (tiles + 4 * a.tiles_per_wave - 1) / (4 * a.tiles_per_wave);
-    hipLaunchKernelGGL((k_act<NT, NT2>), dim3((unsigned)(a.blocks_per_group * G)), dim3(256), lds, st, a);
+    a.waves_per_group = (tiles + a.tiles_per_wave - 1) / a.tiles_per_wave;
+    const long long waves = (long long)a.waves_per_group * G;
+    hipLaunchKernelGGL((k_act<S1, NT, NT2>), dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, st, a);
     return hipGetLastError();
 }
 
-static hipError_t dispatch_act(ActArgs& a, hipStream_t st) {
+template <int S1>
+static hipError_t dispatch_act_s(ActArgs& a, hipStream_t st) {
     const int nt = (a.n1.n_actions + 15) / 16;
     const int nt2 = a.n2.n_groups > 0 ? (a.n2.n_actions + 15) / 16 : 0;
 #define MS_ACT(T, T2) \
-    if (nt <= T && nt2 == T2) return launch_act_t<T, T2>(a, st);
+    if (nt <= T && nt2 == T2) return launch_act_t<S1, T, T2>(a, st);
     if (nt2 == 0) {
         MS_ACT(1, 0) MS_ACT(2, 0) MS_ACT(4, 0) MS_ACT(8, 0)
     } else if (nt2 == 1) {
@@ -332,9 +401,19 @@ static hipError_t dispatch_act(ActArgs& a, hipStream_t st) {
     } else if (nt2 == 2) {
         MS_ACT(1, 2) MS_ACT(2, 2) MS_ACT(4, 2)
     } else if (nt2 <= 8) {
-        if (nt <= 4) return launch_act_t<4, 8>(a, st);
+        if (nt <= 4) return launch_act_t<S1, 4, 8>(a, st);
     }
 #undef MS_ACT
+    return hipErrorInvalidValue;
+}
+
+static hipError_t dispatch_act(ActArgs& a, hipStream_t st) {
+    const int s1 = (a.stride + 31) / 32;
+    if (a.n2.n_groups > 0 && a.n2.in_dim != 4) return hipErrorInvalidValue;
+    if (s1 <= 1) return dispatch_act_s<1>(a, st);
+    if (s1 <= 2) return dispatch_act_s<2>(a, st);
+    if (s1 <= 4) return dispatch_act_s<4>(a, st);
+    if (s1 <= 8) return dispatch_act_s<8>(a, st);
     return hipErrorInvalidValue;
 }
 
@@ -411,6 +490,51 @@ __global__ void __launch_bounds__(256) k_returns(const float* __restrict__ rewar
     const float sd = T > 1 ? (float)sqrt(v / (T - 1)) : NAN;  // rewards.std() (unbiased)
     const float den = sd + 1e-7f;
     for (int t = 0; t < T; t++) o[t] = (o[t] - mean) / den;
+}
+
+// Returns of sequence (e, g) = unit unit_of_group[g] of replica e, gathered from the rollout
+// rewards [T][E][U] and written time-major [T][E][G] (coalesced: g is the fastest thread index).
+// Same arithmetic as k_returns: float64 scan, f32 values, mean and unbiased std over T.
+__global__ void __launch_bounds__(256) k_unit_returns(const void* __restrict__ rewards, int is_i32, int T, int64_t E,
+                                                      int U, const int32_t* __restrict__ unit_of_group, int G,
+                                                      double gamma, float* __restrict__ out) {
+    const int64_t m = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (m >= E * G) return;
+    const int64_t e = m / G;
+    const int g = (int)(m - e * G);
+    const int u = unit_of_group[g];
+    const int64_t EG = E * G;
+    double Gs = 0.0, s = 0.0;
+    for (int t = T - 1; t >= 0; t--) {
+        const int64_t idx = ((int64_t)t * E + e) * U + u;
+        const double r = is_i32 ? (double)static_cast<const int32_t*>(rewards)[idx]
+                                : (double)static_cast<const float*>(rewards)[idx];
+        Gs = r + gamma * Gs;
+        const float f = (float)Gs;
+        out[(int64_t)t * EG + m] = f;
+        s += (double)f;
+    }
+    const float mean = (float)(s / T);
+    double v = 0.0;
+    for (int t = 0; t < T; t++) {
+        const double d = (double)out[(int64_t)t * EG + m] - (double)mean;
+        v += d * d;
+    }
+    const float sd = T > 1 ? (float)sqrt(v / (T - 1)) : NAN;
+    const float den = sd + 1e-7f;
+    for (int t = 0; t < T; t++) {
+        float* o = out + (int64_t)t * EG + m;
+        *o = (*o - mean) / den;
+    }
+}
+
+hipError_t launch_unit_returns(const void* rewards, int is_i32, int T, int64_t E, int U, const int32_t* unit_of_group,
+                               int G, double gamma, float* out, hipStream_t st) {
+    const int64_t M = E * G;
+    if (M <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_unit_returns, dim3((unsigned)((M + 255) / 256)), dim3(256), 0, st, rewards, is_i32, T, E, U,
+                       unit_of_group, G, gamma, out);
+    return hipGetLastError();
 }
 
 hipError_t launch_returns(const float* rewards, int T, int64_t M, int64_t row_stride, double gamma, float* out,

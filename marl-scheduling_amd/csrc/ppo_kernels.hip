@@ -4,17 +4,25 @@
 // d/dθ of  mean_r[ -min(ratio*adv, clamp(ratio)*adv) ] + 0.5*mean_r[(V-G)^2] - 0.01*mean_r[H]
 // over R = T*E rows (torch Categorical semantics: probs renormalised,
 // logits = log(clamp(p, eps, 1-eps)), entropy -sum(logits*p)). k_ppo_grad
-// computes it in one pass over the int8 rollout buffer: for each 16-row tile a
-// wave runs the actor and critic forward, the per-row loss derivatives and the
-// backward pass on the f32 MFMA (v_mfma_f32_16x16x4_f32: an exact k-ordered
-// fmaf chain), keeping the batch on the MFMA's column (lane) axis so that every
-// layer's output feeds the next layer's B operand with no data movement (the
-// A-operand weights are read with a permuted k order instead). The weight
-// gradients are batch reductions, i.e. MFMAs with K = rows: their operands are
-// the activations transposed through a small LDS tile, their accumulators stay
-// in registers for the whole chunk. Each block writes one partial gradient
-// vector; k_ppo_reduce sums the partials in a fixed order (deterministic) into
-// the torch .grad tensors.
+// computes it in one pass over the int8 rollout buffer.
+//
+// Work split: a block is 4 waves of one group sharing the group's weights in
+// LDS; each wave walks a contiguous range of 16-row tiles and accumulates its
+// own partial gradient. Per tile:
+//  * forward on v_mfma_f32_16x16x4_f32 with the batch on the MFMA column (lane)
+//    axis, so every layer's accumulator is the next layer's B operand. Layer 1
+//    takes its B operand straight from the prefetched observation dwords
+//    (k order permuted to match: step (m, b) = byte b of dword g4+4m); the
+//    weights are read with the same permutation (ds_read_b128);
+//  * softmax / renormalisation / clamped log / entropy, the per-row loss
+//    derivatives (torch.minimum splits ties, clamp backward is inclusive) and
+//    the backward pass through the tanh layers, on the accumulator layout;
+//  * weight gradients as MFMAs with K = rows. Their operands go through small
+//    LDS transposes whose pitch (20 floats) and row order make both the writes
+//    and the ds_read_b128 reads bank-conflict free. Layer 1's input tile is
+//    staged with byte D set to 1, so column D of dW1 is the bias gradient.
+// Each wave writes one partial gradient vector; k_ppo_reduce sums them in a
+// fixed order (deterministic) into the torch .grad tensors.
 #include <hip/hip_runtime.h>
 #include <math.h>
 
@@ -45,63 +53,83 @@ __device__ __forceinline__ float xmax4g(float v) {
     return v;
 }
 
-// NQ = ceil(D/16) input tiles, NT = ceil(A/16) action tiles. One wave per block.
+// tanh(x) = sign(x) (1 - t) / (1 + t), t = exp(-2|x|): absolute error ~1e-7 everywhere
+// (the relative error near 0 does not matter downstream: h feeds sums of O(1) terms).
+__device__ __forceinline__ float fast_tanh(float x) {
+    const float t = __builtin_amdgcn_exp2f(-2.8853900817779268f * fabsf(x));  // exp2(-2|x| log2 e)
+    const float r = (1.f - t) * __builtin_amdgcn_rcpf(1.f + t);
+    return copysignf(r, x);
+}
+__device__ __forceinline__ float fast_exp(float x) { return __builtin_amdgcn_exp2f(x * 1.4426950408889634f); }
+__device__ __forceinline__ float fast_log(float x) { return __builtin_amdgcn_logf(x) * 0.69314718055994531f; }
+
 template <int NQ, int NT>
-__global__ void __launch_bounds__(64) k_ppo_grad(PpoArgs p) {
-    constexpr int TP = 17;  // transpose tile pitch (floats)
-    constexpr int NTR = 7 + NT;
-    const int lane = threadIdx.x;
+struct GradLds {
+    static constexpr int D16 = 16 * NQ;     // layer-1 inputs padded to the dW1 tiles
+    static constexpr int W1P = D16 + 4;     // W1 row pitch (conflict-free ds_read_b128)
+    static constexpr int XP = 16 * NQ;      // staged input row pitch (bytes)
+    static constexpr int TP = 20;           // transpose pitch (floats)
+    static constexpr int NTR = 7 + NT;      // transposed arrays per tile
+    static constexpr int shared_floats = 2 * 16 * W1P + 2 * 256 + 256 * NT + 16 * 5 + 16 * NT + 4;
+    static constexpr int wave_floats = NTR * 16 * TP + 16 * XP / 4;
+};
+
+// NQ = 16-wide input tiles with 16*NQ > D, NT = ceil(A/16) action tiles. 4 waves per block.
+template <int NQ, int NT>
+__global__ void __launch_bounds__(256, (NQ * NT >= 32) ? 1 : 2) k_ppo_grad(PpoArgs p) {
+    using L = GradLds<NQ, NT>;
+    constexpr int TP = L::TP, W1P = L::W1P, XP = L::XP;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int g4 = lane >> 4;  // MFMA k-group / C-row group
     const int j = lane & 15;   // batch row within the tile (C column)
-    const int grp = blockIdx.x / p.n_chunks;
-    const int chunk = blockIdx.x % p.n_chunks;
+    const int blocks_per_group = p.n_chunks >> 2;
+    const int grp = blockIdx.x / blocks_per_group;
+    const int chunk = (blockIdx.x - grp * blocks_per_group) * 4 + wave;
     const int D = p.D, A = p.A;
-    const int D4 = (D + 3) & ~3;
-    const int S1 = D4 / 4;
     const int u = p.unit_of_group[grp];
 
     extern __shared__ __align__(16) float sm[];
-    float* sW1 = sm;                   // [16][D4]
-    float* sC1 = sW1 + 16 * D4;        // [16][D4]
-    float* sW2 = sC1 + 16 * D4;        // [16][16]
-    float* sC2 = sW2 + 256;            // [16][16]
-    float* sW3 = sC2 + 256;            // [16*NT][16] (zero rows >= A)
-    float* sb1 = sW3 + 256 * NT;       // 16
-    float* sb2 = sb1 + 16;             // 16
-    float* sb3 = sb2 + 16;             // 16*NT
-    float* sc3 = sb3 + 16 * NT;        // 16 (critic output row)
-    float* scb1 = sc3 + 16;            // 16
-    float* scb2 = scb1 + 16;           // 16
-    float* scb3 = scb2 + 16;           // 1 (+3 pad)
-    float* sT = scb3 + 4;              // [NTR][16][TP] transposes
-    int8_t* sX = reinterpret_cast<int8_t*>(sT + NTR * 16 * TP);  // [16][stride]
+    float* sW1 = sm;                    // [16][W1P] (zero beyond D)
+    float* sC1 = sW1 + 16 * W1P;        // [16][W1P]
+    float* sW2 = sC1 + 16 * W1P;        // [16][16]
+    float* sC2 = sW2 + 256;             // [16][16]
+    float* sW3 = sC2 + 256;             // [16*NT][16] (zero rows >= A)
+    float* sb1 = sW3 + 256 * NT;        // 16
+    float* sb2 = sb1 + 16;              // 16
+    float* sc3 = sb2 + 16;              // 16 (critic output row)
+    float* scb1 = sc3 + 16;             // 16
+    float* scb2 = scb1 + 16;            // 16
+    float* sb3 = scb2 + 16;             // 16*NT
+    float* scb3 = sb3 + 16 * NT;        // 1 (+3 pad)
+    float* sT = sm + L::shared_floats + wave * L::wave_floats;  // [NTR][16][TP]
+    uint32_t* sX = reinterpret_cast<uint32_t*>(sT + L::NTR * 16 * TP);  // [16][XP/4] dwords
 
-    // ---- stage this group's weights
+    // ---- stage this group's weights (once per block)
     {
         const float* W1 = p.w1 + (size_t)grp * 16 * D;
         const float* C1 = p.cw1 + (size_t)grp * 16 * D;
-        for (int i = lane; i < 16 * D4; i += 64) {
-            int r = i / D4, c = i % D4;
+        for (int i = tid; i < 16 * W1P; i += 256) {
+            const int r = i / W1P, c = i - r * W1P;
             sW1[i] = c < D ? W1[r * D + c] : 0.f;
             sC1[i] = c < D ? C1[r * D + c] : 0.f;
         }
-        for (int i = lane; i < 256; i += 64) {
+        for (int i = tid; i < 256; i += 256) {
             sW2[i] = p.w2[(size_t)grp * 256 + i];
             sC2[i] = p.cw2[(size_t)grp * 256 + i];
         }
-        for (int i = lane; i < 256 * NT; i += 64) {
-            int a = i / 16;
-            sW3[i] = a < A ? p.w3[((size_t)grp * A + a) * 16 + (i % 16)] : 0.f;
+        for (int i = tid; i < 256 * NT; i += 256) {
+            const int a = i >> 4;
+            sW3[i] = a < A ? p.w3[((size_t)grp * A + a) * 16 + (i & 15)] : 0.f;
         }
-        for (int i = lane; i < 16 * NT; i += 64) sb3[i] = i < A ? p.b3[(size_t)grp * A + i] : 0.f;
-        if (lane < 16) {
-            sb1[lane] = p.b1[grp * 16 + lane];
-            sb2[lane] = p.b2[grp * 16 + lane];
-            sc3[lane] = p.cw3[grp * 16 + lane];
-            scb1[lane] = p.cb1[grp * 16 + lane];
-            scb2[lane] = p.cb2[grp * 16 + lane];
+        for (int i = tid; i < 16 * NT; i += 256) sb3[i] = i < A ? p.b3[(size_t)grp * A + i] : 0.f;
+        if (tid < 16) {
+            sb1[tid] = p.b1[grp * 16 + tid];
+            sb2[tid] = p.b2[grp * 16 + tid];
+            sc3[tid] = p.cw3[grp * 16 + tid];
+            scb1[tid] = p.cb1[grp * 16 + tid];
+            scb2[tid] = p.cb2[grp * 16 + tid];
         }
-        if (lane == 0) scb3[0] = p.cb3[grp];
+        if (tid == 0) scb3[0] = p.cb3[grp];
     }
     __syncthreads();
 
@@ -111,22 +139,23 @@ __global__ void __launch_bounds__(64) k_ppo_grad(PpoArgs p) {
     for (int q = 0; q < NQ; q++) gW1[q] = gC1[q] = (f4){0, 0, 0, 0};
 #pragma unroll
     for (int t = 0; t < NT; t++) gW3[t] = (f4){0, 0, 0, 0};
-    float db1[4] = {0, 0, 0, 0}, db2[4] = {0, 0, 0, 0}, cdb1[4] = {0, 0, 0, 0}, cdb2[4] = {0, 0, 0, 0};
+    float db2[4] = {0, 0, 0, 0}, cdb2[4] = {0, 0, 0, 0}, gC3[4] = {0, 0, 0, 0};
     float db3[NT][4];
 #pragma unroll
     for (int t = 0; t < NT; t++) db3[t][0] = db3[t][1] = db3[t][2] = db3[t][3] = 0.f;
-    float gC3[4] = {0, 0, 0, 0}, cdb3 = 0.f;
-    float l_min = 0.f, l_mse = 0.f, l_ent = 0.f;
+    float cdb3 = 0.f, l_min = 0.f, l_mse = 0.f, l_ent = 0.f;
     const float eps = 1.1920928955078125e-07f;
 
     const int stride4 = p.stride >> 2;
-    const int R = (int)p.R, E = (int)p.E;
+    const int R = (int)p.R;
     const int tile0 = chunk * p.chunk_tiles;
     const int tile_end = min(tile0 + p.chunk_tiles, (R + 15) >> 4);
-    // lane (j, g4) copies dwords g4 + 4m of tile row j and owns row j's scalars; the next
-    // tile's loads are issued before the current tile is processed (register prefetch)
-    constexpr int kPreW = 16;  // 16 rows x 256 B / 64 lanes
-    uint32_t pre[kPreW];
+    // input byte D of every staged row reads 1 (the bias column of dW1)
+    const int one_dw = D >> 2;
+    const uint32_t one_bit = 1u << (8 * (D & 3));
+    // lane (j, g4) loads dwords g4 + 4m of tile row j and owns row j's scalars; the next tile's
+    // loads are issued before the current tile is processed (register prefetch)
+    uint32_t pre[NQ];
     int pre_act = 0;
     float pre_olp = 0.f, pre_G = 0.f;
     auto prefetch = [&](int tile) {
@@ -135,62 +164,74 @@ __global__ void __launch_bounds__(64) k_ppo_grad(PpoArgs p) {
         const size_t ru = (size_t)(ok ? r : 0) * p.U + u;
         const uint32_t* src = reinterpret_cast<const uint32_t*>(p.states + ru * p.stride);
 #pragma unroll
-        for (int m = 0; m < kPreW; m++) {
+        for (int m = 0; m < NQ; m++) {
             const int cc = g4 + 4 * m;
-            pre[m] = (ok && cc < stride4) ? src[cc] : 0u;
+            uint32_t w = (ok && cc < stride4) ? src[cc] : 0u;
+            pre[m] = (cc == one_dw) ? (w | one_bit) : w;
         }
         pre_act = ok ? p.actions[ru] : 0;
         pre_olp = ok ? p.old_lp[ru] : 0.f;
-        const int t = ok ? r / E : 0;
-        pre_G = ok ? p.ret[((size_t)(r - t * E) * p.G + grp) * p.T + t] : 0.f;
+        pre_G = ok ? p.ret[(size_t)r * p.G + grp] : 0.f;
     };
     if (tile0 < tile_end) prefetch(tile0);
     for (int tile = tile0; tile < tile_end; tile++) {
-        // ---- stage the tile's 16 observation rows (int8) in LDS, then start the next tile's loads
+        // ---- the tile's input rows: registers (forward) and LDS (dW1); then start the next loads
+        uint32_t xw[NQ];
 #pragma unroll
-        for (int m = 0; m < kPreW; m++) {
-            const int cc = g4 + 4 * m;
-            if (cc < stride4) reinterpret_cast<uint32_t*>(sX)[j * stride4 + cc] = pre[m];
+        for (int m = 0; m < NQ; m++) {
+            xw[m] = pre[m];
+            sX[j * (XP / 4) + g4 + 4 * m] = pre[m];
         }
         const bool valid = tile * 16 + j < R;
         const int act = pre_act;
         const float olp = pre_olp, G = pre_G;
         if (tile + 1 < tile_end) prefetch(tile + 1);
-        __syncthreads();
 
-        // ---- forward, layer 1 (actor + critic share the X operand)
+        // ---- forward, layer 1 (actor + critic share the B operand): step (m, b) is input
+        //      feature 16m + 4*g4 + b, byte b of dword g4 + 4m
         f4 a1 = {0, 0, 0, 0}, c1 = {0, 0, 0, 0};
-        for (int s = 0; s < S1; s++) {
-            float x = (float)sX[j * p.stride + 4 * s + g4];
-            a1 = mfma4(sW1[j * D4 + 4 * s + g4], x, a1);
-            c1 = mfma4(sC1[j * D4 + 4 * s + g4], x, c1);
+#pragma unroll
+        for (int m = 0; m < NQ; m++) {
+            const f4 wa = *reinterpret_cast<const f4*>(sW1 + j * W1P + 16 * m + 4 * g4);
+            const f4 wc = *reinterpret_cast<const f4*>(sC1 + j * W1P + 16 * m + 4 * g4);
+#pragma unroll
+            for (int b = 0; b < 4; b++) {
+                const float x = (float)(int8_t)(xw[m] >> (8 * b));
+                a1 = mfma4(wa[b], x, a1);
+                c1 = mfma4(wc[b], x, c1);
+            }
         }
         float h1[4], hc1[4];
 #pragma unroll
         for (int q = 0; q < 4; q++) {
-            h1[q] = tanhf(a1[q] + sb1[4 * g4 + q]);
-            hc1[q] = tanhf(c1[q] + scb1[4 * g4 + q]);
+            h1[q] = fast_tanh(a1[q] + sb1[4 * g4 + q]);
+            hc1[q] = fast_tanh(c1[q] + scb1[4 * g4 + q]);
         }
         // layer 2: B operand = layer-1 output as is; A reads W2 with k permuted (k_true = 4*g4 + s)
         f4 a2 = {0, 0, 0, 0}, c2 = {0, 0, 0, 0};
+        {
+            const f4 w2 = *reinterpret_cast<const f4*>(sW2 + j * 16 + 4 * g4);
+            const f4 cw2 = *reinterpret_cast<const f4*>(sC2 + j * 16 + 4 * g4);
 #pragma unroll
-        for (int s = 0; s < 4; s++) {
-            a2 = mfma4(sW2[j * 16 + 4 * g4 + s], h1[s], a2);
-            c2 = mfma4(sC2[j * 16 + 4 * g4 + s], hc1[s], c2);
+            for (int s = 0; s < 4; s++) {
+                a2 = mfma4(w2[s], h1[s], a2);
+                c2 = mfma4(cw2[s], hc1[s], c2);
+            }
         }
         float h2[4], hc2[4];
 #pragma unroll
         for (int q = 0; q < 4; q++) {
-            h2[q] = tanhf(a2[q] + sb2[4 * g4 + q]);
-            hc2[q] = tanhf(c2[q] + scb2[4 * g4 + q]);
+            h2[q] = fast_tanh(a2[q] + sb2[4 * g4 + q]);
+            hc2[q] = fast_tanh(c2[q] + scb2[4 * g4 + q]);
         }
         // actor layer 3 -> logits z[a = 16t + 4*g4 + q][row j]
         float z[NT][4];
 #pragma unroll
         for (int t = 0; t < NT; t++) {
+            const f4 w3 = *reinterpret_cast<const f4*>(sW3 + (16 * t + j) * 16 + 4 * g4);
             f4 zz = {0, 0, 0, 0};
 #pragma unroll
-            for (int s = 0; s < 4; s++) zz = mfma4(sW3[(16 * t + j) * 16 + 4 * g4 + s], h2[s], zz);
+            for (int s = 0; s < 4; s++) zz = mfma4(w3[s], h2[s], zz);
 #pragma unroll
             for (int q = 0; q < 4; q++) z[t][q] = zz[q] + sb3[16 * t + 4 * g4 + q];
         }
@@ -201,22 +242,22 @@ __global__ void __launch_bounds__(64) k_ppo_grad(PpoArgs p) {
         const float V = xsum4g(vp) + scb3[0];
 
         // ---- softmax (nn.Softmax) + Categorical(probs) renormalisation, log-prob, entropy
-        float m = -INFINITY;
+        float mx = -INFINITY;
 #pragma unroll
         for (int t = 0; t < NT; t++)
 #pragma unroll
             for (int q = 0; q < 4; q++)
-                if (16 * t + 4 * g4 + q < A) m = fmaxf(m, z[t][q]);
-        m = xmax4g(m);
+                if (16 * t + 4 * g4 + q < A) mx = fmaxf(mx, z[t][q]);
+        mx = xmax4g(mx);
         float pe[NT][4], s0 = 0.f;
 #pragma unroll
         for (int t = 0; t < NT; t++)
 #pragma unroll
             for (int q = 0; q < 4; q++) {
-                pe[t][q] = (16 * t + 4 * g4 + q < A) ? expf(z[t][q] - m) : 0.f;
+                pe[t][q] = (16 * t + 4 * g4 + q < A) ? fast_exp(z[t][q] - mx) : 0.f;
                 s0 += pe[t][q];
             }
-        const float inv0 = 1.f / xsum4g(s0);
+        const float inv0 = __builtin_amdgcn_rcpf(xsum4g(s0));
         float s1 = 0.f;
 #pragma unroll
         for (int t = 0; t < NT; t++)
@@ -225,16 +266,15 @@ __global__ void __launch_bounds__(64) k_ppo_grad(PpoArgs p) {
                 pe[t][q] *= inv0;  // softmax output (same arithmetic as k_act)
                 s1 += pe[t][q];
             }
-        const float inv1 = 1.f / xsum4g(s1);
+        const float inv1 = __builtin_amdgcn_rcpf(xsum4g(s1));
         float pn[NT][4], cl[NT][4], lp = 0.f, ent = 0.f;
 #pragma unroll
         for (int t = 0; t < NT; t++)
 #pragma unroll
             for (int q = 0; q < 4; q++) {
-                int a = 16 * t + 4 * g4 + q;
+                const int a = 16 * t + 4 * g4 + q;
                 pn[t][q] = pe[t][q] * inv1;
-                float pc = fminf(fmaxf(pn[t][q], eps), 1.f - eps);
-                cl[t][q] = logf(pc);
+                cl[t][q] = fast_log(fminf(fmaxf(pn[t][q], eps), 1.f - eps));
                 if (a < A) {
                     if (a == act) lp += cl[t][q];
                     ent -= cl[t][q] * pn[t][q];
@@ -244,19 +284,14 @@ __global__ void __launch_bounds__(64) k_ppo_grad(PpoArgs p) {
         ent = xsum4g(ent);
 
         // ---- per-row loss derivatives (loss.mean() over R rows)
-        const float ratio = expf(lp - olp);
+        const float ratio = fast_exp(lp - olp);
         const float adv = G - V;
         const float sur1 = ratio * adv;
         const float rc = fminf(fmaxf(ratio, 1.f - p.eps_clip), 1.f + p.eps_clip);
         const float sur2 = rc * adv;
         const float inr = (ratio >= 1.f - p.eps_clip && ratio <= 1.f + p.eps_clip) ? 1.f : 0.f;
-        float dmin;  // d min(s1, s2) / d ratio (torch.minimum splits ties)
-        if (sur1 < sur2)
-            dmin = adv;
-        else if (sur2 < sur1)
-            dmin = adv * inr;
-        else
-            dmin = 0.5f * adv + 0.5f * adv * inr;
+        // d min(s1, s2) / d ratio (torch.minimum splits ties)
+        const float dmin = sur1 < sur2 ? adv : (sur2 < sur1 ? adv * inr : 0.5f * adv + 0.5f * adv * inr);
         const float w = valid ? p.inv_R : 0.f;
         const float g_lp = -dmin * w * ratio;  // d loss / d logp (exp backward uses the result)
         const float g_v = (V - G) * w;         // 0.5 * d MSE / d V
@@ -267,30 +302,29 @@ __global__ void __launch_bounds__(64) k_ppo_grad(PpoArgs p) {
             l_ent += ent;
         }
         // d loss / d pn  -> d / d p (renormalisation) -> d / d z (softmax)
-        float dpn[NT][4], x1 = 0.f;
+        float gz[NT][4], x1 = 0.f;
 #pragma unroll
         for (int t = 0; t < NT; t++)
 #pragma unroll
             for (int q = 0; q < 4; q++) {
-                int a = 16 * t + 4 * g4 + q;
+                const int a = 16 * t + 4 * g4 + q;
                 float v = 0.f;
                 if (a < A) {
-                    float dc = (a == act ? g_lp : 0.f) - g_h * pn[t][q];
-                    float in = (pn[t][q] >= eps && pn[t][q] <= 1.f - eps) ? 1.f : 0.f;
+                    const float dc = (a == act ? g_lp : 0.f) - g_h * pn[t][q];
+                    const float in = (pn[t][q] >= eps && pn[t][q] <= 1.f - eps) ? 1.f : 0.f;
                     v = dc * in * __builtin_amdgcn_rcpf(fminf(fmaxf(pn[t][q], eps), 1.f - eps)) - g_h * cl[t][q];
                 }
-                dpn[t][q] = v;
+                gz[t][q] = v;
                 x1 += v * pe[t][q];
             }
         x1 = xsum4g(x1);
-        float gz[NT][4], x2 = 0.f;
+        float x2 = 0.f;
 #pragma unroll
         for (int t = 0; t < NT; t++)
 #pragma unroll
             for (int q = 0; q < 4; q++) {
-                float dp = (dpn[t][q] - x1 * inv1) * inv1;
-                gz[t][q] = dp;
-                x2 += dp * pe[t][q];
+                gz[t][q] = (gz[t][q] - x1 * inv1) * inv1;
+                x2 += gz[t][q] * pe[t][q];
             }
         x2 = xsum4g(x2);
 #pragma unroll
@@ -322,12 +356,10 @@ __global__ void __launch_bounds__(64) k_ppo_grad(PpoArgs p) {
             dl1[q] = d1[q] * (1.f - h1[q] * h1[q]);
             dc1[q] = e1[q] * (1.f - hc1[q] * hc1[q]);
         }
-        // bias gradients and the critic output layer (VALU; reduced over rows at the end)
+        // bias gradients of layers 2-3 and the critic output layer (VALU; reduced over rows at the end)
 #pragma unroll
         for (int q = 0; q < 4; q++) {
-            db1[q] += dl1[q];
             db2[q] += dl2[q];
-            cdb1[q] += dc1[q];
             cdb2[q] += dc2[q];
             gC3[q] = fmaf(g_v, hc2[q], gC3[q]);
 #pragma unroll
@@ -335,7 +367,9 @@ __global__ void __launch_bounds__(64) k_ppo_grad(PpoArgs p) {
         }
         if (g4 == 0) cdb3 += g_v;
 
-        // ---- weight gradients: batch reductions as MFMAs with K = rows (operands transposed via LDS)
+        // ---- weight gradients: batch reductions as MFMAs with K = rows. Transposes: value of
+        //      (feature f, row r) at T[f*TP + 4*(r%4) + r/4], so lane (j, g4) reads rows
+        //      g4, g4+4, g4+8, g4+12 of feature j with one ds_read_b128 (k step s = row g4 + 4s).
         float* T_d1 = sT;
         float* T_d2 = sT + 1 * 16 * TP;
         float* T_h1 = sT + 2 * 16 * TP;
@@ -344,139 +378,180 @@ __global__ void __launch_bounds__(64) k_ppo_grad(PpoArgs p) {
         float* T_e2 = sT + 5 * 16 * TP;
         float* T_k1 = sT + 6 * 16 * TP;
         float* T_gz = sT + 7 * 16 * TP;
+        const int pr = 4 * (j & 3) + (j >> 2);  // this lane's row position
 #pragma unroll
         for (int q = 0; q < 4; q++) {
-            int f = 4 * g4 + q;
-            T_d1[f * TP + j] = dl1[q];
-            T_d2[f * TP + j] = dl2[q];
-            T_h1[f * TP + j] = h1[q];
-            T_h2[f * TP + j] = h2[q];
-            T_e1[f * TP + j] = dc1[q];
-            T_e2[f * TP + j] = dc2[q];
-            T_k1[f * TP + j] = hc1[q];
+            const int f = (4 * g4 + q) * TP + pr;
+            T_d1[f] = dl1[q];
+            T_d2[f] = dl2[q];
+            T_h1[f] = h1[q];
+            T_h2[f] = h2[q];
+            T_e1[f] = dc1[q];
+            T_e2[f] = dc2[q];
+            T_k1[f] = hc1[q];
 #pragma unroll
-            for (int t = 0; t < NT; t++) T_gz[(t * 16 + f) * TP + j] = gz[t][q];
+            for (int t = 0; t < NT; t++) T_gz[t * 16 * TP + f] = gz[t][q];
         }
-        __syncthreads();
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        const int rd = j * TP + 4 * g4;
+        const f4 ad1 = *reinterpret_cast<const f4*>(T_d1 + rd);
+        const f4 ae1 = *reinterpret_cast<const f4*>(T_e1 + rd);
+        const f4 ad2 = *reinterpret_cast<const f4*>(T_d2 + rd);
+        const f4 ae2 = *reinterpret_cast<const f4*>(T_e2 + rd);
+        const f4 bh1 = *reinterpret_cast<const f4*>(T_h1 + rd);
+        const f4 bk1 = *reinterpret_cast<const f4*>(T_k1 + rd);
+        const f4 bh2 = *reinterpret_cast<const f4*>(T_h2 + rd);
+        f4 agz[NT];
+#pragma unroll
+        for (int t = 0; t < NT; t++) agz[t] = *reinterpret_cast<const f4*>(T_gz + t * 16 * TP + rd);
 #pragma unroll
         for (int s = 0; s < 4; s++) {
-            const int rr = 4 * s + g4;  // tile row supplied by this lane at k-step s
-            const float ad1 = T_d1[j * TP + rr];
-            const float ae1 = T_e1[j * TP + rr];
+            // dW1 / dC1: output column j of tile q is input feature NQ*j + q (one LDS read per step)
+            const int rr = g4 + 4 * s;
+            const uint8_t* xrow = reinterpret_cast<const uint8_t*>(sX) + rr * XP + NQ * j;
+            uint32_t xb[(NQ + 3) / 4];
+            if (NQ == 1) {
+                xb[0] = xrow[0];
+            } else if (NQ == 2) {
+                xb[0] = *reinterpret_cast<const uint16_t*>(xrow);
+            } else {
+#pragma unroll
+                for (int i = 0; i < NQ / 4; i++) xb[i] = reinterpret_cast<const uint32_t*>(xrow)[i];
+            }
 #pragma unroll
             for (int q = 0; q < NQ; q++) {
-                int d = 16 * q + j;
-                float xv = d < D ? (float)sX[rr * p.stride + d] : 0.f;
-                gW1[q] = mfma4(ad1, xv, gW1[q]);
-                gC1[q] = mfma4(ae1, xv, gC1[q]);
+                const float xv = (float)(int8_t)(xb[q >> 2] >> (8 * (q & 3)));
+                gW1[q] = mfma4(ad1[s], xv, gW1[q]);
+                gC1[q] = mfma4(ae1[s], xv, gC1[q]);
             }
-            gW2 = mfma4(T_d2[j * TP + rr], T_h1[j * TP + rr], gW2);
-            gC2 = mfma4(T_e2[j * TP + rr], T_k1[j * TP + rr], gC2);
-            const float bh2 = T_h2[j * TP + rr];
+            gW2 = mfma4(ad2[s], bh1[s], gW2);
+            gC2 = mfma4(ae2[s], bk1[s], gC2);
 #pragma unroll
-            for (int t = 0; t < NT; t++) gW3[t] = mfma4(T_gz[(t * 16 + j) * TP + rr], bh2, gW3[t]);
+            for (int t = 0; t < NT; t++) gW3[t] = mfma4(agz[t][s], bh2[s], gW3[t]);
+        }
+        __builtin_amdgcn_wave_barrier();
+    }
+
+    // ---- the block's partial gradient: the 4 waves' vectors summed in LDS in wave order
+    //      (deterministic), then one coalesced store per block
+    const POff o = poff(D, A);
+    auto write_partial = [&](auto&& put) {
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            const int f = 4 * g4 + q;  // C row (output feature) held in register q
+#pragma unroll
+            for (int qq = 0; qq < NQ; qq++) {
+                const int d = NQ * j + qq;
+                if (d < D) {
+                    put(o.w1 + f * D + d, gW1[qq][q]);
+                    put(o.cw1 + f * D + d, gC1[qq][q]);
+                } else if (d == D) {  // the ones column: layer-1 bias gradients
+                    put(o.b1 + f, gW1[qq][q]);
+                    put(o.cb1 + f, gC1[qq][q]);
+                }
+            }
+            put(o.w2 + f * 16 + j, gW2[q]);
+            put(o.cw2 + f * 16 + j, gC2[q]);
+#pragma unroll
+            for (int t = 0; t < NT; t++) {
+                const int a = 16 * t + f;
+                if (a < A) put(o.w3 + a * 16 + j, gW3[t][q]);
+            }
+            float v;
+            v = xsum16(db2[q]);
+            if (j == 0) put(o.b2 + f, v);
+            v = xsum16(cdb2[q]);
+            if (j == 0) put(o.cb2 + f, v);
+            v = xsum16(gC3[q]);
+            if (j == 0) put(o.cw3 + f, v);
+#pragma unroll
+            for (int t = 0; t < NT; t++) {
+                v = xsum16(db3[t][q]);
+                if (j == 0 && 16 * t + f < A) put(o.b3 + 16 * t + f, v);
+            }
+        }
+        float v = xsum16(cdb3);
+        if (lane == 0) put(o.cb3, v);
+        v = xsum16(l_min);
+        if (lane == 0) put(o.loss + 0, v * p.inv_R);
+        v = xsum16(l_mse);
+        if (lane == 0) put(o.loss + 1, v * p.inv_R);
+        v = xsum16(l_ent);
+        if (lane == 0) put(o.loss + 2, v * p.inv_R);
+    };
+    __syncthreads();  // every wave is done with the weights and its transposes
+    float* acc = sm;
+    for (int wv = 0; wv < 4; wv++) {
+        if (wave == wv) {
+            auto put = [&](int i, float x) {
+                if (wv == 0)
+                    acc[i] = x;
+                else
+                    acc[i] += x;
+            };
+            write_partial(put);
         }
         __syncthreads();
     }
-
-    // ---- write this block's partial gradient vector
-    const POff o = poff(D, A);
-    float* out = p.partials + ((size_t)grp * p.n_chunks + chunk) * p.P;
-#pragma unroll
-    for (int q = 0; q < 4; q++) {
-        const int f = 4 * g4 + q;  // C row (output feature) held in register q
-#pragma unroll
-        for (int qq = 0; qq < NQ; qq++) {
-            int d = 16 * qq + j;
-            if (d < D) {
-                out[o.w1 + f * D + d] = gW1[qq][q];
-                out[o.cw1 + f * D + d] = gC1[qq][q];
-            }
-        }
-        out[o.w2 + f * 16 + j] = gW2[q];
-        out[o.cw2 + f * 16 + j] = gC2[q];
-#pragma unroll
-        for (int t = 0; t < NT; t++) {
-            int a = 16 * t + f;
-            if (a < A) out[o.w3 + a * 16 + j] = gW3[t][q];
-        }
-        float v;
-        v = xsum16(db1[q]);
-        if (j == 0) out[o.b1 + f] = v;
-        v = xsum16(db2[q]);
-        if (j == 0) out[o.b2 + f] = v;
-        v = xsum16(cdb1[q]);
-        if (j == 0) out[o.cb1 + f] = v;
-        v = xsum16(cdb2[q]);
-        if (j == 0) out[o.cb2 + f] = v;
-        v = xsum16(gC3[q]);
-        if (j == 0) out[o.cw3 + f] = v;
-#pragma unroll
-        for (int t = 0; t < NT; t++) {
-            v = xsum16(db3[t][q]);
-            if (j == 0 && 16 * t + f < A) out[o.b3 + 16 * t + f] = v;
-        }
-    }
-    float v = xsum16(cdb3);
-    if (lane == 0) out[o.cb3] = v;
-    v = xsum16(l_min);
-    if (lane == 0) out[o.loss + 0] = v * p.inv_R;
-    v = xsum16(l_mse);
-    if (lane == 0) out[o.loss + 1] = v * p.inv_R;
-    v = xsum16(l_ent);
-    if (lane == 0) out[o.loss + 2] = v * p.inv_R;
+    float* outp = p.partials + ((size_t)grp * blocks_per_group + (chunk >> 2)) * p.P;
+    for (int i = tid; i < p.P; i += 256) outp[i] = acc[i];
 }
 
-// Sum the partials of every chunk (fixed order) and scatter into the .grad tensors.
-__global__ void __launch_bounds__(256) k_ppo_reduce(const float* __restrict__ partials, int G, int n_chunks, int P,
+// Sum the blocks' partial vectors (fixed order: 4 interleaved row sets, then a fixed tree) and
+// scatter into the .grad tensors. Block = 64 parameters x 4 row sets.
+__global__ void __launch_bounds__(256) k_ppo_reduce(const float* __restrict__ partials, int G, int n_rows, int P,
                                                     int D, int A, GradOut go) {
+    __shared__ float part[4][64];
     const int grp = blockIdx.y;
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= P) return;
-    const float* src = partials + (size_t)grp * n_chunks * P + i;
+    const int pi = threadIdx.x & 63, rs = threadIdx.x >> 6;
+    const int i = blockIdx.x * 64 + pi;
     float s = 0.f;
-    for (int c = 0; c < n_chunks; c++) s += src[(size_t)c * P];
+    if (i < P) {
+        const float* src = partials + (size_t)grp * n_rows * P + i;
+        for (int c = rs; c < n_rows; c += 4) s += src[(size_t)c * P];
+    }
+    part[rs][pi] = s;
+    __syncthreads();
+    if (rs != 0 || i >= P) return;
+    s = (part[0][pi] + part[1][pi]) + (part[2][pi] + part[3][pi]);
     const POff o = poff(D, A);
     float* dst;
-    int k;
-    if (i < o.b1) { dst = go.w1; k = 16 * D; }
-    else if (i < o.w2) { dst = go.b1; k = 16; }
-    else if (i < o.b2) { dst = go.w2; k = 256; }
-    else if (i < o.w3) { dst = go.b2; k = 16; }
-    else if (i < o.b3) { dst = go.w3; k = 16 * A; }
-    else if (i < o.cw1) { dst = go.b3; k = A; }
-    else if (i < o.cb1) { dst = go.cw1; k = 16 * D; }
-    else if (i < o.cw2) { dst = go.cb1; k = 16; }
-    else if (i < o.cb2) { dst = go.cw2; k = 256; }
-    else if (i < o.cw3) { dst = go.cb2; k = 16; }
-    else if (i < o.cb3) { dst = go.cw3; k = 16; }
-    else if (i < o.loss) { dst = go.cb3; k = 1; }
-    else { dst = go.loss; k = 3; }
-    int base;
-    if (dst == go.w1) base = o.w1; else if (dst == go.b1) base = o.b1; else if (dst == go.w2) base = o.w2;
-    else if (dst == go.b2) base = o.b2; else if (dst == go.w3) base = o.w3; else if (dst == go.b3) base = o.b3;
-    else if (dst == go.cw1) base = o.cw1; else if (dst == go.cb1) base = o.cb1; else if (dst == go.cw2) base = o.cw2;
-    else if (dst == go.cb2) base = o.cb2; else if (dst == go.cw3) base = o.cw3; else if (dst == go.cb3) base = o.cb3;
-    else base = o.loss;
+    int k, base;
+    if (i < o.b1) { dst = go.w1; k = 16 * D; base = o.w1; }
+    else if (i < o.w2) { dst = go.b1; k = 16; base = o.b1; }
+    else if (i < o.b2) { dst = go.w2; k = 256; base = o.w2; }
+    else if (i < o.w3) { dst = go.b2; k = 16; base = o.b2; }
+    else if (i < o.b3) { dst = go.w3; k = 16 * A; base = o.w3; }
+    else if (i < o.cw1) { dst = go.b3; k = A; base = o.b3; }
+    else if (i < o.cb1) { dst = go.cw1; k = 16 * D; base = o.cw1; }
+    else if (i < o.cw2) { dst = go.cb1; k = 16; base = o.cb1; }
+    else if (i < o.cb2) { dst = go.cw2; k = 256; base = o.cw2; }
+    else if (i < o.cw3) { dst = go.cb2; k = 16; base = o.cb2; }
+    else if (i < o.cb3) { dst = go.cw3; k = 16; base = o.cw3; }
+    else if (i < o.loss) { dst = go.cb3; k = 1; base = o.cb3; }
+    else { dst = go.loss; k = 3; base = o.loss; }
     if (dst) dst[(size_t)grp * k + (i - base)] = s;
 }
 
 template <int NQ, int NT>
 static hipError_t launch_grad_t(const PpoArgs& a, hipStream_t st) {
-    const int D4 = (a.D + 3) & ~3;
-    size_t lds = sizeof(float) * (2 * 16 * D4 + 2 * 256 + 256 * NT + 16 * 2 + 16 * NT + 16 * 3 + 4 + (7 + NT) * 16 * 17) +
-                 16 * (size_t)a.stride;
-    hipLaunchKernelGGL((k_ppo_grad<NQ, NT>), dim3((unsigned)(a.G * a.n_chunks)), dim3(64), lds, st, a);
+    using L = GradLds<NQ, NT>;
+    const size_t lds = sizeof(float) * (L::shared_floats + 4 * L::wave_floats);
+    if ((size_t)a.P > L::shared_floats + 4 * L::wave_floats) return hipErrorInvalidValue;  // block partial in LDS
+    hipLaunchKernelGGL((k_ppo_grad<NQ, NT>), dim3((unsigned)(a.G * (a.n_chunks / 4))), dim3(256), lds, st, a);
     return hipGetLastError();
 }
 
 hipError_t launch_ppo_grad(const PpoArgs& a, const GradOut& go, hipStream_t st) {
-    const int nq = (a.D + 15) / 16, nt = (a.A + 15) / 16;
+    const int nq = a.D / 16 + 1;  // 16*NQ > D leaves room for the ones column
+    const int nt = (a.A + 15) / 16;
+    if (a.n_chunks % 4 != 0) return hipErrorInvalidValue;
     hipError_t e;
-#define MS_PPO_CASE(Q, T)                                       \
-    if (nq <= Q && nt <= T) {                                   \
-        e = launch_grad_t<Q, T>(a, st);                         \
-        goto reduce;                                            \
+#define MS_PPO_CASE(Q, T)                \
+    if (nq <= Q && nt <= T) {            \
+        e = launch_grad_t<Q, T>(a, st);  \
+        goto reduce;                     \
     }
     if (nt <= 1) {
         MS_PPO_CASE(1, 1) MS_PPO_CASE(2, 1) MS_PPO_CASE(4, 1) MS_PPO_CASE(8, 1) MS_PPO_CASE(16, 1)
@@ -493,8 +568,8 @@ reduce:
     if (e != hipSuccess) return e;
     {
         const int P = poff(a.D, a.A).total;
-        hipLaunchKernelGGL(k_ppo_reduce, dim3((P + 255) / 256, a.G), dim3(256), 0, st, a.partials, a.G, a.n_chunks, P,
-                           a.D, a.A, go);
+        hipLaunchKernelGGL(k_ppo_reduce, dim3((P + 63) / 64, a.G), dim3(256), 0, st, a.partials, a.G, a.n_chunks / 4,
+                           P, a.D, a.A, go);
     }
     return hipGetLastError();
 }

@@ -10,7 +10,7 @@ runs on the HIP library at E = 1:
 * the env round is ``ms_env_step``; the hard-coded auctioneer is ``ms_env_auctioneer``;
 * action selection is ``ms_policy_act`` / ``ms_offer_act_free``, with the experience
   buffers kept on the device;
-* ``updateAgents`` is ``ms_discounted_returns`` + ``ms_ppo_grad`` + Adam.
+* ``updateAgents`` is ``ms_unit_returns`` + ``ms_ppo_grad`` + Adam.
 
 Python's global ``random`` stream is the env's stream, as in the reference, where
 world.py, Auctioneer.py and Agent.py all call the ``random`` module. Before a call
@@ -259,11 +259,10 @@ class Units:
             return []
         if len(self.rewards) != T:
             raise RuntimeError("%d rewards saved for %d actions" % (len(self.rewards), T))
-        sel = torch.as_tensor(u_sel, dtype=torch.long)
-        r = torch.from_numpy(np.stack(self.rewards).astype(np.float32))[:, sel].to(self.device)
-        ret = ppo.discounted_returns(r, self.group.gamma)  # [G, T]
-        return self.group.update_fused(self.states[:T], self.actions[:T], self.logprobs[:T], ret,
-                                       sel.to(torch.int32).to(self.device), T, 1)
+        sel = torch.as_tensor(u_sel, dtype=torch.int32).to(self.device)
+        r = torch.from_numpy(np.stack(self.rewards).astype(np.float32)).view(T, 1, self.U).to(self.device)
+        ret = ppo.unit_returns(r, sel, self.group.gamma)  # [T][1][G]
+        return self.group.update_fused(self.states[:T], self.actions[:T], self.logprobs[:T], ret, sel, T, 1)
 
 
 def reference_nets(order, dims):

@@ -158,6 +158,20 @@ def discounted_returns(rewards_tm: torch.Tensor, gamma: float, stream=None) -> t
     return out
 
 
+def unit_returns(rewards_teu: torch.Tensor, unit_of_group: torch.Tensor, gamma: float, stream=None) -> torch.Tensor:
+    """PPO.update's return estimate (PPOmodules.py:128-137) for the unit each group trains on, read
+    straight from the rollout rewards [T, E, U] (f32 or int32). unit_of_group [G] int32 on the device.
+    Returns [T, E, G] f32 normalised per (replica, group) sequence (the ms_ppo_batch layout)."""
+    assert rewards_teu.dim() == 3 and rewards_teu.is_contiguous()
+    assert rewards_teu.dtype in (torch.float32, torch.int32) and unit_of_group.dtype == torch.int32
+    T, E, U = rewards_teu.shape
+    G = unit_of_group.numel()
+    out = torch.empty((T, E, G), dtype=torch.float32, device=rewards_teu.device)
+    check(lib.ms_unit_returns(ptr(rewards_teu), int(rewards_teu.dtype == torch.int32), T, E, U, ptr(unit_of_group),
+                              G, ct.c_double(gamma), ptr(out), stream_ptr(stream)))
+    return out
+
+
 class PPOGroup:
     """Policy / policy_old pair + Adam for one unit type (PPOmodules.py:75-174)."""
 
@@ -211,12 +225,12 @@ class PPOGroup:
         self.last_losses = losses
         return losses
 
-    def update_fused(self, states_i8, actions_i8, old_logprobs, returns_egt, unit_of_group, T: int, E: int,
+    def update_fused(self, states_i8, actions_i8, old_logprobs, returns_teg, unit_of_group, T: int, E: int,
                      stream=None):
         """The same K epochs with the gradient from the fused HIP kernel (ms_ppo_grad).
 
         states_i8 [R, U, stride] int8 rollout rows (R = T*E, row r = t*E + e), actions_i8 [R, U],
-        old_logprobs [R, U] f32, returns_egt [E, G, T] f32 normalised, unit_of_group [G] int32
+        old_logprobs [R, U] f32, returns_teg [T, E, G] f32 normalised (unit_returns), unit_of_group [G] int32
         (device). Adam (torch) applies the gradient; with several ranks the gradient is
         all-reduced first."""
         pol = self.policy
@@ -230,7 +244,7 @@ class PPOGroup:
         c = pol.critic_mlp_params()
         ws_bytes = lib.ms_ppo_workspace_bytes(ct.byref(a), R)
         ws = torch.empty(((ws_bytes + 3) // 4,), dtype=torch.float32, device=states_i8.device)
-        batch = abi.MsPpoBatch(ptr(states_i8), ptr(actions_i8), ptr(old_logprobs), ptr(returns_egt),
+        batch = abi.MsPpoBatch(ptr(states_i8), ptr(actions_i8), ptr(old_logprobs), ptr(returns_teg),
                                ptr(unit_of_group), stride, T, U, E)
         grads = abi.MsPpoGrads(*[ptr(getattr(pol, k).grad) for k in ACTOR_KEYS + CRITIC_KEYS], ptr(loss_buf))
         losses = []

@@ -27,7 +27,7 @@ import torch
 
 from . import abi
 from .env import BatchedEnv
-from .ppo import PPOGroup, discounted_returns, offer_act_free
+from .ppo import PPOGroup, discounted_returns, offer_act_free, unit_returns
 
 
 @dataclass
@@ -277,9 +277,8 @@ class Trainer:
             ls = []
             for u_sel in sel[u.name]:
                 if self.fused:
-                    G = u_sel.numel()
-                    r = u.rewards.index_select(2, u_sel).float().reshape(T, E * G)
-                    ret = discounted_returns(r, u.group.gamma)  # [E*G, T] = [E][G][T]
+                    sel32 = u_sel.to(torch.int32)
+                    ret = unit_returns(u.rewards, sel32, u.group.gamma)  # [T][E][G]
                     ls += u.group.update_fused(states.reshape(T * E, u.U, u.stride), u.actions.view(T * E, u.U),
                                                u.logprobs.view(T * E, u.U), ret, u_sel.to(torch.int32), T, E)
                 else:

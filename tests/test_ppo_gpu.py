@@ -81,6 +81,23 @@ def test_returns_kernel_matches_reference(ms):
         np.testing.assert_allclose(got[m].numpy(), want.numpy(), rtol=1e-5, atol=2e-6)
 
 
+@pytest.mark.parametrize("dtype", [torch.int32, torch.float32])
+def test_unit_returns_gathers_and_matches_reference(ms, dtype):
+    ppo = _ppo(ms)
+    gen = torch.Generator().manual_seed(8)
+    T, E, U, G = 60, 33, 24, 8
+    r = torch.randint(-20, 30, (T, E, U), generator=gen)
+    r = r.to(dtype) if dtype == torch.int32 else (0.5 * r).float()
+    sel = torch.randint(0, U, (G,), generator=gen).to(torch.int32)
+    ref = RefPPO(4, 3, 0.1, 0.1, 0.9, 0.2, 1)
+    got = ppo.unit_returns(r.cuda(), sel.cuda(), 0.9).cpu()
+    assert got.shape == (T, E, G)
+    for e in (0, 7, E - 1):
+        for g in range(G):
+            want = ref.returns([float(x) for x in r[:, e, sel[g]]])
+            np.testing.assert_allclose(got[:, e, g].numpy(), want.numpy(), rtol=1e-5, atol=2e-6)
+
+
 def test_grouped_update_on_device_matches_reference(ms):
     ppo = _ppo(ms)
     G, T, D, A, K = 4, 200, 51, 25, 2
@@ -130,7 +147,8 @@ def _rand_batch(G, T, E, U, D, stride, A, seed):
 
 @pytest.mark.parametrize("G,T,E,U,D,stride,A,K", [(8, 20, 37, 64, 51, 52, 25, 1), (8, 13, 11, 24, 18, 20, 9, 2),
                                                    (8, 9, 50, 24, 4, 4, 13, 1), (3, 7, 9, 3, 11, 12, 5, 2),
-                                                   (2, 5, 16, 4, 195, 196, 97, 1)])
+                                                   (2, 5, 16, 4, 195, 196, 97, 1), (2, 6, 21, 3, 16, 16, 5, 1),
+                                                   (1, 3, 333, 2, 99, 100, 49, 1)])
 def test_fused_grad_matches_autograd(ms, G, T, E, U, D, stride, A, K):
     ppo = _ppo(ms)
     torch.manual_seed(21)
@@ -147,7 +165,7 @@ def test_fused_grad_matches_autograd(ms, G, T, E, U, D, stride, A, K):
     rt = ret.permute(1, 2, 0).reshape(G, R).cuda()  # [G][t][e] -> r = t*E + e
     ref_losses = ref.update(x, a, lp, rt)
     ref_grads = {k: getattr(ref.policy, k).grad.clone() for k in ppo.ACTOR_KEYS + ppo.CRITIC_KEYS}
-    fus_losses = fus.update_fused(states.cuda(), actions.cuda(), old_lp.cuda(), ret.cuda(),
+    fus_losses = fus.update_fused(states.cuda(), actions.cuda(), old_lp.cuda(), ret.permute(2, 0, 1).contiguous().cuda(),
                                   u_sel.to(torch.int32).cuda(), T, E)
     for rl, fl in zip(ref_losses, fus_losses):
         np.testing.assert_allclose(fl.cpu().numpy(), rl.cpu().numpy(), rtol=1e-5, atol=1e-6)
@@ -156,9 +174,16 @@ def test_fused_grad_matches_autograd(ms, G, T, E, U, D, stride, A, K):
         scale = g.abs().max().item() + 1e-12
         err = (fg - g).abs().max().item()
         assert err <= 1e-4 * scale + 1e-7, (k, err, scale)
+    # after Adam: Adam's first steps move every weight by about lr * sign(g), so elements whose
+    # gradient is at the f32 noise floor (|g| < 1e-3 max|g|) may move either way; all others agree
     for k in ppo.ACTOR_KEYS + ppo.CRITIC_KEYS:
-        np.testing.assert_allclose(getattr(fus.policy, k).detach().cpu().numpy(),
-                                   getattr(ref.policy, k).detach().cpu().numpy(), rtol=1e-4, atol=1e-5, err_msg=k)
+        wf = getattr(fus.policy, k).detach().cpu()
+        wr = getattr(ref.policy, k).detach().cpu()
+        g = ref_grads[k].abs().cpu()
+        firm = g > 1e-3 * g.max()
+        np.testing.assert_allclose(wf[firm].numpy(), wr[firm].numpy(), rtol=1e-4, atol=1e-5, err_msg=k)
+        lr = 0.003 if k in ppo.ACTOR_KEYS else 0.01
+        assert ((wf - wr)[~firm].abs() <= 2 * lr * K + 1e-6).all(), k
 
 
 def test_trainer_fused_matches_torch_update(ms):
