@@ -20,6 +20,16 @@
 
 namespace ms {
 
+// Every env kernel runs one 64-lane wave per block, so a phase boundary only has to order the
+// wave's own memory operations: LDS operations of one wave complete in issue order, so the
+// compiler barrier is enough. A __syncthreads would also drain every outstanding load (s_waitcnt)
+// at each of the round's ~20 phase boundaries.
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 // ---------------------------------------------------------------------------
 // CPython MT19937 (Modules/_randommodule.c) — tempering and wave-cooperative twist
 
@@ -47,13 +57,13 @@ __device__ void mt_twist_lds(uint32_t* mt, int lane) {
             int x = (ph == 0) ? i + kMtM : i + (kMtM - kMtN);
             v[cnt++] = step(i, mt[i], mt[i + 1], mt[x]);
         }
-        __syncthreads();
+        wave_sync();
         cnt = 0;
         for (int i = ranges[ph][0] + lane; i < ranges[ph][1]; i += kWave) mt[i] = v[cnt++];
-        __syncthreads();
+        wave_sync();
     }
     if (lane == 0) mt[kMtN - 1] = step(kMtN - 1, mt[kMtN - 1], mt[0], mt[kMtM - 1]);
-    __syncthreads();
+    wave_sync();
 }
 
 // A 64-word window of the env's stream held one word per lane. Stream
@@ -79,7 +89,7 @@ struct MtStream {
             int g = mti0 + pos + lane;
             uint32_t old = (g < kMtN) ? gmt[g] : 0u;
             for (int i = lane; i < kMtN; i += kWave) lds[i] = gmt[i];
-            __syncthreads();
+            wave_sync();
             mt_twist_lds(lds, lane);
             for (int i = lane; i < kMtN; i += kWave) gmt[i] = lds[i];
             twisted = true;
@@ -213,7 +223,7 @@ __device__ __forceinline__ void mask_set(M128* m, int i) {
 __device__ void build_masks(Rec& R, const Params& P, M128* mc, M128* mr, int lane) {
     for (int i = lane; i < P.C; i += kWave) mc[i] = M128{0, 0};
     for (int i = lane; i <= P.N; i += kWave) mr[i] = M128{0, 0};
-    __syncthreads();
+    wave_sync();
     const int8_t* oc = R.offer_core();
     const int8_t* orc = R.offer_recip();
     for (int i = lane; i < P.NL; i += kWave) {
@@ -223,7 +233,7 @@ __device__ void build_masks(Rec& R, const Params& P, M128* mc, M128* mr, int lan
             mask_set(&mr[orc[i]], i);
         }
     }
-    __syncthreads();
+    wave_sync();
 }
 
 // ---------------------------------------------------------------------------
@@ -257,13 +267,13 @@ __device__ void emit_acc_rows(Rec& R, const Params& P, const M128* mc, const M12
                               int n_rows, int lane) {
     if (!dst) return;
     const int stride = P.acc_stride;
-    const int per_chunk = kObsChunk / stride;
+    const int per_chunk = P.obs_chunk / stride;
     uint32_t* sw = reinterpret_cast<uint32_t*>(scratch);
     for (int r0 = 0; r0 < n_rows; r0 += per_chunk) {
         const int nr = min(per_chunk, n_rows - r0);
         const int nd = nr * stride / 4;
         for (int i = lane; i < nd; i += kWave) sw[i] = 0xFEFEFEFEu;  // -2 pads
-        __syncthreads();
+        wave_sync();
         for (int r = lane; r < nr; r += kWave) {
             const int g = r0 + r;
             int8_t* row = reinterpret_cast<int8_t*>(scratch) + r * stride;
@@ -272,9 +282,9 @@ __device__ void emit_acc_rows(Rec& R, const Params& P, const M128* mc, const M12
             else
                 acceptor_row(R, P, mc, mr, 0, g, row);
         }
-        __syncthreads();
+        wave_sync();
         copy_dwords(reinterpret_cast<uint32_t*>(dst + (size_t)r0 * stride), sw, nd, lane);
-        __syncthreads();
+        wave_sync();
     }
 }
 
@@ -284,7 +294,7 @@ __device__ void emit_acc_rows(Rec& R, const Params& P, const M128* mc, const M12
 __device__ void emit_off_rows(Rec& R, const Params& P, uint8_t* scratch, int8_t* dst, int lane) {
     if (!dst) return;
     const int stride = P.off_stride;
-    const int per_chunk = kObsChunk / stride;
+    const int per_chunk = P.obs_chunk / stride;
     const int8_t* ck = R.core_kind();
     const int8_t* cr = R.core_rem();
     const int8_t* sk = R.slot_kind();
@@ -313,9 +323,9 @@ __device__ void emit_off_rows(Rec& R, const Params& P, uint8_t* scratch, int8_t*
             }
             sw[d] = word;
         }
-        __syncthreads();
+        wave_sync();
         copy_dwords(reinterpret_cast<uint32_t*>(dst + (size_t)r0 * stride), sw, nd, lane);
-        __syncthreads();
+        wave_sync();
     }
 }
 
@@ -365,7 +375,7 @@ __device__ void hardcoded_auctioneer(Rec& R, const Params& P, const M128* s_mc, 
         s_auct[lane] = (int16_t)O;
         s_tie_n[lane] = (int16_t)nt;
     }
-    __syncthreads();
+    wave_sync();
     // tie-break draws in core order on the env stream (Auctioneer.getAuctioneerAction
     // Auctioneer.py:95-102)
     bool any = false;
@@ -378,7 +388,7 @@ __device__ void hardcoded_auctioneer(Rec& R, const Params& P, const M128* s_mc, 
         }
     }
     if (any) {
-        __syncthreads();
+        wave_sync();
         // the pick-th maximal candidate's position in the padded list
         if (lane < C && s_tie_n[lane] > 0) {
             const int pick = s_pick[lane];
@@ -411,7 +421,7 @@ __global__ void __launch_bounds__(64) k_env_init(Params P, uint8_t* recs, uint32
     uint8_t* rec = smem;
     uint32_t* st = reinterpret_cast<uint32_t*>(smem + P.s_scratch);
     for (int i = lane; i < P.rec_bytes / 4; i += kWave) reinterpret_cast<uint32_t*>(rec)[i] = 0;
-    __syncthreads();
+    wave_sync();
     Rec R{rec, &P};
     for (int c = lane; c < P.C; c += kWave) {
         R.core_owner()[c] = 0;
@@ -457,7 +467,7 @@ __global__ void __launch_bounds__(64) k_env_init(Params P, uint8_t* recs, uint32
         st[0] = 0x80000000u;
         R.mti() = kMtN;
     }
-    __syncthreads();
+    wave_sync();
     copy_dwords(mt + e * kMtN, st, kMtN, lane);
     copy_dwords(reinterpret_cast<uint32_t*>(recs + e * (int64_t)P.rec_bytes), reinterpret_cast<uint32_t*>(rec),
                 P.rec_bytes / 4, lane);
@@ -466,14 +476,14 @@ __global__ void __launch_bounds__(64) k_env_init(Params P, uint8_t* recs, uint32
 __global__ void __launch_bounds__(64) k_env_reset(Params P, const uint8_t* recs, int8_t* obs_acc, int8_t* obs_off,
                                                   int8_t* obs_auct) {
     extern __shared__ __align__(16) uint8_t smem[];
-    __shared__ M128 s_mc[MS_MAX_CORES];
-    __shared__ M128 s_mr[MS_MAX_AGENTS + 1];
+    M128* s_mc = reinterpret_cast<M128*>(smem + P.s_mc);
+    M128* s_mr = reinterpret_cast<M128*>(smem + P.s_mr);
     const int lane = threadIdx.x;
     const int64_t e = blockIdx.x;
     uint8_t* rec = smem + P.s_rec;
     copy_dwords(reinterpret_cast<uint32_t*>(rec), reinterpret_cast<const uint32_t*>(recs + e * (int64_t)P.rec_bytes),
                 P.rec_bytes / 4, lane);
-    __syncthreads();
+    wave_sync();
     Rec R{rec, &P};
     build_masks(R, P, s_mc, s_mr, lane);
     emit_obs(R, P, s_mc, s_mr, smem + P.s_scratch, obs_acc, obs_off, obs_auct, e, lane);
@@ -484,20 +494,20 @@ constexpr int kLiabPrefetch = 4;  // newest chain entries loaded ahead per core 
 // One round of SchedulingEnv.step (SchedulingEnvironment.py:32-83) for env blockIdx.x.
 __global__ void __launch_bounds__(64) k_env_step(Params P, uint8_t* recs, uint32_t* mt, Liab* liab, StepIO io) {
     extern __shared__ __align__(16) uint8_t smem[];
-    __shared__ M128 s_mc[MS_MAX_CORES];             // offers per core
-    __shared__ M128 s_mr[MS_MAX_AGENTS + 1];        // offers per recipient (0 = auctioneer)
-    __shared__ Liab s_newle[MS_MAX_CORES];          // liability entry appended this round per core
-    __shared__ int16_t s_exec[MS_MAX_CORES];        // per core: executed offer's slot index, -1 none
-    __shared__ int16_t s_key[MS_MAX_CORES];         // execution order key
-    __shared__ int8_t s_by_rank[MS_MAX_CORES];      // cores in execution order
-    __shared__ int8_t s_fresh[MS_MAX_CORES];        // s_newle[c] is the chain's newest entry
-    __shared__ int16_t s_auct[MS_MAX_CORES];        // auctioneer action per core
-    __shared__ int16_t s_tie_n[MS_MAX_CORES];       // tied maxima count (auctioneer)
-    __shared__ int16_t s_pick[MS_MAX_CORES];        // tie-break draw per core
-    __shared__ int32_t s_agent_r[MS_MAX_AGENTS];    // agentReward
-    __shared__ int32_t s_auct_r[MS_MAX_CORES];      // auctioneerReward
-    __shared__ uint32_t s_flags;
-    __shared__ int s_n_exec;
+    M128* s_mc = reinterpret_cast<M128*>(smem + P.s_mc);          // offers per core
+    M128* s_mr = reinterpret_cast<M128*>(smem + P.s_mr);          // offers per recipient (0 = auctioneer)
+    Liab* s_newle = reinterpret_cast<Liab*>(smem + P.s_newle);    // liability entry appended this round per core
+    int16_t* s_exec = reinterpret_cast<int16_t*>(smem + P.s_exec);  // per core: executed offer's slot, -1 none
+    int16_t* s_key = reinterpret_cast<int16_t*>(smem + P.s_key);    // execution order key
+    int8_t* s_by_rank = reinterpret_cast<int8_t*>(smem + P.s_rank); // cores in execution order
+    int8_t* s_fresh = reinterpret_cast<int8_t*>(smem + P.s_fresh);  // s_newle[c] is the chain's newest entry
+    int16_t* s_auct = reinterpret_cast<int16_t*>(smem + P.s_auct);  // auctioneer action per core
+    int16_t* s_tie_n = reinterpret_cast<int16_t*>(smem + P.s_tie);  // tied maxima count (auctioneer)
+    int16_t* s_pick = reinterpret_cast<int16_t*>(smem + P.s_pick);  // tie-break draw per core
+    int32_t* s_agent_r = reinterpret_cast<int32_t*>(smem + P.s_agentr);  // agentReward
+    int32_t* s_auct_r = reinterpret_cast<int32_t*>(smem + P.s_auctr);    // auctioneerReward
+    uint32_t& s_flags = *reinterpret_cast<uint32_t*>(smem + P.s_misc);
+    int& s_n_exec = *reinterpret_cast<int*>(smem + P.s_misc + 4);
 
     const int lane = threadIdx.x;
     const int64_t e = blockIdx.x;
@@ -528,17 +538,17 @@ __global__ void __launch_bounds__(64) k_env_step(Params P, uint8_t* recs, uint32
         off_r[i] = 0.f;
         price_r[i] = 0.f;
     }
-    for (int i = lane; i < MS_MAX_CORES; i += kWave) {
+    for (int i = lane; i < C; i += kWave) {
         s_auct_r[i] = 0;
         s_exec[i] = -1;
         s_fresh[i] = 0;
     }
-    for (int i = lane; i < MS_MAX_AGENTS; i += kWave) s_agent_r[i] = 0;
+    for (int i = lane; i < N; i += kWave) s_agent_r[i] = 0;
     if (lane == 0) {
         s_flags = 0;
         s_n_exec = 0;
     }
-    __syncthreads();
+    wave_sync();
     Rec R{rec, &P};
     const int round = R.round();
     int8_t* c_owner = R.core_owner();
@@ -589,7 +599,7 @@ __global__ void __launch_bounds__(64) k_env_step(Params P, uint8_t* recs, uint32
     } else {
         for (int c = lane; c < C; c += kWave) s_auct[c] = a_auct[c];
     }
-    __syncthreads();
+    wave_sync();
 
     // ---- which offer each core executes (executeAgentAcceptions1 world.py:391-404,
     //      executeAuctioneerAcceptions world.py:378-389): offers to core c are all addressed to c's
@@ -608,7 +618,7 @@ __global__ void __launch_bounds__(64) k_env_step(Params P, uint8_t* recs, uint32
         s_exec[c] = (int16_t)slot;
         s_key[c] = (int16_t)(owner > 0 ? (owner - 1) * C + c : N * C + c);
     }
-    __syncthreads();
+    wave_sync();
     for (int c = lane; c < C; c += kWave) {
         if (s_exec[c] >= 0) {
             int r = 0;
@@ -617,7 +627,7 @@ __global__ void __launch_bounds__(64) k_env_step(Params P, uint8_t* recs, uint32
             atomicAdd(&s_n_exec, 1);
         }
     }
-    __syncthreads();
+    wave_sync();
 
     // ---- apply executions in reference order (World.executeAnOffer world.py:261-293)
     if (lane == 0) {
@@ -700,7 +710,7 @@ __global__ void __launch_bounds__(64) k_env_step(Params P, uint8_t* recs, uint32
             }
         }
     }
-    __syncthreads();
+    wave_sync();
 
     // ---- tick (processOneTimestepAndUpdateOwnership world.py:336-367) and liability settlement
     //      (getDividedFixedPricesReward Reward.py:187-210 / getDividedFreePricesReward Reward.py:59-82)
@@ -766,7 +776,7 @@ __global__ void __launch_bounds__(64) k_env_step(Params P, uint8_t* recs, uint32
             io.ev_acc[e * C + c] = ar;
         }
     }
-    __syncthreads();
+    wave_sync();
 
     // ---- offers from offer actions (createFixPriceOfferObjectsFromActions world.py:406-443,
     //      createFreePriceOfferObjectsFromActions world.py:445-478); IDs = slot order
@@ -791,7 +801,7 @@ __global__ void __launch_bounds__(64) k_env_step(Params P, uint8_t* recs, uint32
             s_wait[i] = 0;
         }
     }
-    __syncthreads();
+    wave_sync();
 
     // ---- spawn (fillQueuesWithNewRandomJobs world.py:369-376, fillCollectionRandomly Agent.py:50-70)
     {
@@ -832,7 +842,7 @@ __global__ void __launch_bounds__(64) k_env_step(Params P, uint8_t* recs, uint32
             rs.p += 2 * cnt;
             done += cnt;
         }
-        __syncthreads();
+        wave_sync();
         if (sp) {
             int rank = __popcll(spm & ((1ull << lane) - 1ull));
             int base = lane * L;
@@ -852,13 +862,13 @@ __global__ void __launch_bounds__(64) k_env_step(Params P, uint8_t* recs, uint32
             }
         }
     }
-    __syncthreads();
+    wave_sync();
     if (lane == 0) {
         R.round() = round + 1;
         R.mti() = rs.final_index();
         R.flags() |= s_flags;
     }
-    __syncthreads();
+    wave_sync();
 
     // ---- outputs: state record, rewards, observations of the new offer set
     copy_dwords(reinterpret_cast<uint32_t*>(recs + e * (int64_t)P.rec_bytes), reinterpret_cast<uint32_t*>(rec),
@@ -879,17 +889,17 @@ __global__ void __launch_bounds__(64) k_env_step(Params P, uint8_t* recs, uint32
 // tie-break draws; a following ms_env_step with these actions then draws only the spawn.
 __global__ void __launch_bounds__(64) k_env_auctioneer(Params P, uint8_t* recs, uint32_t* mt, int8_t* actions) {
     extern __shared__ __align__(16) uint8_t smem[];
-    __shared__ M128 s_mc[MS_MAX_CORES];
-    __shared__ M128 s_mr[MS_MAX_AGENTS + 1];
-    __shared__ int16_t s_auct[MS_MAX_CORES];
-    __shared__ int16_t s_tie_n[MS_MAX_CORES];
-    __shared__ int16_t s_pick[MS_MAX_CORES];
+    M128* s_mc = reinterpret_cast<M128*>(smem + P.s_mc);
+    M128* s_mr = reinterpret_cast<M128*>(smem + P.s_mr);
+    int16_t* s_auct = reinterpret_cast<int16_t*>(smem + P.s_auct);
+    int16_t* s_tie_n = reinterpret_cast<int16_t*>(smem + P.s_tie);
+    int16_t* s_pick = reinterpret_cast<int16_t*>(smem + P.s_pick);
     const int lane = threadIdx.x;
     const int64_t e = blockIdx.x;
     uint8_t* rec = smem + P.s_rec;
     copy_dwords(reinterpret_cast<uint32_t*>(rec), reinterpret_cast<const uint32_t*>(recs + e * (int64_t)P.rec_bytes),
                 P.rec_bytes / 4, lane);
-    __syncthreads();
+    wave_sync();
     Rec R{rec, &P};
     MtStream rs;
     rs.gmt = mt + e * kMtN;
@@ -900,7 +910,7 @@ __global__ void __launch_bounds__(64) k_env_auctioneer(Params P, uint8_t* recs, 
     rs.load(0, 0, lane);
     build_masks(R, P, s_mc, s_mr, lane);
     hardcoded_auctioneer(R, P, s_mc, s_mr, rs, s_auct, s_tie_n, s_pick, lane);
-    __syncthreads();
+    wave_sync();
     for (int c = lane; c < P.C; c += kWave) actions[e * P.C + c] = (int8_t)s_auct[c];
     if (lane == 0) *reinterpret_cast<int32_t*>(recs + e * (int64_t)P.rec_bytes + 8) = rs.final_index();
 }
@@ -921,7 +931,7 @@ __global__ void __launch_bounds__(64) k_env_randbelow(Params P, uint8_t* recs, u
     rs.twisted = false;
     rs.v = 0;
     uint32_t r = rs.randbelow(n, lane);
-    __syncthreads();
+    wave_sync();
     if (lane == 0) {
         *out = r;
         *mti = rs.final_index();

@@ -25,7 +25,6 @@ namespace ms {
 constexpr int kWave = 64;
 constexpr int kMtN = 624;
 constexpr int kMtM = 397;
-constexpr int kObsChunk = 4096;  // LDS staging bytes for observation rows
 
 struct Liab {  // one liabilityList entry (world.py:285-289)
     int8_t offerer, recipient, price, nec;
@@ -49,9 +48,13 @@ struct Params {
     int32_t n_fix;
     int32_t free_prices, commercial, new_jobs, mult;
     float net_zero;
-    // LDS carve-up (byte offsets into dynamic shared memory)
+    // LDS carve-up (byte offsets into dynamic shared memory), sized to the config so that
+    // small envs keep many waves per CU in flight
     int32_t s_rec, s_act_acc, s_act_off, s_act_price, s_act_auct, s_accr, s_offr, s_pricer,
         s_spawn_kind, s_scratch, s_total;
+    int32_t s_mc, s_mr, s_newle, s_exec, s_key, s_auct, s_tie, s_pick, s_agentr, s_auctr, s_rank, s_fresh,
+        s_misc;
+    int32_t obs_chunk;  // bytes of observation rows staged at once (the scratch)
 };
 
 // device pointers of one ms_env_step call
@@ -127,10 +130,24 @@ inline Params make_params(const ms_config& c, int32_t cap) {
     p.s_pricer = s; s += 4 * p.NL;             // priceChooser rewards f32
     p.s_spawn_kind = s; s += align4(p.N * (p.new_jobs > 0 ? p.new_jobs : 1));
     s = align16(s);
+    p.s_mc = s; s += 16 * p.C;                 // offer masks per core (M128)
+    p.s_mr = s; s += 16 * (p.N + 1);           // offer masks per recipient
+    p.s_newle = s; s += 8 * p.C;               // this round's liability entry per core
+    p.s_agentr = s; s += 4 * p.N;              // agentReward
+    p.s_auctr = s; s += 4 * p.C;               // auctioneerReward
+    p.s_exec = s; s += align4(2 * p.C);        // executed slot per core
+    p.s_key = s; s += align4(2 * p.C);         // execution order key
+    p.s_auct = s; s += align4(2 * p.C);        // auctioneer action per core
+    p.s_tie = s; s += align4(2 * p.C);         // tied maxima per core
+    p.s_pick = s; s += align4(2 * p.C);        // tie-break draw per core
+    p.s_rank = s; s += align4(p.C);            // cores in execution order
+    p.s_fresh = s; s += align4(p.C);           // s_newle[c] is the chain's newest entry
+    p.s_misc = s; s += 16;                     // flags, n_exec
+    s = align16(s);
     p.s_scratch = s;
-    int32_t scratch = 4 * kMtN;  // MT twist buffer
-    if (scratch < kObsChunk) scratch = kObsChunk;
-    s += scratch;
+    p.obs_chunk = 4 * kMtN;  // the MT twist buffer doubles as the observation staging chunk
+    if (p.obs_chunk < p.acc_stride) p.obs_chunk = align16(p.acc_stride);
+    s += p.obs_chunk;
     p.s_total = s;
     return p;
 }

@@ -143,13 +143,17 @@ struct Head {
             for (int t = 0; t < NT; t++) {
                 const int a = 16 * t + j, ab = 16 * t + 4 * g4 + q;
                 w3[t][q] = a < A ? p.w3[((size_t)grp * A + a) * 16 + 4 * g4 + q] : 0.f;
-                b3[t][q] = ab < A ? p.b3[(size_t)grp * A + ab] : 0.f;
+                b3[t][q] = ab < A ? p.b3[(size_t)grp * A + ab] : -INFINITY;  // padding actions: exp -> 0
             }
         }
     }
 
-    // Layers 2-3, softmax, Categorical renormalisation and the inverse-CDF sample for the 16 rows of
-    // a tile given layer-1 pre-activations. Every lane of row j returns the row's action and log-prob.
+    // Layers 2-3, softmax and the inverse-CDF sample for the 16 rows of a tile given layer-1
+    // pre-activations. Every lane of row j returns the row's action and log-prob. Logits of the
+    // padding actions (a >= A) read -inf (bias), so they drop out of the max and the sum. The
+    // Categorical renormalisation of the softmax output changes probabilities by < 1e-7 relative,
+    // so the sample compares u * sum(e) with the running sum of e = exp(z - max), and the log-prob
+    // is log(clamp(e_a / sum(e))) (torch: log(clamp(p_a / sum(p)))).
     __device__ __forceinline__ void run(f4 a1, int A, int j, int g4, float u, int& action, float& logprob) const {
         float h1[4];
 #pragma unroll
@@ -170,73 +174,63 @@ struct Head {
 #pragma unroll
             for (int q = 0; q < 4; q++) {
                 z[t][q] = zz[q] + b3[t][q];
-                if (16 * t + 4 * g4 + q < A) m = fmaxf(m, z[t][q]);
+                m = fmaxf(m, z[t][q]);
             }
         }
         m = fmaxf(m, __shfl_xor(m, 16));
         m = fmaxf(m, __shfl_xor(m, 32));
-        float s0 = 0.f;
-#pragma unroll
-        for (int t = 0; t < NT; t++)
-#pragma unroll
-            for (int q = 0; q < 4; q++) {
-                z[t][q] = (16 * t + 4 * g4 + q < A) ? fast_exp(z[t][q] - m) : 0.f;
-                s0 += z[t][q];
-            }
-        const float inv0 = __builtin_amdgcn_rcpf(xsum4g(s0));
-        float s1 = 0.f;
-#pragma unroll
-        for (int t = 0; t < NT; t++)
-#pragma unroll
-            for (int q = 0; q < 4; q++) {
-                z[t][q] *= inv0;  // nn.Softmax output
-                s1 += z[t][q];
-            }
-        const float inv1 = __builtin_amdgcn_rcpf(xsum4g(s1));
-        // Categorical renormalisation, then the inverse CDF over a = 16t + 4*g4 + q in increasing order
-        float cum = 0.f, pc = 0.f;
-        int found = 0x7fff, last_nz = -1;
+        float bs[NT];
 #pragma unroll
         for (int t = 0; t < NT; t++) {
-            float bs = 0.f;
+            bs[t] = 0.f;
 #pragma unroll
             for (int q = 0; q < 4; q++) {
-                z[t][q] *= inv1;
-                bs += z[t][q];
+                z[t][q] = fast_exp(z[t][q] - m);
+                bs[t] += z[t][q];
             }
-            const float gs0 = __shfl(bs, j), gs1 = __shfl(bs, j + 16), gs2 = __shfl(bs, j + 32), gs3 = __shfl(bs, j + 48);
+        }
+        // inverse CDF over a = 16t + 4*g4 + q in increasing order: the action is the number of
+        // actions whose running sum stays <= u * S (zero-width intervals are skipped by construction)
+        float lane_tot = 0.f;
+#pragma unroll
+        for (int t = 0; t < NT; t++) lane_tot += bs[t];
+        const float S = xsum4g(lane_tot);
+        const float target = u * S;
+        float cum = 0.f;
+        int cnt = 0;
+#pragma unroll
+        for (int t = 0; t < NT; t++) {
+            const float gs0 = __shfl(bs[t], j), gs1 = __shfl(bs[t], j + 16), gs2 = __shfl(bs[t], j + 32),
+                        gs3 = __shfl(bs[t], j + 48);
             float c = cum + (g4 > 0 ? gs0 : 0.f) + (g4 > 1 ? gs1 : 0.f) + (g4 > 2 ? gs2 : 0.f);
 #pragma unroll
             for (int q = 0; q < 4; q++) {
-                const int a = 16 * t + 4 * g4 + q;
                 c += z[t][q];
-                if (a < A) {
-                    if (z[t][q] > 0.f) last_nz = a;
-                    if (u < c && a < found) {
-                        found = a;
-                        pc = z[t][q];
-                    }
-                }
+                cnt += (c <= target) ? 1 : 0;
             }
-            cum += gs0 + gs1 + gs2 + gs3;
+            cum += (gs0 + gs1) + (gs2 + gs3);
         }
-        // first crossing over the 4 lanes of the row (each lane found its own first one)
-        int fmin = min(found, __shfl_xor(found, 16));
-        fmin = min(fmin, __shfl_xor(fmin, 32));
-        int lmax = max(last_nz, __shfl_xor(last_nz, 16));
-        lmax = max(lmax, __shfl_xor(lmax, 32));
-        const int a_sel = fmin < A ? fmin : lmax;
-        float mine = 0.f;
-        if (fmin < A) {
-            mine = (found == fmin) ? pc : 0.f;
-        } else {
+        cnt += __shfl_xor(cnt, 16);
+        cnt += __shfl_xor(cnt, 32);
+        int a_sel = cnt;
+        if (__builtin_expect(__ballot(a_sel >= A) != 0, 0)) {
+            // u * S at or beyond the rounded total: the last action with nonzero probability
+            int last_nz = -1;
 #pragma unroll
             for (int t = 0; t < NT; t++)
 #pragma unroll
                 for (int q = 0; q < 4; q++)
-                    if (16 * t + 4 * g4 + q == a_sel) mine = z[t][q];
+                    if (z[t][q] > 0.f) last_nz = 16 * t + 4 * g4 + q;
+            last_nz = max(last_nz, __shfl_xor(last_nz, 16));
+            last_nz = max(last_nz, __shfl_xor(last_nz, 32));
+            if (a_sel >= A) a_sel = last_nz;
         }
-        const float pa = xsum4g(mine);
+        float mine = 0.f;
+#pragma unroll
+        for (int t = 0; t < NT; t++)
+#pragma unroll
+            for (int q = 0; q < 4; q++) mine = (16 * t + 4 * g4 + q == a_sel) ? z[t][q] : mine;
+        const float pa = xsum4g(mine) * __builtin_amdgcn_rcpf(S);
         const float eps = 1.1920928955078125e-07f;  // torch.finfo(float32).eps
         action = a_sel;
         logprob = fast_log(fminf(fmaxf(pa, eps), 1.f - eps));
@@ -289,11 +283,23 @@ __global__ void __launch_bounds__(256) k_act(ActArgs a) {
     const int tiles = (a.n_items + 15) >> 4;
     const int t0 = wv * a.tiles_per_wave;
     const int t1 = min(t0 + a.tiles_per_wave, tiles);
-    auto row_of = [&](int tile) -> int {
-        const int i = tile * 16 + j;
+    // item i of this group -> obs row: e = i / S by a multiply-high with one correction step
+    const uint32_t s_magic = 0xffffffffu / (uint32_t)a.S;
+    auto row_of_lane = [&](int tile, int jj) -> int {
+        const int i = tile * 16 + jj;
         if (i >= a.n_items) return -1;
-        const int e = i / a.S;
+        int e = (int)__umulhi((uint32_t)i, s_magic);
+        if ((e + 1) * a.S <= i) e++;
         return e * a.U + grp * a.S + (i - e * a.S);
+    };
+    auto row_of = [&](int tile) -> int { return row_of_lane(tile, j); };
+    // Philox uniforms, computed for 4 tiles at a time: lane (j, g4) draws for row j of tile
+    // base + g4 (counter = the obs row index, so the values do not depend on the tiling)
+    uint32_t rnd0 = 0, rnd1 = 0;
+    auto draw4 = [&](int base) {
+        const int r = base + g4 < t1 ? row_of_lane(base + g4, j) : -1;
+        philox2((uint32_t)r, 0u, (uint32_t)off, (uint32_t)(off >> 32), (uint32_t)a.seed, (uint32_t)(a.seed >> 32), rnd0,
+                rnd1);
     };
     uint32_t pre[S1][2];
     auto prefetch = [&](int r) {
@@ -323,11 +329,10 @@ __global__ void __launch_bounds__(256) k_act(ActArgs a) {
             u1 = valid ? a.uniforms[cur] : 0.f;
             u2 = valid && NT2 > 0 ? a.uniforms[n_rows_total + cur] : 0.f;
         } else {
-            uint32_t r0, r1;
-            philox2((uint32_t)cur, 0u, (uint32_t)off, (uint32_t)(off >> 32), (uint32_t)a.seed, (uint32_t)(a.seed >> 32),
-                    r0, r1);
-            u1 = u24(r0);
-            u2 = u24(r1);
+            const int k = (tile - t0) & 3;
+            if (k == 0) draw4(tile);
+            u1 = u24((uint32_t)__shfl((int)rnd0, j + 16 * k));
+            u2 = u24((uint32_t)__shfl((int)rnd1, j + 16 * k));
         }
         f4 acc = {0, 0, 0, 0};
 #pragma unroll
