@@ -1,10 +1,13 @@
 // env_kernels.hip — the batched marl-scheduling round as one HIP kernel for gfx950.
 //
-// One 64-lane wave steps one env replica per round. The env's packed state
-// record (ms_layout.h) is staged in LDS and the round runs as wave-parallel
-// phases. The offer set of a round (at most N*L <= 126 offers, one per slot,
-// offer-ID order = slot order) is indexed by 128-bit masks, one per core and
-// one per recipient, built with LDS atomic ORs: every ordered selection of the
+// A group of LPE lanes (a power of two >= max(C, N); 64 / LPE groups per
+// 64-lane wave) steps one env replica per round, so the wave's scalar control
+// flow and the lane-serial parts (the offer executions, the MT19937 draws) are
+// shared by several envs. The env's packed state record (ms_layout.h) is staged
+// in the group's LDS slice and the round runs as group-parallel phases. The
+// offer set of a round (at most N*L <= 126 offers, one per slot, offer-ID
+// order = slot order) is indexed by 128-bit masks, one per core and one per
+// recipient, built with LDS atomic ORs: every ordered selection of the
 // reference — the idx-th offer of (recipient, core) behind an acceptor action,
 // the auctioneer's tied maxima, the offers listed in an acceptor observation —
 // is a walk over the set bits of mask(core) & mask(recipient). The loads the
@@ -15,6 +18,7 @@
 // (paths relative to /root/reference/src) are cited per phase; the CPU
 // restatement that checks this kernel bit-for-bit is oracle/ms_oracle.c.
 #include <hip/hip_runtime.h>
+#include <string.h>
 
 #include "ms_layout.h"
 
@@ -30,8 +34,39 @@ __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// Phase timing for the separate profiling build only (tools/build_phase_probe.sh defines
+// MS_PHASE_TIMING): lane 0 of every wave adds the cycles since the previous mark to a per-phase
+// counter. The product library is built without it and the marks compile to nothing.
+#ifdef MS_PHASE_TIMING
+constexpr int kProbeSlots = 65536;
+__device__ unsigned long long g_phase_cycles[kProbeSlots][16];  // per block, summed on the host
+#define MS_MARK(k)                                                     \
+    do {                                                               \
+        const uint64_t t_now = __builtin_amdgcn_s_memtime();          \
+        t_acc[k] += t_now - t_prev;                                    \
+        t_prev = t_now;                                                \
+    } while (0)
+#else
+#define MS_MARK(k) \
+    do {           \
+    } while (0)
+#endif
+
+// The LPE lanes of one env within the wave.
+template <int LPE>
+struct Lanes {
+    int gl;     // lane within the group
+    int gbase;  // the group's first lane in the wave
+    __device__ explicit Lanes(int lane) : gl(lane & (LPE - 1)), gbase(lane & ~(LPE - 1)) {}
+    __device__ __forceinline__ uint64_t ballot(bool p) const {
+        const uint64_t m = __ballot(p);
+        return LPE == 64 ? m : (m >> gbase) & ((1ull << (LPE & 63)) - 1ull);
+    }
+    __device__ __forceinline__ uint32_t shfl(uint32_t v, int src) const { return (uint32_t)__shfl((int)v, gbase + src); }
+};
+
 // ---------------------------------------------------------------------------
-// CPython MT19937 (Modules/_randommodule.c) — tempering and wave-cooperative twist
+// CPython MT19937 (Modules/_randommodule.c) — tempering and group-cooperative twist
 
 __device__ __forceinline__ uint32_t mt_temper(uint32_t y) {
     y ^= (y >> 11);
@@ -41,86 +76,96 @@ __device__ __forceinline__ uint32_t mt_temper(uint32_t y) {
     return y;
 }
 
-// In-place twist of 624 words held in LDS by one wave. The three parallel
-// phases respect the sequential recurrence: words [0,227) read only old words,
-// [227,454) read new [0,227), [454,623) read new [227,396), 623 reads new 0/396.
-__device__ void mt_twist_lds(uint32_t* mt, int lane) {
-    auto step = [&](int i, uint32_t hi_src, uint32_t lo_src, uint32_t xsrc) -> uint32_t {
-        uint32_t y = (hi_src & 0x80000000u) | (lo_src & 0x7fffffffu);
+// In-place twist of the env's 624 state words in HBM by one lane group (once per ~39 rounds of
+// an env). The three phases respect the sequential recurrence: words [0,227) read only old
+// words, [227,454) read new [0,227), [454,623) read new [227,396), 623 reads new 0/396. Inside a
+// phase a chunk of LPE words is computed from old words (i, i+1 not yet written), then stored.
+// The loads bypass the CU's L1 (agent-scope relaxed atomics: they read the XCD's L2, where this
+// wave's stores land) and workgroup-scope fences order each chunk's stores before the group's
+// next loads. (An agent-scope fence would write the whole L2 back to make it visible to the
+// other XCDs, which nothing here needs.)
+__device__ __forceinline__ uint32_t mt_ld(const uint32_t* p) {
+    return __hip_atomic_load(const_cast<uint32_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void mt_st(uint32_t* p, uint32_t v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+template <int LPE>
+__device__ void mt_twist_global(uint32_t* mt, int gl) {
+    auto step = [](uint32_t hi_src, uint32_t lo_src, uint32_t xsrc) -> uint32_t {
+        const uint32_t y = (hi_src & 0x80000000u) | (lo_src & 0x7fffffffu);
         return xsrc ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
     };
     const int ranges[3][2] = {{0, kMtN - kMtM}, {kMtN - kMtM, 2 * (kMtN - kMtM)}, {2 * (kMtN - kMtM), kMtN - 1}};
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
     for (int ph = 0; ph < 3; ph++) {
-        uint32_t v[4];
-        int cnt = 0;
-        for (int i = ranges[ph][0] + lane; i < ranges[ph][1]; i += kWave) {
-            int x = (ph == 0) ? i + kMtM : i + (kMtM - kMtN);
-            v[cnt++] = step(i, mt[i], mt[i + 1], mt[x]);
+        for (int c0 = ranges[ph][0]; c0 < ranges[ph][1]; c0 += LPE) {
+            const int i = c0 + gl;
+            uint32_t v = 0;
+            if (i < ranges[ph][1]) {
+                const int x = (ph == 0) ? i + kMtM : i + (kMtM - kMtN);
+                v = step(mt_ld(mt + i), mt_ld(mt + i + 1), mt_ld(mt + x));
+            }
+            __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+            if (i < ranges[ph][1]) mt_st(mt + i, v);
+            __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
         }
-        wave_sync();
-        cnt = 0;
-        for (int i = ranges[ph][0] + lane; i < ranges[ph][1]; i += kWave) mt[i] = v[cnt++];
-        wave_sync();
     }
-    if (lane == 0) mt[kMtN - 1] = step(kMtN - 1, mt[kMtN - 1], mt[0], mt[kMtM - 1]);
-    wave_sync();
+    if (gl == 0) mt_st(mt + kMtN - 1, step(mt_ld(mt + kMtN - 1), mt_ld(mt), mt_ld(mt + kMtM - 1)));
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
 }
 
-// A 64-word window of the env's stream held one word per lane. Stream
-// positions are relative to the env's mti at kernel entry; positions at or
-// beyond 624 - mti0 come from the twisted state (computed at most once per
-// launch, only when a consumer actually needs such a word, so the stored
-// state always equals CPython's after the same draws).
+// A window of LPE words of the env's stream held one word per group lane. Stream positions are
+// relative to the env's mti at kernel entry; positions at or beyond 624 - mti0 come from the
+// twisted state, computed at most once per launch and only when a consumer actually needs such
+// a word, so the stored state always equals CPython's after the same draws.
+template <int LPE>
 struct MtStream {
     uint32_t* gmt;    // env's 624 state words in HBM
-    uint32_t* lds;    // 624-word LDS scratch (valid after the twist)
     int mti0;         // mti at entry
     int wb, wend;     // window covers stream positions [wb, wend)
     int p;            // next unconsumed stream position
     bool twisted;
-    uint32_t v;       // this lane's tempered word (position wb + lane)
+    bool store;       // false for a padding group: never twist (its draws are discarded)
+    uint32_t v;       // this lane's tempered word (position wb + gl)
 
-    // Window at stream position pos. need = words the caller is about to
-    // consume; need == 0 only peeks (never twists; the window may be empty).
-    __device__ void load(int pos, int need, int lane) {
-        int limit = twisted ? 0x3fffffff : (kMtN - mti0);  // old words end here
+    // Window at stream position pos. need = words the caller is about to consume; need == 0
+    // only peeks (never twists; the window may be empty).
+    __device__ void load(int pos, int need, const Lanes<LPE>& L) {
+        const int limit = twisted ? 0x3fffffff : (kMtN - mti0);  // old words end here
+        const int g = mti0 + pos + L.gl;
         if (!twisted && need > 0 && pos + need > limit) {
-            // read the old words of this window before the state is replaced
-            int g = mti0 + pos + lane;
-            uint32_t old = (g < kMtN) ? gmt[g] : 0u;
-            for (int i = lane; i < kMtN; i += kWave) lds[i] = gmt[i];
-            wave_sync();
-            mt_twist_lds(lds, lane);
-            for (int i = lane; i < kMtN; i += kWave) gmt[i] = lds[i];
+            const uint32_t old = (g < kMtN) ? gmt[g] : 0u;  // old words of this window
+            if (store) mt_twist_global<LPE>(gmt, L.gl);
             twisted = true;
-            v = mt_temper((g < kMtN) ? old : lds[g - kMtN]);
+            v = mt_temper((g < kMtN) ? old : (g < 2 * kMtN ? mt_ld(gmt + g - kMtN) : 0u));
             wb = pos;
-            wend = pos + kWave;
+            wend = pos + LPE;
             return;
         }
-        int g = mti0 + pos + lane;
         uint32_t raw = 0;
         if (twisted)
-            raw = (g >= kMtN && g < 2 * kMtN) ? lds[g - kMtN] : 0u;
+            raw = (g >= kMtN && g < 2 * kMtN) ? mt_ld(gmt + g - kMtN) : 0u;
         else if (g < kMtN)
             raw = gmt[g];
         v = mt_temper(raw);
         wb = pos;
-        wend = twisted ? pos + kWave : min(pos + kWave, limit);
+        wend = twisted ? pos + LPE : min(pos + LPE, limit);
     }
 
-    // Random._randbelow_with_getrandbits(n) (random.py:239-249), wave-uniform result
-    __device__ uint32_t randbelow(uint32_t n, int lane) {
-        int k = 32 - __clz(n);  // n.bit_length()
-        int sh = 32 - k;
+    // Random._randbelow_with_getrandbits(n) (random.py:239-249), group-uniform result
+    __device__ uint32_t randbelow(uint32_t n, const Lanes<LPE>& L) {
+        const int k = 32 - __clz(n);  // n.bit_length()
+        const int sh = 32 - k;
         for (;;) {
-            if (p >= wend) load(p, 1, lane);
-            int pos = wb + lane;
-            bool ok = pos >= p && pos < wend && ((v >> sh) < n);
-            uint64_t m = __ballot(ok);
+            if (p >= wend) load(p, 1, L);
+            const int pos = wb + L.gl;
+            const bool ok = pos >= p && pos < wend && ((v >> sh) < n);
+            const uint64_t m = L.ballot(ok);
             if (m) {
-                int q = __ffsll((unsigned long long)m) - 1;
-                uint32_t r = __shfl(v, q) >> sh;
+                const int q = __ffsll((unsigned long long)m) - 1;
+                const uint32_t r = L.shfl(v, q) >> sh;
                 p = wb + q + 1;
                 return r;
             }
@@ -138,6 +183,11 @@ struct MtStream {
 struct Rec {
     uint8_t* b;
     const Params* P;
+    const int32_t* kt;  // kind tables in LDS: prio[16], len[16], fix[16] (per-lane lookups must not
+                        // index the kernel-argument struct: that is a memory load per access)
+    __device__ int prio(int k) const { return kt[k]; }
+    __device__ int len(int k) const { return kt[16 + k]; }
+    __device__ int fix(int k) const { return kt[32 + k]; }
     __device__ int32_t& round() { return *reinterpret_cast<int32_t*>(b + 0); }
     __device__ uint32_t& flags() { return *reinterpret_cast<uint32_t*>(b + 4); }
     __device__ int32_t& mti() { return *reinterpret_cast<int32_t*>(b + 8); }
@@ -155,8 +205,34 @@ struct Rec {
     __device__ int32_t* slot_birth() { return reinterpret_cast<int32_t*>(b + P->o_slot_birth); }
 };
 
-__device__ __forceinline__ void copy_dwords(uint32_t* dst, const uint32_t* src, int n, int lane) {
-    for (int i = lane; i < n; i += kWave) dst[i] = src[i];
+// the kind tables of Params copied to LDS once per wave (read back by every group)
+__device__ __forceinline__ void load_kind_tables(const Params& P, int32_t* kt, int lane) {
+    if (lane < 16) {
+        kt[lane] = P.prio[lane];
+        kt[16 + lane] = P.len[lane];
+        kt[32 + lane] = P.fix[lane];
+    }
+}
+
+template <int LPE>
+__device__ __forceinline__ void copy_dwords(uint32_t* dst, const uint32_t* src, int n, int gl) {
+#pragma unroll 8
+    for (int i = gl; i < n; i += LPE) dst[i] = src[i];
+}
+
+// n bytes from global src to LDS dst: dword loads when both sides allow (issued together, then
+// the LDS stores), else byte loads. LDS destinations are 4-byte aligned (ms_layout.h).
+template <int LPE>
+__device__ __forceinline__ void stage_bytes(int8_t* dst, const int8_t* src, int n, int gl) {
+    if ((n & 3) == 0 && (reinterpret_cast<uintptr_t>(src) & 3) == 0) {
+        const uint32_t* s4 = reinterpret_cast<const uint32_t*>(src);
+        uint32_t* d4 = reinterpret_cast<uint32_t*>(dst);
+#pragma unroll 4
+        for (int i = gl; i < n / 4; i += LPE) d4[i] = s4[i];
+    } else {
+#pragma unroll 4
+        for (int i = gl; i < n; i += LPE) dst[i] = src[i];
+    }
 }
 
 // calculateRewardRatio (HardcodedModules.py:5-13) as an exact fraction; the
@@ -219,14 +295,15 @@ __device__ __forceinline__ void mask_set(M128* m, int i) {
 }
 
 // Masks of the current offers: mc[c] = offers to core c, mr[r] = offers to
-// recipient r (0 = auctioneer). Ends with a barrier.
-__device__ void build_masks(Rec& R, const Params& P, M128* mc, M128* mr, int lane) {
-    for (int i = lane; i < P.C; i += kWave) mc[i] = M128{0, 0};
-    for (int i = lane; i <= P.N; i += kWave) mr[i] = M128{0, 0};
+// recipient r (0 = auctioneer). Ends with a phase boundary.
+template <int LPE>
+__device__ void build_masks(Rec& R, const Params& P, M128* mc, M128* mr, int gl) {
+    for (int i = gl; i < P.C; i += LPE) mc[i] = M128{0, 0};
+    for (int i = gl; i <= P.N; i += LPE) mr[i] = M128{0, 0};
     wave_sync();
     const int8_t* oc = R.offer_core();
     const int8_t* orc = R.offer_recip();
-    for (int i = lane; i < P.NL; i += kWave) {
+    for (int i = gl; i < P.NL; i += LPE) {
         const int c = oc[i];
         if (c >= 0) {
             mask_set(&mc[c], i);
@@ -240,120 +317,150 @@ __device__ void build_masks(Rec& R, const Params& P, M128* mc, M128* mr, int lan
 // observations of the current (LDS) state: Agent.py:167-212 (acceptor),
 // Agent.py:271-300 (offer), Auctioneer.py:34-77 (auctioneer)
 
-// One acceptor/auctioneer row over a scratch row prefilled with -2 bytes.
-__device__ __forceinline__ void acceptor_row(Rec& R, const Params& P, const M128* mc, const M128* mr, int recipient,
-                                             int c, int8_t* row) {
-    const bool own = R.core_owner()[c] == recipient;
-    const int kind = R.core_kind()[c];
-    row[0] = own ? 1 : 0;
-    row[1] = (int8_t)(own ? (kind >= 0 ? P.prio[kind] : -1) : -1);
-    row[2] = (int8_t)(own ? R.core_rem()[c] : -1);
-    const int8_t* op = R.offer_price();
-    const int8_t* sr = R.slot_rem();
-    int w = 3;
-    for (MaskIter it(mand(mc[c], mr[recipient])); it.more();) {  // (price, necT) in offer-ID order
-        const int i = it.next();
-        row[w] = op[i];
-        row[w + 1] = sr[i];
-        w += 2;
+// Observations. At emission time every offer to core c is addressed to c's owner: offers are
+// created after the tick with recipient = the core's owner (world.py:428) and ownership changes
+// only in the next round's executions (ms_env_import checks the same invariant). So the acceptor
+// row of (agent a, core c) (Agent.py:167-212) is the core's "owner row"
+//   [1, prio, rem, (price, necT) per offer to c in offer-ID order, (-2, -2) pad, 0 stride pad]
+// when a owns c, and otherwise the constant "foreign row" [0, -1, -1, (-2, -2) * O, 0 pad]; the
+// auctioneer row of core c (Auctioneer.py:34-77) is the same with the auctioneer as owner.
+// The C owner rows are built in LDS, then every output row is streamed with one dword store
+// per lane (the group's lanes cover one row's dwords).
+
+// dword k of the foreign row
+__device__ __forceinline__ uint32_t foreign_dword(int k, int d_acc) {
+    uint32_t w = 0;
+#pragma unroll
+    for (int b = 0; b < 4; b++) {
+        const int col = 4 * k + b;
+        const uint32_t v = col == 0 ? 0x00u : (col < 3 ? 0xFFu : (col < d_acc ? 0xFEu : 0x00u));
+        w |= v << (8 * b);
     }
-    for (int z = P.d_acc; z < P.acc_stride; z++) row[z] = 0;
+    return w;
 }
 
-// Acceptor rows (KIND 0, row g = agent g / C, core g % C) or auctioneer rows
-// (KIND 2, row g = core g), staged in LDS chunks and streamed to dst.
-template <int KIND>
-__device__ void emit_acc_rows(Rec& R, const Params& P, const M128* mc, const M128* mr, uint8_t* scratch, int8_t* dst,
-                              int n_rows, int lane) {
-    if (!dst) return;
-    const int stride = P.acc_stride;
-    const int per_chunk = P.obs_chunk / stride;
-    uint32_t* sw = reinterpret_cast<uint32_t*>(scratch);
-    for (int r0 = 0; r0 < n_rows; r0 += per_chunk) {
-        const int nr = min(per_chunk, n_rows - r0);
-        const int nd = nr * stride / 4;
-        for (int i = lane; i < nd; i += kWave) sw[i] = 0xFEFEFEFEu;  // -2 pads
-        wave_sync();
-        for (int r = lane; r < nr; r += kWave) {
-            const int g = r0 + r;
-            int8_t* row = reinterpret_cast<int8_t*>(scratch) + r * stride;
-            if (KIND == 0)
-                acceptor_row(R, P, mc, mr, g / P.C + 1, g - (g / P.C) * P.C, row);
-            else
-                acceptor_row(R, P, mc, mr, 0, g, row);
+// The owner rows of all C cores in LDS ([C][acc_stride] bytes), built by the core lanes.
+template <int LPE>
+__device__ void build_owner_rows(Rec& R, const Params& P, const M128* mc, const M128* mr, uint32_t* crow, int gl) {
+    const int nw = P.acc_stride / 4;
+    for (int i = gl; i < P.C * nw; i += LPE) {
+        const int k = i - (i / nw) * nw;
+        crow[i] = foreign_dword(k, P.d_acc);
+    }
+    wave_sync();
+    for (int c = gl; c < P.C; c += LPE) {
+        int8_t* row = reinterpret_cast<int8_t*>(crow) + c * P.acc_stride;
+        const int kind = R.core_kind()[c];
+        row[0] = 1;
+        row[1] = (int8_t)(kind >= 0 ? R.prio(kind) : -1);
+        row[2] = R.core_rem()[c];
+        const int8_t* op = R.offer_price();
+        const int8_t* sr = R.slot_rem();
+        int w = 3;
+        for (MaskIter it(mand(mc[c], mr[R.core_owner()[c]])); it.more();) {
+            const int i = it.next();
+            row[w] = op[i];
+            row[w + 1] = sr[i];
+            w += 2;
         }
-        wave_sync();
-        copy_dwords(reinterpret_cast<uint32_t*>(dst + (size_t)r0 * stride), sw, nd, lane);
-        wave_sync();
+    }
+    wave_sync();
+}
+
+// Acceptor rows [N][C] (auct == false) or auctioneer rows [C] (auct == true) of one env.
+template <int LPE>
+__device__ void emit_acc_rows(Rec& R, const Params& P, const uint32_t* crow, int8_t* dst, bool auct, int gl) {
+    if (!dst) return;
+    const int C = P.C, nw = P.acc_stride / 4;
+    uint32_t* out = reinterpret_cast<uint32_t*>(dst);
+    const int8_t* owner = R.core_owner();
+    const int n_agents = auct ? 1 : P.N;
+    for (int k0 = 0; k0 < nw; k0 += LPE) {  // dword columns of a row covered by the group
+        const int k = k0 + gl;
+        const bool lane_on = k < nw;
+        const uint32_t fw = foreign_dword(k, P.d_acc);
+#pragma unroll 4
+        for (int c = 0; c < C; c++) {
+            const int oc = owner[c];                       // group-uniform LDS broadcast
+            const uint32_t cw = crow[c * nw + (lane_on ? k : 0)];
+            for (int a = 0; a < n_agents; a++) {
+                const int who = auct ? 0 : a + 1;
+                if (lane_on) out[(a * C + c) * nw + k] = oc == who ? cw : fw;
+            }
+        }
     }
 }
 
-// Offer rows: the (prio, rem) pairs of all cores — the same for every row of
-// the env — then the slot's own pair, zero padded to the stride. Built one
-// dword per lane (strides are multiples of 4, so a dword never spans rows).
-__device__ void emit_off_rows(Rec& R, const Params& P, uint8_t* scratch, int8_t* dst, int lane) {
+// Offer rows [N][L] (Agent.py:271-300): the (prio, rem) pairs of all cores — the same for every
+// row of the env — then the slot's own pair, zero padded to the stride. Each lane owns one dword
+// column: the core-pair bytes of its column are computed once, the slot pair merged per row.
+template <int LPE>
+__device__ void emit_off_rows(Rec& R, const Params& P, uint16_t* slot_pair, int8_t* dst, int gl) {
     if (!dst) return;
-    const int stride = P.off_stride;
-    const int per_chunk = P.obs_chunk / stride;
+    const int C = P.C, nw = P.off_stride / 4;
     const int8_t* ck = R.core_kind();
     const int8_t* cr = R.core_rem();
-    const int8_t* sk = R.slot_kind();
-    const int8_t* srem = R.slot_rem();
-    uint32_t* sw = reinterpret_cast<uint32_t*>(scratch);
-    for (int r0 = 0; r0 < P.NL; r0 += per_chunk) {
-        const int nr = min(per_chunk, P.NL - r0);
-        const int nd = nr * stride / 4;
-        for (int d = lane; d < nd; d += kWave) {
-            const int r = (4 * d) / stride;
-            const int col0 = 4 * d - r * stride;
-            const int s = r0 + r;
-            uint32_t word = 0;
+    for (int s = gl; s < P.NL; s += LPE) {  // the slot pairs, once
+        const int k = R.slot_kind()[s];
+        const uint32_t pr = (uint8_t)(k < 0 ? -1 : R.prio(k));
+        const uint32_t rm = (uint8_t)(k < 0 ? -1 : R.slot_rem()[s]);
+        slot_pair[s] = (uint16_t)(pr | (rm << 8));
+    }
+    wave_sync();
+    uint32_t* out = reinterpret_cast<uint32_t*>(dst);
+    for (int k0 = 0; k0 < nw; k0 += LPE) {
+        const int k = k0 + gl;
+        const bool lane_on = k < nw;
+        uint32_t cw = 0;  // core-pair bytes of this dword column
 #pragma unroll
-            for (int b = 0; b < 4; b++) {
-                const int col = col0 + b;
-                int v = 0;
-                if (col < 2 * P.C) {
-                    const int c = col >> 1, k = ck[c];
-                    v = k < 0 ? -1 : ((col & 1) ? cr[c] : P.prio[k]);
-                } else if (col < P.d_off) {
-                    const int k = sk[s];
-                    v = k < 0 ? -1 : ((col & 1) ? srem[s] : P.prio[k]);
-                }
-                word |= (uint32_t)(uint8_t)v << (8 * b);
+        for (int b = 0; b < 4; b++) {
+            const int col = 4 * k + b;
+            if (lane_on && col < 2 * C) {
+                const int c = col >> 1, kk = ck[c];
+                const int v = kk < 0 ? -1 : ((col & 1) ? cr[c] : R.prio(kk));
+                cw |= (uint32_t)(uint8_t)v << (8 * b);
             }
-            sw[d] = word;
         }
-        wave_sync();
-        copy_dwords(reinterpret_cast<uint32_t*>(dst + (size_t)r0 * stride), sw, nd, lane);
-        wave_sync();
+        const int off = 2 * C - 4 * k;  // byte position of the slot pair in this dword (0 or 2 if here)
+#pragma unroll 4
+        for (int s = 0; s < P.NL; s++) {
+            uint32_t w = cw;
+            if (off == 0 || off == 2) w |= (uint32_t)slot_pair[s] << (8 * off);
+            if (lane_on) out[s * nw + k] = w;
+        }
     }
 }
 
+// All observations of env e (dst == NULL skips a kind; a padding group passes write = false).
+template <int LPE>
 __device__ void emit_obs(Rec& R, const Params& P, const M128* mc, const M128* mr, uint8_t* scratch, int8_t* acc,
-                         int8_t* off, int8_t* auct, int64_t e, int lane) {
-    emit_acc_rows<0>(R, P, mc, mr, scratch, acc ? acc + e * (int64_t)P.N * P.C * P.acc_stride : nullptr, P.N * P.C,
-                     lane);
-    emit_off_rows(R, P, scratch, off ? off + e * (int64_t)P.NL * P.off_stride : nullptr, lane);
-    emit_acc_rows<2>(R, P, mc, mr, scratch, auct ? auct + e * (int64_t)P.C * P.acc_stride : nullptr, P.C, lane);
+                         int8_t* off, int8_t* auct, int64_t e, bool write, int gl) {
+    uint32_t* crow = reinterpret_cast<uint32_t*>(scratch);
+    uint16_t* slot_pair = reinterpret_cast<uint16_t*>(scratch + P.s_slotpair);
+    if (acc || auct) build_owner_rows<LPE>(R, P, mc, mr, crow, gl);
+    if (acc) emit_acc_rows<LPE>(R, P, crow, write ? acc + e * (int64_t)P.N * P.C * P.acc_stride : nullptr, false, gl);
+    if (auct) emit_acc_rows<LPE>(R, P, crow, write ? auct + e * (int64_t)P.C * P.acc_stride : nullptr, true, gl);
+    if (off) emit_off_rows<LPE>(R, P, slot_pair, write ? off + e * (int64_t)P.NL * P.off_stride : nullptr, gl);
 }
 
 // HardcodedAuctioneerAcceptor.selectAction for every core (HardcodedModules.py:54-78,
 // Auctioneer.getAuctioneerAction Auctioneer.py:95-102) on the staged state: per core the max
-// ratio over the auctioneer's offers and the count of offers attaining it, then one
-// _randbelow(count) per tied core in core order on the env stream. Writes s_auct[c] (O = reject).
-__device__ void hardcoded_auctioneer(Rec& R, const Params& P, const M128* s_mc, const M128* s_mr, MtStream& rs,
-                                     int16_t* s_auct, int16_t* s_tie_n, int16_t* s_pick, int lane) {
-    const int C = P.C, O = P.O;
+// ratio over the auctioneer's offers and the count of offers attaining it (in registers), then
+// one _randbelow(count) per tied core in core order on the env stream. Writes s_auct[c] (O = reject).
+// Needs LPE >= C (group lane c owns core c).
+template <int LPE>
+__device__ void hardcoded_auctioneer(Rec& R, const Params& P, const M128* s_mc, const M128* s_mr, MtStream<LPE>& rs,
+                                     int16_t* s_auct, const Lanes<LPE>& L) {
+    const int C = P.C, O = P.O, gl = L.gl;
     const int8_t* c_owner = R.core_owner();
     const int8_t* o_price = R.offer_price();
     const int8_t* s_rem = R.slot_rem();
     // per core: the max ratio over the auctioneer's offers (the padded list's -1 entries and the
     // own empty job bound it from below) and how many offers attain it
-    int mn = -1, md = 1;
-    if (lane < C) {
-        int nt = 0;
-        if (c_owner[lane] == 0) {
-            const M128 cand = mand(s_mc[lane], s_mr[0]);
+    int mn = -1, md = 1, nt = 0;
+    if (gl < C) {
+        if (c_owner[gl] == 0) {
+            const M128 cand = mand(s_mc[gl], s_mr[0]);
             for (MaskIter it(cand); it.more();) {
                 const int i = it.next();
                 int num, den;
@@ -372,43 +479,34 @@ __device__ void hardcoded_auctioneer(Rec& R, const Params& P, const M128* s_mc, 
                 }
             }
         }
-        s_auct[lane] = (int16_t)O;
-        s_tie_n[lane] = (int16_t)nt;
+        s_auct[gl] = (int16_t)O;
     }
-    wave_sync();
     // tie-break draws in core order on the env stream (Auctioneer.getAuctioneerAction
-    // Auctioneer.py:95-102)
-    bool any = false;
-    for (int c = 0; c < C; c++) {
-        const int nt = s_tie_n[c];
-        if (nt > 0) {
-            const uint32_t pick = rs.randbelow((uint32_t)nt, lane);
-            if (lane == 0) s_pick[c] = (int16_t)pick;
-            any = true;
-        }
+    // Auctioneer.py:95-102), only for the cores with a candidate
+    const uint64_t need = L.ballot(gl < C && nt > 0);
+    int my_pick = 0;
+    for (uint64_t m = need; m; m &= m - 1) {
+        const int c = __ffsll((unsigned long long)m) - 1;
+        const uint32_t pick = rs.randbelow(L.shfl((uint32_t)nt, c), L);
+        if (gl == c) my_pick = (int)pick;
     }
-    if (any) {
-        wave_sync();
-        // the pick-th maximal candidate's position in the padded list
-        if (lane < C && s_tie_n[lane] > 0) {
-            const int pick = s_pick[lane];
-            int k = 0, t = 0;
-            for (MaskIter it(mand(s_mc[lane], s_mr[0])); it.more(); k++) {
-                const int i = it.next();
-                int num, den;
-                ratio_of(o_price[i], s_rem[i], num, den);
-                if (num * md == mn * den) {
-                    if (t == pick) s_auct[lane] = (int16_t)k;
-                    t++;
-                }
+    // the pick-th maximal candidate's position in the padded list
+    if (gl < C && nt > 0) {
+        int k = 0, t = 0;
+        for (MaskIter it(mand(s_mc[gl], s_mr[0])); it.more(); k++) {
+            const int i = it.next();
+            int num, den;
+            ratio_of(o_price[i], s_rem[i], num, den);
+            if (num * md == mn * den) {
+                if (t == my_pick) s_auct[gl] = (int16_t)k;
+                t++;
             }
         }
     }
 }
 
 // ---------------------------------------------------------------------------
-// kernels
-
+// kernels (the host picks LPE; init / reset / auctioneer / randbelow run one env per wave)
 
 // Initial state (world.py:247, Core.__init__ world.py:30-37, JobCollection
 // world.py:118-121) and random.seed(seed + e) (init_by_array of the seed's
@@ -422,7 +520,7 @@ __global__ void __launch_bounds__(64) k_env_init(Params P, uint8_t* recs, uint32
     uint32_t* st = reinterpret_cast<uint32_t*>(smem + P.s_scratch);
     for (int i = lane; i < P.rec_bytes / 4; i += kWave) reinterpret_cast<uint32_t*>(rec)[i] = 0;
     wave_sync();
-    Rec R{rec, &P};
+    Rec R{rec, &P, nullptr};
     for (int c = lane; c < P.C; c += kWave) {
         R.core_owner()[c] = 0;
         R.core_kind()[c] = -1;
@@ -440,9 +538,9 @@ __global__ void __launch_bounds__(64) k_env_init(Params P, uint8_t* recs, uint32
         R.slot_birth()[i] = -1;
     }
     if (lane == 0) {
-        uint64_t s = seed + (uint64_t)e;
-        uint32_t key[2] = {(uint32_t)s, (uint32_t)(s >> 32)};
-        int len = key[1] ? 2 : 1;
+        const uint64_t s = seed + (uint64_t)e;
+        const uint32_t key[2] = {(uint32_t)s, (uint32_t)(s >> 32)};
+        const int len = key[1] ? 2 : 1;
         st[0] = 19650218u;
         for (int i = 1; i < kMtN; i++) st[i] = 1812433253u * (st[i - 1] ^ (st[i - 1] >> 30)) + (uint32_t)i;
         int i = 1, j = 0;
@@ -468,9 +566,9 @@ __global__ void __launch_bounds__(64) k_env_init(Params P, uint8_t* recs, uint32
         R.mti() = kMtN;
     }
     wave_sync();
-    copy_dwords(mt + e * kMtN, st, kMtN, lane);
-    copy_dwords(reinterpret_cast<uint32_t*>(recs + e * (int64_t)P.rec_bytes), reinterpret_cast<uint32_t*>(rec),
-                P.rec_bytes / 4, lane);
+    copy_dwords<kWave>(mt + e * kMtN, st, kMtN, lane);
+    copy_dwords<kWave>(reinterpret_cast<uint32_t*>(recs + e * (int64_t)P.rec_bytes), reinterpret_cast<uint32_t*>(rec),
+                       P.rec_bytes / 4, lane);
 }
 
 __global__ void __launch_bounds__(64) k_env_reset(Params P, const uint8_t* recs, int8_t* obs_acc, int8_t* obs_off,
@@ -481,19 +579,31 @@ __global__ void __launch_bounds__(64) k_env_reset(Params P, const uint8_t* recs,
     const int lane = threadIdx.x;
     const int64_t e = blockIdx.x;
     uint8_t* rec = smem + P.s_rec;
-    copy_dwords(reinterpret_cast<uint32_t*>(rec), reinterpret_cast<const uint32_t*>(recs + e * (int64_t)P.rec_bytes),
-                P.rec_bytes / 4, lane);
+    __shared__ int32_t s_kt[48];
+    load_kind_tables(P, s_kt, lane);
+    copy_dwords<kWave>(reinterpret_cast<uint32_t*>(rec),
+                       reinterpret_cast<const uint32_t*>(recs + e * (int64_t)P.rec_bytes), P.rec_bytes / 4, lane);
     wave_sync();
-    Rec R{rec, &P};
-    build_masks(R, P, s_mc, s_mr, lane);
-    emit_obs(R, P, s_mc, s_mr, smem + P.s_scratch, obs_acc, obs_off, obs_auct, e, lane);
+    Rec R{rec, &P, s_kt};
+    build_masks<kWave>(R, P, s_mc, s_mr, lane);
+    emit_obs<kWave>(R, P, s_mc, s_mr, smem + P.s_scratch, obs_acc, obs_off, obs_auct, e, true, lane);
 }
 
 constexpr int kLiabPrefetch = 4;  // newest chain entries loaded ahead per core that may terminate
 
-// One round of SchedulingEnv.step (SchedulingEnvironment.py:32-83) for env blockIdx.x.
-__global__ void __launch_bounds__(64) k_env_step(Params P, uint8_t* recs, uint32_t* mt, Liab* liab, StepIO io) {
-    extern __shared__ __align__(16) uint8_t smem[];
+// One round of SchedulingEnv.step (SchedulingEnvironment.py:32-83): group g of block b steps env
+// b * (64 / LPE) + g. Each group owns a P.s_total-byte slice of the block's LDS.
+template <int LPE>
+__global__ void __launch_bounds__(64) k_env_step(Params P, int64_t E, uint8_t* recs, uint32_t* mt, Liab* liab,
+                                                 StepIO io) {
+    extern __shared__ __align__(16) uint8_t smem_all[];
+    const int lane = threadIdx.x;
+    const Lanes<LPE> Lg(lane);
+    const int gl = Lg.gl;
+    const int64_t e_raw = (int64_t)blockIdx.x * (kWave / LPE) + (lane / LPE);
+    const bool active = e_raw < E;  // padding groups of the last wave replay env E-1 without writing
+    const int64_t e = active ? e_raw : E - 1;
+    uint8_t* smem = smem_all + (lane / LPE) * P.s_total;
     M128* s_mc = reinterpret_cast<M128*>(smem + P.s_mc);          // offers per core
     M128* s_mr = reinterpret_cast<M128*>(smem + P.s_mr);          // offers per recipient (0 = auctioneer)
     Liab* s_newle = reinterpret_cast<Liab*>(smem + P.s_newle);    // liability entry appended this round per core
@@ -502,16 +612,16 @@ __global__ void __launch_bounds__(64) k_env_step(Params P, uint8_t* recs, uint32
     int8_t* s_by_rank = reinterpret_cast<int8_t*>(smem + P.s_rank); // cores in execution order
     int8_t* s_fresh = reinterpret_cast<int8_t*>(smem + P.s_fresh);  // s_newle[c] is the chain's newest entry
     int16_t* s_auct = reinterpret_cast<int16_t*>(smem + P.s_auct);  // auctioneer action per core
-    int16_t* s_tie_n = reinterpret_cast<int16_t*>(smem + P.s_tie);  // tied maxima count (auctioneer)
-    int16_t* s_pick = reinterpret_cast<int16_t*>(smem + P.s_pick);  // tie-break draw per core
     int32_t* s_agent_r = reinterpret_cast<int32_t*>(smem + P.s_agentr);  // agentReward
     int32_t* s_auct_r = reinterpret_cast<int32_t*>(smem + P.s_auctr);    // auctioneerReward
     uint32_t& s_flags = *reinterpret_cast<uint32_t*>(smem + P.s_misc);
     int& s_n_exec = *reinterpret_cast<int*>(smem + P.s_misc + 4);
 
-    const int lane = threadIdx.x;
-    const int64_t e = blockIdx.x;
     const int N = P.N, C = P.C, L = P.L, NL = P.NL, O = P.O;
+#ifdef MS_PHASE_TIMING
+    uint64_t t_prev = __builtin_amdgcn_s_memtime();
+    uint64_t t_acc[16] = {};
+#endif
 
     uint8_t* rec = smem + P.s_rec;
     int8_t* a_acc = reinterpret_cast<int8_t*>(smem + P.s_act_acc);
@@ -525,31 +635,32 @@ __global__ void __launch_bounds__(64) k_env_step(Params P, uint8_t* recs, uint32
     uint8_t* scratch = smem + P.s_scratch;
 
     // ---- stage state and actions in LDS
-    copy_dwords(reinterpret_cast<uint32_t*>(rec), reinterpret_cast<const uint32_t*>(recs + e * (int64_t)P.rec_bytes),
-                P.rec_bytes / 4, lane);
-    for (int i = lane; i < N * C; i += kWave) a_acc[i] = io.act_acc[e * N * C + i];
-    for (int i = lane; i < NL; i += kWave) {
-        a_off[i] = io.act_off[e * NL + i];
-        a_price[i] = io.act_price ? io.act_price[e * NL + i] : 0;
-    }
-    for (int i = lane; i < C; i += kWave) a_auct[i] = io.act_auct ? io.act_auct[e * C + i] : 0;
-    for (int i = lane; i < N * C; i += kWave) acc_r[i] = 0;
-    for (int i = lane; i < NL; i += kWave) {
+    __shared__ int32_t s_kt[48];
+    load_kind_tables(P, s_kt, lane);
+    copy_dwords<LPE>(reinterpret_cast<uint32_t*>(rec),
+                     reinterpret_cast<const uint32_t*>(recs + e * (int64_t)P.rec_bytes), P.rec_bytes / 4, gl);
+    stage_bytes<LPE>(a_acc, io.act_acc + e * N * C, N * C, gl);
+    stage_bytes<LPE>(a_off, io.act_off + e * NL, NL, gl);
+    if (io.act_price) stage_bytes<LPE>(a_price, io.act_price + e * NL, NL, gl);
+    if (io.act_auct) stage_bytes<LPE>(a_auct, io.act_auct + e * C, C, gl);
+    for (int i = gl; i < N * C; i += LPE) acc_r[i] = 0;
+    for (int i = gl; i < NL; i += LPE) {
         off_r[i] = 0.f;
         price_r[i] = 0.f;
     }
-    for (int i = lane; i < C; i += kWave) {
+    for (int i = gl; i < C; i += LPE) {
         s_auct_r[i] = 0;
         s_exec[i] = -1;
         s_fresh[i] = 0;
     }
-    for (int i = lane; i < N; i += kWave) s_agent_r[i] = 0;
-    if (lane == 0) {
+    for (int i = gl; i < N; i += LPE) s_agent_r[i] = 0;
+    if (gl == 0) {
         s_flags = 0;
         s_n_exec = 0;
     }
     wave_sync();
-    Rec R{rec, &P};
+    MS_MARK(1);
+    Rec R{rec, &P, s_kt};
     const int round = R.round();
     int8_t* c_owner = R.core_owner();
     int8_t* c_kind = R.core_kind();
@@ -569,49 +680,51 @@ __global__ void __launch_bounds__(64) k_env_step(Params P, uint8_t* recs, uint32
     //      yet) and the newest liability entries of every core that may terminate
     //      this round, i.e. whose current job or one of the jobs offered to it has
     //      one round left (its chain is settled in the tick below)
-    MtStream rs;
+    MtStream<LPE> rs;
     rs.gmt = mt + e * kMtN;
-    rs.lds = reinterpret_cast<uint32_t*>(scratch);
     rs.mti0 = R.mti();
     rs.p = 0;
     rs.twisted = false;
-    rs.load(0, 0, lane);
-    build_masks(R, P, s_mc, s_mr, lane);
+    rs.store = active;
+    rs.load(0, 0, Lg);
+    build_masks<LPE>(R, P, s_mc, s_mr, gl);
     Liab pf[kLiabPrefetch];
     int pf_n = 0;
-    if (lane < C) {
-        bool maybe = c_kind[lane] >= 0 && c_rem[lane] == 1;
-        for (MaskIter it(s_mc[lane]); it.more() && !maybe;) maybe = s_rem[it.next()] == 1;
+    if (gl < C) {
+        bool maybe = c_kind[gl] >= 0 && c_rem[gl] == 1;
+        for (MaskIter it(s_mc[gl]); it.more() && !maybe;) maybe = s_rem[it.next()] == 1;
         if (maybe) {
-            const int n = l_n[lane];
+            const int n = l_n[gl];
             pf_n = min(n, kLiabPrefetch);
-            const Liab* chain = my_liab + lane * P.cap;
+            const Liab* chain = my_liab + gl * P.cap;
 #pragma unroll
             for (int q = 0; q < kLiabPrefetch; q++)
                 if (q < pf_n) pf[q] = chain[n - 1 - q];
         }
     }
 
+    MS_MARK(2);
     // ---- auctioneer actions: HardcodedAuctioneerAcceptor (HardcodedModules.py:54-78), asked by the
     //      driver before env.step (trainPPO.py:162); ties broken with random.sample -> _randbelow
     if (!io.act_auct) {
-        hardcoded_auctioneer(R, P, s_mc, s_mr, rs, s_auct, s_tie_n, s_pick, lane);
+        hardcoded_auctioneer<LPE>(R, P, s_mc, s_mr, rs, s_auct, Lg);
     } else {
-        for (int c = lane; c < C; c += kWave) s_auct[c] = a_auct[c];
+        for (int c = gl; c < C; c += LPE) s_auct[c] = a_auct[c];
     }
     wave_sync();
+    MS_MARK(3);
 
     // ---- which offer each core executes (executeAgentAcceptions1 world.py:391-404,
     //      executeAuctioneerAcceptions world.py:378-389): offers to core c are all addressed to c's
     //      owner (created after the tick with recipient = owner, world.py:428), so only the owner's
     //      acceptor (or the auctioneer) can pick one, and each core executes at most once per round.
-    for (int i = lane; i < N * C; i += kWave) {
-        int a = a_acc[i];
+    for (int i = gl; i < N * C; i += LPE) {
+        const int a = a_acc[i];
         if (a < 0 || a > O) atomicOr(&s_flags, MS_FLAG_BAD_ACTION);
     }
-    for (int c = lane; c < C; c += kWave) {
-        int owner = c_owner[c];
-        int idx = owner > 0 ? a_acc[(owner - 1) * C + c] : s_auct[c];
+    for (int c = gl; c < C; c += LPE) {
+        const int owner = c_owner[c];
+        const int idx = owner > 0 ? a_acc[(owner - 1) * C + c] : s_auct[c];
         if (owner == 0 && (idx < 0 || idx > O)) atomicOr(&s_flags, MS_FLAG_BAD_ACTION);
         int slot = -1;
         if (idx >= 0 && idx < O) slot = kth_bit(mand(s_mc[c], s_mr[owner]), idx);
@@ -619,7 +732,7 @@ __global__ void __launch_bounds__(64) k_env_step(Params P, uint8_t* recs, uint32
         s_key[c] = (int16_t)(owner > 0 ? (owner - 1) * C + c : N * C + c);
     }
     wave_sync();
-    for (int c = lane; c < C; c += kWave) {
+    for (int c = gl; c < C; c += LPE) {
         if (s_exec[c] >= 0) {
             int r = 0;
             for (int d = 0; d < C; d++) r += (s_exec[d] >= 0 && s_key[d] < s_key[c]);
@@ -628,30 +741,33 @@ __global__ void __launch_bounds__(64) k_env_step(Params P, uint8_t* recs, uint32
         }
     }
     wave_sync();
+    MS_MARK(4);
 
-    // ---- apply executions in reference order (World.executeAnOffer world.py:261-293)
-    if (lane == 0) {
-        int n_exec = s_n_exec;
+    // ---- apply executions in reference order (World.executeAnOffer world.py:261-293); the
+    //      groups' leaders run their envs' loops side by side
+    if (gl == 0) {
+        const int n_exec = s_n_exec;
         for (int r = 0; r < n_exec; r++) {
-            int c = s_by_rank[r];
-            int i = s_exec[c];
-            int offerer = i / L + 1, slot = i % L;
-            int recip = o_recip[i];
-            int nk = s_kind[i], nrem = s_rem[i], nbirth = s_birth[i];
-            int price = o_price[i];
+            const int c = s_by_rank[r];
+            const int i = s_exec[c];
+            const int offerer = i / L + 1, slot = i - (offerer - 1) * L;
+            const int recip = o_recip[i];
+            const int nk = s_kind[i], nrem = s_rem[i], nbirth = s_birth[i];
+            const int price = o_price[i];
             // removeAndReturnEntry (world.py:135-141); newJob.wait = False (world.py:276)
             s_kind[i] = -1;
             s_rem[i] = -1;
             s_wait[i] = 0;
             s_birth[i] = -1;
             // dispatchNewJobAndReturnOldOne (world.py:61-76)
-            int ok = c_kind[c], orem = c_rem[c], obirth = c_birth[c];
+            const int ok = c_kind[c], orem = c_rem[c], obirth = c_birth[c];
             c_kind[c] = (int8_t)nk;
             c_rem[c] = (int8_t)nrem;
             c_birth[c] = nbirth;
             c_owner[c] = (int8_t)offerer;
             if (recip != 0) {  // insertJob into the recipient's first empty slot (world.py:123-133)
-                int base = (recip - 1) * L, placed = 0;
+                const int base = (recip - 1) * L;
+                int placed = 0;
                 for (int s = 0; s < L; s++)
                     if (s_kind[base + s] < 0) {
                         s_kind[base + s] = (int8_t)ok;
@@ -664,7 +780,7 @@ __global__ void __launch_bounds__(64) k_env_step(Params P, uint8_t* recs, uint32
                 if (!placed) s_flags |= MS_FLAG_COLLECTION_FULL;
             }
             // liability entry (deepcopy, round = world.round), appendleft (world.py:285-289)
-            int n = l_n[c];
+            const int n = l_n[c];
             if (n < P.cap) {
                 Liab le;
                 le.offerer = (int8_t)offerer;
@@ -672,7 +788,7 @@ __global__ void __launch_bounds__(64) k_env_step(Params P, uint8_t* recs, uint32
                 le.price = (int8_t)price;
                 le.nec = (int8_t)nrem;
                 le.round = round;
-                my_liab[c * P.cap + n] = le;
+                if (active) my_liab[c * P.cap + n] = le;
                 s_newle[c] = le;
                 s_fresh[c] = 1;
                 l_n[c] = (uint8_t)(n + 1);
@@ -680,11 +796,11 @@ __global__ void __launch_bounds__(64) k_env_step(Params P, uint8_t* recs, uint32
                 s_flags |= MS_FLAG_LIABILITY_OVERFLOW;
             }
             // offer-side rewards from world.acceptedOffers (Reward.py:164-170 / :23-49)
-            int prio1 = P.prio[nk];
+            const int prio1 = R.prio(nk);
             if (!P.free_prices) {
                 off_r[i] = (float)prio1;
             } else {
-                int diff = prio1 - price;
+                const int diff = prio1 - price;
                 float pc;
                 if (P.commercial)
                     pc = diff == 0 ? P.net_zero : (float)diff;
@@ -693,7 +809,7 @@ __global__ void __launch_bounds__(64) k_env_step(Params P, uint8_t* recs, uint32
                 off_r[i] = (float)prio1;
                 price_r[i] = pc;
             }
-            if (io.ev_acc) {
+            if (io.ev_acc && active) {
                 ms_accept_rec ar;
                 ar.valid = 1;
                 ar.offerer = (int8_t)offerer;
@@ -711,23 +827,25 @@ __global__ void __launch_bounds__(64) k_env_step(Params P, uint8_t* recs, uint32
         }
     }
     wave_sync();
+    MS_MARK(5);
 
     // ---- tick (processOneTimestepAndUpdateOwnership world.py:336-367) and liability settlement
     //      (getDividedFixedPricesReward Reward.py:187-210 / getDividedFreePricesReward Reward.py:59-82)
-    for (int c = lane; c < C; c += kWave) {
+    if (gl < C) {
+        const int c = gl;
         ms_term_rec tr = {0, 0, 0, 0, 0};
         if (c_kind[c] >= 0) {
-            int rem = c_rem[c] - 1;
+            const int rem = c_rem[c] - 1;
             c_rem[c] = (int8_t)rem;
             if (rem == 0) {
-                int owner = c_owner[c];
-                int kind = c_kind[c];
-                int gen = P.mult * P.prio[kind];
-                int ts = round + 1;
+                const int owner = c_owner[c];
+                const int kind = c_kind[c];
+                const int gen = P.mult * R.prio(kind);
+                const int ts = round + 1;
                 tr.valid = 1;
                 tr.owner = (int8_t)owner;
-                tr.prio = (int8_t)P.prio[kind];
-                tr.init_len = (int8_t)P.len[kind];
+                tr.prio = (int8_t)R.prio(kind);
+                tr.init_len = (int8_t)R.len(kind);
                 tr.dwell = round - c_birth[c];
                 // Core.assignCoreToAuctioneer (world.py:57-59)
                 c_kind[c] = -1;
@@ -756,8 +874,8 @@ __global__ void __launch_bounds__(64) k_env_step(Params P, uint8_t* recs, uint32
                     }
                     tm += last - le.round;
                     last = le.round;
-                    double ratio = (double)le.price / (double)le.nec;  // Python true division
-                    int traded = (int)rint(ratio * (double)tm);        // Python round(): half-even
+                    const double ratio = (double)le.price / (double)le.nec;  // Python true division
+                    const int traded = (int)rint(ratio * (double)tm);        // Python round(): half-even
                     acc_r[(le.offerer - 1) * C + c] -= traded;
                     atomicAdd(&s_agent_r[le.offerer - 1], -traded);
                     if (le.recipient > 0) {
@@ -770,25 +888,28 @@ __global__ void __launch_bounds__(64) k_env_step(Params P, uint8_t* recs, uint32
                 l_n[c] = 0;  // resetLiabilityListForACore
             }
         }
-        if (io.ev_term) io.ev_term[e * C + c] = tr;
-        if (io.ev_acc && s_exec[c] < 0) {
-            ms_accept_rec ar = {};
-            io.ev_acc[e * C + c] = ar;
+        if (active) {
+            if (io.ev_term) io.ev_term[e * C + c] = tr;
+            if (io.ev_acc && s_exec[c] < 0) {
+                ms_accept_rec ar = {};
+                io.ev_acc[e * C + c] = ar;
+            }
         }
     }
     wave_sync();
+    MS_MARK(6);
 
     // ---- offers from offer actions (createFixPriceOfferObjectsFromActions world.py:406-443,
     //      createFreePriceOfferObjectsFromActions world.py:445-478); IDs = slot order
-    for (int i = lane; i < NL; i += kWave) {
-        int act = a_off[i];
-        int cidx = (act >= 0 && act < C) ? act : -1;
-        int kind = s_kind[i];
+    for (int i = gl; i < NL; i += LPE) {
+        const int act = a_off[i];
+        const int cidx = (act >= 0 && act < C) ? act : -1;
+        const int kind = s_kind[i];
         int price;
         if (P.free_prices)
             price = a_price[i];
         else
-            price = P.fix[kind >= 0 ? kind : P.n_fix - 1];
+            price = R.fix(kind >= 0 ? kind : P.n_fix - 1);
         if (cidx >= 0 && kind >= 0 && !s_wait[i]) {
             o_core[i] = (int8_t)cidx;
             o_recip[i] = c_owner[cidx];
@@ -802,31 +923,31 @@ __global__ void __launch_bounds__(64) k_env_step(Params P, uint8_t* recs, uint32
         }
     }
     wave_sync();
+    MS_MARK(7);
 
     // ---- spawn (fillQueuesWithNewRandomJobs world.py:369-376, fillCollectionRandomly Agent.py:50-70)
     {
         const int k = P.new_jobs;
         bool sp = false;
-        if (lane < N) {
+        if (gl < N) {
             int owned = 0, free_slots = 0;
-            for (int c = 0; c < C; c++) owned += (c_owner[c] == lane + 1);
-            for (int s = 0; s < L; s++) free_slots += (s_kind[lane * L + s] < 0);
+            for (int c = 0; c < C; c++) owned += (c_owner[c] == gl + 1);
+            for (int s = 0; s < L; s++) free_slots += (s_kind[gl * L + s] < 0);
             sp = owned + k <= free_slots;
         }
-        uint64_t spm = __ballot(sp);
-        int n_sp = __popcll(spm);
-        int total_pairs = n_sp * k;
+        const uint64_t spm = Lg.ballot(sp);
+        const int total_pairs = __popcll(spm) * k;
         int done = 0;
         while (done < total_pairs) {
-            if (rs.wend - rs.p < 2) rs.load(rs.p, 2, lane);
-            int avail = (rs.wend - rs.p) / 2;
-            int cnt = min(avail, total_pairs - done);
-            int off0 = rs.p - rs.wb;
-            uint32_t wa = __shfl(rs.v, (off0 + 2 * lane) & 63);
-            uint32_t wb2 = __shfl(rs.v, (off0 + 2 * lane + 1) & 63);
-            if (lane < cnt) {
+            if (rs.wend - rs.p < 2) rs.load(rs.p, 2, Lg);
+            const int avail = (rs.wend - rs.p) / 2;
+            const int cnt = min(avail, total_pairs - done);
+            const int off0 = rs.p - rs.wb;
+            const uint32_t wa = Lg.shfl(rs.v, (off0 + 2 * gl) & (LPE - 1));
+            const uint32_t wb2 = Lg.shfl(rs.v, (off0 + 2 * gl + 1) & (LPE - 1));
+            if (gl < cnt) {
                 // random(): (a>>5 * 2^26 + b>>6) / 2^53 (Modules/_randommodule.c)
-                double u = ((double)(wa >> 5) * 67108864.0 + (double)(wb2 >> 6)) * (1.0 / 9007199254740992.0);
+                const double u = ((double)(wa >> 5) * 67108864.0 + (double)(wb2 >> 6)) * (1.0 / 9007199254740992.0);
                 int kind = -1;
                 for (int q = 0; q < P.K; q++)
                     if (u < P.acc[q]) {
@@ -837,22 +958,22 @@ __global__ void __launch_bounds__(64) k_env_step(Params P, uint8_t* recs, uint32
                     kind = P.K - 1;
                     atomicOr(&s_flags, MS_FLAG_SPAWN_EDGE);
                 }
-                spawn_kind[done + lane] = (int8_t)kind;
+                spawn_kind[done + gl] = (int8_t)kind;
             }
             rs.p += 2 * cnt;
             done += cnt;
         }
         wave_sync();
         if (sp) {
-            int rank = __popcll(spm & ((1ull << lane) - 1ull));
-            int base = lane * L;
+            const int rank = __popcll(spm & ((1ull << gl) - 1ull));
+            const int base = gl * L;
             for (int j = 0; j < k; j++) {
-                int kind = spawn_kind[rank * k + j];
+                const int kind = spawn_kind[rank * k + j];
                 int placed = 0;
                 for (int s = 0; s < L; s++)
                     if (s_kind[base + s] < 0) {
                         s_kind[base + s] = (int8_t)kind;
-                        s_rem[base + s] = (int8_t)P.len[kind];
+                        s_rem[base + s] = (int8_t)R.len(kind);
                         s_wait[base + s] = 0;
                         s_birth[base + s] = round;
                         placed = 1;
@@ -863,25 +984,42 @@ __global__ void __launch_bounds__(64) k_env_step(Params P, uint8_t* recs, uint32
         }
     }
     wave_sync();
-    if (lane == 0) {
+    MS_MARK(8);
+    if (gl == 0) {
         R.round() = round + 1;
         R.mti() = rs.final_index();
         R.flags() |= s_flags;
     }
     wave_sync();
+    MS_MARK(9);
 
     // ---- outputs: state record, rewards, observations of the new offer set
-    copy_dwords(reinterpret_cast<uint32_t*>(recs + e * (int64_t)P.rec_bytes), reinterpret_cast<uint32_t*>(rec),
-                P.rec_bytes / 4, lane);
-    if (io.rew_acc) copy_dwords(reinterpret_cast<uint32_t*>(io.rew_acc + e * N * C), reinterpret_cast<uint32_t*>(acc_r), N * C, lane);
-    if (io.rew_offer) copy_dwords(reinterpret_cast<uint32_t*>(io.rew_offer + e * NL), reinterpret_cast<uint32_t*>(off_r), NL, lane);
-    if (io.rew_price) copy_dwords(reinterpret_cast<uint32_t*>(io.rew_price + e * NL), reinterpret_cast<uint32_t*>(price_r), NL, lane);
-    if (io.rew_agent)
-        for (int a = lane; a < N; a += kWave) io.rew_agent[e * N + a] = s_agent_r[a];
-    if (io.rew_auct)
-        for (int c = lane; c < C; c += kWave) io.rew_auct[e * C + c] = s_auct_r[c];
-    build_masks(R, P, s_mc, s_mr, lane);
-    emit_obs(R, P, s_mc, s_mr, scratch, io.obs_acc, io.obs_off, io.obs_auct, e, lane);
+    if (active) {
+        copy_dwords<LPE>(reinterpret_cast<uint32_t*>(recs + e * (int64_t)P.rec_bytes), reinterpret_cast<uint32_t*>(rec),
+                         P.rec_bytes / 4, gl);
+        if (io.rew_acc)
+            copy_dwords<LPE>(reinterpret_cast<uint32_t*>(io.rew_acc + e * N * C), reinterpret_cast<uint32_t*>(acc_r),
+                             N * C, gl);
+        if (io.rew_offer)
+            copy_dwords<LPE>(reinterpret_cast<uint32_t*>(io.rew_offer + e * NL), reinterpret_cast<uint32_t*>(off_r), NL,
+                             gl);
+        if (io.rew_price)
+            copy_dwords<LPE>(reinterpret_cast<uint32_t*>(io.rew_price + e * NL), reinterpret_cast<uint32_t*>(price_r),
+                             NL, gl);
+        if (io.rew_agent)
+            for (int a = gl; a < N; a += LPE) io.rew_agent[e * N + a] = s_agent_r[a];
+        if (io.rew_auct)
+            for (int c = gl; c < C; c += LPE) io.rew_auct[e * C + c] = s_auct_r[c];
+    }
+    MS_MARK(10);
+    build_masks<LPE>(R, P, s_mc, s_mr, gl);
+    MS_MARK(11);
+    emit_obs<LPE>(R, P, s_mc, s_mr, scratch, io.obs_acc, io.obs_off, io.obs_auct, e, active, gl);
+    MS_MARK(12);
+#ifdef MS_PHASE_TIMING
+    if (lane == 0)
+        for (int k = 0; k < 16; k++) g_phase_cycles[blockIdx.x % kProbeSlots][k] += t_acc[k];
+#endif
 }
 
 // Auctioneer.getAuctioneerAction (Auctioneer.py:95-102) on its own, as the driver calls it
@@ -892,24 +1030,25 @@ __global__ void __launch_bounds__(64) k_env_auctioneer(Params P, uint8_t* recs, 
     M128* s_mc = reinterpret_cast<M128*>(smem + P.s_mc);
     M128* s_mr = reinterpret_cast<M128*>(smem + P.s_mr);
     int16_t* s_auct = reinterpret_cast<int16_t*>(smem + P.s_auct);
-    int16_t* s_tie_n = reinterpret_cast<int16_t*>(smem + P.s_tie);
-    int16_t* s_pick = reinterpret_cast<int16_t*>(smem + P.s_pick);
     const int lane = threadIdx.x;
+    const Lanes<kWave> Lg(lane);
     const int64_t e = blockIdx.x;
     uint8_t* rec = smem + P.s_rec;
-    copy_dwords(reinterpret_cast<uint32_t*>(rec), reinterpret_cast<const uint32_t*>(recs + e * (int64_t)P.rec_bytes),
-                P.rec_bytes / 4, lane);
+    __shared__ int32_t s_kt[48];
+    load_kind_tables(P, s_kt, lane);
+    copy_dwords<kWave>(reinterpret_cast<uint32_t*>(rec),
+                       reinterpret_cast<const uint32_t*>(recs + e * (int64_t)P.rec_bytes), P.rec_bytes / 4, lane);
     wave_sync();
-    Rec R{rec, &P};
-    MtStream rs;
+    Rec R{rec, &P, s_kt};
+    MtStream<kWave> rs;
     rs.gmt = mt + e * kMtN;
-    rs.lds = reinterpret_cast<uint32_t*>(smem + P.s_scratch);
     rs.mti0 = R.mti();
     rs.p = 0;
     rs.twisted = false;
-    rs.load(0, 0, lane);
-    build_masks(R, P, s_mc, s_mr, lane);
-    hardcoded_auctioneer(R, P, s_mc, s_mr, rs, s_auct, s_tie_n, s_pick, lane);
+    rs.store = true;
+    rs.load(0, 0, Lg);
+    build_masks<kWave>(R, P, s_mc, s_mr, lane);
+    hardcoded_auctioneer<kWave>(R, P, s_mc, s_mr, rs, s_auct, Lg);
     wave_sync();
     for (int c = lane; c < P.C; c += kWave) actions[e * P.C + c] = (int8_t)s_auct[c];
     if (lane == 0) *reinterpret_cast<int32_t*>(recs + e * (int64_t)P.rec_bytes + 8) = rs.final_index();
@@ -921,16 +1060,17 @@ __global__ void __launch_bounds__(64) k_env_randbelow(Params P, uint8_t* recs, u
                                                       uint32_t* out) {
     extern __shared__ __align__(16) uint8_t smem[];
     const int lane = threadIdx.x;
+    const Lanes<kWave> Lg(lane);
     uint8_t* rec = recs + e * (int64_t)P.rec_bytes;
     int32_t* mti = reinterpret_cast<int32_t*>(rec + 8);
-    MtStream rs;
+    MtStream<kWave> rs;
     rs.gmt = mt + e * kMtN;
-    rs.lds = reinterpret_cast<uint32_t*>(smem + P.s_scratch);
     rs.mti0 = *mti;
     rs.wb = rs.wend = rs.p = 0;
     rs.twisted = false;
+    rs.store = true;
     rs.v = 0;
-    uint32_t r = rs.randbelow(n, lane);
+    const uint32_t r = rs.randbelow(n, Lg);
     wave_sync();
     if (lane == 0) {
         *out = r;
@@ -940,11 +1080,30 @@ __global__ void __launch_bounds__(64) k_env_randbelow(Params P, uint8_t* recs, u
 
 }  // namespace ms
 
+#ifdef MS_PHASE_TIMING
+// profiling build only: read (and optionally clear) the per-phase cycle counters
+extern "C" int ms_probe_phase_cycles(unsigned long long* out, int clear) {
+    static unsigned long long host[ms::kProbeSlots][16];
+    if (hipMemcpyFromSymbol(host, HIP_SYMBOL(ms::g_phase_cycles), sizeof(host)) != hipSuccess) return -1;
+    for (int k = 0; k < 16; k++) {
+        out[k] = 0;
+        for (int b = 0; b < ms::kProbeSlots; b++) out[k] += host[b][k];
+    }
+    if (clear) {
+        memset(host, 0, sizeof(host));
+        if (hipMemcpyToSymbol(HIP_SYMBOL(ms::g_phase_cycles), host, sizeof(host)) != hipSuccess) return -1;
+    }
+    return 0;
+}
+#endif
+
 // launch wrappers used by capi.cpp
 namespace ms {
 hipError_t launch_env_init(const Params& P, int64_t E, uint8_t* recs, uint32_t* mt, Liab* liab, uint64_t seed,
                            hipStream_t s) {
-    hipLaunchKernelGGL(k_env_init, dim3((unsigned)E), dim3(kWave), P.s_total, s, P, recs, mt, liab, seed);
+    // the seeding runs in the scratch, which k_env_init needs at MT-state size
+    const size_t lds = (size_t)P.s_scratch + 4 * kMtN > (size_t)P.s_total ? (size_t)P.s_scratch + 4 * kMtN : P.s_total;
+    hipLaunchKernelGGL(k_env_init, dim3((unsigned)E), dim3(kWave), lds, s, P, recs, mt, liab, seed);
     return hipGetLastError();
 }
 hipError_t launch_env_reset(const Params& P, int64_t E, const uint8_t* recs, int8_t* a, int8_t* o, int8_t* u,
@@ -952,10 +1111,33 @@ hipError_t launch_env_reset(const Params& P, int64_t E, const uint8_t* recs, int
     hipLaunchKernelGGL(k_env_reset, dim3((unsigned)E), dim3(kWave), P.s_total, s, P, recs, a, o, u);
     return hipGetLastError();
 }
+
+// lanes per env: the smallest power of two >= max(C, N) and >= 16 (a 16-word MT window), so a
+// wave steps 4 (cfg2/cfg3), 2 (cfg4) or 1 (cfg5) envs
+static int lanes_per_env(const Params& P) {
+    int need = P.C > P.N ? P.C : P.N;
+    int lpe = 16;
+    while (lpe < need) lpe *= 2;
+    return lpe;
+}
+
+template <int LPE>
+static hipError_t launch_step_t(const Params& P, int64_t E, uint8_t* recs, uint32_t* mt, Liab* liab, const StepIO& io,
+                                hipStream_t s) {
+    constexpr int G = kWave / LPE;
+    const int64_t blocks = (E + G - 1) / G;
+    hipLaunchKernelGGL((k_env_step<LPE>), dim3((unsigned)blocks), dim3(kWave), (size_t)P.s_total * G, s, P, E, recs,
+                       mt, liab, io);
+    return hipGetLastError();
+}
+
 hipError_t launch_env_step(const Params& P, int64_t E, uint8_t* recs, uint32_t* mt, Liab* liab, const StepIO& io,
                            hipStream_t s) {
-    hipLaunchKernelGGL(k_env_step, dim3((unsigned)E), dim3(kWave), P.s_total, s, P, recs, mt, liab, io);
-    return hipGetLastError();
+    switch (lanes_per_env(P)) {
+        case 16: return launch_step_t<16>(P, E, recs, mt, liab, io, s);
+        case 32: return launch_step_t<32>(P, E, recs, mt, liab, io, s);
+        default: return launch_step_t<64>(P, E, recs, mt, liab, io, s);
+    }
 }
 hipError_t launch_env_auctioneer(const Params& P, int64_t E, uint8_t* recs, uint32_t* mt, int8_t* actions,
                                  hipStream_t s) {

@@ -52,9 +52,9 @@ struct Params {
     // small envs keep many waves per CU in flight
     int32_t s_rec, s_act_acc, s_act_off, s_act_price, s_act_auct, s_accr, s_offr, s_pricer,
         s_spawn_kind, s_scratch, s_total;
-    int32_t s_mc, s_mr, s_newle, s_exec, s_key, s_auct, s_tie, s_pick, s_agentr, s_auctr, s_rank, s_fresh,
-        s_misc;
-    int32_t obs_chunk;  // bytes of observation rows staged at once (the scratch)
+    int32_t s_mc, s_mr, s_newle, s_exec, s_key, s_auct, s_agentr, s_auctr, s_rank, s_fresh, s_misc;
+    int32_t scratch_bytes;  // owner rows + slot pairs of the observations
+    int32_t s_slotpair;     // slot pairs' offset inside the scratch
 };
 
 // device pointers of one ms_env_step call
@@ -138,16 +138,15 @@ inline Params make_params(const ms_config& c, int32_t cap) {
     p.s_exec = s; s += align4(2 * p.C);        // executed slot per core
     p.s_key = s; s += align4(2 * p.C);         // execution order key
     p.s_auct = s; s += align4(2 * p.C);        // auctioneer action per core
-    p.s_tie = s; s += align4(2 * p.C);         // tied maxima per core
-    p.s_pick = s; s += align4(2 * p.C);        // tie-break draw per core
     p.s_rank = s; s += align4(p.C);            // cores in execution order
     p.s_fresh = s; s += align4(p.C);           // s_newle[c] is the chain's newest entry
     p.s_misc = s; s += 16;                     // flags, n_exec
     s = align16(s);
     p.s_scratch = s;
-    p.obs_chunk = 4 * kMtN;  // the MT twist buffer doubles as the observation staging chunk
-    if (p.obs_chunk < p.acc_stride) p.obs_chunk = align16(p.acc_stride);
-    s += p.obs_chunk;
+    // observation scratch: C owner rows, then NL slot pairs
+    p.s_slotpair = align16(p.C * p.acc_stride);
+    p.scratch_bytes = align16(p.s_slotpair + 2 * p.NL);
+    s += p.scratch_bytes;
     p.s_total = s;
     return p;
 }

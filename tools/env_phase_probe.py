@@ -1,0 +1,72 @@
+"""Cycle attribution of k_env_step phases (profiling only; uses tools/_probe/libmarlsched_probe.so
+built by tools/build_phase_probe.sh, never the product library's code path).
+
+Runs cfg3 at E replicas with random actions and prints, per phase mark, the average cycles one
+wave spends between the previous mark and this one (lane 0's s_memtime deltas)."""
+import ctypes as ct
+import importlib
+import os
+import sys
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+abi = importlib.import_module("marl-scheduling_amd.abi")
+NAMES = {1: "stage", 2: "MT peek + masks + liab prefetch", 3: "auctioneer", 4: "exec select + rank",
+         5: "leader executions", 6: "tick + settlement", 7: "offers", 8: "spawn", 9: "record round/mti",
+         10: "write record + rewards", 11: "rebuild masks", 12: "emit observations"}
+
+
+def main(E=16384, steps=20, lpe=16):
+    lib = ct.CDLL(os.path.join(ROOT, "tools", "_probe", "libmarlsched_probe.so"))
+    lib.ms_env_create.argtypes = [ct.POINTER(abi.MsConfig), ct.c_int64, ct.c_uint64, ct.POINTER(ct.c_void_p)]
+    lib.ms_env_step.argtypes = [ct.c_void_p, ct.POINTER(abi.MsActions), ct.POINTER(abi.MsObsOut),
+                                ct.POINTER(abi.MsRewardOut), ct.c_void_p, ct.c_void_p]
+    lib.ms_env_shape.argtypes = [ct.c_void_p, ct.POINTER(abi.MsShape)]
+    lib.ms_probe_phase_cycles.argtypes = [ct.POINTER(ct.c_ulonglong), ct.c_int]
+    cfg = abi.named_config("cfg3")
+    h = ct.c_void_p()
+    assert lib.ms_env_create(ct.byref(cfg), E, 0, ct.byref(h)) == 0
+    sh = abi.MsShape()
+    lib.ms_env_shape(h, ct.byref(sh))
+    N, C, L, O = sh.n_agents, sh.n_cores, sh.collection_length, sh.max_offers
+    d = torch.device("cuda")
+    g = torch.Generator(device=d).manual_seed(0)
+    acc = torch.randint(0, O + 1, (steps + 5, E, N, C), device=d, generator=g, dtype=torch.int32).to(torch.int8)
+    off = torch.randint(0, C + 1, (steps + 5, E, N, L), device=d, generator=g, dtype=torch.int32).to(torch.int8)
+    price = torch.randint(0, 13, (steps + 5, E, N, L), device=d, generator=g, dtype=torch.int32).to(torch.int8)
+    oa = torch.empty((E, N, C, sh.acc_obs_stride), dtype=torch.int8, device=d)
+    oo = torch.empty((E, N, L, sh.off_obs_stride), dtype=torch.int8, device=d)
+    rw = [torch.empty((E, N, L), device=d), torch.empty((E, N, L), device=d),
+          torch.empty((E, N, C), dtype=torch.int32, device=d), torch.empty((E, C), dtype=torch.int32, device=d),
+          torch.empty((E, N), dtype=torch.int32, device=d)]
+    obs = abi.MsObsOut(oa.data_ptr(), oo.data_ptr(), None)
+    rew = abi.MsRewardOut(*[t.data_ptr() for t in rw])
+    buf = (ct.c_ulonglong * 16)()
+
+    def run(t):
+        a = abi.MsActions(acc[t].data_ptr(), off[t].data_ptr(), price[t].data_ptr(), None)
+        assert lib.ms_env_step(h, ct.byref(a), ct.byref(obs), ct.byref(rew), None, None) == 0
+
+    for t in range(5):
+        run(t)
+    torch.cuda.synchronize()
+    lib.ms_probe_phase_cycles(buf, 1)
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    ev[0].record()
+    for t in range(steps):
+        run(5 + t)
+    ev[1].record()
+    torch.cuda.synchronize()
+    lib.ms_probe_phase_cycles(buf, 0)
+    waves = (E + 64 // lpe - 1) // (64 // lpe)
+    tot = sum(buf[k] for k in range(1, 13))
+    print("k_env_step (probe build) %.1f us/step; per wave: %.0f cycles" % (ev[0].elapsed_time(ev[1]) * 1e3 / steps,
+                                                                        tot / waves / steps))
+    for k in range(1, 13):
+        print("  %2d %-34s %8.0f cycles/wave  %5.1f%%" % (k, NAMES[k], buf[k] / waves / steps, 100.0 * buf[k] / tot))
+
+
+if __name__ == "__main__":
+    main()
