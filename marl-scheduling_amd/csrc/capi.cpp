@@ -163,7 +163,7 @@ int ms_env_create(const ms_config* cfg, int64_t n_envs, uint64_t seed, ms_env** 
     env->round = 0;
     HIP_TRY(hipGetDevice(&env->device));
     size_t rec_b = (size_t)n_envs * env->P.rec_bytes;
-    size_t mt_b = (size_t)n_envs * ms::kMtN * sizeof(uint32_t);
+    size_t mt_b = (size_t)n_envs * 2 * ms::kMtN * sizeof(uint32_t);  // current block + successor
     size_t liab_b = (size_t)n_envs * env->P.C * env->P.cap * sizeof(ms::Liab);
     if (hipMalloc(&env->recs, rec_b) != hipSuccess || hipMalloc(&env->mt, mt_b) != hipSuccess ||
         hipMalloc(&env->liab, liab_b) != hipSuccess || hipMalloc(&env->scratch_u32, 16) != hipSuccess) {
@@ -259,12 +259,17 @@ int ms_env_auctioneer(ms_env* env, int8_t* actions, void* stream) {
     return MS_OK;
 }
 
+// word offset of env e's current MT block (record header word 3 = mt_sel, bit 0 = current half)
+static size_t mt_block(int64_t e, int32_t sel) { return ((size_t)e * 2 + (sel & 1)) * ms::kMtN; }
+
 int ms_env_get_rng(ms_env* env, int64_t e, uint32_t* words, int32_t* index, void* stream) {
     if (!env || !words || !index) return fail(MS_EINVAL, "NULL argument");
     if (e < 0 || e >= env->E) return fail(MS_EINVAL, "env index out of range");
     HIP_TRY(hipStreamSynchronize((hipStream_t)stream));
-    HIP_TRY(hipMemcpy(words, env->mt + e * ms::kMtN, 4 * ms::kMtN, hipMemcpyDeviceToHost));
-    HIP_TRY(hipMemcpy(index, env->recs + e * env->P.rec_bytes + 8, 4, hipMemcpyDeviceToHost));
+    int32_t hdr[4];
+    HIP_TRY(hipMemcpy(hdr, env->recs + e * env->P.rec_bytes, sizeof(hdr), hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(words, env->mt + mt_block(e, hdr[3]), 4 * ms::kMtN, hipMemcpyDeviceToHost));
+    *index = hdr[2];
     return MS_OK;
 }
 
@@ -273,8 +278,10 @@ int ms_env_set_rng(ms_env* env, int64_t e, const uint32_t* words, int32_t index,
     if (e < 0 || e >= env->E) return fail(MS_EINVAL, "env index out of range");
     if (index < 0 || index > ms::kMtN) return fail(MS_EINVAL, "MT index must be in [0, 624]");
     HIP_TRY(hipStreamSynchronize((hipStream_t)stream));
-    HIP_TRY(hipMemcpy(env->mt + e * ms::kMtN, words, 4 * ms::kMtN, hipMemcpyHostToDevice));
-    HIP_TRY(hipMemcpy(env->recs + e * env->P.rec_bytes + 8, &index, 4, hipMemcpyHostToDevice));
+    // current block = half 0; the successor half is recomputed before the env's next draw
+    const int32_t hdr[2] = {index, 0};
+    HIP_TRY(hipMemcpy(env->mt + mt_block(e, 0), words, 4 * ms::kMtN, hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(env->recs + e * env->P.rec_bytes + 8, hdr, sizeof(hdr), hipMemcpyHostToDevice));
     return MS_OK;
 }
 
@@ -287,7 +294,7 @@ int ms_env_export(ms_env* env, const ms_state_host* o, void* stream) {
     const ms::Params& P = env->P;
     HIP_TRY(hipStreamSynchronize((hipStream_t)stream));
     std::vector<uint8_t> rec((size_t)env->E * P.rec_bytes);
-    std::vector<uint32_t> mt((size_t)env->E * ms::kMtN);
+    std::vector<uint32_t> mt((size_t)env->E * 2 * ms::kMtN);
     std::vector<ms::Liab> lb((size_t)env->E * P.C * P.cap);
     HIP_TRY(hipMemcpy(rec.data(), env->recs, rec.size(), hipMemcpyDeviceToHost));
     HIP_TRY(hipMemcpy(mt.data(), env->mt, mt.size() * 4, hipMemcpyDeviceToHost));
@@ -330,7 +337,7 @@ int ms_env_export(ms_env* env, const ms_state_host* o, void* stream) {
             if (o->offer_recip) o->offer_recip[j] = REC_I8(b, P.o_offer_recip, i);
             if (o->offer_price) o->offer_price[j] = REC_I8(b, P.o_offer_price, i);
         }
-        if (o->mt) memcpy(o->mt + e * ms::kMtN, mt.data() + e * ms::kMtN, ms::kMtN * 4);
+        if (o->mt) memcpy(o->mt + e * ms::kMtN, mt.data() + mt_block(e, REC_I32(b, 12, 0)), ms::kMtN * 4);
     }
     return MS_OK;
 }
@@ -410,7 +417,9 @@ int ms_env_import(ms_env* env, const ms_state_host* in, void* stream) {
     }
     HIP_TRY(hipStreamSynchronize((hipStream_t)stream));
     HIP_TRY(hipMemcpy(env->recs, rec.data(), rec.size(), hipMemcpyHostToDevice));
-    HIP_TRY(hipMemcpy(env->mt, in->mt, (size_t)env->E * ms::kMtN * 4, hipMemcpyHostToDevice));
+    // current blocks = half 0 (record header mt_sel = 0: successors are recomputed on the device)
+    HIP_TRY(hipMemcpy2D(env->mt, 2 * ms::kMtN * 4, in->mt, ms::kMtN * 4, ms::kMtN * 4, (size_t)env->E,
+                        hipMemcpyHostToDevice));
     HIP_TRY(hipMemcpy(env->liab, lb.data(), lb.size() * sizeof(ms::Liab), hipMemcpyHostToDevice));
     env->round = in->round[0];
     return MS_OK;

@@ -40,6 +40,7 @@ __device__ __forceinline__ void wave_sync() {
 #ifdef MS_PHASE_TIMING
 constexpr int kProbeSlots = 65536;
 __device__ unsigned long long g_phase_cycles[kProbeSlots][16];  // per block, summed on the host
+__device__ unsigned long long g_wave_span[kProbeSlots][2];      // last launch: s_memrealtime at entry / exit
 #define MS_MARK(k)                                                     \
     do {                                                               \
         const uint64_t t_now = __builtin_amdgcn_s_memtime();          \
@@ -76,14 +77,94 @@ __device__ __forceinline__ uint32_t mt_temper(uint32_t y) {
     return y;
 }
 
-// In-place twist of the env's 624 state words in HBM by one lane group (once per ~39 rounds of
-// an env). The three phases respect the sequential recurrence: words [0,227) read only old
-// words, [227,454) read new [0,227), [454,623) read new [227,396), 623 reads new 0/396. Inside a
-// phase a chunk of LPE words is computed from old words (i, i+1 not yet written), then stored.
-// The loads bypass the CU's L1 (agent-scope relaxed atomics: they read the XCD's L2, where this
-// wave's stores land) and workgroup-scope fences order each chunk's stores before the group's
-// next loads. (An agent-scope fence would write the whole L2 back to make it visible to the
-// other XCDs, which nothing here needs.)
+__device__ __forceinline__ uint32_t mt_step(uint32_t hi_src, uint32_t lo_src, uint32_t xsrc) {
+    const uint32_t y = (hi_src & 0x80000000u) | (lo_src & 0x7fffffffu);
+    return xsrc ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
+}
+
+// The twist's three phases respect the sequential recurrence: words [0,227) read only old words,
+// [227,454) read new [0,227), [454,623) read new [227,396), 623 reads new 0/396. Inside a phase a
+// chunk of lanes computes from old words (i, i+1 not yet written), then stores.
+__device__ __forceinline__ void mt_phase_range(int ph, int& lo, int& hi) {
+    lo = ph * (kMtN - kMtM);
+    hi = ph < 2 ? (ph + 1) * (kMtN - kMtM) : kMtN - 1;
+}
+
+// Twist of 624 words in LDS by a whole wave.
+__device__ void mt_twist_lds_wave(uint32_t* st, int lane) {
+    for (int ph = 0; ph < 3; ph++) {
+        int lo, hi;
+        mt_phase_range(ph, lo, hi);
+        for (int c0 = lo; c0 < hi; c0 += kWave) {
+            const int i = c0 + lane;
+            uint32_t v = 0;
+            if (i < hi) v = mt_step(st[i], st[i + 1], st[ph == 0 ? i + kMtM : i + (kMtM - kMtN)]);
+            wave_sync();
+            if (i < hi) st[i] = v;
+            wave_sync();
+        }
+    }
+    if (lane == 0) st[kMtN - 1] = mt_step(st[kMtN - 1], st[0], st[kMtM - 1]);
+    wave_sync();
+}
+
+// successor half := twist(current half) of one env's blocks, by the whole wave in LDS
+__device__ void mt_twist_into_successor(uint32_t* mt_env, uint32_t sel, uint8_t* lds, int lane) {
+    uint32_t* st = reinterpret_cast<uint32_t*>(lds);
+    const uint32_t h = sel & 1u;
+    const uint32_t* cur = mt_env + h * kMtN;
+    uint32_t* nxt = mt_env + (h ^ 1u) * kMtN;
+    for (int i = lane; i < kMtN; i += kWave) st[i] = cur[i];
+    wave_sync();
+    mt_twist_lds_wave(st, lane);
+    for (int i = lane; i < kMtN; i += kWave) nxt[i] = st[i];
+    // the stores complete before this wave's later loads of the successor (other lanes' words)
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    wave_sync();
+}
+
+// Each env keeps two 624-word blocks in HBM ([E][2][624]): its current CPython state words and
+// their successor twist(current), so the round's draws never wait for a twist. Header word 3 of
+// the record (mt_sel) says which half is current (bit 0) and whether the other half holds its
+// successor (bit 1). An env whose stream crossed into the successor block in the previous round
+// gets the next successor at the start of the round: the whole wave twists it in LDS (the LDS is
+// not staged yet), once per ~40 rounds of an env.
+template <int LPE>
+__device__ void mt_refill_next(uint32_t* mt, const uint8_t* recs, const Params& P, bool active, uint8_t* lds,
+                               int lane) {
+    const int gl = lane & (LPE - 1);
+    const int64_t e0 = (int64_t)blockIdx.x * (kWave / LPE);
+    uint32_t sel = 0;
+    if (active && gl == 0) sel = *reinterpret_cast<const uint32_t*>(recs + (e0 + lane / LPE) * P.rec_bytes + 12);
+    uint64_t need = __ballot(active && gl == 0 && !(sel & 2u));
+    while (need) {
+        const int src = __ffsll((unsigned long long)need) - 1;
+        need &= need - 1;
+        mt_twist_into_successor(mt + (e0 + src / LPE) * 2 * kMtN, (uint32_t)__shfl((int)sel, src), lds, lane);
+    }
+}
+
+// New (mt_sel, mti) after a round whose draws ended at stream index fin (relative to the current
+// block): CPython's state is the block holding index fin - 1 with mti = the index within it.
+__device__ __forceinline__ void mt_commit(int fin, int32_t* mti, uint32_t* sel) {
+    const uint32_t h = *sel & 1u;
+    if (fin > 2 * kMtN) {  // fallback: the current half holds twist(successor), no successor yet
+        *sel = h;
+        *mti = fin - 2 * kMtN;
+    } else if (fin > kMtN) {  // crossed into the successor; its own successor comes next round
+        *sel = h ^ 1u;
+        *mti = fin - kMtN;
+    } else {
+        *sel = h | 2u;
+        *mti = fin;
+    }
+}
+
+// Fallback for a round that needs more than the current block's rest plus the successor (never
+// for the shipped configs): cur := twist(nxt), in place in HBM by one lane group. The loads bypass
+// the CU's L1 (agent-scope relaxed atomics read the XCD's L2, where this wave's stores land) and
+// workgroup-scope fences order each chunk's stores before the group's next loads.
 __device__ __forceinline__ uint32_t mt_ld(const uint32_t* p) {
     return __hip_atomic_load(const_cast<uint32_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -92,66 +173,67 @@ __device__ __forceinline__ void mt_st(uint32_t* p, uint32_t v) {
 }
 
 template <int LPE>
-__device__ void mt_twist_global(uint32_t* mt, int gl) {
-    auto step = [](uint32_t hi_src, uint32_t lo_src, uint32_t xsrc) -> uint32_t {
-        const uint32_t y = (hi_src & 0x80000000u) | (lo_src & 0x7fffffffu);
-        return xsrc ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
-    };
-    const int ranges[3][2] = {{0, kMtN - kMtM}, {kMtN - kMtM, 2 * (kMtN - kMtM)}, {2 * (kMtN - kMtM), kMtN - 1}};
+__device__ void mt_twist_from(uint32_t* cur, const uint32_t* nxt, int gl) {
+    for (int i = gl; i < kMtN; i += LPE) mt_st(cur + i, nxt[i]);
     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
     for (int ph = 0; ph < 3; ph++) {
-        for (int c0 = ranges[ph][0]; c0 < ranges[ph][1]; c0 += LPE) {
+        int lo, hi;
+        mt_phase_range(ph, lo, hi);
+        for (int c0 = lo; c0 < hi; c0 += LPE) {
             const int i = c0 + gl;
             uint32_t v = 0;
-            if (i < ranges[ph][1]) {
-                const int x = (ph == 0) ? i + kMtM : i + (kMtM - kMtN);
-                v = step(mt_ld(mt + i), mt_ld(mt + i + 1), mt_ld(mt + x));
-            }
+            if (i < hi) v = mt_step(mt_ld(cur + i), mt_ld(cur + i + 1), mt_ld(cur + (ph == 0 ? i + kMtM : i + (kMtM - kMtN))));
             __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
-            if (i < ranges[ph][1]) mt_st(mt + i, v);
+            if (i < hi) mt_st(cur + i, v);
             __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
         }
     }
-    if (gl == 0) mt_st(mt + kMtN - 1, step(mt_ld(mt + kMtN - 1), mt_ld(mt), mt_ld(mt + kMtM - 1)));
+    if (gl == 0) mt_st(cur + kMtN - 1, mt_step(mt_ld(cur + kMtN - 1), mt_ld(cur), mt_ld(cur + kMtM - 1)));
     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
 }
 
 // A window of LPE words of the env's stream held one word per group lane. Stream positions are
-// relative to the env's mti at kernel entry; positions at or beyond 624 - mti0 come from the
-// twisted state, computed at most once per launch and only when a consumer actually needs such
-// a word, so the stored state always equals CPython's after the same draws.
+// relative to the env's mti at kernel entry; index mti0 + pos < 624 reads the current block,
+// < 1248 its successor, beyond that the fallback block.
 template <int LPE>
 struct MtStream {
-    uint32_t* gmt;    // env's 624 state words in HBM
+    uint32_t* cur;    // current block (CPython's state words)
+    uint32_t* nxt;    // its successor (mt_refill_next made it valid)
     int mti0;         // mti at entry
     int wb, wend;     // window covers stream positions [wb, wend)
     int p;            // next unconsumed stream position
-    bool twisted;
-    bool store;       // false for a padding group: never twist (its draws are discarded)
+    bool fell_back;   // cur was overwritten with twist(nxt)
+    bool store;       // false for a padding group: never write (its draws are discarded)
     uint32_t v;       // this lane's tempered word (position wb + gl)
 
+    __device__ void init(uint32_t* mt_env, uint32_t sel, int mti, bool active) {
+        cur = mt_env + (sel & 1u) * kMtN;
+        nxt = mt_env + ((sel & 1u) ^ 1u) * kMtN;
+        mti0 = mti;
+        wb = wend = p = 0;
+        fell_back = false;
+        store = active;
+        v = 0;
+    }
+
     // Window at stream position pos. need = words the caller is about to consume; need == 0
-    // only peeks (never twists; the window may be empty).
+    // only peeks (never falls back; the window may be empty).
     __device__ void load(int pos, int need, const Lanes<LPE>& L) {
-        const int limit = twisted ? 0x3fffffff : (kMtN - mti0);  // old words end here
-        const int g = mti0 + pos + L.gl;
-        if (!twisted && need > 0 && pos + need > limit) {
-            const uint32_t old = (g < kMtN) ? gmt[g] : 0u;  // old words of this window
-            if (store) mt_twist_global<LPE>(gmt, L.gl);
-            twisted = true;
-            v = mt_temper((g < kMtN) ? old : (g < 2 * kMtN ? mt_ld(gmt + g - kMtN) : 0u));
-            wb = pos;
-            wend = pos + LPE;
-            return;
+        if (!fell_back && need > 0 && mti0 + pos + need > 2 * kMtN) {
+            if (store) mt_twist_from<LPE>(cur, nxt, L.gl);
+            fell_back = true;
         }
+        const int g = mti0 + pos + L.gl;
         uint32_t raw = 0;
-        if (twisted)
-            raw = (g >= kMtN && g < 2 * kMtN) ? mt_ld(gmt + g - kMtN) : 0u;
-        else if (g < kMtN)
-            raw = gmt[g];
+        if (g < kMtN)
+            raw = cur[g];
+        else if (g < 2 * kMtN)
+            raw = nxt[g - kMtN];
+        else if (g < 3 * kMtN)
+            raw = mt_ld(cur + g - 2 * kMtN);
         v = mt_temper(raw);
         wb = pos;
-        wend = twisted ? pos + LPE : min(pos + LPE, limit);
+        wend = fell_back ? pos + LPE : min(pos + LPE, 2 * kMtN - mti0);
     }
 
     // Random._randbelow_with_getrandbits(n) (random.py:239-249), group-uniform result
@@ -173,8 +255,8 @@ struct MtStream {
         }
     }
 
-    // final mti (CPython's index after the same draws)
-    __device__ int final_index() const { return twisted ? (mti0 + p - kMtN) : (mti0 + p); }
+    // stream index after the draws, relative to the entry block (see mt_commit)
+    __device__ int end_index() const { return mti0 + p; }
 };
 
 // ---------------------------------------------------------------------------
@@ -191,6 +273,7 @@ struct Rec {
     __device__ int32_t& round() { return *reinterpret_cast<int32_t*>(b + 0); }
     __device__ uint32_t& flags() { return *reinterpret_cast<uint32_t*>(b + 4); }
     __device__ int32_t& mti() { return *reinterpret_cast<int32_t*>(b + 8); }
+    __device__ uint32_t& mt_sel() { return *reinterpret_cast<uint32_t*>(b + 12); }
     __device__ int8_t* core_owner() { return reinterpret_cast<int8_t*>(b + P->o_core_owner); }
     __device__ int8_t* core_kind() { return reinterpret_cast<int8_t*>(b + P->o_core_kind); }
     __device__ int8_t* core_rem() { return reinterpret_cast<int8_t*>(b + P->o_core_rem); }
@@ -219,6 +302,58 @@ __device__ __forceinline__ void copy_dwords(uint32_t* dst, const uint32_t* src, 
 #pragma unroll 8
     for (int i = gl; i < n; i += LPE) dst[i] = src[i];
 }
+
+// Output arrays written with 16-byte write-through stores (sc1): the line leaves the XCD's L2
+// with the store, so the kernel ends without megabytes of dirty L2 lines to write back at its
+// boundary (the next kernel reads them from another XCD's side anyway). Addressed as a raw buffer
+// over the whole array (wave-uniform base, per-lane 31-bit byte offsets).
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+struct WtOut {
+    __amdgpu_buffer_rsrc_t r;
+    bool ok;  // 16-B aligned base and an array that fits the buffer range
+    __device__ WtOut(void* base, int64_t bytes) {
+        ok = base != nullptr && (reinterpret_cast<uintptr_t>(base) & 15) == 0 && bytes <= 0x7fffffff;
+        r = __builtin_amdgcn_make_buffer_rsrc(base, 0, ok ? (int)bytes : 0, 0x00020000);
+    }
+    __device__ __forceinline__ void st4(int64_t off, uint32_t a, uint32_t b, uint32_t c, uint32_t d) const {
+        const u32x4 v = {a, b, c, d};
+        __builtin_amdgcn_raw_buffer_store_b128(v, r, (int)off, 0, 16 /* sc1 */);
+    }
+};
+
+// n_dw dwords from LDS to env e's block (env_off bytes into the array): write-through 16-B stores
+// when the block allows, else plain dword stores to dst.
+template <int LPE>
+__device__ __forceinline__ void copy_out(const WtOut& o, int64_t env_off, uint32_t* dst, const uint32_t* src, int n_dw,
+                                         int gl) {
+    if (o.ok && (n_dw & 3) == 0 && (env_off & 15) == 0) {
+        for (int k = gl; 4 * k < n_dw; k += LPE)
+            o.st4(env_off + 16 * k, src[4 * k], src[4 * k + 1], src[4 * k + 2], src[4 * k + 3]);
+    } else {
+        copy_dwords<LPE>(dst, src, n_dw, gl);
+    }
+}
+
+// Up to R dwords per lane of n from global to LDS, all loads issued before the first LDS store
+// (with stage_dwords_rest for n > R * LPE): the staged arrays then cost one memory round trip.
+template <int LPE, int R>
+struct DwordBatch {
+    uint32_t v[R];
+    __device__ __forceinline__ void load(const uint32_t* src, int n, int gl) {
+#pragma unroll
+        for (int i = 0; i < R; i++) {
+            const int k = gl + i * LPE;
+            v[i] = k < n ? src[k] : 0u;
+        }
+    }
+    __device__ __forceinline__ void store(uint32_t* dst, int n, int gl) const {
+#pragma unroll
+        for (int i = 0; i < R; i++) {
+            const int k = gl + i * LPE;
+            if (k < n) dst[k] = v[i];
+        }
+    }
+};
 
 // n bytes from global src to LDS dst: dword loads when both sides allow (issued together, then
 // the LDS stores), else byte loads. LDS destinations are 4-byte aligned (ms_layout.h).
@@ -323,9 +458,14 @@ __device__ void build_masks(Rec& R, const Params& P, M128* mc, M128* mr, int gl)
 // row of (agent a, core c) (Agent.py:167-212) is the core's "owner row"
 //   [1, prio, rem, (price, necT) per offer to c in offer-ID order, (-2, -2) pad, 0 stride pad]
 // when a owns c, and otherwise the constant "foreign row" [0, -1, -1, (-2, -2) * O, 0 pad]; the
-// auctioneer row of core c (Auctioneer.py:34-77) is the same with the auctioneer as owner.
-// The C owner rows are built in LDS, then every output row is streamed with one dword store
-// per lane (the group's lanes cover one row's dwords).
+// auctioneer row of core c (Auctioneer.py:34-77) is the same with the auctioneer as owner. An
+// offer row (Agent.py:271-300) is the env's core-pair template with the slot's own pair merged.
+//
+// The source rows are built in LDS; then each of the env's observation blocks is streamed as a
+// flat dword array. The strides are multiples of 4, so every dword lies in one row and is a
+// dword of that row's source. With 16-B aligned blocks each lane stores 4 consecutive dwords
+// with one global_store_dwordx4: the store-instruction count per CU, not the bytes, bounded the
+// row-at-a-time emission.
 
 // dword k of the foreign row
 __device__ __forceinline__ uint32_t foreign_dword(int k, int d_acc) {
@@ -339,94 +479,106 @@ __device__ __forceinline__ uint32_t foreign_dword(int k, int d_acc) {
     return w;
 }
 
-// The owner rows of all C cores in LDS ([C][acc_stride] bytes), built by the core lanes.
+// The LDS sources of env e's observations:
+//   crow [C+1][acc_stride]: the owner rows of the C cores, then the foreign row;
+//   rowsel [N*C]: source row of acceptor row (a, c): c if agent a owns core c, else C;
+//   otmpl [off_stride]: offer-row template (the (prio, rem) pairs of all cores, zero tail);
+//   slot_pair [NL]: (prio, rem) of every slot.
 template <int LPE>
-__device__ void build_owner_rows(Rec& R, const Params& P, const M128* mc, const M128* mr, uint32_t* crow, int gl) {
-    const int nw = P.acc_stride / 4;
-    for (int i = gl; i < P.C * nw; i += LPE) {
-        const int k = i - (i / nw) * nw;
-        crow[i] = foreign_dword(k, P.d_acc);
-    }
-    wave_sync();
-    for (int c = gl; c < P.C; c += LPE) {
-        int8_t* row = reinterpret_cast<int8_t*>(crow) + c * P.acc_stride;
-        const int kind = R.core_kind()[c];
-        row[0] = 1;
-        row[1] = (int8_t)(kind >= 0 ? R.prio(kind) : -1);
-        row[2] = R.core_rem()[c];
-        const int8_t* op = R.offer_price();
-        const int8_t* sr = R.slot_rem();
-        int w = 3;
-        for (MaskIter it(mand(mc[c], mr[R.core_owner()[c]])); it.more();) {
-            const int i = it.next();
-            row[w] = op[i];
-            row[w + 1] = sr[i];
-            w += 2;
-        }
-    }
-    wave_sync();
-}
-
-// Acceptor rows [N][C] (auct == false) or auctioneer rows [C] (auct == true) of one env.
-template <int LPE>
-__device__ void emit_acc_rows(Rec& R, const Params& P, const uint32_t* crow, int8_t* dst, bool auct, int gl) {
-    if (!dst) return;
+__device__ void build_obs_sources(Rec& R, const Params& P, const M128* mc, const M128* mr, uint8_t* scratch, bool acc,
+                                  bool auct, bool off, int gl) {
     const int C = P.C, nw = P.acc_stride / 4;
-    uint32_t* out = reinterpret_cast<uint32_t*>(dst);
+    uint32_t* crow = reinterpret_cast<uint32_t*>(scratch);
     const int8_t* owner = R.core_owner();
-    const int n_agents = auct ? 1 : P.N;
-    for (int k0 = 0; k0 < nw; k0 += LPE) {  // dword columns of a row covered by the group
-        const int k = k0 + gl;
-        const bool lane_on = k < nw;
-        const uint32_t fw = foreign_dword(k, P.d_acc);
-#pragma unroll 4
-        for (int c = 0; c < C; c++) {
-            const int oc = owner[c];                       // group-uniform LDS broadcast
-            const uint32_t cw = crow[c * nw + (lane_on ? k : 0)];
-            for (int a = 0; a < n_agents; a++) {
-                const int who = auct ? 0 : a + 1;
-                if (lane_on) out[(a * C + c) * nw + k] = oc == who ? cw : fw;
-            }
-        }
-    }
-}
-
-// Offer rows [N][L] (Agent.py:271-300): the (prio, rem) pairs of all cores — the same for every
-// row of the env — then the slot's own pair, zero padded to the stride. Each lane owns one dword
-// column: the core-pair bytes of its column are computed once, the slot pair merged per row.
-template <int LPE>
-__device__ void emit_off_rows(Rec& R, const Params& P, uint16_t* slot_pair, int8_t* dst, int gl) {
-    if (!dst) return;
-    const int C = P.C, nw = P.off_stride / 4;
     const int8_t* ck = R.core_kind();
     const int8_t* cr = R.core_rem();
-    for (int s = gl; s < P.NL; s += LPE) {  // the slot pairs, once
-        const int k = R.slot_kind()[s];
-        const uint32_t pr = (uint8_t)(k < 0 ? -1 : R.prio(k));
-        const uint32_t rm = (uint8_t)(k < 0 ? -1 : R.slot_rem()[s]);
-        slot_pair[s] = (uint16_t)(pr | (rm << 8));
+    if (acc || auct) {
+        for (int i = gl; i < (C + 1) * nw; i += LPE) {
+            const int k = i - (i / nw) * nw;
+            crow[i] = foreign_dword(k, P.d_acc);
+        }
+    }
+    if (acc) {
+        uint8_t* rowsel = scratch + P.s_rowsel;
+        for (int r = gl; r < P.N * C; r += LPE) {
+            const int a = r / C, c = r - a * C;
+            rowsel[r] = (uint8_t)(owner[c] == a + 1 ? c : C);
+        }
+    }
+    if (off) {
+        uint32_t* otmpl = reinterpret_cast<uint32_t*>(scratch + P.s_otmpl);
+        for (int k = gl; k < P.off_stride / 4; k += LPE) {
+            uint32_t cw = 0;
+#pragma unroll
+            for (int b = 0; b < 4; b++) {
+                const int col = 4 * k + b;
+                if (col < 2 * C) {
+                    const int c = col >> 1, kk = ck[c];
+                    const int v = kk < 0 ? -1 : ((col & 1) ? cr[c] : R.prio(kk));
+                    cw |= (uint32_t)(uint8_t)v << (8 * b);
+                }
+            }
+            otmpl[k] = cw;
+        }
+        uint16_t* slot_pair = reinterpret_cast<uint16_t*>(scratch + P.s_slotpair);
+        for (int s = gl; s < P.NL; s += LPE) {
+            const int k = R.slot_kind()[s];
+            const uint32_t pr = (uint8_t)(k < 0 ? -1 : R.prio(k));
+            const uint32_t rm = (uint8_t)(k < 0 ? -1 : R.slot_rem()[s]);
+            slot_pair[s] = (uint16_t)(pr | (rm << 8));
+        }
     }
     wave_sync();
-    uint32_t* out = reinterpret_cast<uint32_t*>(dst);
-    for (int k0 = 0; k0 < nw; k0 += LPE) {
-        const int k = k0 + gl;
-        const bool lane_on = k < nw;
-        uint32_t cw = 0;  // core-pair bytes of this dword column
-#pragma unroll
-        for (int b = 0; b < 4; b++) {
-            const int col = 4 * k + b;
-            if (lane_on && col < 2 * C) {
-                const int c = col >> 1, kk = ck[c];
-                const int v = kk < 0 ? -1 : ((col & 1) ? cr[c] : R.prio(kk));
-                cw |= (uint32_t)(uint8_t)v << (8 * b);
+    if (acc || auct) {
+        const int8_t* op = R.offer_price();
+        const int8_t* sr = R.slot_rem();
+        for (int c = gl; c < C; c += LPE) {
+            int8_t* row = reinterpret_cast<int8_t*>(crow) + c * P.acc_stride;
+            const int kind = ck[c];
+            row[0] = 1;
+            row[1] = (int8_t)(kind >= 0 ? R.prio(kind) : -1);
+            row[2] = cr[c];
+            int w = 3;
+            for (MaskIter it(mand(mc[c], mr[owner[c]])); it.more();) {
+                const int i = it.next();
+                row[w] = op[i];
+                row[w + 1] = sr[i];
+                w += 2;
             }
         }
-        const int off = 2 * C - 4 * k;  // byte position of the slot pair in this dword (0 or 2 if here)
-#pragma unroll 4
-        for (int s = 0; s < P.NL; s++) {
-            uint32_t w = cw;
-            if (off == 0 || off == 2) w |= (uint32_t)slot_pair[s] << (8 * off);
-            if (lane_on) out[s * nw + k] = w;
+    }
+    wave_sync();
+}
+
+__device__ __forceinline__ int div_mag(uint32_t w, uint32_t mag, int d) { return d == 1 ? (int)w : (int)__umulhi(w, mag); }
+
+// Block e of an [E][n_dw] dword array: dword w = val(w / nw, w % nw), LPE lanes, 4 dwords per
+// lane-store (write-through) when aligned.
+template <int LPE, class F>
+__device__ __forceinline__ void emit_flat(uint32_t* base, int64_t e, int64_t E, int n_dw, int nw, uint32_t mag, int gl,
+                                          F val) {
+    const WtOut o(base, E * n_dw * 4);
+    if (o.ok && (n_dw & 3) == 0) {
+        const int64_t env_off = e * n_dw * 4;
+        for (int k = gl; 4 * k < n_dw; k += LPE) {
+            const int w0 = 4 * k;
+            int r = div_mag(w0, mag, nw), col = w0 - r * nw;
+            uint32_t v[4];
+#pragma unroll
+            for (int i = 0; i < 4; i++) {
+                v[i] = val(r, col);
+                if (++col == nw) {
+                    col = 0;
+                    r++;
+                }
+            }
+            o.st4(env_off + 4 * w0, v[0], v[1], v[2], v[3]);
+        }
+    } else {
+        uint32_t* dst = base + e * n_dw;
+        for (int w = gl; w < n_dw; w += LPE) {
+            const int r = div_mag(w, mag, nw);
+            dst[w] = val(r, w - r * nw);
         }
     }
 }
@@ -434,13 +586,35 @@ __device__ void emit_off_rows(Rec& R, const Params& P, uint16_t* slot_pair, int8
 // All observations of env e (dst == NULL skips a kind; a padding group passes write = false).
 template <int LPE>
 __device__ void emit_obs(Rec& R, const Params& P, const M128* mc, const M128* mr, uint8_t* scratch, int8_t* acc,
-                         int8_t* off, int8_t* auct, int64_t e, bool write, int gl) {
-    uint32_t* crow = reinterpret_cast<uint32_t*>(scratch);
-    uint16_t* slot_pair = reinterpret_cast<uint16_t*>(scratch + P.s_slotpair);
-    if (acc || auct) build_owner_rows<LPE>(R, P, mc, mr, crow, gl);
-    if (acc) emit_acc_rows<LPE>(R, P, crow, write ? acc + e * (int64_t)P.N * P.C * P.acc_stride : nullptr, false, gl);
-    if (auct) emit_acc_rows<LPE>(R, P, crow, write ? auct + e * (int64_t)P.C * P.acc_stride : nullptr, true, gl);
-    if (off) emit_off_rows<LPE>(R, P, slot_pair, write ? off + e * (int64_t)P.NL * P.off_stride : nullptr, gl);
+                         int8_t* off, int8_t* auct, int64_t e, int64_t E, bool write, int gl) {
+    build_obs_sources<LPE>(R, P, mc, mr, scratch, acc != nullptr, auct != nullptr, off != nullptr, gl);
+    if (!write) return;
+    const int C = P.C, nw = P.acc_stride / 4, nwo = P.off_stride / 4;
+    const uint32_t* crow = reinterpret_cast<const uint32_t*>(scratch);
+    if (acc) {
+        const uint8_t* rowsel = scratch + P.s_rowsel;
+        const int n_dw = P.N * C * nw;
+        emit_flat<LPE>(reinterpret_cast<uint32_t*>(acc), e, E, n_dw, nw, P.mag_acc, gl,
+                       [&](int r, int col) { return crow[rowsel[r] * nw + col]; });
+    }
+    if (auct) {
+        const int8_t* owner = R.core_owner();
+        const int n_dw = C * nw;
+        emit_flat<LPE>(reinterpret_cast<uint32_t*>(auct), e, E, n_dw, nw, P.mag_acc, gl,
+                       [&](int c, int col) { return crow[(owner[c] == 0 ? c : C) * nw + col]; });
+    }
+    if (off) {
+        const uint32_t* otmpl = reinterpret_cast<const uint32_t*>(scratch + P.s_otmpl);
+        const uint16_t* slot_pair = reinterpret_cast<const uint16_t*>(scratch + P.s_slotpair);
+        const int pcol = (2 * C) >> 2, pshift = 8 * ((2 * C) & 3);
+        const int n_dw = P.NL * nwo;
+        emit_flat<LPE>(reinterpret_cast<uint32_t*>(off), e, E, n_dw, nwo, P.mag_off, gl,
+                       [&](int s, int col) {
+                           uint32_t v = otmpl[col];
+                           if (col == pcol) v |= (uint32_t)slot_pair[s] << pshift;
+                           return v;
+                       });
+    }
 }
 
 // HardcodedAuctioneerAcceptor.selectAction for every core (HardcodedModules.py:54-78,
@@ -564,9 +738,13 @@ __global__ void __launch_bounds__(64) k_env_init(Params P, uint8_t* recs, uint32
         }
         st[0] = 0x80000000u;
         R.mti() = kMtN;
+        R.mt_sel() = 2u;  // current = half 0, half 1 = its successor
     }
     wave_sync();
-    copy_dwords<kWave>(mt + e * kMtN, st, kMtN, lane);
+    copy_dwords<kWave>(mt + e * 2 * kMtN, st, kMtN, lane);
+    wave_sync();
+    mt_twist_lds_wave(st, lane);
+    copy_dwords<kWave>(mt + e * 2 * kMtN + kMtN, st, kMtN, lane);
     copy_dwords<kWave>(reinterpret_cast<uint32_t*>(recs + e * (int64_t)P.rec_bytes), reinterpret_cast<uint32_t*>(rec),
                        P.rec_bytes / 4, lane);
 }
@@ -586,7 +764,7 @@ __global__ void __launch_bounds__(64) k_env_reset(Params P, const uint8_t* recs,
     wave_sync();
     Rec R{rec, &P, s_kt};
     build_masks<kWave>(R, P, s_mc, s_mr, lane);
-    emit_obs<kWave>(R, P, s_mc, s_mr, smem + P.s_scratch, obs_acc, obs_off, obs_auct, e, true, lane);
+    emit_obs<kWave>(R, P, s_mc, s_mr, smem + P.s_scratch, obs_acc, obs_off, obs_auct, e, gridDim.x, true, lane);
 }
 
 constexpr int kLiabPrefetch = 4;  // newest chain entries loaded ahead per core that may terminate
@@ -621,6 +799,7 @@ __global__ void __launch_bounds__(64) k_env_step(Params P, int64_t E, uint8_t* r
 #ifdef MS_PHASE_TIMING
     uint64_t t_prev = __builtin_amdgcn_s_memtime();
     uint64_t t_acc[16] = {};
+    const uint64_t rt_start = __builtin_amdgcn_s_memrealtime();
 #endif
 
     uint8_t* rec = smem + P.s_rec;
@@ -634,15 +813,44 @@ __global__ void __launch_bounds__(64) k_env_step(Params P, int64_t E, uint8_t* r
     int8_t* spawn_kind = reinterpret_cast<int8_t*>(smem + P.s_spawn_kind);
     uint8_t* scratch = smem + P.s_scratch;
 
-    // ---- stage state and actions in LDS
+    // ---- successor MT blocks of the envs that crossed into theirs last round (whole wave, LDS
+    //      not staged yet), then stage state and actions in LDS
+    mt_refill_next<LPE>(mt, recs, P, active, smem_all, lane);
     __shared__ int32_t s_kt[48];
     load_kind_tables(P, s_kt, lane);
-    copy_dwords<LPE>(reinterpret_cast<uint32_t*>(rec),
-                     reinterpret_cast<const uint32_t*>(recs + e * (int64_t)P.rec_bytes), P.rec_bytes / 4, gl);
-    stage_bytes<LPE>(a_acc, io.act_acc + e * N * C, N * C, gl);
-    stage_bytes<LPE>(a_off, io.act_off + e * NL, NL, gl);
-    if (io.act_price) stage_bytes<LPE>(a_price, io.act_price + e * NL, NL, gl);
-    if (io.act_auct) stage_bytes<LPE>(a_auct, io.act_auct + e * C, C, gl);
+    {
+        // the record and the dword-aligned action arrays: one batch of loads, then the LDS stores
+        const uint32_t* src_rec = reinterpret_cast<const uint32_t*>(recs + e * (int64_t)P.rec_bytes);
+        const int rec_dw = P.rec_bytes / 4;
+        const int8_t* a_src[4] = {io.act_acc + e * N * C, io.act_off + e * NL,
+                                  io.act_price ? io.act_price + e * NL : nullptr,
+                                  io.act_auct ? io.act_auct + e * C : nullptr};
+        int8_t* a_dst[4] = {a_acc, a_off, a_price, a_auct};
+        const int a_len[4] = {N * C, NL, NL, C};
+        int a_dw[4];
+#pragma unroll
+        for (int i = 0; i < 4; i++)
+            a_dw[i] = (a_src[i] && (a_len[i] & 3) == 0 && (reinterpret_cast<uintptr_t>(a_src[i]) & 3) == 0)
+                          ? a_len[i] / 4
+                          : 0;
+        constexpr int RB = (96 + LPE - 1) / LPE;  // records up to 384 B in the batch
+        DwordBatch<LPE, RB> br;
+        DwordBatch<LPE, 1> ba[4];
+        br.load(src_rec, rec_dw, gl);
+#pragma unroll
+        for (int i = 0; i < 4; i++) ba[i].load(reinterpret_cast<const uint32_t*>(a_src[i]), a_dw[i], gl);
+        br.store(reinterpret_cast<uint32_t*>(rec), rec_dw, gl);
+#pragma unroll
+        for (int i = 0; i < 4; i++) ba[i].store(reinterpret_cast<uint32_t*>(a_dst[i]), a_dw[i], gl);
+        // the rest (large records / action arrays, unaligned arrays)
+        for (int k = gl + RB * LPE; k < rec_dw; k += LPE) reinterpret_cast<uint32_t*>(rec)[k] = src_rec[k];
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            for (int k = gl + LPE; k < a_dw[i]; k += LPE)
+                reinterpret_cast<uint32_t*>(a_dst[i])[k] = reinterpret_cast<const uint32_t*>(a_src[i])[k];
+            if (a_src[i] && a_dw[i] == 0) stage_bytes<LPE>(a_dst[i], a_src[i], a_len[i], gl);
+        }
+    }
     for (int i = gl; i < N * C; i += LPE) acc_r[i] = 0;
     for (int i = gl; i < NL; i += LPE) {
         off_r[i] = 0.f;
@@ -681,11 +889,7 @@ __global__ void __launch_bounds__(64) k_env_step(Params P, int64_t E, uint8_t* r
     //      this round, i.e. whose current job or one of the jobs offered to it has
     //      one round left (its chain is settled in the tick below)
     MtStream<LPE> rs;
-    rs.gmt = mt + e * kMtN;
-    rs.mti0 = R.mti();
-    rs.p = 0;
-    rs.twisted = false;
-    rs.store = active;
+    rs.init(mt + e * 2 * kMtN, R.mt_sel(), R.mti(), active);
     rs.load(0, 0, Lg);
     build_masks<LPE>(R, P, s_mc, s_mr, gl);
     Liab pf[kLiabPrefetch];
@@ -987,7 +1191,7 @@ __global__ void __launch_bounds__(64) k_env_step(Params P, int64_t E, uint8_t* r
     MS_MARK(8);
     if (gl == 0) {
         R.round() = round + 1;
-        R.mti() = rs.final_index();
+        mt_commit(rs.end_index(), &R.mti(), &R.mt_sel());
         R.flags() |= s_flags;
     }
     wave_sync();
@@ -997,28 +1201,29 @@ __global__ void __launch_bounds__(64) k_env_step(Params P, int64_t E, uint8_t* r
     if (active) {
         copy_dwords<LPE>(reinterpret_cast<uint32_t*>(recs + e * (int64_t)P.rec_bytes), reinterpret_cast<uint32_t*>(rec),
                          P.rec_bytes / 4, gl);
-        if (io.rew_acc)
-            copy_dwords<LPE>(reinterpret_cast<uint32_t*>(io.rew_acc + e * N * C), reinterpret_cast<uint32_t*>(acc_r),
-                             N * C, gl);
-        if (io.rew_offer)
-            copy_dwords<LPE>(reinterpret_cast<uint32_t*>(io.rew_offer + e * NL), reinterpret_cast<uint32_t*>(off_r), NL,
-                             gl);
-        if (io.rew_price)
-            copy_dwords<LPE>(reinterpret_cast<uint32_t*>(io.rew_price + e * NL), reinterpret_cast<uint32_t*>(price_r),
-                             NL, gl);
-        if (io.rew_agent)
-            for (int a = gl; a < N; a += LPE) io.rew_agent[e * N + a] = s_agent_r[a];
-        if (io.rew_auct)
-            for (int c = gl; c < C; c += LPE) io.rew_auct[e * C + c] = s_auct_r[c];
+        // rewards: write-through (consumed by the update, rounds later)
+        auto rew = [&](void* base, int per_env, const void* src) {
+            if (!base) return;
+            copy_out<LPE>(WtOut(base, E * per_env * 4), e * per_env * 4, reinterpret_cast<uint32_t*>(base) + e * per_env,
+                          reinterpret_cast<const uint32_t*>(src), per_env, gl);
+        };
+        rew(io.rew_acc, N * C, acc_r);
+        rew(io.rew_offer, NL, off_r);
+        rew(io.rew_price, NL, price_r);
+        rew(io.rew_agent, N, s_agent_r);
+        rew(io.rew_auct, C, s_auct_r);
     }
     MS_MARK(10);
     build_masks<LPE>(R, P, s_mc, s_mr, gl);
     MS_MARK(11);
-    emit_obs<LPE>(R, P, s_mc, s_mr, scratch, io.obs_acc, io.obs_off, io.obs_auct, e, active, gl);
+    emit_obs<LPE>(R, P, s_mc, s_mr, scratch, io.obs_acc, io.obs_off, io.obs_auct, e, E, active, gl);
     MS_MARK(12);
 #ifdef MS_PHASE_TIMING
-    if (lane == 0)
+    if (lane == 0) {
         for (int k = 0; k < 16; k++) g_phase_cycles[blockIdx.x % kProbeSlots][k] += t_acc[k];
+        g_wave_span[blockIdx.x % kProbeSlots][0] = rt_start;
+        g_wave_span[blockIdx.x % kProbeSlots][1] = __builtin_amdgcn_s_memrealtime();
+    }
 #endif
 }
 
@@ -1035,23 +1240,23 @@ __global__ void __launch_bounds__(64) k_env_auctioneer(Params P, uint8_t* recs, 
     const int64_t e = blockIdx.x;
     uint8_t* rec = smem + P.s_rec;
     __shared__ int32_t s_kt[48];
+    mt_refill_next<kWave>(mt, recs, P, true, smem, lane);
     load_kind_tables(P, s_kt, lane);
     copy_dwords<kWave>(reinterpret_cast<uint32_t*>(rec),
                        reinterpret_cast<const uint32_t*>(recs + e * (int64_t)P.rec_bytes), P.rec_bytes / 4, lane);
     wave_sync();
     Rec R{rec, &P, s_kt};
     MtStream<kWave> rs;
-    rs.gmt = mt + e * kMtN;
-    rs.mti0 = R.mti();
-    rs.p = 0;
-    rs.twisted = false;
-    rs.store = true;
+    rs.init(mt + e * 2 * kMtN, R.mt_sel(), R.mti(), true);
     rs.load(0, 0, Lg);
     build_masks<kWave>(R, P, s_mc, s_mr, lane);
     hardcoded_auctioneer<kWave>(R, P, s_mc, s_mr, rs, s_auct, Lg);
     wave_sync();
     for (int c = lane; c < P.C; c += kWave) actions[e * P.C + c] = (int8_t)s_auct[c];
-    if (lane == 0) *reinterpret_cast<int32_t*>(recs + e * (int64_t)P.rec_bytes + 8) = rs.final_index();
+    if (lane == 0) {
+        int32_t* hdr = reinterpret_cast<int32_t*>(recs + e * (int64_t)P.rec_bytes);
+        mt_commit(rs.end_index(), hdr + 2, reinterpret_cast<uint32_t*>(hdr + 3));
+    }
 }
 
 // random._randbelow(n) on env e's stream (random.randint in the update schedulers,
@@ -1063,18 +1268,15 @@ __global__ void __launch_bounds__(64) k_env_randbelow(Params P, uint8_t* recs, u
     const Lanes<kWave> Lg(lane);
     uint8_t* rec = recs + e * (int64_t)P.rec_bytes;
     int32_t* mti = reinterpret_cast<int32_t*>(rec + 8);
+    uint32_t* sel = reinterpret_cast<uint32_t*>(rec + 12);
+    if (!(*sel & 2u)) mt_twist_into_successor(mt + e * 2 * kMtN, *sel, smem, lane);
     MtStream<kWave> rs;
-    rs.gmt = mt + e * kMtN;
-    rs.mti0 = *mti;
-    rs.wb = rs.wend = rs.p = 0;
-    rs.twisted = false;
-    rs.store = true;
-    rs.v = 0;
+    rs.init(mt + e * 2 * kMtN, *sel, *mti, true);
     const uint32_t r = rs.randbelow(n, Lg);
     wave_sync();
     if (lane == 0) {
         *out = r;
-        *mti = rs.final_index();
+        mt_commit(rs.end_index(), mti, sel);
     }
 }
 
@@ -1093,6 +1295,14 @@ extern "C" int ms_probe_phase_cycles(unsigned long long* out, int clear) {
         memset(host, 0, sizeof(host));
         if (hipMemcpyToSymbol(HIP_SYMBOL(ms::g_phase_cycles), host, sizeof(host)) != hipSuccess) return -1;
     }
+    return 0;
+}
+// entry / exit s_memrealtime (100 MHz) of every block of the last launch: out[2 * n_blocks]
+extern "C" int ms_probe_wave_spans(unsigned long long* out, int n_blocks) {
+    static unsigned long long host[ms::kProbeSlots][2];
+    if (n_blocks > ms::kProbeSlots) return -1;
+    if (hipMemcpyFromSymbol(host, HIP_SYMBOL(ms::g_wave_span), sizeof(host)) != hipSuccess) return -1;
+    memcpy(out, host, sizeof(unsigned long long) * 2 * n_blocks);
     return 0;
 }
 #endif
@@ -1114,9 +1324,12 @@ hipError_t launch_env_reset(const Params& P, int64_t E, const uint8_t* recs, int
 
 // lanes per env: the smallest power of two >= max(C, N) and >= 16 (a 16-word MT window), so a
 // wave steps 4 (cfg2/cfg3), 2 (cfg4) or 1 (cfg5) envs
+#ifndef MS_MIN_LPE
+#define MS_MIN_LPE 16
+#endif
 static int lanes_per_env(const Params& P) {
     int need = P.C > P.N ? P.C : P.N;
-    int lpe = 16;
+    int lpe = MS_MIN_LPE;
     while (lpe < need) lpe *= 2;
     return lpe;
 }
@@ -1126,14 +1339,15 @@ static hipError_t launch_step_t(const Params& P, int64_t E, uint8_t* recs, uint3
                                 hipStream_t s) {
     constexpr int G = kWave / LPE;
     const int64_t blocks = (E + G - 1) / G;
-    hipLaunchKernelGGL((k_env_step<LPE>), dim3((unsigned)blocks), dim3(kWave), (size_t)P.s_total * G, s, P, E, recs,
-                       mt, liab, io);
+    const size_t lds = (size_t)P.s_total * G > 4 * kMtN ? (size_t)P.s_total * G : 4 * kMtN;  // >= one MT block
+    hipLaunchKernelGGL((k_env_step<LPE>), dim3((unsigned)blocks), dim3(kWave), lds, s, P, E, recs, mt, liab, io);
     return hipGetLastError();
 }
 
 hipError_t launch_env_step(const Params& P, int64_t E, uint8_t* recs, uint32_t* mt, Liab* liab, const StepIO& io,
                            hipStream_t s) {
     switch (lanes_per_env(P)) {
+        case 8: return launch_step_t<8>(P, E, recs, mt, liab, io, s);
         case 16: return launch_step_t<16>(P, E, recs, mt, liab, io, s);
         case 32: return launch_step_t<32>(P, E, recs, mt, liab, io, s);
         default: return launch_step_t<64>(P, E, recs, mt, liab, io, s);
@@ -1141,12 +1355,13 @@ hipError_t launch_env_step(const Params& P, int64_t E, uint8_t* recs, uint32_t* 
 }
 hipError_t launch_env_auctioneer(const Params& P, int64_t E, uint8_t* recs, uint32_t* mt, int8_t* actions,
                                  hipStream_t s) {
-    hipLaunchKernelGGL(k_env_auctioneer, dim3((unsigned)E), dim3(kWave), P.s_total, s, P, recs, mt, actions);
+    const size_t lds = (size_t)P.s_total > 4 * kMtN ? (size_t)P.s_total : 4 * kMtN;
+    hipLaunchKernelGGL(k_env_auctioneer, dim3((unsigned)E), dim3(kWave), lds, s, P, recs, mt, actions);
     return hipGetLastError();
 }
 hipError_t launch_env_randbelow(const Params& P, uint8_t* recs, uint32_t* mt, int64_t e, uint32_t n, uint32_t* out,
                                 hipStream_t s) {
-    hipLaunchKernelGGL(k_env_randbelow, dim3(1), dim3(kWave), P.s_total, s, P, recs, mt, e, n, out);
+    hipLaunchKernelGGL(k_env_randbelow, dim3(1), dim3(kWave), 4 * kMtN, s, P, recs, mt, e, n, out);
     return hipGetLastError();
 }
 }  // namespace ms

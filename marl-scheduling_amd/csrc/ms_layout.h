@@ -53,8 +53,12 @@ struct Params {
     int32_t s_rec, s_act_acc, s_act_off, s_act_price, s_act_auct, s_accr, s_offr, s_pricer,
         s_spawn_kind, s_scratch, s_total;
     int32_t s_mc, s_mr, s_newle, s_exec, s_key, s_auct, s_agentr, s_auctr, s_rank, s_fresh, s_misc;
-    int32_t scratch_bytes;  // owner rows + slot pairs of the observations
-    int32_t s_slotpair;     // slot pairs' offset inside the scratch
+    // observation scratch (offsets inside s_scratch): C owner rows + the foreign row
+    // [C+1][acc_stride], the source row of every acceptor row [N*C] bytes, the offer-row
+    // template [off_stride] and the slot pairs [NL] u16
+    int32_t scratch_bytes, s_rowsel, s_otmpl, s_slotpair;
+    // w / nw == umulhi(w, mag) for the dword counts of one env's acceptor / offer rows
+    uint32_t mag_acc, mag_off;
 };
 
 // device pointers of one ms_env_step call
@@ -77,6 +81,9 @@ struct StepIO {
 
 inline int32_t align4(int32_t x) { return (x + 3) & ~3; }
 inline int32_t align16(int32_t x) { return (x + 15) & ~15; }
+// w / d == umulhi(w, magic_div(d)) for every w < 2^32 / d and d >= 2 (d == 1 is the emitters'
+// special case: the quotient is w).
+inline uint32_t magic_div(uint32_t d) { return d < 2 ? 0u : (uint32_t)(0x100000000ull / d + 1); }
 
 // Build the record layout and LDS plan for a validated config.
 inline Params make_params(const ms_config& c, int32_t cap) {
@@ -143,12 +150,16 @@ inline Params make_params(const ms_config& c, int32_t cap) {
     p.s_misc = s; s += 16;                     // flags, n_exec
     s = align16(s);
     p.s_scratch = s;
-    // observation scratch: C owner rows, then NL slot pairs
-    p.s_slotpair = align16(p.C * p.acc_stride);
+    p.s_rowsel = (p.C + 1) * p.acc_stride;
+    p.s_otmpl = align4(p.s_rowsel + p.N * p.C);
+    p.s_slotpair = p.s_otmpl + p.off_stride;
     p.scratch_bytes = align16(p.s_slotpair + 2 * p.NL);
     s += p.scratch_bytes;
     p.s_total = s;
+    p.mag_acc = magic_div(p.acc_stride / 4);
+    p.mag_off = magic_div(p.off_stride / 4);
     return p;
 }
+
 
 }  // namespace ms

@@ -18,8 +18,9 @@ NAMES = {1: "stage", 2: "MT peek + masks + liab prefetch", 3: "auctioneer", 4: "
          10: "write record + rewards", 11: "rebuild masks", 12: "emit observations"}
 
 
-def main(E=16384, steps=20, lpe=16):
-    lib = ct.CDLL(os.path.join(ROOT, "tools", "_probe", "libmarlsched_probe.so"))
+def main(E=16384, steps=20, min_lpe=None):
+    d = "_probe" + ("_lpe%d" % min_lpe if min_lpe else "")
+    lib = ct.CDLL(os.path.join(ROOT, "tools", d, "libmarlsched_probe.so"))
     lib.ms_env_create.argtypes = [ct.POINTER(abi.MsConfig), ct.c_int64, ct.c_uint64, ct.POINTER(ct.c_void_p)]
     lib.ms_env_step.argtypes = [ct.c_void_p, ct.POINTER(abi.MsActions), ct.POINTER(abi.MsObsOut),
                                 ct.POINTER(abi.MsRewardOut), ct.c_void_p, ct.c_void_p]
@@ -47,26 +48,48 @@ def main(E=16384, steps=20, lpe=16):
 
     def run(t):
         a = abi.MsActions(acc[t].data_ptr(), off[t].data_ptr(), price[t].data_ptr(), None)
-        assert lib.ms_env_step(h, ct.byref(a), ct.byref(obs), ct.byref(rew), None, None) == 0
+        st = ct.c_void_p(torch.cuda.current_stream().cuda_stream)
+        assert lib.ms_env_step(h, ct.byref(a), ct.byref(obs), ct.byref(rew), None, st) == 0
 
     for t in range(5):
         run(t)
     torch.cuda.synchronize()
+    graph = torch.cuda.CUDAGraph()  # device time without host gaps between launches
+    with torch.cuda.graph(graph):
+        for t in range(steps):
+            run(5 + t)
+    torch.cuda.synchronize()
     lib.ms_probe_phase_cycles(buf, 1)
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
     ev[0].record()
-    for t in range(steps):
-        run(5 + t)
+    graph.replay()
     ev[1].record()
     torch.cuda.synchronize()
     lib.ms_probe_phase_cycles(buf, 0)
+    lpe = min_lpe or 16
+    while lpe < max(N, C):
+        lpe *= 2
     waves = (E + 64 // lpe - 1) // (64 // lpe)
     tot = sum(buf[k] for k in range(1, 13))
-    print("k_env_step (probe build) %.1f us/step; per wave: %.0f cycles" % (ev[0].elapsed_time(ev[1]) * 1e3 / steps,
+    print("k_env_step (probe build, %d lanes/env) %.1f us/step; per wave: %.0f cycles" % (lpe, ev[0].elapsed_time(ev[1]) * 1e3 / steps,
                                                                         tot / waves / steps))
     for k in range(1, 13):
         print("  %2d %-34s %8.0f cycles/wave  %5.1f%%" % (k, NAMES[k], buf[k] / waves / steps, 100.0 * buf[k] / tot))
+    # entry / exit times of every wave of the last launch (s_memrealtime, 100 MHz)
+    import numpy as np
+    spans = (ct.c_ulonglong * (2 * waves))()
+    lib.ms_probe_wave_spans.argtypes = [ct.POINTER(ct.c_ulonglong), ct.c_int]
+    assert lib.ms_probe_wave_spans(spans, waves) == 0
+    sp = np.array(spans[:], dtype=np.float64).reshape(waves, 2) / 100.0  # us
+    t0 = sp[:, 0].min()
+    st, en, life = sp[:, 0] - t0, sp[:, 1] - t0, sp[:, 1] - sp[:, 0]
+    q = [0, 10, 50, 90, 99, 100]
+    fmt = lambda a: " ".join("%6.1f" % v for v in np.percentile(a, q))
+    print("  wave spans of the last launch (us; percentiles %s):" % q)
+    print("    entry    %s" % fmt(st))
+    print("    exit     %s" % fmt(en))
+    print("    lifetime %s" % fmt(life))
 
 
 if __name__ == "__main__":
-    main()
+    main(min_lpe=int(sys.argv[1]) if len(sys.argv) > 1 else None)
