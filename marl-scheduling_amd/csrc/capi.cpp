@@ -35,6 +35,7 @@ static void ppo_split(int64_t rows, int G, int* chunk_tiles, int* n_chunks) {
     int64_t tiles = (rows + 15) / 16;
     int64_t ct = (tiles * G + 8191) / 8192;
     if (ct < 8) ct = 8;
+    ct = (ct + 1) & ~1LL;  // whole tile pairs (the dW1 step runs on 32 rows)
     *chunk_tiles = (int)ct;
     int64_t nc = (tiles + ct - 1) / ct;
     *n_chunks = (int)((nc + 3) / 4 * 4);

@@ -131,10 +131,10 @@ __device__ void mt_twist_into_successor(uint32_t* mt_env, uint32_t sel, uint8_t*
 // gets the next successor at the start of the round: the whole wave twists it in LDS (the LDS is
 // not staged yet), once per ~40 rounds of an env.
 template <int LPE>
-__device__ void mt_refill_next(uint32_t* mt, const uint8_t* recs, const Params& P, bool active, uint8_t* lds,
-                               int lane) {
+__device__ void mt_refill_next(uint32_t* mt, const uint8_t* recs, const Params& P, int64_t slot, bool active,
+                               uint8_t* lds, int lane) {
     const int gl = lane & (LPE - 1);
-    const int64_t e0 = (int64_t)blockIdx.x * (kWave / LPE);
+    const int64_t e0 = slot * (kWave / LPE);
     uint32_t sel = 0;
     if (active && gl == 0) sel = *reinterpret_cast<const uint32_t*>(recs + (e0 + lane / LPE) * P.rec_bytes + 12);
     uint64_t need = __ballot(active && gl == 0 && !(sel & 2u));
@@ -481,7 +481,8 @@ __device__ __forceinline__ uint32_t foreign_dword(int k, int d_acc) {
 
 // The LDS sources of env e's observations:
 //   crow [C+1][acc_stride]: the owner rows of the C cores, then the foreign row;
-//   rowsel [N*C]: source row of acceptor row (a, c): c if agent a owns core c, else C;
+//   rowsrc [N*C] u16: dword offset in crow of acceptor row (a, c)'s source: row c if agent a owns
+//                     core c, else the foreign row C;
 //   otmpl [off_stride]: offer-row template (the (prio, rem) pairs of all cores, zero tail);
 //   slot_pair [NL]: (prio, rem) of every slot.
 template <int LPE>
@@ -499,10 +500,10 @@ __device__ void build_obs_sources(Rec& R, const Params& P, const M128* mc, const
         }
     }
     if (acc) {
-        uint8_t* rowsel = scratch + P.s_rowsel;
+        uint16_t* rowsrc = reinterpret_cast<uint16_t*>(scratch + P.s_rowsel);
         for (int r = gl; r < P.N * C; r += LPE) {
             const int a = r / C, c = r - a * C;
-            rowsel[r] = (uint8_t)(owner[c] == a + 1 ? c : C);
+            rowsrc[r] = (uint16_t)((owner[c] == a + 1 ? c : C) * nw);
         }
     }
     if (off) {
@@ -583,6 +584,41 @@ __device__ __forceinline__ void emit_flat(uint32_t* base, int64_t e, int64_t E, 
     }
 }
 
+// Block e of an [E][n_rows][nw] dword array, streamed in row groups: RG = lcm(nw, 4) / nw rows
+// are CG = lcm(nw, 4) / 4 16-byte chunks. Lane l < GPI * CG (GPI = LPE / CG row groups per pass)
+// owns chunk j = l % CG of every GPI-th row group, so the (row in group, column) of its four
+// dwords are fixed per lane: src(row, col, i) is one lookup per dword. Other shapes (CG > LPE,
+// unaligned arrays) take emit_flat.
+template <int LPE, class Src>
+__device__ __forceinline__ void emit_rows(uint32_t* base, int64_t e, int64_t E, int n_rows, int nw, uint32_t mag,
+                                          int gl, Src src) {
+    const int n_dw = n_rows * nw;
+    const int g4 = (nw & 1) ? 4 : ((nw & 2) ? 2 : 1);  // RG
+    const int CG = g4 * nw / 4;
+    const WtOut o(base, E * n_dw * 4);
+    if (!o.ok || (n_dw & 3) != 0 || CG > LPE) {
+        emit_flat<LPE>(base, e, E, n_dw, nw, mag, gl, [&](int r, int col) { return src(r, col, 0); });
+        return;
+    }
+    const int GPI = LPE / CG;
+    const int j = gl % CG, q0 = gl / CG;
+    if (q0 >= GPI) return;
+    int ri[4], col[4];
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        const int d = 4 * j + i;
+        ri[i] = d / nw;
+        col[i] = d - ri[i] * nw;
+    }
+    const int64_t env_off = e * n_dw * 4;
+    const int n_groups = n_rows / g4;
+    for (int q = q0; q < n_groups; q += GPI) {
+        const int r0 = q * g4;
+        o.st4(env_off + 4 * (r0 * nw + 4 * j), src(r0 + ri[0], col[0], 0), src(r0 + ri[1], col[1], 1),
+              src(r0 + ri[2], col[2], 2), src(r0 + ri[3], col[3], 3));
+    }
+}
+
 // All observations of env e (dst == NULL skips a kind; a padding group passes write = false).
 template <int LPE>
 __device__ void emit_obs(Rec& R, const Params& P, const M128* mc, const M128* mr, uint8_t* scratch, int8_t* acc,
@@ -592,28 +628,24 @@ __device__ void emit_obs(Rec& R, const Params& P, const M128* mc, const M128* mr
     const int C = P.C, nw = P.acc_stride / 4, nwo = P.off_stride / 4;
     const uint32_t* crow = reinterpret_cast<const uint32_t*>(scratch);
     if (acc) {
-        const uint8_t* rowsel = scratch + P.s_rowsel;
-        const int n_dw = P.N * C * nw;
-        emit_flat<LPE>(reinterpret_cast<uint32_t*>(acc), e, E, n_dw, nw, P.mag_acc, gl,
-                       [&](int r, int col) { return crow[rowsel[r] * nw + col]; });
+        const uint16_t* rowsrc = reinterpret_cast<const uint16_t*>(scratch + P.s_rowsel);
+        emit_rows<LPE>(reinterpret_cast<uint32_t*>(acc), e, E, P.N * C, nw, P.mag_acc, gl,
+                       [&](int r, int col, int) { return crow[rowsrc[r] + col]; });
     }
     if (auct) {
         const int8_t* owner = R.core_owner();
-        const int n_dw = C * nw;
-        emit_flat<LPE>(reinterpret_cast<uint32_t*>(auct), e, E, n_dw, nw, P.mag_acc, gl,
-                       [&](int c, int col) { return crow[(owner[c] == 0 ? c : C) * nw + col]; });
+        emit_rows<LPE>(reinterpret_cast<uint32_t*>(auct), e, E, C, nw, P.mag_acc, gl,
+                       [&](int c, int col, int) { return crow[(owner[c] == 0 ? c : C) * nw + col]; });
     }
     if (off) {
         const uint32_t* otmpl = reinterpret_cast<const uint32_t*>(scratch + P.s_otmpl);
         const uint16_t* slot_pair = reinterpret_cast<const uint16_t*>(scratch + P.s_slotpair);
         const int pcol = (2 * C) >> 2, pshift = 8 * ((2 * C) & 3);
-        const int n_dw = P.NL * nwo;
-        emit_flat<LPE>(reinterpret_cast<uint32_t*>(off), e, E, n_dw, nwo, P.mag_off, gl,
-                       [&](int s, int col) {
-                           uint32_t v = otmpl[col];
-                           if (col == pcol) v |= (uint32_t)slot_pair[s] << pshift;
-                           return v;
-                       });
+        emit_rows<LPE>(reinterpret_cast<uint32_t*>(off), e, E, P.NL, nwo, P.mag_off, gl, [&](int s, int col, int) {
+            uint32_t v = otmpl[col];
+            if (col == pcol) v |= (uint32_t)slot_pair[s] << pshift;
+            return v;
+        });
     }
 }
 
@@ -772,13 +804,13 @@ constexpr int kLiabPrefetch = 4;  // newest chain entries loaded ahead per core 
 // One round of SchedulingEnv.step (SchedulingEnvironment.py:32-83): group g of block b steps env
 // b * (64 / LPE) + g. Each group owns a P.s_total-byte slice of the block's LDS.
 template <int LPE>
-__global__ void __launch_bounds__(64) k_env_step(Params P, int64_t E, uint8_t* recs, uint32_t* mt, Liab* liab,
-                                                 StepIO io) {
+__device__ __forceinline__ void env_round(const Params& P, int64_t E, uint8_t* recs, uint32_t* mt, Liab* liab,
+                                          const StepIO& io, int64_t slot) {
     extern __shared__ __align__(16) uint8_t smem_all[];
     const int lane = threadIdx.x;
     const Lanes<LPE> Lg(lane);
     const int gl = Lg.gl;
-    const int64_t e_raw = (int64_t)blockIdx.x * (kWave / LPE) + (lane / LPE);
+    const int64_t e_raw = slot * (kWave / LPE) + (lane / LPE);
     const bool active = e_raw < E;  // padding groups of the last wave replay env E-1 without writing
     const int64_t e = active ? e_raw : E - 1;
     uint8_t* smem = smem_all + (lane / LPE) * P.s_total;
@@ -799,7 +831,6 @@ __global__ void __launch_bounds__(64) k_env_step(Params P, int64_t E, uint8_t* r
 #ifdef MS_PHASE_TIMING
     uint64_t t_prev = __builtin_amdgcn_s_memtime();
     uint64_t t_acc[16] = {};
-    const uint64_t rt_start = __builtin_amdgcn_s_memrealtime();
 #endif
 
     uint8_t* rec = smem + P.s_rec;
@@ -815,7 +846,7 @@ __global__ void __launch_bounds__(64) k_env_step(Params P, int64_t E, uint8_t* r
 
     // ---- successor MT blocks of the envs that crossed into theirs last round (whole wave, LDS
     //      not staged yet), then stage state and actions in LDS
-    mt_refill_next<LPE>(mt, recs, P, active, smem_all, lane);
+    mt_refill_next<LPE>(mt, recs, P, slot, active, smem_all, lane);
     __shared__ int32_t s_kt[48];
     load_kind_tables(P, s_kt, lane);
     {
@@ -1219,8 +1250,23 @@ __global__ void __launch_bounds__(64) k_env_step(Params P, int64_t E, uint8_t* r
     emit_obs<LPE>(R, P, s_mc, s_mr, scratch, io.obs_acc, io.obs_off, io.obs_auct, e, E, active, gl);
     MS_MARK(12);
 #ifdef MS_PHASE_TIMING
-    if (lane == 0) {
+    if (lane == 0)
         for (int k = 0; k < 16; k++) g_phase_cycles[blockIdx.x % kProbeSlots][k] += t_acc[k];
+#endif
+}
+
+// One round for the 64 / LPE envs of wave slot blockIdx.x. (A persistent loop over several slots
+// per wave would let one slot's observation stores drain under the next slot's compute, but the
+// compiler then keeps the whole round's state live across iterations: 3x the VGPRs.)
+template <int LPE>
+__global__ void __launch_bounds__(64) k_env_step(Params P, int64_t E, uint8_t* recs, uint32_t* mt, Liab* liab,
+                                                 StepIO io) {
+#ifdef MS_PHASE_TIMING
+    const uint64_t rt_start = __builtin_amdgcn_s_memrealtime();
+#endif
+    env_round<LPE>(P, E, recs, mt, liab, io, blockIdx.x);
+#ifdef MS_PHASE_TIMING
+    if (threadIdx.x == 0) {
         g_wave_span[blockIdx.x % kProbeSlots][0] = rt_start;
         g_wave_span[blockIdx.x % kProbeSlots][1] = __builtin_amdgcn_s_memrealtime();
     }
@@ -1240,7 +1286,7 @@ __global__ void __launch_bounds__(64) k_env_auctioneer(Params P, uint8_t* recs, 
     const int64_t e = blockIdx.x;
     uint8_t* rec = smem + P.s_rec;
     __shared__ int32_t s_kt[48];
-    mt_refill_next<kWave>(mt, recs, P, true, smem, lane);
+    mt_refill_next<kWave>(mt, recs, P, blockIdx.x, true, smem, lane);
     load_kind_tables(P, s_kt, lane);
     copy_dwords<kWave>(reinterpret_cast<uint32_t*>(rec),
                        reinterpret_cast<const uint32_t*>(recs + e * (int64_t)P.rec_bytes), P.rec_bytes / 4, lane);

@@ -54,8 +54,8 @@ struct Params {
         s_spawn_kind, s_scratch, s_total;
     int32_t s_mc, s_mr, s_newle, s_exec, s_key, s_auct, s_agentr, s_auctr, s_rank, s_fresh, s_misc;
     // observation scratch (offsets inside s_scratch): C owner rows + the foreign row
-    // [C+1][acc_stride], the source row of every acceptor row [N*C] bytes, the offer-row
-    // template [off_stride] and the slot pairs [NL] u16
+    // [C+1][acc_stride], the source-row dword offset of every acceptor row [N*C] u16, the
+    // offer-row template [off_stride] and the slot pairs [NL] u16
     int32_t scratch_bytes, s_rowsel, s_otmpl, s_slotpair;
     // w / nw == umulhi(w, mag) for the dword counts of one env's acceptor / offer rows
     uint32_t mag_acc, mag_off;
@@ -151,7 +151,7 @@ inline Params make_params(const ms_config& c, int32_t cap) {
     s = align16(s);
     p.s_scratch = s;
     p.s_rowsel = (p.C + 1) * p.acc_stride;
-    p.s_otmpl = align4(p.s_rowsel + p.N * p.C);
+    p.s_otmpl = align4(p.s_rowsel + 2 * p.N * p.C);
     p.s_slotpair = p.s_otmpl + p.off_stride;
     p.scratch_bytes = align16(p.s_slotpair + 2 * p.NL);
     s += p.scratch_bytes;

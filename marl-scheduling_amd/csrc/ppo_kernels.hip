@@ -63,35 +63,86 @@ __device__ __forceinline__ float fast_tanh(float x) {
 __device__ __forceinline__ float fast_exp(float x) { return __builtin_amdgcn_exp2f(x * 1.4426950408889634f); }
 __device__ __forceinline__ float fast_log(float x) { return __builtin_amdgcn_logf(x) * 0.69314718055994531f; }
 
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef uint32_t u4v __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ f4 mfma_bf16(const u4v& a, const u4v& b, f4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), c, 0, 0,
+                                                   0);
+}
+// bf16 (upper half of the f32 bits) of two floats packed into one dword
+__device__ __forceinline__ uint32_t pack_hi(float lo, float hi) {
+    return (__float_as_uint(lo) >> 16) | (__float_as_uint(hi) & 0xffff0000u);
+}
+__device__ __forceinline__ float trunc_bf16(float x) { return __uint_as_float(__float_as_uint(x) & 0xffff0000u); }
+
+// 8 floats as three bf16 fragments with v = hi + mid + lo exactly (truncation leaves exact residuals)
+__device__ __forceinline__ void split3(const float (&v)[8], u4v& hi, u4v& mid, u4v& lo) {
+#pragma unroll
+    for (int d = 0; d < 4; d++) {
+        float h[2], m[2], l[2];
+#pragma unroll
+        for (int t = 0; t < 2; t++) {
+            h[t] = trunc_bf16(v[2 * d + t]);
+            const float r = v[2 * d + t] - h[t];
+            m[t] = trunc_bf16(r);
+            l[t] = r - m[t];
+        }
+        hi[d] = pack_hi(h[0], h[1]);
+        mid[d] = pack_hi(m[0], m[1]);
+        lo[d] = pack_hi(l[0], l[1]);
+    }
+}
+
+// int8 values (exact in bf16) packed in pairs
+__device__ __forceinline__ uint32_t pack_i8(int a, int b) { return pack_hi((float)a, (float)b); }
+__device__ __forceinline__ u4v bytes_to_bf16(uint32_t d0, uint32_t d1) {
+    u4v r;
+    r[0] = pack_i8((int8_t)d0, (int8_t)(d0 >> 8));
+    r[1] = pack_i8((int8_t)(d0 >> 16), (int8_t)(d0 >> 24));
+    r[2] = pack_i8((int8_t)d1, (int8_t)(d1 >> 8));
+    r[3] = pack_i8((int8_t)(d1 >> 16), (int8_t)(d1 >> 24));
+    return r;
+}
+
 template <int NQ, int NT>
 struct GradLds {
-    static constexpr int D16 = 16 * NQ;     // layer-1 inputs padded to the dW1 tiles
-    static constexpr int W1P = D16 + 4;     // W1 row pitch (conflict-free ds_read_b128)
-    static constexpr int XP = 16 * NQ;      // staged input row pitch (bytes)
-    static constexpr int TP = 20;           // transpose pitch (floats)
-    static constexpr int NTR = 7 + NT;      // transposed arrays per tile
-    static constexpr int shared_floats = 2 * 16 * W1P + 2 * 256 + 256 * NT + 16 * 5 + 16 * NT + 4;
-    static constexpr int wave_floats = NTR * 16 * TP + 16 * XP / 4;
+    static constexpr int S1 = (NQ + 1) / 2;           // 32-input k-steps of layer 1 (16*NQ inputs)
+    static constexpr int W1B = 32 * S1 + 8;           // bf16 pitch of a split W1 row (+16 B: no conflicts)
+    static constexpr int XPD = (NQ & 1) ? 4 * NQ + 6 : 4 * NQ + 2;  // staged input row pitch (dwords)
+    static constexpr int TP = 20;                     // 16-row transpose pitch (floats)
+    static constexpr int TP2 = 36;                    // 32-row transpose pitch (floats)
+    static constexpr int NTR = 5 + NT;                // 16-row transposed arrays per tile
+    // block: split W1 / C1 [2][3][16][W1B] bf16, then W2, C2, W3 and the biases (floats)
+    static constexpr int w1s_floats = 2 * 3 * 16 * W1B / 2;
+    static constexpr int shared_floats = w1s_floats + 2 * 256 + 256 * NT + 16 * 5 + 16 * NT + 4;
+    // per wave: d1 / e1 transposes over a tile pair, the per-tile transposes, 32 staged input rows
+    static constexpr int wave_floats = 2 * 16 * TP2 + NTR * 16 * TP + 32 * XPD;
+    // waves per block: 4 when they fit the 160 KB of LDS, else 2 (each wave then walks two chunks)
+    static constexpr int WPB = shared_floats + 4 * wave_floats <= 40960 ? 4 : 2;
+    static constexpr int lds_floats = shared_floats + WPB * wave_floats;
 };
 
-// NQ = 16-wide input tiles with 16*NQ > D, NT = ceil(A/16) action tiles. 4 waves per block.
+// NQ = 16-wide input tiles with 16*NQ > D, NT = ceil(A/16) action tiles. A block owns 4 chunks
+// of one group and has L::WPB waves.
 template <int NQ, int NT>
-__global__ void __launch_bounds__(256, (NQ * NT >= 32) ? 1 : 2) k_ppo_grad(PpoArgs p) {
+__global__ void __launch_bounds__((64 * GradLds<NQ, NT>::WPB), ((NQ * NT >= 32) ? 1 : 2)) k_ppo_grad(PpoArgs p) {
     using L = GradLds<NQ, NT>;
-    constexpr int TP = L::TP, W1P = L::W1P, XP = L::XP;
+    constexpr int TP = L::TP, TP2 = L::TP2, XPD = L::XPD, S1 = L::S1, W1B = L::W1B;
+    constexpr int NTH = 64 * L::WPB, CPW = 4 / L::WPB;  // threads per block, chunks per wave
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int g4 = lane >> 4;  // MFMA k-group / C-row group
     const int j = lane & 15;   // batch row within the tile (C column)
     const int blocks_per_group = p.n_chunks >> 2;
     const int grp = blockIdx.x / blocks_per_group;
-    const int chunk = (blockIdx.x - grp * blocks_per_group) * 4 + wave;
+    const int blk = blockIdx.x - grp * blocks_per_group;
+    const int chunk = blk * 4 + wave * CPW;
     const int D = p.D, A = p.A;
     const int u = p.unit_of_group[grp];
 
     extern __shared__ __align__(16) float sm[];
-    float* sW1 = sm;                    // [16][W1P] (zero beyond D)
-    float* sC1 = sW1 + 16 * W1P;        // [16][W1P]
-    float* sW2 = sC1 + 16 * W1P;        // [16][16]
+    uint16_t* sW1s = reinterpret_cast<uint16_t*>(sm);  // [net][hi/mid/lo][16][W1B] bf16 (zero beyond D)
+    float* sW2 = sm + L::w1s_floats;    // [16][16]
     float* sC2 = sW2 + 256;             // [16][16]
     float* sW3 = sC2 + 256;             // [16*NT][16] (zero rows >= A)
     float* sb1 = sW3 + 256 * NT;        // 16
@@ -101,27 +152,35 @@ __global__ void __launch_bounds__(256, (NQ * NT >= 32) ? 1 : 2) k_ppo_grad(PpoAr
     float* scb2 = scb1 + 16;            // 16
     float* sb3 = scb2 + 16;             // 16*NT
     float* scb3 = sb3 + 16 * NT;        // 1 (+3 pad)
-    float* sT = sm + L::shared_floats + wave * L::wave_floats;  // [NTR][16][TP]
-    uint32_t* sX = reinterpret_cast<uint32_t*>(sT + L::NTR * 16 * TP);  // [16][XP/4] dwords
+    float* sT = sm + L::shared_floats + wave * L::wave_floats;
+    float* T_d1 = sT;                   // [16 features][TP2]: 32 rows of the tile pair
+    float* T_e1 = sT + 16 * TP2;
+    float* sT1 = sT + 2 * 16 * TP2;     // [NTR][16][TP]
+    uint32_t* sX = reinterpret_cast<uint32_t*>(sT1 + L::NTR * 16 * TP);  // [32][XPD] dwords
 
-    // ---- stage this group's weights (once per block)
+    // ---- stage this group's weights (once per block); W1 / C1 as three exact bf16 terms
     {
         const float* W1 = p.w1 + (size_t)grp * 16 * D;
         const float* C1 = p.cw1 + (size_t)grp * 16 * D;
-        for (int i = tid; i < 16 * W1P; i += 256) {
-            const int r = i / W1P, c = i - r * W1P;
-            sW1[i] = c < D ? W1[r * D + c] : 0.f;
-            sC1[i] = c < D ? C1[r * D + c] : 0.f;
+        for (int i = tid; i < 2 * 16 * 32 * S1; i += NTH) {
+            const int net = i / (16 * 32 * S1), rem = i - net * 16 * 32 * S1;
+            const int r = rem / (32 * S1), c = rem - r * (32 * S1);
+            const float w = c < D ? (net ? C1 : W1)[r * D + c] : 0.f;
+            const float h = trunc_bf16(w), rr = w - h, m = trunc_bf16(rr), l = rr - m;
+            uint16_t* base = sW1s + net * 3 * 16 * W1B + r * W1B + c;
+            base[0] = (uint16_t)(__float_as_uint(h) >> 16);
+            base[16 * W1B] = (uint16_t)(__float_as_uint(m) >> 16);
+            base[2 * 16 * W1B] = (uint16_t)(__float_as_uint(l) >> 16);
         }
-        for (int i = tid; i < 256; i += 256) {
+        for (int i = tid; i < 256; i += NTH) {
             sW2[i] = p.w2[(size_t)grp * 256 + i];
             sC2[i] = p.cw2[(size_t)grp * 256 + i];
         }
-        for (int i = tid; i < 256 * NT; i += 256) {
+        for (int i = tid; i < 256 * NT; i += NTH) {
             const int a = i >> 4;
             sW3[i] = a < A ? p.w3[((size_t)grp * A + a) * 16 + (i & 15)] : 0.f;
         }
-        for (int i = tid; i < 16 * NT; i += 256) sb3[i] = i < A ? p.b3[(size_t)grp * A + i] : 0.f;
+        for (int i = tid; i < 16 * NT; i += NTH) sb3[i] = i < A ? p.b3[(size_t)grp * A + i] : 0.f;
         if (tid < 16) {
             sb1[tid] = p.b1[grp * 16 + tid];
             sb2[tid] = p.b2[grp * 16 + tid];
@@ -149,13 +208,14 @@ __global__ void __launch_bounds__(256, (NQ * NT >= 32) ? 1 : 2) k_ppo_grad(PpoAr
     const int stride4 = p.stride >> 2;
     const int R = (int)p.R;
     const int tile0 = chunk * p.chunk_tiles;
-    const int tile_end = min(tile0 + p.chunk_tiles, (R + 15) >> 4);
+    const int tile_end = min(tile0 + CPW * p.chunk_tiles, (R + 15) >> 4);
     // input byte D of every staged row reads 1 (the bias column of dW1)
     const int one_dw = D >> 2;
     const uint32_t one_bit = 1u << (8 * (D & 3));
-    // lane (j, g4) loads dwords g4 + 4m of tile row j and owns row j's scalars; the next tile's
-    // loads are issued before the current tile is processed (register prefetch)
-    uint32_t pre[NQ];
+    // lane (j, g4) loads dwords 8s + 2*g4 + {0, 1} of tile row j (its bf16 B fragment of k-step s)
+    // and owns row j's scalars; the next tile's loads are issued before the current tile is
+    // processed (register prefetch)
+    uint32_t pre[S1][2];
     int pre_act = 0;
     float pre_olp = 0.f, pre_G = 0.f;
     auto prefetch = [&](int tile) {
@@ -164,41 +224,49 @@ __global__ void __launch_bounds__(256, (NQ * NT >= 32) ? 1 : 2) k_ppo_grad(PpoAr
         const size_t ru = (size_t)(ok ? r : 0) * p.U + u;
         const uint32_t* src = reinterpret_cast<const uint32_t*>(p.states + ru * p.stride);
 #pragma unroll
-        for (int m = 0; m < NQ; m++) {
-            const int cc = g4 + 4 * m;
-            uint32_t w = (ok && cc < stride4) ? src[cc] : 0u;
-            pre[m] = (cc == one_dw) ? (w | one_bit) : w;
-        }
+        for (int s = 0; s < S1; s++)
+#pragma unroll
+            for (int h = 0; h < 2; h++) {
+                const int cc = 8 * s + 2 * g4 + h;
+                const uint32_t w = (ok && cc < stride4) ? src[cc] : 0u;
+                pre[s][h] = (cc == one_dw) ? (w | one_bit) : w;
+            }
         pre_act = ok ? p.actions[ru] : 0;
         pre_olp = ok ? p.old_lp[ru] : 0.f;
         pre_G = ok ? p.ret[(size_t)r * p.G + grp] : 0.f;
     };
     if (tile0 < tile_end) prefetch(tile0);
     for (int tile = tile0; tile < tile_end; tile++) {
+        // wide inputs: re-read the split W1 from LDS per tile instead of holding it in registers
+        if (S1 > 2) __asm__ volatile("" ::: "memory");
+        const int half = (tile - tile0) & 1;  // position in the tile pair of the dW1 step
         // ---- the tile's input rows: registers (forward) and LDS (dW1); then start the next loads
-        uint32_t xw[NQ];
+        uint32_t xw[S1][2];
 #pragma unroll
-        for (int m = 0; m < NQ; m++) {
-            xw[m] = pre[m];
-            sX[j * (XP / 4) + g4 + 4 * m] = pre[m];
-        }
+        for (int s = 0; s < S1; s++)
+#pragma unroll
+            for (int h = 0; h < 2; h++) {
+                xw[s][h] = pre[s][h];
+                const int cc = 8 * s + 2 * g4 + h;
+                if (cc < 4 * NQ) sX[(16 * half + j) * XPD + cc] = pre[s][h];
+            }
         const bool valid = tile * 16 + j < R;
         const int act = pre_act;
         const float olp = pre_olp, G = pre_G;
         if (tile + 1 < tile_end) prefetch(tile + 1);
 
-        // ---- forward, layer 1 (actor + critic share the B operand): step (m, b) is input
-        //      feature 16m + 4*g4 + b, byte b of dword g4 + 4m
+        // ---- forward, layer 1 on the bf16 MFMA: the int8 inputs are exact in bf16, the weights
+        //      are hi + mid + lo; actor and critic share the B operand
         f4 a1 = {0, 0, 0, 0}, c1 = {0, 0, 0, 0};
 #pragma unroll
-        for (int m = 0; m < NQ; m++) {
-            const f4 wa = *reinterpret_cast<const f4*>(sW1 + j * W1P + 16 * m + 4 * g4);
-            const f4 wc = *reinterpret_cast<const f4*>(sC1 + j * W1P + 16 * m + 4 * g4);
+        for (int s = 0; s < S1; s++) {
+            const u4v xb = bytes_to_bf16(xw[s][0], xw[s][1]);
 #pragma unroll
-            for (int b = 0; b < 4; b++) {
-                const float x = (float)(int8_t)(xw[m] >> (8 * b));
-                a1 = mfma4(wa[b], x, a1);
-                c1 = mfma4(wc[b], x, c1);
+            for (int t = 0; t < 3; t++) {
+                const u4v wa = *reinterpret_cast<const u4v*>(sW1s + (0 * 3 + t) * 16 * W1B + j * W1B + 32 * s + 8 * g4);
+                const u4v wc = *reinterpret_cast<const u4v*>(sW1s + (1 * 3 + t) * 16 * W1B + j * W1B + 32 * s + 8 * g4);
+                a1 = mfma_bf16(wa, xb, a1);
+                c1 = mfma_bf16(wc, xb, c1);
             }
         }
         float h1[4], hc1[4];
@@ -367,36 +435,43 @@ __global__ void __launch_bounds__(256, (NQ * NT >= 32) ? 1 : 2) k_ppo_grad(PpoAr
         }
         if (g4 == 0) cdb3 += g_v;
 
-        // ---- weight gradients: batch reductions as MFMAs with K = rows. Transposes: value of
-        //      (feature f, row r) at T[f*TP + 4*(r%4) + r/4], so lane (j, g4) reads rows
+        // ---- weight gradients: batch reductions as MFMAs with K = rows. 16-row transposes:
+        //      value of (feature f, row r) at T[f*TP + 4*(r%4) + r/4], so lane (j, g4) reads rows
         //      g4, g4+4, g4+8, g4+12 of feature j with one ds_read_b128 (k step s = row g4 + 4s).
-        float* T_d1 = sT;
-        float* T_d2 = sT + 1 * 16 * TP;
-        float* T_h1 = sT + 2 * 16 * TP;
-        float* T_h2 = sT + 3 * 16 * TP;
-        float* T_e1 = sT + 4 * 16 * TP;
-        float* T_e2 = sT + 5 * 16 * TP;
-        float* T_k1 = sT + 6 * 16 * TP;
-        float* T_gz = sT + 7 * 16 * TP;
+        //      d1 / e1 go to the tile pair's 32-row transposes (row 16*half + j at T2[f*TP2 + row]).
+        float* T_d2 = sT1;
+        float* T_h1 = sT1 + 1 * 16 * TP;
+        float* T_h2 = sT1 + 2 * 16 * TP;
+        float* T_e2 = sT1 + 3 * 16 * TP;
+        float* T_k1 = sT1 + 4 * 16 * TP;
+        float* T_gz = sT1 + 5 * 16 * TP;
         const int pr = 4 * (j & 3) + (j >> 2);  // this lane's row position
 #pragma unroll
         for (int q = 0; q < 4; q++) {
             const int f = (4 * g4 + q) * TP + pr;
-            T_d1[f] = dl1[q];
             T_d2[f] = dl2[q];
             T_h1[f] = h1[q];
             T_h2[f] = h2[q];
-            T_e1[f] = dc1[q];
             T_e2[f] = dc2[q];
             T_k1[f] = hc1[q];
 #pragma unroll
             for (int t = 0; t < NT; t++) T_gz[t * 16 * TP + f] = gz[t][q];
+            const int f2 = (4 * g4 + q) * TP2 + 16 * half + j;
+            T_d1[f2] = dl1[q];
+            T_e1[f2] = dc1[q];
+        }
+        const bool pair_done = half == 1 || tile + 1 == tile_end;
+        if (half == 0 && pair_done) {  // odd tile count: the pair's second half contributes zero
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                const int f2 = (4 * g4 + q) * TP2 + 16 + j;
+                T_d1[f2] = 0.f;
+                T_e1[f2] = 0.f;
+            }
         }
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
         const int rd = j * TP + 4 * g4;
-        const f4 ad1 = *reinterpret_cast<const f4*>(T_d1 + rd);
-        const f4 ae1 = *reinterpret_cast<const f4*>(T_e1 + rd);
         const f4 ad2 = *reinterpret_cast<const f4*>(T_d2 + rd);
         const f4 ae2 = *reinterpret_cast<const f4*>(T_e2 + rd);
         const f4 bh1 = *reinterpret_cast<const f4*>(T_h1 + rd);
@@ -407,28 +482,58 @@ __global__ void __launch_bounds__(256, (NQ * NT >= 32) ? 1 : 2) k_ppo_grad(PpoAr
         for (int t = 0; t < NT; t++) agz[t] = *reinterpret_cast<const f4*>(T_gz + t * 16 * TP + rd);
 #pragma unroll
         for (int s = 0; s < 4; s++) {
-            // dW1 / dC1: output column j of tile q is input feature NQ*j + q (one LDS read per step)
-            const int rr = g4 + 4 * s;
-            const uint8_t* xrow = reinterpret_cast<const uint8_t*>(sX) + rr * XP + NQ * j;
-            uint32_t xb[(NQ + 3) / 4];
-            if (NQ == 1) {
-                xb[0] = xrow[0];
-            } else if (NQ == 2) {
-                xb[0] = *reinterpret_cast<const uint16_t*>(xrow);
-            } else {
-#pragma unroll
-                for (int i = 0; i < NQ / 4; i++) xb[i] = reinterpret_cast<const uint32_t*>(xrow)[i];
-            }
-#pragma unroll
-            for (int q = 0; q < NQ; q++) {
-                const float xv = (float)(int8_t)(xb[q >> 2] >> (8 * (q & 3)));
-                gW1[q] = mfma4(ad1[s], xv, gW1[q]);
-                gC1[q] = mfma4(ae1[s], xv, gC1[q]);
-            }
             gW2 = mfma4(ad2[s], bh1[s], gW2);
             gC2 = mfma4(ae2[s], bk1[s], gC2);
 #pragma unroll
             for (int t = 0; t < NT; t++) gW3[t] = mfma4(agz[t][s], bh2[s], gW3[t]);
+        }
+        if (pair_done) {
+            // dW1 / dC1 over the pair's 32 rows on the bf16 MFMA: A = d1 (e1) of rows 8*g4..+7 of
+            // hidden unit j as three exact bf16 terms, B = the int8 inputs of those rows; output
+            // column j of tile q is input feature NQ*j + q
+            float v[8];
+            u4v dh, dm, dl, eh, em, el;
+            const f4 d_lo = *reinterpret_cast<const f4*>(T_d1 + j * TP2 + 8 * g4);
+            const f4 d_hi = *reinterpret_cast<const f4*>(T_d1 + j * TP2 + 8 * g4 + 4);
+#pragma unroll
+            for (int e = 0; e < 4; e++) v[e] = d_lo[e], v[4 + e] = d_hi[e];
+            split3(v, dh, dm, dl);
+            const f4 e_lo = *reinterpret_cast<const f4*>(T_e1 + j * TP2 + 8 * g4);
+            const f4 e_hi = *reinterpret_cast<const f4*>(T_e1 + j * TP2 + 8 * g4 + 4);
+#pragma unroll
+            for (int e = 0; e < 4; e++) v[e] = e_lo[e], v[4 + e] = e_hi[e];
+            split3(v, eh, em, el);
+            // the NQ input bytes NQ*j .. NQ*j + NQ-1 of rows 8*g4 + r, a dword (4 tiles q) at a time
+            constexpr int XW = (NQ + 3) / 4;
+#pragma unroll
+            for (int w = 0; w < XW; w++) {
+                uint32_t xr[8];
+#pragma unroll
+                for (int r = 0; r < 8; r++) {
+                    const uint8_t* row = reinterpret_cast<const uint8_t*>(sX + (8 * g4 + r) * XPD) + NQ * j;
+                    if (NQ == 1)
+                        xr[r] = row[0];
+                    else if (NQ == 2)
+                        xr[r] = *reinterpret_cast<const uint16_t*>(row);
+                    else
+                        xr[r] = reinterpret_cast<const uint32_t*>(row)[w];
+                }
+#pragma unroll
+                for (int qq = 0; qq < 4; qq++) {
+                    const int q = 4 * w + qq;
+                    if (q >= NQ) break;
+                    u4v xb;
+#pragma unroll
+                    for (int d = 0; d < 4; d++)
+                        xb[d] = pack_i8((int)(int8_t)(xr[2 * d] >> (8 * qq)), (int)(int8_t)(xr[2 * d + 1] >> (8 * qq)));
+                    gW1[q] = mfma_bf16(dh, xb, gW1[q]);
+                    gW1[q] = mfma_bf16(dm, xb, gW1[q]);
+                    gW1[q] = mfma_bf16(dl, xb, gW1[q]);
+                    gC1[q] = mfma_bf16(eh, xb, gC1[q]);
+                    gC1[q] = mfma_bf16(em, xb, gC1[q]);
+                    gC1[q] = mfma_bf16(el, xb, gC1[q]);
+                }
+            }
         }
         __builtin_amdgcn_wave_barrier();
     }
@@ -482,7 +587,7 @@ __global__ void __launch_bounds__(256, (NQ * NT >= 32) ? 1 : 2) k_ppo_grad(PpoAr
     };
     __syncthreads();  // every wave is done with the weights and its transposes
     float* acc = sm;
-    for (int wv = 0; wv < 4; wv++) {
+    for (int wv = 0; wv < L::WPB; wv++) {
         if (wave == wv) {
             auto put = [&](int i, float x) {
                 if (wv == 0)
@@ -494,8 +599,8 @@ __global__ void __launch_bounds__(256, (NQ * NT >= 32) ? 1 : 2) k_ppo_grad(PpoAr
         }
         __syncthreads();
     }
-    float* outp = p.partials + ((size_t)grp * blocks_per_group + (chunk >> 2)) * p.P;
-    for (int i = tid; i < p.P; i += 256) outp[i] = acc[i];
+    float* outp = p.partials + ((size_t)grp * blocks_per_group + blk) * p.P;
+    for (int i = tid; i < p.P; i += NTH) outp[i] = acc[i];
 }
 
 // Sum the blocks' partial vectors (fixed order: 4 interleaved row sets, then a fixed tree) and
@@ -537,9 +642,9 @@ __global__ void __launch_bounds__(256) k_ppo_reduce(const float* __restrict__ pa
 template <int NQ, int NT>
 static hipError_t launch_grad_t(const PpoArgs& a, hipStream_t st) {
     using L = GradLds<NQ, NT>;
-    const size_t lds = sizeof(float) * (L::shared_floats + 4 * L::wave_floats);
-    if ((size_t)a.P > L::shared_floats + 4 * L::wave_floats) return hipErrorInvalidValue;  // block partial in LDS
-    hipLaunchKernelGGL((k_ppo_grad<NQ, NT>), dim3((unsigned)(a.G * (a.n_chunks / 4))), dim3(256), lds, st, a);
+    const size_t lds = sizeof(float) * L::lds_floats;
+    if (lds > 160 * 1024 || (size_t)a.P > (size_t)L::lds_floats) return hipErrorInvalidValue;  // partial in LDS
+    hipLaunchKernelGGL((k_ppo_grad<NQ, NT>), dim3((unsigned)(a.G * (a.n_chunks / 4))), dim3(64 * L::WPB), lds, st, a);
     return hipGetLastError();
 }
 
