@@ -258,7 +258,7 @@ struct ActArgs {
 // with the weights split in three bf16 terms (exact f32 weights; the int8 inputs are exact in bf16):
 // lane (j, g) loads dwords 8s + 2g, 8s + 2g + 1 of tile row j, which are exactly its B fragment of
 // k-step s. S1 = ceil(stride / 32) k-steps.
-template <int S1, int NT, int NT2>
+template <int S1, int NT, int NT2, bool EXT_U>
 __global__ void __launch_bounds__(256) k_act(ActArgs a) {
     const int tid = threadIdx.x, lane = tid & 63;
     const int gw = blockIdx.x * 4 + (tid >> 6);  // global wave index
@@ -302,6 +302,8 @@ __global__ void __launch_bounds__(256) k_act(ActArgs a) {
                 rnd1);
     };
     uint32_t pre[S1][2];
+    // unconditional loads from clamped addresses, used as loaded: the rows past the end are never
+    // written and the dwords past the row meet zero weights (so the wait lands at the use)
     auto prefetch = [&](int r) {
         const uint32_t* src = reinterpret_cast<const uint32_t*>(a.obs + (size_t)(r < 0 ? 0 : r) * a.stride);
 #pragma unroll
@@ -309,7 +311,7 @@ __global__ void __launch_bounds__(256) k_act(ActArgs a) {
 #pragma unroll
             for (int h = 0; h < 2; h++) {
                 const int cc = 8 * s + 2 * g4 + h;
-                pre[s][h] = (r >= 0 && cc < stride4) ? src[cc] : 0u;
+                pre[s][h] = src[cc < stride4 ? cc : stride4 - 1];
             }
     };
     int row = t0 < t1 ? row_of(t0) : -1;
@@ -325,7 +327,7 @@ __global__ void __launch_bounds__(256) k_act(ActArgs a) {
         }
         const bool valid = cur >= 0;
         float u1, u2;
-        if (a.uniforms) {
+        if (EXT_U) {
             u1 = valid ? a.uniforms[cur] : 0.f;
             u2 = valid && NT2 > 0 ? a.uniforms[n_rows_total + cur] : 0.f;
         } else {
@@ -382,6 +384,7 @@ __global__ void __launch_bounds__(256) k_act(ActArgs a) {
 
 template <int S1, int NT, int NT2>
 static hipError_t launch_act_t(ActArgs& a, hipStream_t st) {
+    auto kern = a.uniforms ? k_act<S1, NT, NT2, true> : k_act<S1, NT, NT2, false>;
     const int G = a.n1.n_groups;
     const int tiles = (a.n_items + 15) / 16;
     // ~8192 waves over all groups; each wave walks a contiguous tile range with a register prefetch
@@ -389,7 +392,7 @@ static hipError_t launch_act_t(ActArgs& a, hipStream_t st) {
     a.tiles_per_wave = tpw < 1 ? 1 : tpw;
     a.waves_per_group = (tiles + a.tiles_per_wave - 1) / a.tiles_per_wave;
     const long long waves = (long long)a.waves_per_group * G;
-    hipLaunchKernelGGL((k_act<S1, NT, NT2>), dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, st, a);
+    hipLaunchKernelGGL(kern, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, st, a);
     return hipGetLastError();
 }
 

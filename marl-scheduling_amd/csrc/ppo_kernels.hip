@@ -228,12 +228,13 @@ __global__ void __launch_bounds__((64 * GradLds<NQ, NT>::WPB), ((NQ * NT >= 32) 
 #pragma unroll
             for (int h = 0; h < 2; h++) {
                 const int cc = 8 * s + 2 * g4 + h;
-                const uint32_t w = (ok && cc < stride4) ? src[cc] : 0u;
-                pre[s][h] = (cc == one_dw) ? (w | one_bit) : w;
+                pre[s][h] = src[cc < stride4 ? cc : stride4 - 1];  // clamped, masked at the use
             }
-        pre_act = ok ? p.actions[ru] : 0;
-        pre_olp = ok ? p.old_lp[ru] : 0.f;
-        pre_G = ok ? p.ret[(size_t)r * p.G + grp] : 0.f;
+        // rows past the end load row 0's values: their loss weight is 0, so every derivative of
+        // theirs is exactly 0 (all inputs finite)
+        pre_act = p.actions[ru];
+        pre_olp = p.old_lp[ru];
+        pre_G = p.ret[(size_t)(ok ? r : 0) * p.G + grp];
     };
     if (tile0 < tile_end) prefetch(tile0);
     for (int tile = tile0; tile < tile_end; tile++) {
@@ -246,9 +247,10 @@ __global__ void __launch_bounds__((64 * GradLds<NQ, NT>::WPB), ((NQ * NT >= 32) 
         for (int s = 0; s < S1; s++)
 #pragma unroll
             for (int h = 0; h < 2; h++) {
-                xw[s][h] = pre[s][h];
                 const int cc = 8 * s + 2 * g4 + h;
-                if (cc < 4 * NQ) sX[(16 * half + j) * XPD + cc] = pre[s][h];
+                const uint32_t w = cc < stride4 ? pre[s][h] : 0u;  // bytes past the row read 0
+                xw[s][h] = cc == one_dw ? (w | one_bit) : w;
+                if (cc < 4 * NQ) sX[(16 * half + j) * XPD + cc] = xw[s][h];
             }
         const bool valid = tile * 16 + j < R;
         const int act = pre_act;
