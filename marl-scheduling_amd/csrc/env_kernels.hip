@@ -1,22 +1,22 @@
 // env_kernels.hip — the batched marl-scheduling round as one HIP kernel for gfx950.
 //
-// A group of LPE lanes (a power of two >= max(C, N); 64 / LPE groups per
-// 64-lane wave) steps one env replica per round, so the wave's scalar control
-// flow and the lane-serial parts (the offer executions, the MT19937 draws) are
-// shared by several envs. The env's packed state record (ms_layout.h) is staged
-// in the group's LDS slice and the round runs as group-parallel phases. The
-// offer set of a round (at most N*L <= 126 offers, one per slot, offer-ID
-// order = slot order) is indexed by 128-bit masks, one per core and one per
-// recipient, built with LDS atomic ORs: every ordered selection of the
-// reference — the idx-th offer of (recipient, core) behind an acceptor action,
-// the auctioneer's tied maxima, the offers listed in an acceptor observation —
-// is a walk over the set bits of mask(core) & mask(recipient). The loads the
-// round depends on (MT19937 window, liability chains of cores that may
-// terminate) are issued right after staging so their latency overlaps the
-// selection phases. Observations are assembled in LDS (prefilled with the -2
-// pad by dword stores) and streamed out with dword stores. Reference semantics
-// (paths relative to /root/reference/src) are cited per phase; the CPU
-// restatement that checks this kernel bit-for-bit is oracle/ms_oracle.c.
+// A group of LPE lanes (a power of two >= max(C, N), at least 16; 64 / LPE
+// groups per 64-lane wave) steps one env replica per round, so the wave's
+// scalar control flow and the lane-serial parts (the offer executions, the
+// MT19937 draws) are shared by several envs. The env's packed state record
+// (ms_layout.h) is staged in the group's LDS slice with one batch of loads and
+// the round runs as group-parallel phases. The offer set of a round (at most
+// N*L <= 126 offers, one per slot, offer-ID order = slot order) is indexed by
+// 128-bit masks, one per core and one per recipient, built with LDS atomic ORs:
+// every ordered selection of the reference — the idx-th offer of (recipient,
+// core) behind an acceptor action, the auctioneer's tied maxima, the offers
+// listed in an acceptor observation — is a walk over the set bits of
+// mask(core) & mask(recipient). The MT19937 stream reads two state blocks (the
+// current one and its precomputed successor), so no draw waits for a twist.
+// Observations are built from per-core owner rows in LDS and streamed with
+// 16-byte write-through stores. Reference semantics (paths relative to
+// /root/reference/src) are cited per phase; the CPU restatement that checks
+// this kernel bit-for-bit is oracle/ms_oracle.c.
 #include <hip/hip_runtime.h>
 #include <string.h>
 
