@@ -69,18 +69,22 @@ __device__ __forceinline__ f4 mfma_bf16(const u4v& a, const u4v& b, f4 c) {
                                                    0);
 }
 
-// tanh(x) = sign(x) (1 - t) / (1 + t), t = exp(-2|x|): absolute error ~1e-7 everywhere.
+// tanh(x) = 1 - 2 / (1 + exp(2x)): exp overflows to inf for large x (-> 1) and underflows to 0 for
+// large -x (-> -1); absolute error ~1e-7 (what feeds the next layers' sums of O(1) terms).
 __device__ __forceinline__ float fast_tanh(float x) {
-    const float t = __builtin_amdgcn_exp2f(-2.8853900817779268f * fabsf(x));
-    const float r = (1.f - t) * __builtin_amdgcn_rcpf(1.f + t);
-    return copysignf(r, x);
+    const float t = __builtin_amdgcn_exp2f(2.8853900817779268f * x);  // exp(2x)
+    return fmaf(-2.f, __builtin_amdgcn_rcpf(1.f + t), 1.f);
 }
 __device__ __forceinline__ float fast_exp(float x) { return __builtin_amdgcn_exp2f(x * 1.4426950408889634f); }
+// exp(x - m) as exp2(x log2e - m log2e) with one fma (m_l2e = m * log2e)
+__device__ __forceinline__ float fast_exp_sub(float x, float m_l2e) {
+    return __builtin_amdgcn_exp2f(fmaf(x, 1.4426950408889634f, -m_l2e));
+}
 __device__ __forceinline__ float fast_log(float x) { return __builtin_amdgcn_logf(x) * 0.69314718055994531f; }
 
 // bf16 (upper half of the f32 bits) of elements 2i, 2i+1 packed into one dword
 __device__ __forceinline__ uint32_t pack_hi(float lo, float hi) {
-    return (__float_as_uint(lo) >> 16) | (__float_as_uint(hi) & 0xffff0000u);
+    return __builtin_amdgcn_perm(__float_as_uint(hi), __float_as_uint(lo), 0x07060302u);  // one v_perm_b32
 }
 __device__ __forceinline__ float trunc_bf16(float x) { return __uint_as_float(__float_as_uint(x) & 0xffff0000u); }
 
@@ -180,12 +184,13 @@ struct Head {
         m = fmaxf(m, __shfl_xor(m, 16));
         m = fmaxf(m, __shfl_xor(m, 32));
         float bs[NT];
+        const float m_l2e = m * 1.4426950408889634f;
 #pragma unroll
         for (int t = 0; t < NT; t++) {
             bs[t] = 0.f;
 #pragma unroll
             for (int q = 0; q < 4; q++) {
-                z[t][q] = fast_exp(z[t][q] - m);
+                z[t][q] = fast_exp_sub(z[t][q], m_l2e);
                 bs[t] += z[t][q];
             }
         }
@@ -484,7 +489,7 @@ __global__ void __launch_bounds__(256) k_returns(const float* __restrict__ rewar
     double G = 0.0;
     for (int t = T - 1; t >= 0; t--) {
         // discounted_reward = reward + gamma * discounted_reward (Python floats)
-        G = (double)rewards[(int64_t)t * row_stride + m] + gamma * G;
+        G = __dadd_rn((double)rewards[(int64_t)t * row_stride + m], __dmul_rn(gamma, G));  // two roundings
         o[t] = (float)G;  // torch.tensor(rewards, dtype=torch.float32)
     }
     double s = 0.0;
@@ -517,7 +522,7 @@ __global__ void __launch_bounds__(256) k_unit_returns(const void* __restrict__ r
         const int64_t idx = ((int64_t)t * E + e) * U + u;
         const double r = is_i32 ? (double)static_cast<const int32_t*>(rewards)[idx]
                                 : (double)static_cast<const float*>(rewards)[idx];
-        Gs = r + gamma * Gs;
+        Gs = __dadd_rn(r, __dmul_rn(gamma, Gs));  // Python: two roundings, never an fma
         const float f = (float)Gs;
         out[(int64_t)t * EG + m] = f;
         s += (double)f;

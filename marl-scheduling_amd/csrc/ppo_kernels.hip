@@ -54,13 +54,17 @@ __device__ __forceinline__ float xmax4g(float v) {
 }
 
 // tanh(x) = sign(x) (1 - t) / (1 + t), t = exp(-2|x|): absolute error ~1e-7 everywhere
-// (the relative error near 0 does not matter downstream: h feeds sums of O(1) terms).
+// tanh(x) = 1 - 2 / (1 + exp(2x)): exp overflows to inf for large x (-> 1) and underflows to 0 for
+// large -x (-> -1); absolute error ~1e-7 (what feeds the next layers' sums of O(1) terms).
 __device__ __forceinline__ float fast_tanh(float x) {
-    const float t = __builtin_amdgcn_exp2f(-2.8853900817779268f * fabsf(x));  // exp2(-2|x| log2 e)
-    const float r = (1.f - t) * __builtin_amdgcn_rcpf(1.f + t);
-    return copysignf(r, x);
+    const float t = __builtin_amdgcn_exp2f(2.8853900817779268f * x);  // exp(2x)
+    return fmaf(-2.f, __builtin_amdgcn_rcpf(1.f + t), 1.f);
 }
 __device__ __forceinline__ float fast_exp(float x) { return __builtin_amdgcn_exp2f(x * 1.4426950408889634f); }
+// exp(x - m) as exp2(x log2e - m log2e) with one fma (m_l2e = m * log2e)
+__device__ __forceinline__ float fast_exp_sub(float x, float m_l2e) {
+    return __builtin_amdgcn_exp2f(fmaf(x, 1.4426950408889634f, -m_l2e));
+}
 __device__ __forceinline__ float fast_log(float x) { return __builtin_amdgcn_logf(x) * 0.69314718055994531f; }
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
@@ -72,7 +76,7 @@ __device__ __forceinline__ f4 mfma_bf16(const u4v& a, const u4v& b, f4 c) {
 }
 // bf16 (upper half of the f32 bits) of two floats packed into one dword
 __device__ __forceinline__ uint32_t pack_hi(float lo, float hi) {
-    return (__float_as_uint(lo) >> 16) | (__float_as_uint(hi) & 0xffff0000u);
+    return __builtin_amdgcn_perm(__float_as_uint(hi), __float_as_uint(lo), 0x07060302u);  // one v_perm_b32
 }
 __device__ __forceinline__ float trunc_bf16(float x) { return __uint_as_float(__float_as_uint(x) & 0xffff0000u); }
 
@@ -319,12 +323,13 @@ __global__ void __launch_bounds__((64 * GradLds<NQ, NT>::WPB), ((NQ * NT >= 32) 
             for (int q = 0; q < 4; q++)
                 if (16 * t + 4 * g4 + q < A) mx = fmaxf(mx, z[t][q]);
         mx = xmax4g(mx);
+        const float mx_l2e = mx * 1.4426950408889634f;
         float pe[NT][4], s0 = 0.f;
 #pragma unroll
         for (int t = 0; t < NT; t++)
 #pragma unroll
             for (int q = 0; q < 4; q++) {
-                pe[t][q] = (16 * t + 4 * g4 + q < A) ? fast_exp(z[t][q] - mx) : 0.f;
+                pe[t][q] = (16 * t + 4 * g4 + q < A) ? fast_exp_sub(z[t][q], mx_l2e) : 0.f;
                 s0 += pe[t][q];
             }
         const float inv0 = __builtin_amdgcn_rcpf(xsum4g(s0));

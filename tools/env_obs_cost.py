@@ -48,4 +48,6 @@ def main(E=16384, steps=30):
 
 
 if __name__ == "__main__":
-    main()
+    for E in ([int(a) for a in sys.argv[1:]] or [16384]):
+        print("E = %d" % E)
+        main(E=E)

@@ -70,6 +70,7 @@ def main(E=16384, steps=20, min_lpe=None):
     while lpe < max(N, C):
         lpe *= 2
     waves = (E + 64 // lpe - 1) // (64 // lpe)
+    n_blocks = waves
     tot = sum(buf[k] for k in range(1, 13))
     print("k_env_step (probe build, %d lanes/env) %.1f us/step; per wave: %.0f cycles" % (lpe, ev[0].elapsed_time(ev[1]) * 1e3 / steps,
                                                                         tot / waves / steps))
@@ -77,10 +78,10 @@ def main(E=16384, steps=20, min_lpe=None):
         print("  %2d %-34s %8.0f cycles/wave  %5.1f%%" % (k, NAMES[k], buf[k] / waves / steps, 100.0 * buf[k] / tot))
     # entry / exit times of every wave of the last launch (s_memrealtime, 100 MHz)
     import numpy as np
-    spans = (ct.c_ulonglong * (2 * waves))()
+    spans = (ct.c_ulonglong * (2 * n_blocks))()
     lib.ms_probe_wave_spans.argtypes = [ct.POINTER(ct.c_ulonglong), ct.c_int]
-    assert lib.ms_probe_wave_spans(spans, waves) == 0
-    sp = np.array(spans[:], dtype=np.float64).reshape(waves, 2) / 100.0  # us
+    assert lib.ms_probe_wave_spans(spans, n_blocks) == 0
+    sp = np.array(spans[:], dtype=np.float64).reshape(n_blocks, 2) / 100.0  # us
     t0 = sp[:, 0].min()
     st, en, life = sp[:, 0] - t0, sp[:, 1] - t0, sp[:, 1] - sp[:, 0]
     q = [0, 10, 50, 90, 99, 100]
