@@ -242,6 +242,15 @@ int ms_policy_act(const ms_mlp_params* p, const int8_t* obs, int32_t obs_stride,
                   uint64_t seed, uint64_t offset, const uint64_t* offset_dev, const float* uniforms,
                   int8_t* action, float* logprob, void* stream);
 
+/* ms_policy_act where many observation rows equal one common row (device, obs_stride bytes):
+ * the acceptor rows of cores an agent does not own are all [0, -1, -1, (-2, -2) * O, 0 pad]
+ * (Agent.py:167-212). The common row's network output is computed once per wave and every row
+ * equal to it is sampled from that table; outputs are bit-identical to ms_policy_act's. */
+int ms_policy_act_common(const ms_mlp_params* p, const int8_t* obs, int32_t obs_stride,
+                         int64_t n_envs, int32_t n_units, int32_t units_per_group, const int8_t* common_row,
+                         uint64_t seed, uint64_t offset, const uint64_t* offset_dev, const float* uniforms,
+                         int8_t* action, float* logprob, void* stream);
+
 /* FreePriceOfferPPO.selectAction (PPOmodules.py:312-332) in one launch: the core
  * chooser acts on the offer observation (D_off = 2C+2); the price chooser acts on
  * price_state = [obs[2a], obs[2a+1], obs[2C], obs[2C+1]] or [-5,-5,-5,-5] when a == 0

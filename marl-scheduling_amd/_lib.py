@@ -52,6 +52,8 @@ def _load():
         "ms_env_export": (ct.c_int, [P, ct.POINTER(abi.MsStateHost), P]),
         "ms_env_import": (ct.c_int, [P, ct.POINTER(abi.MsStateHost), P]),
         "ms_policy_act": (ct.c_int, [ct.POINTER(abi.MsMlpParams), P, i32, i64, i32, i32, u64, u64, P, P, P, P, P]),
+        "ms_policy_act_common": (ct.c_int, [ct.POINTER(abi.MsMlpParams), P, i32, i64, i32, i32, P, u64, u64, P, P, P,
+                                            P, P]),
         "ms_offer_act_free": (ct.c_int, [ct.POINTER(abi.MsMlpParams), ct.POINTER(abi.MsMlpParams), P, i32, i64, i32,
                                          i32, i32, u64, u64, P, P, P, P, P, P, P, P, P]),
         "ms_discounted_returns": (ct.c_int, [P, i32, i64, i64, ct.c_double, P, P]),
@@ -77,7 +79,7 @@ EXPORTED = (
     "ms_last_error", "ms_abi_version", "ms_config_shape", "ms_env_create", "ms_env_destroy", "ms_env_shape",
     "ms_env_reset", "ms_env_step", "ms_env_round", "ms_env_flags", "ms_env_randbelow", "ms_env_auctioneer",
     "ms_env_get_rng", "ms_env_set_rng", "ms_env_export",
-    "ms_env_import", "ms_policy_act", "ms_offer_act_free", "ms_discounted_returns", "ms_unit_returns",
+    "ms_env_import", "ms_policy_act", "ms_policy_act_common", "ms_offer_act_free", "ms_discounted_returns", "ms_unit_returns",
     "ms_ppo_workspace_bytes", "ms_ppo_grad",
 )
 

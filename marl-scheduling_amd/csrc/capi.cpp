@@ -19,8 +19,8 @@ hipError_t launch_env_reset(const Params&, int64_t, const uint8_t*, int8_t*, int
 hipError_t launch_env_step(const Params&, int64_t, uint8_t*, uint32_t*, Liab*, const StepIO&, hipStream_t);
 hipError_t launch_env_randbelow(const Params&, uint8_t*, uint32_t*, int64_t, uint32_t, uint32_t*, hipStream_t);
 hipError_t launch_env_auctioneer(const Params&, int64_t, uint8_t*, uint32_t*, int8_t*, hipStream_t);
-hipError_t launch_policy_act(const ms_mlp_params*, const int8_t*, int, int64_t, int, int, uint64_t, uint64_t,
-                             const uint64_t*, const float*, int8_t*, float*, hipStream_t);
+hipError_t launch_policy_act(const ms_mlp_params*, const int8_t*, int, int64_t, int, int, const int8_t*, uint64_t,
+                             uint64_t, const uint64_t*, const float*, int8_t*, float*, hipStream_t);
 hipError_t launch_offer_act_free(const ms_mlp_params*, const ms_mlp_params*, const int8_t*, int, int64_t, int, int, int,
                                  uint64_t, uint64_t, const uint64_t*, const float*, int8_t*, float*, int8_t*, int8_t*,
                                  float*, int8_t*, hipStream_t);
@@ -445,8 +445,21 @@ int ms_policy_act(const ms_mlp_params* p, const int8_t* obs, int32_t obs_stride,
     int rc = check_mlp(p, obs_stride, n_units, units_per_group);
     if (rc) return rc;
     if (n_envs < 1) return fail(MS_EINVAL, "n_envs must be >= 1");
-    HIP_TRY(ms::launch_policy_act(p, obs, obs_stride, n_envs, n_units, units_per_group, seed, offset, offset_dev,
-                                  uniforms, action, logprob, (hipStream_t)stream));
+    HIP_TRY(ms::launch_policy_act(p, obs, obs_stride, n_envs, n_units, units_per_group, nullptr, seed, offset,
+                                  offset_dev, uniforms, action, logprob, (hipStream_t)stream));
+    return MS_OK;
+}
+
+int ms_policy_act_common(const ms_mlp_params* p, const int8_t* obs, int32_t obs_stride, int64_t n_envs,
+                         int32_t n_units, int32_t units_per_group, const int8_t* common_row, uint64_t seed,
+                         uint64_t offset, const uint64_t* offset_dev, const float* uniforms, int8_t* action,
+                         float* logprob, void* stream) {
+    if (!obs || !action || !logprob || !common_row) return fail(MS_EINVAL, "NULL argument");
+    int rc = check_mlp(p, obs_stride, n_units, units_per_group);
+    if (rc) return rc;
+    if (n_envs < 1) return fail(MS_EINVAL, "n_envs must be >= 1");
+    HIP_TRY(ms::launch_policy_act(p, obs, obs_stride, n_envs, n_units, units_per_group, common_row, seed, offset,
+                                  offset_dev, uniforms, action, logprob, (hipStream_t)stream));
     return MS_OK;
 }
 

@@ -152,13 +152,12 @@ struct Head {
         }
     }
 
-    // Layers 2-3, softmax and the inverse-CDF sample for the 16 rows of a tile given layer-1
-    // pre-activations. Every lane of row j returns the row's action and log-prob. Logits of the
-    // padding actions (a >= A) read -inf (bias), so they drop out of the max and the sum. The
-    // Categorical renormalisation of the softmax output changes probabilities by < 1e-7 relative,
-    // so the sample compares u * sum(e) with the running sum of e = exp(z - max), and the log-prob
-    // is log(clamp(e_a / sum(e))) (torch: log(clamp(p_a / sum(p)))).
-    __device__ __forceinline__ void run(f4 a1, int A, int j, int g4, float u, int& action, float& logprob) const {
+    // Layers 2-3 and the softmax numerators of the 16 rows of a tile given layer-1 pre-activations:
+    // z[t][q] = exp(logit - max) of action a = 16t + 4*g4 + q of row j, S = the row's sum of z and
+    // c[t][q] = the running sum of z over actions 0..a (in increasing action order). Logits of the
+    // padding actions (a >= A) read -inf (bias), so they drop out of the max and the sums.
+    __device__ __forceinline__ void numerators(f4 a1, int j, int g4, float (&z)[NT][4], float (&c)[NT][4],
+                                               float& S) const {
         float h1[4];
 #pragma unroll
         for (int q = 0; q < 4; q++) h1[q] = fast_tanh(a1[q] + b1[q]);
@@ -168,7 +167,6 @@ struct Head {
         float h2[4];
 #pragma unroll
         for (int q = 0; q < 4; q++) h2[q] = fast_tanh(a2[q] + b2[q]);
-        float z[NT][4];
         float m = -INFINITY;
 #pragma unroll
         for (int t = 0; t < NT; t++) {
@@ -194,40 +192,45 @@ struct Head {
                 bs[t] += z[t][q];
             }
         }
-        // inverse CDF over a = 16t + 4*g4 + q in increasing order: the action is the number of
-        // actions whose running sum stays <= u * S (zero-width intervals are skipped by construction)
         float lane_tot = 0.f;
 #pragma unroll
         for (int t = 0; t < NT; t++) lane_tot += bs[t];
-        const float S = xsum4g(lane_tot);
-        const float target = u * S;
+        S = xsum4g(lane_tot);
         float cum = 0.f;
-        int cnt = 0;
 #pragma unroll
         for (int t = 0; t < NT; t++) {
             const float gs0 = __shfl(bs[t], j), gs1 = __shfl(bs[t], j + 16), gs2 = __shfl(bs[t], j + 32),
                         gs3 = __shfl(bs[t], j + 48);
-            float c = cum + (g4 > 0 ? gs0 : 0.f) + (g4 > 1 ? gs1 : 0.f) + (g4 > 2 ? gs2 : 0.f);
+            float cc = cum + (g4 > 0 ? gs0 : 0.f) + (g4 > 1 ? gs1 : 0.f) + (g4 > 2 ? gs2 : 0.f);
 #pragma unroll
             for (int q = 0; q < 4; q++) {
-                c += z[t][q];
-                cnt += (c <= target) ? 1 : 0;
+                cc += z[t][q];
+                c[t][q] = cc;
             }
             cum += (gs0 + gs1) + (gs2 + gs3);
         }
+    }
+
+    // The inverse-CDF sample and log-prob of row j given its uniform u: every lane of row j returns
+    // them. The Categorical renormalisation of the softmax output changes probabilities by < 1e-7
+    // relative, so the sample compares u * S with the running sums (the action is the number of
+    // actions whose running sum stays <= u * S; zero-width intervals are skipped by construction)
+    // and the log-prob is log(clamp(z_a / S)) (torch: log(clamp(p_a / sum(p)))).
+    __device__ __forceinline__ void run(f4 a1, int A, int j, int g4, float u, int& action, float& logprob) const {
+        float z[NT][4], c[NT][4], S;
+        numerators(a1, j, g4, z, c, S);
+        const float target = u * S;
+        int cnt = 0;
+#pragma unroll
+        for (int t = 0; t < NT; t++)
+#pragma unroll
+            for (int q = 0; q < 4; q++) cnt += (c[t][q] <= target) ? 1 : 0;
         cnt += __shfl_xor(cnt, 16);
         cnt += __shfl_xor(cnt, 32);
         int a_sel = cnt;
         if (__builtin_expect(__ballot(a_sel >= A) != 0, 0)) {
             // u * S at or beyond the rounded total: the last action with nonzero probability
-            int last_nz = -1;
-#pragma unroll
-            for (int t = 0; t < NT; t++)
-#pragma unroll
-                for (int q = 0; q < 4; q++)
-                    if (z[t][q] > 0.f) last_nz = 16 * t + 4 * g4 + q;
-            last_nz = max(last_nz, __shfl_xor(last_nz, 16));
-            last_nz = max(last_nz, __shfl_xor(last_nz, 32));
+            const int last_nz = last_nonzero(z, g4);
             if (a_sel >= A) a_sel = last_nz;
         }
         float mine = 0.f;
@@ -235,10 +238,49 @@ struct Head {
         for (int t = 0; t < NT; t++)
 #pragma unroll
             for (int q = 0; q < 4; q++) mine = (16 * t + 4 * g4 + q == a_sel) ? z[t][q] : mine;
-        const float pa = xsum4g(mine) * __builtin_amdgcn_rcpf(S);
-        const float eps = 1.1920928955078125e-07f;  // torch.finfo(float32).eps
         action = a_sel;
-        logprob = fast_log(fminf(fmaxf(pa, eps), 1.f - eps));
+        logprob = clamped_log(xsum4g(mine) * __builtin_amdgcn_rcpf(S));
+    }
+
+    __device__ __forceinline__ static int last_nonzero(const float (&z)[NT][4], int g4) {
+        int last_nz = -1;
+#pragma unroll
+        for (int t = 0; t < NT; t++)
+#pragma unroll
+            for (int q = 0; q < 4; q++)
+                if (z[t][q] > 0.f) last_nz = 16 * t + 4 * g4 + q;
+        last_nz = max(last_nz, __shfl_xor(last_nz, 16));
+        last_nz = max(last_nz, __shfl_xor(last_nz, 32));
+        return last_nz;
+    }
+
+    __device__ __forceinline__ static float clamped_log(float pa) {
+        const float eps = 1.1920928955078125e-07f;  // torch.finfo(float32).eps
+        return fast_log(fminf(fmaxf(pa, eps), 1.f - eps));
+    }
+
+    // The sampling table of one row (all 16 rows of the tile equal): cum[a] = running sum through
+    // action a, lp[a] = the log-prob run() returns for action a, *S and *last_nz. With it, a row equal
+    // to this one samples and scores exactly as run() would.
+    __device__ __forceinline__ void table(f4 a1, int j, int g4, float* cum, float* lp, float* S_out,
+                                          int* last_nz_out) const {
+        float z[NT][4], c[NT][4], S;
+        numerators(a1, j, g4, z, c, S);
+        const int last_nz = last_nonzero(z, g4);
+        if (j == 0) {
+#pragma unroll
+            for (int t = 0; t < NT; t++)
+#pragma unroll
+                for (int q = 0; q < 4; q++) {
+                    const int a = 16 * t + 4 * g4 + q;
+                    cum[a] = c[t][q];
+                    lp[a] = clamped_log(z[t][q] * __builtin_amdgcn_rcpf(S));
+                }
+            if (g4 == 0) {
+                *S_out = S;
+                *last_nz_out = last_nz;
+            }
+        }
     }
 };
 
@@ -257,6 +299,8 @@ struct ActArgs {
     int8_t* price_action;
     float* price_logprob;
     int8_t* env_price;
+    const int8_t* common;  // [stride] or NULL (k_act_common)
+    int items_per_wave;    // k_act_common
 };
 
 // One wave = a contiguous range of 16-row tiles of one group; no LDS. Layer 1 runs on the bf16 MFMA
@@ -387,6 +431,173 @@ __global__ void __launch_bounds__(256) k_act(ActArgs a) {
     }
 }
 
+// ---------------------------------------------------------------------------
+// k_act_common: ActorCritic.act where many rows equal one common row. Acceptor observations are
+// mostly the constant row [0, -1, -1, (-2, -2) * O] of a core the agent does not own
+// (Agent.py:167-212: no own job, and every offer to the core is addressed to its owner), so the
+// network output of those rows is the same: the wave computes the common row's sampling table
+// once (Head::table, the exact arithmetic of Head::run) and samples each row equal to it from its
+// own uniform with a handful of compares. The other rows are collected in LDS and run through the
+// MFMA tiles as in k_act. Outputs are bit-identical to k_act's.
+constexpr int kCommonSeg = 512;  // most rows per wave = capacity of the wave's LDS row list
+
+template <int S1, int NT, bool EXT_U>
+__global__ void __launch_bounds__(256) k_act_common(ActArgs a) {
+    __shared__ int32_t s_list[4][kCommonSeg];
+    __shared__ float s_cum[4][16 * NT], s_lp[4][16 * NT], s_S[4];
+    __shared__ int s_lnz[4];
+    __shared__ uint32_t s_tmpl[4][8 * S1];
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int gw = blockIdx.x * 4 + wid;
+    const int grp = gw / a.waves_per_group;
+    const int wv = gw - grp * a.waves_per_group;
+    if (grp >= a.n1.n_groups) return;  // whole waves only: the kernel has no block barrier
+    const int j = lane & 15, g4 = lane >> 4;
+    const int A = a.n1.n_actions;
+    const int stride4 = a.stride >> 2;
+    W1Split<S1> w1;
+    w1.load(a.n1.w1 + (size_t)grp * 16 * a.n1.in_dim, a.n1.in_dim, j, g4);
+    Head<NT> h1;
+    h1.load(a.n1, grp, j, g4);
+    const uint64_t off = a.offset + (a.offset_dev ? *a.offset_dev : 0ull);
+    int32_t* list = s_list[wid];
+    // the common row's dwords (zero past the row: they meet zero weights, like k_act's clamped loads)
+    const uint32_t* crow = reinterpret_cast<const uint32_t*>(a.common);
+    for (int d = lane; d < 8 * S1; d += 64) s_tmpl[wid][d] = d < stride4 ? crow[d] : 0u;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    {
+        f4 acc = {0, 0, 0, 0};
+#pragma unroll
+        for (int s = 0; s < S1; s++) {
+            const u4v x = bytes_to_bf16(s_tmpl[wid][8 * s + 2 * g4], s_tmpl[wid][8 * s + 2 * g4 + 1]);
+            acc = mfma_bf16(w1.hi[s], x, acc);
+            acc = mfma_bf16(w1.mid[s], x, acc);
+            acc = mfma_bf16(w1.lo[s], x, acc);
+        }
+        h1.table(acc, j, g4, s_cum[wid], s_lp[wid], &s_S[wid], &s_lnz[wid]);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    // the table is wave-uniform: scalar registers
+    float cum[16 * NT];
+#pragma unroll
+    for (int k = 0; k < 16 * NT; k++) cum[k] = __uint_as_float(__builtin_amdgcn_readfirstlane(__float_as_uint(s_cum[wid][k])));
+    uint32_t tw[8 * S1];
+#pragma unroll
+    for (int d = 0; d < 8 * S1; d++) tw[d] = __builtin_amdgcn_readfirstlane(s_tmpl[wid][d]);
+    const float S = s_S[wid];
+    const int last_nz = s_lnz[wid];
+    const uint32_t s_magic = 0xffffffffu / (uint32_t)a.S;
+    auto row_of_item = [&](int i) -> int {
+        int e = (int)__umulhi((uint32_t)i, s_magic);
+        if ((e + 1) * a.S <= i) e++;
+        return e * a.U + grp * a.S + (i - e * a.S);
+    };
+    auto uniform_of = [&](int row) -> float {
+        if (EXT_U) return a.uniforms[row];
+        uint32_t r0, r1;
+        philox2((uint32_t)row, 0u, (uint32_t)off, (uint32_t)(off >> 32), (uint32_t)a.seed, (uint32_t)(a.seed >> 32), r0, r1);
+        return u24(r0);
+    };
+    const int i_begin = wv * a.items_per_wave;
+    const int i_end = min(i_begin + a.items_per_wave, a.n_items);  // <= kCommonSeg rows
+    const uint64_t below = (1ull << lane) - 1ull;
+    int n_list = 0;
+    // ---- scan (one 64-row step ahead in registers): rows equal to the common row are sampled
+    //      from the table, the others listed
+    uint32_t nx[8 * S1];
+    int n_row = 0;
+    bool n_in = false;
+    auto load_step = [&](int i0) {
+        const int i = i0 + lane;
+        n_in = i < i_end;
+        n_row = n_in ? row_of_item(i) : 0;
+        const uint32_t* src = reinterpret_cast<const uint32_t*>(a.obs + (size_t)n_row * a.stride);
+#pragma unroll
+        for (int d = 0; d < 8 * S1; d++) nx[d] = d < stride4 ? src[d] : tw[d];
+    };
+    if (i_begin < i_end) load_step(i_begin);
+    for (int i0 = i_begin; i0 < i_end; i0 += 64) {
+        uint32_t diff = 0;
+#pragma unroll
+        for (int d = 0; d < 8 * S1; d++) diff |= nx[d] ^ tw[d];
+        const int row = n_row;
+        const bool in = n_in;
+        if (i0 + 64 < i_end) load_step(i0 + 64);
+        const bool common = in && diff == 0;
+        if (common) {
+            const float target = uniform_of(row) * S;
+            int cnt = 0;
+#pragma unroll
+            for (int k = 0; k < 16 * NT; k++) cnt += (cum[k] <= target) ? 1 : 0;
+            const int act = cnt >= A ? last_nz : cnt;
+            a.action[row] = (int8_t)act;
+            a.logprob[row] = s_lp[wid][act];
+        }
+        const bool other = in && !common;
+        const uint64_t m = __ballot(other);
+        if (other) list[n_list + __popcll(m & below)] = row;
+        n_list += __popcll(m);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    // ---- the listed rows in 16-row MFMA tiles (k_act's per-tile path, next tile's rows prefetched)
+    uint32_t tp[S1][2];
+    int t_row = 0;
+    auto load_tile = [&](int t0) {
+        const int k = t0 + j;
+        t_row = list[k < n_list ? k : t0];
+        const uint32_t* src = reinterpret_cast<const uint32_t*>(a.obs + (size_t)t_row * a.stride);
+#pragma unroll
+        for (int s = 0; s < S1; s++) {
+            const int c0 = 8 * s + 2 * g4;
+            tp[s][0] = src[c0 < stride4 ? c0 : stride4 - 1];
+            tp[s][1] = src[c0 + 1 < stride4 ? c0 + 1 : stride4 - 1];
+        }
+    };
+    if (n_list > 0) load_tile(0);
+    for (int t0 = 0; t0 < n_list; t0 += 16) {
+        const bool valid = t0 + j < n_list;
+        const int row = t_row;
+        f4 acc = {0, 0, 0, 0};
+#pragma unroll
+        for (int s = 0; s < S1; s++) {
+            const u4v x = bytes_to_bf16(tp[s][0], tp[s][1]);
+            acc = mfma_bf16(w1.hi[s], x, acc);
+            acc = mfma_bf16(w1.mid[s], x, acc);
+            acc = mfma_bf16(w1.lo[s], x, acc);
+        }
+        if (t0 + 16 < n_list) load_tile(t0 + 16);
+        int act;
+        float lp;
+        h1.run(acc, A, j, g4, uniform_of(row), act, lp);
+        if (valid && g4 == 0) {
+            a.action[row] = (int8_t)act;
+            a.logprob[row] = lp;
+        }
+    }
+}
+
+template <int S1, int NT>
+static hipError_t launch_act_common_t(ActArgs& a, hipStream_t st) {
+    auto kern = a.uniforms ? k_act_common<S1, NT, true> : k_act_common<S1, NT, false>;
+    const int G = a.n1.n_groups;
+    // ~3072 waves over all groups (measured best for cfg3), whole 64-row scan steps each, at most
+    // one LDS list of rows
+    long long ipw = ((long long)a.n_items * G + 3071) / 3072;
+    ipw = (ipw + 63) / 64 * 64;
+    ipw = ipw < 64 ? 64 : (ipw > kCommonSeg ? kCommonSeg : ipw);
+    a.items_per_wave = (int)ipw;
+    a.waves_per_group = (a.n_items + a.items_per_wave - 1) / a.items_per_wave;
+    const long long waves = (long long)a.waves_per_group * G;
+    hipLaunchKernelGGL(kern, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, st, a);
+    return hipGetLastError();
+}
+
 template <int S1, int NT, int NT2>
 static hipError_t launch_act_t(ActArgs& a, hipStream_t st) {
     auto kern = a.uniforms ? k_act<S1, NT, NT2, true> : k_act<S1, NT, NT2, false>;
@@ -407,6 +618,13 @@ static hipError_t dispatch_act_s(ActArgs& a, hipStream_t st) {
     const int nt2 = a.n2.n_groups > 0 ? (a.n2.n_actions + 15) / 16 : 0;
 #define MS_ACT(T, T2) \
     if (nt <= T && nt2 == T2) return launch_act_t<S1, T, T2>(a, st);
+    if (a.common) {
+        if (nt2 != 0) return hipErrorInvalidValue;
+        if (nt <= 1) return launch_act_common_t<S1, 1>(a, st);
+        if (nt <= 2) return launch_act_common_t<S1, 2>(a, st);
+        if (nt <= 4) return launch_act_common_t<S1, 4>(a, st);
+        return launch_act_common_t<S1, 8>(a, st);
+    }
     if (nt2 == 0) {
         MS_ACT(1, 0) MS_ACT(2, 0) MS_ACT(4, 0) MS_ACT(8, 0)
     } else if (nt2 == 1) {
@@ -431,9 +649,10 @@ static hipError_t dispatch_act(ActArgs& a, hipStream_t st) {
 }
 
 hipError_t launch_policy_act(const ms_mlp_params* p, const int8_t* obs, int stride, int64_t E, int U, int S,
-                             uint64_t seed, uint64_t offset, const uint64_t* offset_dev, const float* uniforms,
-                             int8_t* action, float* logprob, hipStream_t st) {
+                             const int8_t* common, uint64_t seed, uint64_t offset, const uint64_t* offset_dev,
+                             const float* uniforms, int8_t* action, float* logprob, hipStream_t st) {
     ActArgs a{};
+    a.common = common;
     a.n1 = *p;
     a.n2.n_groups = 0;
     a.obs = obs;

@@ -114,9 +114,11 @@ class GroupedActorCritic(nn.Module):
 
     @torch.no_grad()
     def act(self, obs_i8, n_units: int, seed: int, offset: int, uniforms=None, action=None, logprob=None, stream=None,
-            offset_dev=None):
+            offset_dev=None, common_row=None):
         """ActorCritic.act (PPOmodules.py:53-63) for obs [E, n_units, stride] int8 on the HIP kernel.
-        Unit u uses group u // (n_units // G). Returns (action int8 [E, U], logprob f32 [E, U])."""
+        Unit u uses group u // (n_units // G). Returns (action int8 [E, U], logprob f32 [E, U]).
+        common_row (int8 [stride] on the device, optional): rows equal to it share one forward pass
+        (``ms_policy_act_common``; same outputs)."""
         E, U, stride = obs_i8.shape
         assert U == n_units and U % self.G == 0 and obs_i8.dtype == torch.int8 and obs_i8.is_contiguous()
         dev = obs_i8.device
@@ -125,6 +127,12 @@ class GroupedActorCritic(nn.Module):
         if logprob is None:
             logprob = torch.empty((E, U), dtype=torch.float32, device=dev)
         p = self.mlp_params()
+        if common_row is not None:
+            assert common_row.dtype == torch.int8 and common_row.numel() == stride and common_row.device == dev
+            check(lib.ms_policy_act_common(ct.byref(p), ptr(obs_i8), stride, E, U, U // self.G, ptr(common_row),
+                                           ct.c_uint64(seed), ct.c_uint64(offset), ptr(offset_dev), ptr(uniforms),
+                                           ptr(action), ptr(logprob), stream_ptr(stream)))
+            return action, logprob
         check(lib.ms_policy_act(ct.byref(p), ptr(obs_i8), stride, E, U, U // self.G, ct.c_uint64(seed),
                                 ct.c_uint64(offset), ptr(offset_dev), ptr(uniforms), ptr(action), ptr(logprob),
                                 stream_ptr(stream)))

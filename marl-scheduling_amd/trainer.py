@@ -106,7 +106,7 @@ def broadcast_params(groups, group=None):
 class Trainer:
     def __init__(self, cfg: abi.MsConfig, n_envs: int, arch: str = "local", hyper: Hyper | None = None, seed: int = 0,
                  device=None, rank: int = 0, world_size: int = 1, process_group=None, fused: bool = True,
-                 use_graph: bool = True):
+                 use_graph: bool = True, common_rows: bool = True):
         assert arch in ("divided", "local", "global")
         self.fused = fused  # fused HIP gradient (ms_ppo_grad) vs torch autograd
         self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
@@ -154,6 +154,12 @@ class Trainer:
         self.off_obs = torch.zeros((T + 1, self.E, N * L, s.off_obs_stride), dtype=torch.int8, device=dev)
         self.price_obs = torch.zeros((T, self.E, N * L, 4), dtype=torch.int8, device=dev) if self.free else None
         self.env_price = torch.zeros((self.E, N * L), dtype=torch.int8, device=dev)
+        # the acceptor row of a core the agent does not own (Agent.py:167-212): most acceptor rows
+        # equal it, and the act / gradient kernels compute its network output once
+        self.common_rows = common_rows
+        O = s.max_offers
+        crow = [0, -1, -1] + [-2] * (2 * O) + [0] * (s.acc_obs_stride - s.acc_obs_dim)
+        self.acc_common = torch.tensor(crow, dtype=torch.int8, device=dev)
         self.agent_reward = torch.zeros((self.E, N), dtype=torch.int32, device=dev)
         self.auct_reward = torch.zeros((self.E, C), dtype=torch.int32, device=dev)
         self.rng = random.Random(seed)  # sub-unit draws (random.randint), identical on every rank
@@ -206,7 +212,8 @@ class Trainer:
             self.off.group.policy_old.act(self.off_obs[t], N * L, seed, base + 1, action=self.off.actions[t],
                                           logprob=self.off.logprobs[t], offset_dev=self.rng_ctr)
         self.acc.group.policy_old.act(self.acc_obs[t], N * C, seed, base + 3, action=self.acc.actions[t],
-                                      logprob=self.acc.logprobs[t], offset_dev=self.rng_ctr)
+                                      logprob=self.acc.logprobs[t], offset_dev=self.rng_ctr,
+                                      common_row=self.acc_common if self.common_rows else None)
         obs = dict(acceptor=self.acc_obs[t + 1], offer=self.off_obs[t + 1])
         rew = dict(offer=self.off.rewards[t].view(E, N, L), acceptor=self.acc.rewards[t].view(E, N, C),
                    agent=self.agent_reward, auctioneer=self.auct_reward,

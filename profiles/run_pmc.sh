@@ -17,5 +17,6 @@ pass() {  # pass <name> <counters...>
 pass a SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS
 pass b SQ_INSTS_VALU SQ_INSTS_MFMA SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_SALU SQ_WAIT_INST_LDS SQ_INSTS_VMEM_WR
 pass c TCC_EA0_WRREQ_sum TCC_EA0_RDREQ_sum TCC_EA0_WRREQ_64B_sum
-python3 "$R/profiles/pmc_summary.py" "$OUT"/a/run_counter_collection.csv "$OUT"/b/run_counter_collection.csv \
-  "$OUT"/c/run_counter_collection.csv | tee "$OUT/summary.txt"
+pass d FETCH_SIZE
+pass e WRITE_SIZE
+python3 "$R/profiles/pmc_summary.py" "$OUT"/{a,b,c,d,e}/run_counter_collection.csv | tee "$OUT/summary.txt"

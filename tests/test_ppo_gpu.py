@@ -44,6 +44,40 @@ def test_act_kernel_matches_reference(ms, G, per_group, D, stride, A):
         np.testing.assert_allclose(glp[same].numpy(), rlp[same].numpy(), rtol=1e-5, atol=2e-6)
 
 
+def _common_row(D, stride, O):
+    return torch.tensor([0, -1, -1] + [-2] * (2 * O) + [0] * (stride - D), dtype=torch.int8)
+
+
+@pytest.mark.parametrize("G,per_group,O,A,frac", [(8, 8, 24, 25, 0.85), (8, 8, 24, 25, 0.0), (8, 8, 24, 25, 1.0),
+                                                  (1, 16, 12, 13, 0.5), (3, 2, 4, 5, 0.9), (2, 5, 96, 97, 0.8)])
+@pytest.mark.parametrize("ext_u", [False, True])
+def test_act_common_rows_bit_identical(ms, G, per_group, O, A, frac, ext_u):
+    """ms_policy_act_common == ms_policy_act bit for bit (actions and log-probs) on acceptor-shaped
+    observations where a fraction of the rows equal the common (not-owned-core) row, incl. rows
+    that differ from it in one byte only."""
+    ppo = _ppo(ms)
+    D = 3 + 2 * O
+    stride = (D + 3) // 4 * 4
+    torch.manual_seed(5)
+    net = ppo.GroupedActorCritic(G, D, A).cuda()
+    E, U = 1001, G * per_group
+    gen = torch.Generator().manual_seed(6)
+    crow = _common_row(D, stride, O)
+    obs = torch.zeros((E, U, stride), dtype=torch.int8)
+    obs[..., :D] = torch.randint(-5, 13, (E, U, D), generator=gen, dtype=torch.int8)
+    pick = torch.rand((E, U), generator=gen) < frac
+    obs[pick] = crow
+    near = (torch.rand((E, U), generator=gen) < 0.02) & pick  # one byte off the common row
+    col = torch.randint(0, D, (E, U), generator=gen)
+    obs[near, col[near]] = 7
+    u = torch.rand((E, U), generator=gen).cuda() if ext_u else None
+    dobs = obs.cuda()
+    a0, l0 = net.act(dobs, U, seed=3, offset=11, uniforms=u)
+    a1, l1 = net.act(dobs, U, seed=3, offset=11, uniforms=u, common_row=crow.cuda())
+    assert torch.equal(a0, a1)
+    assert torch.equal(l0.view(torch.int32), l1.view(torch.int32))
+
+
 def test_act_kernel_sampling_distribution(ms):
     """Philox sampling follows the policy distribution (chi-square-like bound)."""
     ppo = _ppo(ms)
