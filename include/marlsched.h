@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define MS_ABI_VERSION 1
+#define MS_ABI_VERSION 2
 
 #define MS_MAX_KINDS 16
 #define MS_MAX_AGENTS 64
@@ -290,6 +290,10 @@ typedef struct ms_ppo_batch {
     const int32_t* unit_of_group;  /* [G] device array */
     int32_t stride, T, U;
     int64_t E;
+    /* optional [stride] device row: rows equal to it (the acceptor rows of cores an agent does not
+     * own, Agent.py:167-212) share one forward pass, and their summed loss derivatives run through
+     * one backward pass (the gradient is linear in them); NULL = every row on its own */
+    const int8_t* common_row;
 } ms_ppo_batch;
 
 typedef struct ms_ppo_grads {  /* device outputs, [G][...] like the weights */

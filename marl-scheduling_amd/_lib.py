@@ -67,7 +67,7 @@ def _load():
         fn = getattr(L, name)
         fn.restype = res
         fn.argtypes = args
-    if L.ms_abi_version() != 1:
+    if L.ms_abi_version() != 2:
         raise ImportError("libmarlsched.so ABI version mismatch")
     return L
 

@@ -161,6 +161,7 @@ class MsPpoBatch(ct.Structure):
         ("T", ct.c_int32),
         ("U", ct.c_int32),
         ("E", ct.c_int64),
+        ("common_row", ct.c_void_p),
     ]
 
 

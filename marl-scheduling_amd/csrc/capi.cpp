@@ -513,6 +513,7 @@ int ms_ppo_grad(const ms_mlp_params* a, const ms_mlp_params* c, const ms_ppo_bat
     p.old_lp = b->old_logprobs;
     p.ret = b->returns;
     p.unit_of_group = b->unit_of_group;
+    p.common = b->common_row;
     p.partials = (float*)ws;
     p.D = a->in_dim;
     p.A = a->n_actions;

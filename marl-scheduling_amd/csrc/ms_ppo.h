@@ -14,6 +14,7 @@ struct PpoArgs {
     const float* old_lp;                             // [R][U]
     const float* ret;                                // [E][G][T] normalised returns
     const int32_t* unit_of_group;                    // [G]
+    const int8_t* common;                            // [stride] rows equal to it share one forward, or NULL
     float* partials;                                 // [G][n_chunks][P]
     int D, A, stride, T, U, G;
     long long E, R;

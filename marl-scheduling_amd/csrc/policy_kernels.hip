@@ -21,6 +21,7 @@
 #include <math.h>
 
 #include "../../include/marlsched.h"
+#include "ms_common.h"
 
 namespace ms {
 
@@ -485,9 +486,9 @@ __global__ void __launch_bounds__(256) k_act_common(ActArgs a) {
     float cum[16 * NT];
 #pragma unroll
     for (int k = 0; k < 16 * NT; k++) cum[k] = __uint_as_float(__builtin_amdgcn_readfirstlane(__float_as_uint(s_cum[wid][k])));
-    uint32_t tw[8 * S1];
-#pragma unroll
-    for (int d = 0; d < 8 * S1; d++) tw[d] = __builtin_amdgcn_readfirstlane(s_tmpl[wid][d]);
+    constexpr int LPR = S1 <= 2 ? 4 : (S1 <= 4 ? 8 : 16);
+    CommonScan<LPR> cs;
+    cs.init(crow, stride4, lane);
     const float S = s_S[wid];
     const int last_nz = s_lnz[wid];
     const uint32_t s_magic = 0xffffffffu / (uint32_t)a.S;
@@ -508,26 +509,23 @@ __global__ void __launch_bounds__(256) k_act_common(ActArgs a) {
     int n_list = 0;
     // ---- scan (one 64-row step ahead in registers): rows equal to the common row are sampled
     //      from the table, the others listed
-    uint32_t nx[8 * S1];
     int n_row = 0;
     bool n_in = false;
     auto load_step = [&](int i0) {
+        cs.load([&](int k) {
+            const int i = i0 + k;
+            return reinterpret_cast<const uint32_t*>(a.obs + (size_t)(i < i_end ? row_of_item(i) : 0) * a.stride);
+        }, lane);
         const int i = i0 + lane;
         n_in = i < i_end;
         n_row = n_in ? row_of_item(i) : 0;
-        const uint32_t* src = reinterpret_cast<const uint32_t*>(a.obs + (size_t)n_row * a.stride);
-#pragma unroll
-        for (int d = 0; d < 8 * S1; d++) nx[d] = d < stride4 ? src[d] : tw[d];
     };
     if (i_begin < i_end) load_step(i_begin);
     for (int i0 = i_begin; i0 < i_end; i0 += 64) {
-        uint32_t diff = 0;
-#pragma unroll
-        for (int d = 0; d < 8 * S1; d++) diff |= nx[d] ^ tw[d];
         const int row = n_row;
         const bool in = n_in;
+        const bool common = cs.lane_row_common(lane) && in;
         if (i0 + 64 < i_end) load_step(i0 + 64);
-        const bool common = in && diff == 0;
         if (common) {
             const float target = uniform_of(row) * S;
             int cnt = 0;
@@ -618,7 +616,7 @@ static hipError_t dispatch_act_s(ActArgs& a, hipStream_t st) {
     const int nt2 = a.n2.n_groups > 0 ? (a.n2.n_actions + 15) / 16 : 0;
 #define MS_ACT(T, T2) \
     if (nt <= T && nt2 == T2) return launch_act_t<S1, T, T2>(a, st);
-    if (a.common) {
+    if (a.common && a.stride >= 16) {
         if (nt2 != 0) return hipErrorInvalidValue;
         if (nt <= 1) return launch_act_common_t<S1, 1>(a, st);
         if (nt <= 2) return launch_act_common_t<S1, 2>(a, st);

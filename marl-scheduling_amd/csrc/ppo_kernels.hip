@@ -27,6 +27,7 @@
 #include <math.h>
 
 #include "../../include/marlsched.h"
+#include "ms_common.h"
 #include "ms_ppo.h"
 
 namespace ms {
@@ -109,7 +110,14 @@ __device__ __forceinline__ u4v bytes_to_bf16(uint32_t d0, uint32_t d1) {
     return r;
 }
 
-template <int NQ, int NT>
+constexpr int kCommonSeg = 1024;  // rows scanned per segment of the common-row path
+
+template <bool B>
+struct BoolC {
+    static constexpr bool value = B;
+};
+
+template <int NQ, int NT, bool CM>
 struct GradLds {
     static constexpr int S1 = (NQ + 1) / 2;           // 32-input k-steps of layer 1 (16*NQ inputs)
     static constexpr int W1B = 32 * S1 + 8;           // bf16 pitch of a split W1 row (+16 B: no conflicts)
@@ -121,7 +129,10 @@ struct GradLds {
     static constexpr int w1s_floats = 2 * 3 * 16 * W1B / 2;
     static constexpr int shared_floats = w1s_floats + 2 * 256 + 256 * NT + 16 * 5 + 16 * NT + 4;
     // per wave: d1 / e1 transposes over a tile pair, the per-tile transposes, 32 staged input rows
-    static constexpr int wave_floats = 2 * 16 * TP2 + NTR * 16 * TP + 32 * XPD;
+    // (common-row path: the common row's clamped logs, V, entropy, the list of the other rows,
+    //  and per lane the summed d loss / d logp of every action, [16*NT][64])
+    static constexpr int CMF = CM ? 16 * NT + 4 + kCommonSeg + 64 + 64 * 16 * NT : 0;
+    static constexpr int wave_floats = 2 * 16 * TP2 + NTR * 16 * TP + 32 * XPD + CMF;
     // waves per block: 4 when they fit the 160 KB of LDS, else 2 (each wave then walks two chunks)
     static constexpr int WPB = shared_floats + 4 * wave_floats <= 40960 ? 4 : 2;
     static constexpr int lds_floats = shared_floats + WPB * wave_floats;
@@ -129,9 +140,9 @@ struct GradLds {
 
 // NQ = 16-wide input tiles with 16*NQ > D, NT = ceil(A/16) action tiles. A block owns 4 chunks
 // of one group and has L::WPB waves.
-template <int NQ, int NT>
-__global__ void __launch_bounds__((64 * GradLds<NQ, NT>::WPB), ((NQ * NT >= 32) ? 1 : 2)) k_ppo_grad(PpoArgs p) {
-    using L = GradLds<NQ, NT>;
+template <int NQ, int NT, bool COMMON>
+__global__ void __launch_bounds__((64 * GradLds<NQ, NT, COMMON>::WPB), ((NQ * NT >= 32) ? 1 : 2)) k_ppo_grad(PpoArgs p) {
+    using L = GradLds<NQ, NT, COMMON>;
     constexpr int TP = L::TP, TP2 = L::TP2, XPD = L::XPD, S1 = L::S1, W1B = L::W1B;
     constexpr int NTH = 64 * L::WPB, CPW = 4 / L::WPB;  // threads per block, chunks per wave
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -161,6 +172,7 @@ __global__ void __launch_bounds__((64 * GradLds<NQ, NT>::WPB), ((NQ * NT >= 32) 
     float* T_e1 = sT + 16 * TP2;
     float* sT1 = sT + 2 * 16 * TP2;     // [NTR][16][TP]
     uint32_t* sX = reinterpret_cast<uint32_t*>(sT1 + L::NTR * 16 * TP);  // [32][XPD] dwords
+    float* sCm = reinterpret_cast<float*>(sX + 32 * XPD);  // common-row path (L::CMF floats)
 
     // ---- stage this group's weights (once per block); W1 / C1 as three exact bf16 terms
     {
@@ -216,53 +228,22 @@ __global__ void __launch_bounds__((64 * GradLds<NQ, NT>::WPB), ((NQ * NT >= 32) 
     // input byte D of every staged row reads 1 (the bias column of dW1)
     const int one_dw = D >> 2;
     const uint32_t one_bit = 1u << (8 * (D & 3));
-    // lane (j, g4) loads dwords 8s + 2*g4 + {0, 1} of tile row j (its bf16 B fragment of k-step s)
-    // and owns row j's scalars; the next tile's loads are issued before the current tile is
-    // processed (register prefetch)
-    uint32_t pre[S1][2];
-    int pre_act = 0;
-    float pre_olp = 0.f, pre_G = 0.f;
-    auto prefetch = [&](int tile) {
-        const int r = tile * 16 + j;
-        const bool ok = r < R;
-        const size_t ru = (size_t)(ok ? r : 0) * p.U + u;
-        const uint32_t* src = reinterpret_cast<const uint32_t*>(p.states + ru * p.stride);
-#pragma unroll
-        for (int s = 0; s < S1; s++)
-#pragma unroll
-            for (int h = 0; h < 2; h++) {
-                const int cc = 8 * s + 2 * g4 + h;
-                pre[s][h] = src[cc < stride4 ? cc : stride4 - 1];  // clamped, masked at the use
-            }
-        // rows past the end load row 0's values: their loss weight is 0, so every derivative of
-        // theirs is exactly 0 (all inputs finite)
-        pre_act = p.actions[ru];
-        pre_olp = p.old_lp[ru];
-        pre_G = p.ret[(size_t)(ok ? r : 0) * p.G + grp];
+    auto row_src = [&](int r) {
+        return reinterpret_cast<const uint32_t*>(p.states + ((size_t)r * p.U + u) * p.stride);
     };
-    if (tile0 < tile_end) prefetch(tile0);
-    for (int tile = tile0; tile < tile_end; tile++) {
-        // wide inputs: re-read the split W1 from LDS per tile instead of holding it in registers
-        if (S1 > 2) __asm__ volatile("" ::: "memory");
-        const int half = (tile - tile0) & 1;  // position in the tile pair of the dW1 step
-        // ---- the tile's input rows: registers (forward) and LDS (dW1); then start the next loads
-        uint32_t xw[S1][2];
-#pragma unroll
-        for (int s = 0; s < S1; s++)
-#pragma unroll
-            for (int h = 0; h < 2; h++) {
-                const int cc = 8 * s + 2 * g4 + h;
-                const uint32_t w = cc < stride4 ? pre[s][h] : 0u;  // bytes past the row read 0
-                xw[s][h] = cc == one_dw ? (w | one_bit) : w;
-                if (cc < 4 * NQ) sX[(16 * half + j) * XPD + cc] = xw[s][h];
-            }
-        const bool valid = tile * 16 + j < R;
-        const int act = pre_act;
-        const float olp = pre_olp, G = pre_G;
-        if (tile + 1 < tile_end) prefetch(tile + 1);
+    const float zero_vs[NT][4] = {};
 
-        // ---- forward, layer 1 on the bf16 MFMA: the int8 inputs are exact in bf16, the weights
-        //      are hi + mid + lo; actor and critic share the B operand
+    // ---- forward of one 16-row tile (lane (j, g4) holds dwords 8s + 2*g4 + {0, 1} of row j as xw,
+    //      byte D set to 1): hidden activations, softmax (nn.Softmax) + Categorical(probs)
+    //      renormalisation, clamped logs, critic output and entropy of row j
+    struct Fwd {
+        float h1[4], hc1[4], h2[4], hc2[4];
+        float pe[NT][4], pn[NT][4], cl[NT][4];
+        float inv1, V, ent;
+    };
+    auto forward = [&](const uint32_t (&xw)[S1][2], Fwd& f) {
+        // layer 1 on the bf16 MFMA: the int8 inputs are exact in bf16, the weights are
+        // hi + mid + lo; actor and critic share the B operand
         f4 a1 = {0, 0, 0, 0}, c1 = {0, 0, 0, 0};
 #pragma unroll
         for (int s = 0; s < S1; s++) {
@@ -275,11 +256,10 @@ __global__ void __launch_bounds__((64 * GradLds<NQ, NT>::WPB), ((NQ * NT >= 32) 
                 c1 = mfma_bf16(wc, xb, c1);
             }
         }
-        float h1[4], hc1[4];
 #pragma unroll
         for (int q = 0; q < 4; q++) {
-            h1[q] = fast_tanh(a1[q] + sb1[4 * g4 + q]);
-            hc1[q] = fast_tanh(c1[q] + scb1[4 * g4 + q]);
+            f.h1[q] = fast_tanh(a1[q] + sb1[4 * g4 + q]);
+            f.hc1[q] = fast_tanh(c1[q] + scb1[4 * g4 + q]);
         }
         // layer 2: B operand = layer-1 output as is; A reads W2 with k permuted (k_true = 4*g4 + s)
         f4 a2 = {0, 0, 0, 0}, c2 = {0, 0, 0, 0};
@@ -288,15 +268,14 @@ __global__ void __launch_bounds__((64 * GradLds<NQ, NT>::WPB), ((NQ * NT >= 32) 
             const f4 cw2 = *reinterpret_cast<const f4*>(sC2 + j * 16 + 4 * g4);
 #pragma unroll
             for (int s = 0; s < 4; s++) {
-                a2 = mfma4(w2[s], h1[s], a2);
-                c2 = mfma4(cw2[s], hc1[s], c2);
+                a2 = mfma4(w2[s], f.h1[s], a2);
+                c2 = mfma4(cw2[s], f.hc1[s], c2);
             }
         }
-        float h2[4], hc2[4];
 #pragma unroll
         for (int q = 0; q < 4; q++) {
-            h2[q] = fast_tanh(a2[q] + sb2[4 * g4 + q]);
-            hc2[q] = fast_tanh(c2[q] + scb2[4 * g4 + q]);
+            f.h2[q] = fast_tanh(a2[q] + sb2[4 * g4 + q]);
+            f.hc2[q] = fast_tanh(c2[q] + scb2[4 * g4 + q]);
         }
         // actor layer 3 -> logits z[a = 16t + 4*g4 + q][row j]
         float z[NT][4];
@@ -305,17 +284,15 @@ __global__ void __launch_bounds__((64 * GradLds<NQ, NT>::WPB), ((NQ * NT >= 32) 
             const f4 w3 = *reinterpret_cast<const f4*>(sW3 + (16 * t + j) * 16 + 4 * g4);
             f4 zz = {0, 0, 0, 0};
 #pragma unroll
-            for (int s = 0; s < 4; s++) zz = mfma4(w3[s], h2[s], zz);
+            for (int s = 0; s < 4; s++) zz = mfma4(w3[s], f.h2[s], zz);
 #pragma unroll
             for (int q = 0; q < 4; q++) z[t][q] = zz[q] + sb3[16 * t + 4 * g4 + q];
         }
         // critic output V (one row of the last layer, summed across the 4 lane groups)
         float vp = 0.f;
 #pragma unroll
-        for (int q = 0; q < 4; q++) vp = fmaf(sc3[4 * g4 + q], hc2[q], vp);
-        const float V = xsum4g(vp) + scb3[0];
-
-        // ---- softmax (nn.Softmax) + Categorical(probs) renormalisation, log-prob, entropy
+        for (int q = 0; q < 4; q++) vp = fmaf(sc3[4 * g4 + q], f.hc2[q], vp);
+        f.V = xsum4g(vp) + scb3[0];
         float mx = -INFINITY;
 #pragma unroll
         for (int t = 0; t < NT; t++)
@@ -324,13 +301,13 @@ __global__ void __launch_bounds__((64 * GradLds<NQ, NT>::WPB), ((NQ * NT >= 32) 
                 if (16 * t + 4 * g4 + q < A) mx = fmaxf(mx, z[t][q]);
         mx = xmax4g(mx);
         const float mx_l2e = mx * 1.4426950408889634f;
-        float pe[NT][4], s0 = 0.f;
+        float s0 = 0.f;
 #pragma unroll
         for (int t = 0; t < NT; t++)
 #pragma unroll
             for (int q = 0; q < 4; q++) {
-                pe[t][q] = (16 * t + 4 * g4 + q < A) ? fast_exp_sub(z[t][q], mx_l2e) : 0.f;
-                s0 += pe[t][q];
+                f.pe[t][q] = (16 * t + 4 * g4 + q < A) ? fast_exp_sub(z[t][q], mx_l2e) : 0.f;
+                s0 += f.pe[t][q];
             }
         const float inv0 = __builtin_amdgcn_rcpf(xsum4g(s0));
         float s1 = 0.f;
@@ -338,43 +315,76 @@ __global__ void __launch_bounds__((64 * GradLds<NQ, NT>::WPB), ((NQ * NT >= 32) 
         for (int t = 0; t < NT; t++)
 #pragma unroll
             for (int q = 0; q < 4; q++) {
-                pe[t][q] *= inv0;  // softmax output (same arithmetic as k_act)
-                s1 += pe[t][q];
+                f.pe[t][q] *= inv0;  // softmax output (same arithmetic as k_act)
+                s1 += f.pe[t][q];
             }
-        const float inv1 = __builtin_amdgcn_rcpf(xsum4g(s1));
-        float pn[NT][4], cl[NT][4], lp = 0.f, ent = 0.f;
+        f.inv1 = __builtin_amdgcn_rcpf(xsum4g(s1));
+        float ent = 0.f;
 #pragma unroll
         for (int t = 0; t < NT; t++)
 #pragma unroll
             for (int q = 0; q < 4; q++) {
-                const int a = 16 * t + 4 * g4 + q;
-                pn[t][q] = pe[t][q] * inv1;
-                cl[t][q] = fast_log(fminf(fmaxf(pn[t][q], eps), 1.f - eps));
-                if (a < A) {
-                    if (a == act) lp += cl[t][q];
-                    ent -= cl[t][q] * pn[t][q];
-                }
+                f.pn[t][q] = f.pe[t][q] * f.inv1;
+                f.cl[t][q] = fast_log(fminf(fmaxf(f.pn[t][q], eps), 1.f - eps));
+                if (16 * t + 4 * g4 + q < A) ent -= f.cl[t][q] * f.pn[t][q];
             }
-        lp = xsum4g(lp);
-        ent = xsum4g(ent);
+        f.ent = xsum4g(ent);
+    };
 
-        // ---- per-row loss derivatives (loss.mean() over R rows)
-        const float ratio = fast_exp(lp - olp);
-        const float adv = G - V;
-        const float sur1 = ratio * adv;
-        const float rc = fminf(fmaxf(ratio, 1.f - p.eps_clip), 1.f + p.eps_clip);
-        const float sur2 = rc * adv;
-        const float inr = (ratio >= 1.f - p.eps_clip && ratio <= 1.f + p.eps_clip) ? 1.f : 0.f;
-        // d min(s1, s2) / d ratio (torch.minimum splits ties)
-        const float dmin = sur1 < sur2 ? adv : (sur2 < sur1 ? adv * inr : 0.5f * adv + 0.5f * adv * inr);
-        const float w = valid ? p.inv_R : 0.f;
-        const float g_lp = -dmin * w * ratio;  // d loss / d logp (exp backward uses the result)
-        const float g_v = (V - G) * w;         // 0.5 * d MSE / d V
-        const float g_h = -0.01f * w;          // d loss / d entropy
-        if (valid && g4 == 0) {
-            l_min += -fminf(sur1, sur2);
-            l_mse += (V - G) * (V - G);
-            l_ent += ent;
+    // ---- one 16-row tile: forward, per-row loss derivatives, backward, weight gradients.
+    //      xr = the rows' raw dwords (B-fragment layout), act/olp/G/valid = row j's scalars.
+    //      VIRT: the common row's virtual tile, whose column-0 derivatives are sums over every
+    //      row equal to the common row (vsum[a] = sum of d loss / d logp over those rows that took
+    //      action a, vgh / vgv = summed entropy / value derivatives; zero in the other columns):
+    //      the backward is linear in them, so one pass gives those rows' summed weight gradients.
+    auto tile_step = [&](auto virt, const uint32_t (&xr)[S1][2], int act, float olp, float G, bool valid, int half,
+                         bool pair_done, const float (&vsum)[NT][4], float vgh, float vgv) {
+        constexpr bool VIRT = decltype(virt)::value;
+        // wide inputs: re-read the split W1 from LDS per tile instead of holding it in registers
+        if (S1 > 2) __asm__ volatile("" ::: "memory");
+        uint32_t xw[S1][2];
+#pragma unroll
+        for (int s = 0; s < S1; s++)
+#pragma unroll
+            for (int h = 0; h < 2; h++) {
+                const int cc = 8 * s + 2 * g4 + h;
+                const uint32_t w = cc < stride4 ? xr[s][h] : 0u;  // bytes past the row read 0
+                xw[s][h] = cc == one_dw ? (w | one_bit) : w;
+                if (cc < 4 * NQ) sX[(16 * half + j) * XPD + cc] = xw[s][h];
+            }
+        Fwd f;
+        forward(xw, f);
+        const float V = f.V;
+        float g_lp = 0.f, g_v, g_h;
+        if (VIRT) {
+            g_v = vgv;
+            g_h = vgh;
+        } else {
+            float lp = 0.f;
+#pragma unroll
+            for (int t = 0; t < NT; t++)
+#pragma unroll
+                for (int q = 0; q < 4; q++)
+                    if (16 * t + 4 * g4 + q < A && 16 * t + 4 * g4 + q == act) lp += f.cl[t][q];
+            lp = xsum4g(lp);
+            // ---- per-row loss derivatives (loss.mean() over R rows)
+            const float ratio = fast_exp(lp - olp);
+            const float adv = G - V;
+            const float sur1 = ratio * adv;
+            const float rc = fminf(fmaxf(ratio, 1.f - p.eps_clip), 1.f + p.eps_clip);
+            const float sur2 = rc * adv;
+            const float inr = (ratio >= 1.f - p.eps_clip && ratio <= 1.f + p.eps_clip) ? 1.f : 0.f;
+            // d min(s1, s2) / d ratio (torch.minimum splits ties)
+            const float dmin = sur1 < sur2 ? adv : (sur2 < sur1 ? adv * inr : 0.5f * adv + 0.5f * adv * inr);
+            const float w = valid ? p.inv_R : 0.f;
+            g_lp = -dmin * w * ratio;  // d loss / d logp (exp backward uses the result)
+            g_v = (V - G) * w;         // 0.5 * d MSE / d V
+            g_h = -0.01f * w;          // d loss / d entropy
+            if (valid && g4 == 0) {
+                l_min += -fminf(sur1, sur2);
+                l_mse += (V - G) * (V - G);
+                l_ent += f.ent;
+            }
         }
         // d loss / d pn  -> d / d p (renormalisation) -> d / d z (softmax)
         float gz[NT][4], x1 = 0.f;
@@ -385,27 +395,29 @@ __global__ void __launch_bounds__((64 * GradLds<NQ, NT>::WPB), ((NQ * NT >= 32) 
                 const int a = 16 * t + 4 * g4 + q;
                 float v = 0.f;
                 if (a < A) {
-                    const float dc = (a == act ? g_lp : 0.f) - g_h * pn[t][q];
-                    const float in = (pn[t][q] >= eps && pn[t][q] <= 1.f - eps) ? 1.f : 0.f;
-                    v = dc * in * __builtin_amdgcn_rcpf(fminf(fmaxf(pn[t][q], eps), 1.f - eps)) - g_h * cl[t][q];
+                    const float dl = VIRT ? vsum[t][q] : (a == act ? g_lp : 0.f);
+                    const float dc = dl - g_h * f.pn[t][q];
+                    const float in = (f.pn[t][q] >= eps && f.pn[t][q] <= 1.f - eps) ? 1.f : 0.f;
+                    v = dc * in * __builtin_amdgcn_rcpf(fminf(fmaxf(f.pn[t][q], eps), 1.f - eps)) - g_h * f.cl[t][q];
                 }
                 gz[t][q] = v;
-                x1 += v * pe[t][q];
+                x1 += v * f.pe[t][q];
             }
         x1 = xsum4g(x1);
+        const float inv1 = f.inv1;
         float x2 = 0.f;
 #pragma unroll
         for (int t = 0; t < NT; t++)
 #pragma unroll
             for (int q = 0; q < 4; q++) {
                 gz[t][q] = (gz[t][q] - x1 * inv1) * inv1;
-                x2 += gz[t][q] * pe[t][q];
+                x2 += gz[t][q] * f.pe[t][q];
             }
         x2 = xsum4g(x2);
 #pragma unroll
         for (int t = 0; t < NT; t++)
 #pragma unroll
-            for (int q = 0; q < 4; q++) gz[t][q] = pe[t][q] * (gz[t][q] - x2);
+            for (int q = 0; q < 4; q++) gz[t][q] = f.pe[t][q] * (gz[t][q] - x2);
 
         // ---- backward through the hidden layers (same no-movement trick, transposed weights)
         f4 d2 = {0, 0, 0, 0};
@@ -416,8 +428,8 @@ __global__ void __launch_bounds__((64 * GradLds<NQ, NT>::WPB), ((NQ * NT >= 32) 
         float dl2[4], dc2[4];
 #pragma unroll
         for (int q = 0; q < 4; q++) {
-            dl2[q] = d2[q] * (1.f - h2[q] * h2[q]);
-            dc2[q] = sc3[4 * g4 + q] * g_v * (1.f - hc2[q] * hc2[q]);
+            dl2[q] = d2[q] * (1.f - f.h2[q] * f.h2[q]);
+            dc2[q] = sc3[4 * g4 + q] * g_v * (1.f - f.hc2[q] * f.hc2[q]);
         }
         f4 d1 = {0, 0, 0, 0}, e1 = {0, 0, 0, 0};
 #pragma unroll
@@ -428,15 +440,15 @@ __global__ void __launch_bounds__((64 * GradLds<NQ, NT>::WPB), ((NQ * NT >= 32) 
         float dl1[4], dc1[4];
 #pragma unroll
         for (int q = 0; q < 4; q++) {
-            dl1[q] = d1[q] * (1.f - h1[q] * h1[q]);
-            dc1[q] = e1[q] * (1.f - hc1[q] * hc1[q]);
+            dl1[q] = d1[q] * (1.f - f.h1[q] * f.h1[q]);
+            dc1[q] = e1[q] * (1.f - f.hc1[q] * f.hc1[q]);
         }
         // bias gradients of layers 2-3 and the critic output layer (VALU; reduced over rows at the end)
 #pragma unroll
         for (int q = 0; q < 4; q++) {
             db2[q] += dl2[q];
             cdb2[q] += dc2[q];
-            gC3[q] = fmaf(g_v, hc2[q], gC3[q]);
+            gC3[q] = fmaf(g_v, f.hc2[q], gC3[q]);
 #pragma unroll
             for (int t = 0; t < NT; t++) db3[t][q] += gz[t][q];
         }
@@ -455,19 +467,18 @@ __global__ void __launch_bounds__((64 * GradLds<NQ, NT>::WPB), ((NQ * NT >= 32) 
         const int pr = 4 * (j & 3) + (j >> 2);  // this lane's row position
 #pragma unroll
         for (int q = 0; q < 4; q++) {
-            const int f = (4 * g4 + q) * TP + pr;
-            T_d2[f] = dl2[q];
-            T_h1[f] = h1[q];
-            T_h2[f] = h2[q];
-            T_e2[f] = dc2[q];
-            T_k1[f] = hc1[q];
+            const int fo = (4 * g4 + q) * TP + pr;
+            T_d2[fo] = dl2[q];
+            T_h1[fo] = f.h1[q];
+            T_h2[fo] = f.h2[q];
+            T_e2[fo] = dc2[q];
+            T_k1[fo] = f.hc1[q];
 #pragma unroll
-            for (int t = 0; t < NT; t++) T_gz[t * 16 * TP + f] = gz[t][q];
+            for (int t = 0; t < NT; t++) T_gz[t * 16 * TP + fo] = gz[t][q];
             const int f2 = (4 * g4 + q) * TP2 + 16 * half + j;
             T_d1[f2] = dl1[q];
             T_e1[f2] = dc1[q];
         }
-        const bool pair_done = half == 1 || tile + 1 == tile_end;
         if (half == 0 && pair_done) {  // odd tile count: the pair's second half contributes zero
 #pragma unroll
             for (int q = 0; q < 4; q++) {
@@ -514,16 +525,16 @@ __global__ void __launch_bounds__((64 * GradLds<NQ, NT>::WPB), ((NQ * NT >= 32) 
             constexpr int XW = (NQ + 3) / 4;
 #pragma unroll
             for (int w = 0; w < XW; w++) {
-                uint32_t xr[8];
+                uint32_t xr8[8];
 #pragma unroll
                 for (int r = 0; r < 8; r++) {
                     const uint8_t* row = reinterpret_cast<const uint8_t*>(sX + (8 * g4 + r) * XPD) + NQ * j;
                     if (NQ == 1)
-                        xr[r] = row[0];
+                        xr8[r] = row[0];
                     else if (NQ == 2)
-                        xr[r] = *reinterpret_cast<const uint16_t*>(row);
+                        xr8[r] = *reinterpret_cast<const uint16_t*>(row);
                     else
-                        xr[r] = reinterpret_cast<const uint32_t*>(row)[w];
+                        xr8[r] = reinterpret_cast<const uint32_t*>(row)[w];
                 }
 #pragma unroll
                 for (int qq = 0; qq < 4; qq++) {
@@ -532,7 +543,7 @@ __global__ void __launch_bounds__((64 * GradLds<NQ, NT>::WPB), ((NQ * NT >= 32) 
                     u4v xb;
 #pragma unroll
                     for (int d = 0; d < 4; d++)
-                        xb[d] = pack_i8((int)(int8_t)(xr[2 * d] >> (8 * qq)), (int)(int8_t)(xr[2 * d + 1] >> (8 * qq)));
+                        xb[d] = pack_i8((int)(int8_t)(xr8[2 * d] >> (8 * qq)), (int)(int8_t)(xr8[2 * d + 1] >> (8 * qq)));
                     gW1[q] = mfma_bf16(dh, xb, gW1[q]);
                     gW1[q] = mfma_bf16(dm, xb, gW1[q]);
                     gW1[q] = mfma_bf16(dl, xb, gW1[q]);
@@ -543,6 +554,203 @@ __global__ void __launch_bounds__((64 * GradLds<NQ, NT>::WPB), ((NQ * NT >= 32) 
             }
         }
         __builtin_amdgcn_wave_barrier();
+    };
+
+    // lane (j, g4) loads dwords 8s + 2*g4 + {0, 1} of row r (its bf16 B fragment of k-step s) and
+    // row r's scalars (register prefetch: issued before the current tile is processed)
+    uint32_t pre[S1][2];
+    int pre_act = 0;
+    float pre_olp = 0.f, pre_G = 0.f;
+    auto prefetch_row = [&](int r) {  // r in [0, R)
+        const uint32_t* src = row_src(r);
+#pragma unroll
+        for (int s = 0; s < S1; s++)
+#pragma unroll
+            for (int h = 0; h < 2; h++) {
+                const int cc = 8 * s + 2 * g4 + h;
+                pre[s][h] = src[cc < stride4 ? cc : stride4 - 1];  // clamped, masked at the use
+            }
+        pre_act = p.actions[(size_t)r * p.U + u];
+        pre_olp = p.old_lp[(size_t)r * p.U + u];
+        pre_G = p.ret[(size_t)r * p.G + grp];
+    };
+
+    if (!COMMON) {
+        // rows past the end load row 0's values: their loss weight is 0, so every derivative of
+        // theirs is exactly 0 (all inputs finite)
+        auto row_of_tile = [&](int tile) { return tile * 16 + j < R ? tile * 16 + j : 0; };
+        if (tile0 < tile_end) prefetch_row(row_of_tile(tile0));
+        for (int tile = tile0; tile < tile_end; tile++) {
+            const int half = (tile - tile0) & 1;  // position in the tile pair of the dW1 step
+            uint32_t xr[S1][2];
+#pragma unroll
+            for (int s = 0; s < S1; s++) xr[s][0] = pre[s][0], xr[s][1] = pre[s][1];
+            const bool valid = tile * 16 + j < R;
+            const int act = pre_act;
+            const float olp = pre_olp, G = pre_G;
+            if (tile + 1 < tile_end) prefetch_row(row_of_tile(tile + 1));
+            tile_step(BoolC<false>{}, xr, act, olp, G, valid, half, half == 1 || tile + 1 == tile_end, zero_vs, 0.f,
+                      0.f);
+        }
+    } else if (tile0 < tile_end) {
+        // ---- rows equal to the common row (acceptor rows of cores the agent does not own) share
+        //      one forward pass: the wave scans its rows one per lane, accumulates their loss
+        //      derivatives by action, and lists the other rows for the MFMA tiles; the summed
+        //      derivatives then run through the common row's backward once (virtual tile)
+        const int rb = tile0 * 16, re = min(tile_end * 16, R);
+        int32_t* list = reinterpret_cast<int32_t*>(sCm + 16 * NT + 4);
+        uint32_t txr[S1][2];
+        const uint32_t* crow = reinterpret_cast<const uint32_t*>(p.common);
+#pragma unroll
+        for (int s = 0; s < S1; s++)
+#pragma unroll
+            for (int h = 0; h < 2; h++) {
+                const int cc = 8 * s + 2 * g4 + h;
+                txr[s][h] = crow[cc < stride4 ? cc : stride4 - 1];
+            }
+        constexpr int LPR = S1 <= 2 ? 4 : (S1 <= 4 ? 8 : 16);
+        CommonScan<LPR> cs;
+        cs.init(crow, stride4, lane);
+        {
+            uint32_t xw[S1][2];
+#pragma unroll
+            for (int s = 0; s < S1; s++)
+#pragma unroll
+                for (int h = 0; h < 2; h++) {
+                    const int cc = 8 * s + 2 * g4 + h;
+                    xw[s][h] = cc < stride4 ? txr[s][h] : 0u;
+                }
+            Fwd f;
+            forward(xw, f);
+            if (j == 0) {
+#pragma unroll
+                for (int t = 0; t < NT; t++)
+#pragma unroll
+                    for (int q = 0; q < 4; q++) sCm[16 * t + 4 * g4 + q] = f.cl[t][q];
+                if (g4 == 0) {
+                    sCm[16 * NT] = f.V;
+                    sCm[16 * NT + 1] = f.ent;
+                }
+            }
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        }
+        const float Vc = sCm[16 * NT], ent_c = sCm[16 * NT + 1];
+        // per lane: summed d loss / d logp of each action over its common rows, in LDS (k-major:
+        // lane l's entry of action k at vsl[64 k + l], conflict-free for any actions)
+        float* vsl = reinterpret_cast<float*>(list + kCommonSeg + 64);
+#pragma unroll
+        for (int k = 0; k < 16 * NT; k++) vsl[64 * k + lane] = 0.f;
+        float sgv = 0.f, sl_min = 0.f, sl_mse = 0.f, sl_ent = 0.f;
+        int scnt = 0;
+        const uint64_t below = (1ull << lane) - 1ull;
+        int n_list = 0, otile = 0;
+        // scan registers (one 64-row step ahead): the rows' chunks (cooperative 16-byte loads) and
+        // row r0 + lane's scalars
+        int n_act = 0;
+        float n_olp = 0.f, n_G = 0.f;
+        bool n_in = false;
+        auto load_step = [&](int r0, int lim) {
+            cs.load([&](int k) { return row_src(r0 + k < lim ? r0 + k : rb); }, lane);
+            const int r = r0 + lane;
+            n_in = r < lim;
+            const int rr = n_in ? r : rb;
+            n_act = p.actions[(size_t)rr * p.U + u];
+            n_olp = p.old_lp[(size_t)rr * p.U + u];
+            n_G = p.ret[(size_t)rr * p.G + grp];
+        };
+        auto owner_tile = [&](int t0, int cnt, bool pair_done) {  // list rows t0 .. t0 + cnt - 1
+            const bool valid = j < cnt;
+            prefetch_row(list[t0 + (valid ? j : 0)]);
+            uint32_t xr[S1][2];
+#pragma unroll
+            for (int s = 0; s < S1; s++) xr[s][0] = pre[s][0], xr[s][1] = pre[s][1];
+            const int half = otile & 1;
+            tile_step(BoolC<false>{}, xr, pre_act, pre_olp, pre_G, valid, half, pair_done || half == 1, zero_vs, 0.f,
+                      0.f);
+            otile++;
+        };
+        for (int seg = rb; seg < re; seg += kCommonSeg) {
+            const int seg_end = min(seg + kCommonSeg, re);
+            load_step(seg, seg_end);
+            for (int r0 = seg; r0 < seg_end; r0 += 64) {
+                const int r = r0 + lane;
+                const bool in = n_in;
+                const bool common = cs.lane_row_common(lane) && in;
+                const int act = n_act;
+                const float olp = n_olp, G = n_G;
+                if (r0 + 64 < seg_end) load_step(r0 + 64, seg_end);
+                if (common) {
+                    // the tile path's per-row derivatives with the common row's forward values
+                    const float lp = (unsigned)act < (unsigned)A ? sCm[act] : 0.f;
+                    const float ratio = fast_exp(lp - olp);
+                    const float adv = G - Vc;
+                    const float sur1 = ratio * adv;
+                    const float rc = fminf(fmaxf(ratio, 1.f - p.eps_clip), 1.f + p.eps_clip);
+                    const float sur2 = rc * adv;
+                    const float inr = (ratio >= 1.f - p.eps_clip && ratio <= 1.f + p.eps_clip) ? 1.f : 0.f;
+                    const float dmin = sur1 < sur2 ? adv : (sur2 < sur1 ? adv * inr : 0.5f * adv + 0.5f * adv * inr);
+                    const float g_lp = -dmin * p.inv_R * ratio;
+                    if ((unsigned)act < (unsigned)A) vsl[64 * act + lane] += g_lp;
+                    sgv += (Vc - G) * p.inv_R;
+                    scnt++;
+                    sl_min += -fminf(sur1, sur2);
+                    sl_mse += (Vc - G) * (Vc - G);
+                    sl_ent += ent_c;
+                }
+                const bool other = in && !common;
+                const uint64_t m = __ballot(other);
+                if (other) list[n_list + __popcll(m & below)] = r;
+                n_list += __popcll(m);
+            }
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            int t0 = 0;
+            for (; t0 + 16 <= n_list; t0 += 16) owner_tile(t0, 16, false);
+            // the rest (< 16 rows) moves to the front of the list
+            const int rest = n_list - t0;
+            const int mv = lane < rest ? list[t0 + lane] : 0;
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            if (lane < rest) list[lane] = mv;
+            n_list = rest;
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        }
+        if (n_list > 0) owner_tile(0, n_list, false);
+        // the virtual tile: column 0 carries the common rows' summed derivatives
+        // wave totals per action (lane k sums action k's 64 entries in lane order), then column 0
+        // of the virtual tile: lane (0, g4) takes actions 16t + 4*g4 + q
+        float tot = 0.f;
+        if (lane < 16 * NT)
+            for (int l = 0; l < 64; l++) tot += vsl[64 * lane + l];
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        if (lane < 16 * NT) vsl[lane] = tot;
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        float vsum[NT][4];
+#pragma unroll
+        for (int t = 0; t < NT; t++)
+#pragma unroll
+            for (int q = 0; q < 4; q++) vsum[t][q] = j == 0 ? vsl[16 * t + 4 * g4 + q] : 0.f;
+        const float gv_tot = xsum16(xsum4g(sgv));
+        const float cnt_tot = (float)(int)xsum16(xsum4g((float)scnt));
+        tile_step(BoolC<true>{}, txr, 0, 0.f, 0.f, true, otile & 1, true, vsum, j == 0 ? -0.01f * p.inv_R * cnt_tot : 0.f,
+                  j == 0 ? gv_tot : 0.f);
+        // the common rows' loss terms join lane group 0's sums
+        const float m_tot = xsum16(xsum4g(sl_min)), q_tot = xsum16(xsum4g(sl_mse)), e_tot = xsum16(xsum4g(sl_ent));
+        if (lane == 0) {
+            l_min += m_tot;
+            l_mse += q_tot;
+            l_ent += e_tot;
+        }
     }
 
     // ---- the block's partial gradient: the 4 waves' vectors summed in LDS in wave order
@@ -646,13 +854,26 @@ __global__ void __launch_bounds__(256) k_ppo_reduce(const float* __restrict__ pa
     if (dst) dst[(size_t)grp * k + (i - base)] = s;
 }
 
-template <int NQ, int NT>
-static hipError_t launch_grad_t(const PpoArgs& a, hipStream_t st) {
-    using L = GradLds<NQ, NT>;
+template <int NQ, int NT, bool CM>
+static hipError_t launch_grad_cm(const PpoArgs& a, hipStream_t st) {
+    using L = GradLds<NQ, NT, CM>;
     const size_t lds = sizeof(float) * L::lds_floats;
     if (lds > 160 * 1024 || (size_t)a.P > (size_t)L::lds_floats) return hipErrorInvalidValue;  // partial in LDS
-    hipLaunchKernelGGL((k_ppo_grad<NQ, NT>), dim3((unsigned)(a.G * (a.n_chunks / 4))), dim3(64 * L::WPB), lds, st, a);
+    hipLaunchKernelGGL((k_ppo_grad<NQ, NT, CM>), dim3((unsigned)(a.G * (a.n_chunks / 4))), dim3(64 * L::WPB), lds, st,
+                       a);
     return hipGetLastError();
+}
+
+// the common-row path for inputs up to 128 bytes (its scan holds a row per lane in registers)
+template <int NQ, int NT>
+static hipError_t launch_grad_t(const PpoArgs& a, hipStream_t st) {
+    if constexpr (NQ <= 8) {
+        if (a.common && a.stride >= 16) {
+            using L = GradLds<NQ, NT, true>;
+            if (sizeof(float) * L::lds_floats <= 160 * 1024) return launch_grad_cm<NQ, NT, true>(a, st);
+        }
+    }
+    return launch_grad_cm<NQ, NT, false>(a, st);
 }
 
 hipError_t launch_ppo_grad(const PpoArgs& a, const GradOut& go, hipStream_t st) {

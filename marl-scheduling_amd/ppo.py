@@ -234,13 +234,14 @@ class PPOGroup:
         return losses
 
     def update_fused(self, states_i8, actions_i8, old_logprobs, returns_teg, unit_of_group, T: int, E: int,
-                     stream=None):
+                     stream=None, common_row=None):
         """The same K epochs with the gradient from the fused HIP kernel (ms_ppo_grad).
 
         states_i8 [R, U, stride] int8 rollout rows (R = T*E, row r = t*E + e), actions_i8 [R, U],
         old_logprobs [R, U] f32, returns_teg [T, E, G] f32 normalised (unit_returns), unit_of_group [G] int32
         (device). Adam (torch) applies the gradient; with several ranks the gradient is
-        all-reduced first."""
+        all-reduced first. common_row (int8 [stride], device, optional): rows equal to it share one
+        forward and one backward pass (same gradient up to f32 summation order)."""
         pol = self.policy
         R, U, stride = states_i8.shape
         assert R == T * E and states_i8.is_contiguous() and actions_i8.is_contiguous()
@@ -253,7 +254,7 @@ class PPOGroup:
         ws_bytes = lib.ms_ppo_workspace_bytes(ct.byref(a), R)
         ws = torch.empty(((ws_bytes + 3) // 4,), dtype=torch.float32, device=states_i8.device)
         batch = abi.MsPpoBatch(ptr(states_i8), ptr(actions_i8), ptr(old_logprobs), ptr(returns_teg),
-                               ptr(unit_of_group), stride, T, U, E)
+                               ptr(unit_of_group), stride, T, U, E, ptr(common_row))
         grads = abi.MsPpoGrads(*[ptr(getattr(pol, k).grad) for k in ACTOR_KEYS + CRITIC_KEYS], ptr(loss_buf))
         losses = []
         for _ in range(self.K):

@@ -286,8 +286,10 @@ class Trainer:
                 if self.fused:
                     sel32 = u_sel.to(torch.int32)
                     ret = unit_returns(u.rewards, sel32, u.group.gamma)  # [T][E][G]
+                    common = self.acc_common if (u is self.acc and self.common_rows) else None
                     ls += u.group.update_fused(states.reshape(T * E, u.U, u.stride), u.actions.view(T * E, u.U),
-                                               u.logprobs.view(T * E, u.U), ret, u_sel.to(torch.int32), T, E)
+                                               u.logprobs.view(T * E, u.U), ret, u_sel.to(torch.int32), T, E,
+                                               common_row=common)
                 else:
                     x, a, lp, ret = u.batch(states, u_sel)
                     ls += u.group.update(x, a, lp, ret)

@@ -220,6 +220,44 @@ def test_fused_grad_matches_autograd(ms, G, T, E, U, D, stride, A, K):
         assert ((wf - wr)[~firm].abs() <= 2 * lr * K + 1e-6).all(), k
 
 
+@pytest.mark.parametrize("G,T,E,U,O,A,K,frac", [(8, 20, 37, 64, 24, 25, 1, 0.9), (8, 13, 111, 8, 24, 25, 2, 1.0),
+                                                  (3, 7, 90, 3, 4, 5, 2, 0.5), (2, 6, 301, 4, 12, 13, 1, 0.0),
+                                                  (1, 41, 250, 2, 48, 49, 1, 0.95)])
+def test_fused_grad_common_rows_matches_autograd(ms, G, T, E, U, O, A, K, frac):
+    """ms_ppo_grad with common_row (rows equal to it share one forward and one summed backward)
+    against torch autograd of PPO.update on the same rows; chunks of > 1024 rows per wave exercise
+    the segment carry-over of the listed rows."""
+    ppo = _ppo(ms)
+    D = 3 + 2 * O
+    stride = (D + 3) // 4 * 4
+    torch.manual_seed(22)
+    ref = ppo.PPOGroup(G, D, A, 0.003, 0.01, 0.9, 0.2, K, device="cuda")
+    torch.manual_seed(22)
+    fus = ppo.PPOGroup(G, D, A, 0.003, 0.01, 0.9, 0.2, K, device="cuda")
+    states, actions, old_lp, ret = _rand_batch(G, T, E, U, D, stride, A, 6)
+    crow = _common_row(D, stride, O)
+    gen = torch.Generator().manual_seed(7)
+    pick = torch.rand(states.shape[:2], generator=gen) < frac
+    states[pick] = crow
+    u_sel = torch.randint(0, U, (G,), generator=torch.Generator().manual_seed(2))
+    R = T * E
+    x = states[:, u_sel, :D].permute(1, 0, 2).float().cuda()
+    a = actions[:, u_sel].T.long().cuda()
+    lp = old_lp[:, u_sel].T.contiguous().cuda()
+    rt = ret.permute(1, 2, 0).reshape(G, R).cuda()
+    ref_losses = ref.update(x, a, lp, rt)
+    ref_grads = {k: getattr(ref.policy, k).grad.clone() for k in ppo.ACTOR_KEYS + ppo.CRITIC_KEYS}
+    fus_losses = fus.update_fused(states.cuda(), actions.cuda(), old_lp.cuda(), ret.permute(2, 0, 1).contiguous().cuda(),
+                                  u_sel.to(torch.int32).cuda(), T, E, common_row=crow.cuda())
+    for rl, fl in zip(ref_losses, fus_losses):
+        np.testing.assert_allclose(fl.cpu().numpy(), rl.cpu().numpy(), rtol=1e-5, atol=1e-6)
+    for k, g in ref_grads.items():
+        fg = getattr(fus.policy, k).grad
+        scale = g.abs().max().item() + 1e-12
+        err = (fg - g).abs().max().item()
+        assert err <= 1e-4 * scale + 1e-7, (k, err, scale)
+
+
 def test_trainer_fused_matches_torch_update(ms):
     tr_mod = importlib.import_module("marl-scheduling_amd.trainer")
     trs = [tr_mod.Trainer.from_named("cfg3", n_envs=32, update_step=20, seed=4, device="cuda:0", fused=f)
