@@ -28,19 +28,24 @@ struct CommonScan {
     }
     // rowptr(k): dword pointer of step row k in [0, 64) (a valid row for rows past the range)
     template <class RowPtr>
-    __device__ __forceinline__ void load(RowPtr rowptr, int lane) {
+    __device__ __forceinline__ void load_into(u4a (&dst)[LPR], RowPtr rowptr, int lane) const {
 #pragma unroll
         for (int i = 0; i < LPR; i++) {
             const uint32_t* src = rowptr(i * RPI + lane / LPR);
-            nx[i] = start >= 0 ? *reinterpret_cast<const u4a*>(src + start) : tc;
+            dst[i] = start >= 0 ? *reinterpret_cast<const u4a*>(src + start) : tc;
         }
     }
-    // whether step row `lane` (of the chunks loaded last) equals the common row
-    __device__ __forceinline__ bool lane_row_common(int lane) const {
+    template <class RowPtr>
+    __device__ __forceinline__ void load(RowPtr rowptr, int lane) {
+        load_into(nx, rowptr, lane);
+    }
+    __device__ __forceinline__ bool lane_row_common(int lane) const { return common_of(nx, lane); }
+    // whether step row `lane` of the chunks in src equals the common row
+    __device__ __forceinline__ bool common_of(const u4a (&src)[LPR], int lane) const {
         uint64_t sel = 0;
 #pragma unroll
         for (int i = 0; i < LPR; i++) {
-            const u4a d = nx[i] ^ tc;
+            const u4a d = src[i] ^ tc;
             const uint64_t m = __ballot((d[0] | d[1] | d[2] | d[3]) != 0u);
             sel = (lane / RPI == i) ? m : sel;
         }

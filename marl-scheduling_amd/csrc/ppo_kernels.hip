@@ -111,6 +111,7 @@ __device__ __forceinline__ u4v bytes_to_bf16(uint32_t d0, uint32_t d1) {
 }
 
 constexpr int kCommonSeg = 1024;  // rows scanned per segment of the common-row path
+constexpr int kScanDepth = 1;     // 64-row scan steps in flight (2 spills registers at <4, 2>: slower)
 
 template <bool B>
 struct BoolC {
@@ -149,8 +150,11 @@ __global__ void __launch_bounds__((64 * GradLds<NQ, NT, COMMON>::WPB), ((NQ * NT
     const int g4 = lane >> 4;  // MFMA k-group / C-row group
     const int j = lane & 15;   // batch row within the tile (C column)
     const int blocks_per_group = p.n_chunks >> 2;
-    const int grp = blockIdx.x / blocks_per_group;
-    const int blk = blockIdx.x - grp * blocks_per_group;
+    // groups interleaved over the block index: the G groups' blocks of the same rows run at the
+    // same time, so the rollout lines they share (rows [r][0..U) of states, actions, log-probs)
+    // come from HBM once and hit in the Infinity Cache for the other groups
+    const int grp = blockIdx.x % p.G;
+    const int blk = blockIdx.x / p.G;
     const int chunk = blk * 4 + wave * CPW;
     const int D = p.D, A = p.A;
     const int u = p.unit_of_group[grp];
@@ -646,72 +650,87 @@ __global__ void __launch_bounds__((64 * GradLds<NQ, NT, COMMON>::WPB), ((NQ * NT
         int scnt = 0;
         const uint64_t below = (1ull << lane) - 1ull;
         int n_list = 0, otile = 0;
-        // scan registers (one 64-row step ahead): the rows' chunks (cooperative 16-byte loads) and
-        // row r0 + lane's scalars
-        int n_act = 0;
-        float n_olp = 0.f, n_G = 0.f;
-        bool n_in = false;
-        auto load_step = [&](int r0, int lim) {
-            cs.load([&](int k) { return row_src(r0 + k < lim ? r0 + k : rb); }, lane);
+        // scan registers, kScanDepth 64-row steps in flight: the rows' chunks (cooperative 16-byte
+        // loads) and row r0 + lane's scalars
+        constexpr int PF = kScanDepth;
+        u4a sc[PF][LPR];
+        int s_act[PF];
+        float s_olp[PF], s_G[PF];
+        auto load_slot = [&](int k, int r0, int lim) {
+            cs.load_into(sc[k], [&](int q) { return row_src(r0 + q < lim ? r0 + q : rb); }, lane);
             const int r = r0 + lane;
-            n_in = r < lim;
-            const int rr = n_in ? r : rb;
-            n_act = p.actions[(size_t)rr * p.U + u];
-            n_olp = p.old_lp[(size_t)rr * p.U + u];
-            n_G = p.ret[(size_t)rr * p.G + grp];
+            const int rr = r < lim ? r : rb;
+            s_act[k] = p.actions[(size_t)rr * p.U + u];
+            s_olp[k] = p.old_lp[(size_t)rr * p.U + u];
+            s_G[k] = p.ret[(size_t)rr * p.G + grp];
         };
-        auto owner_tile = [&](int t0, int cnt, bool pair_done) {  // list rows t0 .. t0 + cnt - 1
-            const bool valid = j < cnt;
-            prefetch_row(list[t0 + (valid ? j : 0)]);
-            uint32_t xr[S1][2];
+        // the listed rows t0 .. t0 + 16*n - 1 (the last tile may be partial: cnt rows in all) in
+        // 16-row tiles, the next tile's rows prefetched
+        auto owner_tiles = [&](int cnt) {
+            auto pf = [&](int t0) { prefetch_row(list[t0 + (t0 + j < cnt ? j : 0)]); };
+            pf(0);
+            for (int t0 = 0; t0 < cnt; t0 += 16) {
+                uint32_t xr[S1][2];
 #pragma unroll
-            for (int s = 0; s < S1; s++) xr[s][0] = pre[s][0], xr[s][1] = pre[s][1];
-            const int half = otile & 1;
-            tile_step(BoolC<false>{}, xr, pre_act, pre_olp, pre_G, valid, half, pair_done || half == 1, zero_vs, 0.f,
-                      0.f);
-            otile++;
+                for (int s = 0; s < S1; s++) xr[s][0] = pre[s][0], xr[s][1] = pre[s][1];
+                const int act = pre_act;
+                const float olp = pre_olp, G = pre_G;
+                const bool valid = t0 + j < cnt;
+                if (t0 + 16 < cnt) pf(t0 + 16);
+                const int half = otile & 1;
+                tile_step(BoolC<false>{}, xr, act, olp, G, valid, half, half == 1, zero_vs, 0.f, 0.f);
+                otile++;
+            }
         };
         for (int seg = rb; seg < re; seg += kCommonSeg) {
             const int seg_end = min(seg + kCommonSeg, re);
-            load_step(seg, seg_end);
-            for (int r0 = seg; r0 < seg_end; r0 += 64) {
-                const int r = r0 + lane;
-                const bool in = n_in;
-                const bool common = cs.lane_row_common(lane) && in;
-                const int act = n_act;
-                const float olp = n_olp, G = n_G;
-                if (r0 + 64 < seg_end) load_step(r0 + 64, seg_end);
-                if (common) {
-                    // the tile path's per-row derivatives with the common row's forward values
-                    const float lp = (unsigned)act < (unsigned)A ? sCm[act] : 0.f;
-                    const float ratio = fast_exp(lp - olp);
-                    const float adv = G - Vc;
-                    const float sur1 = ratio * adv;
-                    const float rc = fminf(fmaxf(ratio, 1.f - p.eps_clip), 1.f + p.eps_clip);
-                    const float sur2 = rc * adv;
-                    const float inr = (ratio >= 1.f - p.eps_clip && ratio <= 1.f + p.eps_clip) ? 1.f : 0.f;
-                    const float dmin = sur1 < sur2 ? adv : (sur2 < sur1 ? adv * inr : 0.5f * adv + 0.5f * adv * inr);
-                    const float g_lp = -dmin * p.inv_R * ratio;
-                    if ((unsigned)act < (unsigned)A) vsl[64 * act + lane] += g_lp;
-                    sgv += (Vc - G) * p.inv_R;
-                    scnt++;
-                    sl_min += -fminf(sur1, sur2);
-                    sl_mse += (Vc - G) * (Vc - G);
-                    sl_ent += ent_c;
+#pragma unroll
+            for (int k = 0; k < PF; k++)
+                if (seg + 64 * k < seg_end) load_slot(k, seg + 64 * k, seg_end);
+            for (int rs0 = seg; rs0 < seg_end; rs0 += 64 * PF) {
+#pragma unroll
+                for (int k = 0; k < PF; k++) {
+                    const int r0 = rs0 + 64 * k;
+                    if (r0 >= seg_end) break;
+                    const int r = r0 + lane;
+                    const bool in = r < seg_end;
+                    const bool common = cs.common_of(sc[k], lane) && in;
+                    const int act = s_act[k];
+                    const float olp = s_olp[k], G = s_G[k];
+                    if (r0 + 64 * PF < seg_end) load_slot(k, r0 + 64 * PF, seg_end);
+                    if (common) {
+                        // the tile path's per-row derivatives with the common row's forward values
+                        const float lp = (unsigned)act < (unsigned)A ? sCm[act] : 0.f;
+                        const float ratio = fast_exp(lp - olp);
+                        const float adv = G - Vc;
+                        const float sur1 = ratio * adv;
+                        const float rc = fminf(fmaxf(ratio, 1.f - p.eps_clip), 1.f + p.eps_clip);
+                        const float sur2 = rc * adv;
+                        const float inr = (ratio >= 1.f - p.eps_clip && ratio <= 1.f + p.eps_clip) ? 1.f : 0.f;
+                        const float dmin =
+                            sur1 < sur2 ? adv : (sur2 < sur1 ? adv * inr : 0.5f * adv + 0.5f * adv * inr);
+                        const float g_lp = -dmin * p.inv_R * ratio;
+                        if ((unsigned)act < (unsigned)A) vsl[64 * act + lane] += g_lp;
+                        sgv += (Vc - G) * p.inv_R;
+                        scnt++;
+                        sl_min += -fminf(sur1, sur2);
+                        sl_mse += (Vc - G) * (Vc - G);
+                        sl_ent += ent_c;
+                    }
+                    const bool other = in && !common;
+                    const uint64_t m = __ballot(other);
+                    if (other) list[n_list + __popcll(m & below)] = r;
+                    n_list += __popcll(m);
                 }
-                const bool other = in && !common;
-                const uint64_t m = __ballot(other);
-                if (other) list[n_list + __popcll(m & below)] = r;
-                n_list += __popcll(m);
             }
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            int t0 = 0;
-            for (; t0 + 16 <= n_list; t0 += 16) owner_tile(t0, 16, false);
+            const int full = n_list & ~15;
+            if (full > 0) owner_tiles(full);
             // the rest (< 16 rows) moves to the front of the list
-            const int rest = n_list - t0;
-            const int mv = lane < rest ? list[t0 + lane] : 0;
+            const int rest = n_list - full;
+            const int mv = lane < rest ? list[full + lane] : 0;
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -721,7 +740,7 @@ __global__ void __launch_bounds__((64 * GradLds<NQ, NT, COMMON>::WPB), ((NQ * NT
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         }
-        if (n_list > 0) owner_tile(0, n_list, false);
+        if (n_list > 0) owner_tiles(n_list);
         // the virtual tile: column 0 carries the common rows' summed derivatives
         // wave totals per action (lane k sums action k's 64 entries in lane order), then column 0
         // of the virtual tile: lane (0, g4) takes actions 16t + 4*g4 + q
