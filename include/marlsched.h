@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define MS_ABI_VERSION 2
+#define MS_ABI_VERSION 3
 
 #define MS_MAX_KINDS 16
 #define MS_MAX_AGENTS 64
@@ -272,7 +272,9 @@ int ms_discounted_returns(const float* rewards, int32_t T, int64_t M, int64_t ro
 
 /* The same returns for the sub-unit each group trains on, read straight from the rollout
  * reward buffer: rewards [T][E][U] (f32, or int32 with rewards_i32 = 1), sequence (e, g) is
- * unit unit_of_group[g] of replica e; out [T][E][G] f32 (the ms_ppo_batch.returns layout). */
+ * unit unit_of_group[g] of replica e; out [T][E][G] f32 (the ms_ppo_batch.returns layout).
+ * unit_of_group may list the sub-units of several update draws (Agent.py:716-728) back to back:
+ * draw d then reads returns + d*G_draw with returns_ld = G. */
 int ms_unit_returns(const void* rewards, int32_t rewards_i32, int32_t T, int64_t E, int32_t U,
                     const int32_t* unit_of_group, int32_t G, double gamma, float* out, void* stream);
 
@@ -294,6 +296,8 @@ typedef struct ms_ppo_batch {
      * own, Agent.py:167-212) share one forward pass, and their summed loss derivatives run through
      * one backward pass (the gradient is linear in them); NULL = every row on its own */
     const int8_t* common_row;
+    /* row pitch of returns in floats (0 = the number of groups): returns[(t*E + e)*ld + g] */
+    int32_t returns_ld;
 } ms_ppo_batch;
 
 typedef struct ms_ppo_grads {  /* device outputs, [G][...] like the weights */
@@ -305,6 +309,24 @@ typedef struct ms_ppo_grads {  /* device outputs, [G][...] like the weights */
 size_t ms_ppo_workspace_bytes(const ms_mlp_params* actor, int64_t rows);
 int ms_ppo_grad(const ms_mlp_params* actor, const ms_mlp_params* critic, const ms_ppo_batch* batch, float eps_clip,
                 void* workspace, size_t workspace_bytes, const ms_ppo_grads* grads, void* stream);
+
+/* ---- Adam step (torch.optim.Adam as PPO.__init__ builds it, PPOmodules.py:100-112) ----
+ * One optimizer.step() over the tensors of one PPO group: tensor i uses lr[lr_group[i]] (actor
+ * and critic parameter groups), betas (beta1, beta2), eps, no weight decay, bias corrections of
+ * step `step` (1-based, the value of torch's state["step"] after its increment). Updates param,
+ * exp_avg and exp_avg_sq in place, in f32 (torch's foreach formula; the scalars are rounded
+ * to f32 as torch passes them). At most MS_ADAM_MAX_TENSORS tensors per call. */
+#define MS_ADAM_MAX_TENSORS 16
+typedef struct ms_adam_tensor {
+    float* param;
+    const float* grad;
+    float* exp_avg;
+    float* exp_avg_sq;
+    int64_t numel;
+    int32_t lr_group;
+} ms_adam_tensor;
+int ms_adam_step(const ms_adam_tensor* tensors, int32_t n_tensors, const double* lr, int32_t n_lr, int64_t step,
+                 double beta1, double beta2, double eps, void* stream);
 
 const char* ms_last_error(void);
 int ms_abi_version(void);

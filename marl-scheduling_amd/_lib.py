@@ -62,12 +62,14 @@ def _load():
         "ms_ppo_grad": (ct.c_int, [ct.POINTER(abi.MsMlpParams), ct.POINTER(abi.MsMlpParams),
                                    ct.POINTER(abi.MsPpoBatch), ct.c_float, P, ct.c_size_t,
                                    ct.POINTER(abi.MsPpoGrads), P]),
+        "ms_adam_step": (ct.c_int, [ct.POINTER(abi.MsAdamTensor), i32, ct.POINTER(ct.c_double), i32, i64, ct.c_double,
+                                    ct.c_double, ct.c_double, P]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)
         fn.restype = res
         fn.argtypes = args
-    if L.ms_abi_version() != 2:
+    if L.ms_abi_version() != 3:
         raise ImportError("libmarlsched.so ABI version mismatch")
     return L
 
@@ -80,7 +82,7 @@ EXPORTED = (
     "ms_env_reset", "ms_env_step", "ms_env_round", "ms_env_flags", "ms_env_randbelow", "ms_env_auctioneer",
     "ms_env_get_rng", "ms_env_set_rng", "ms_env_export",
     "ms_env_import", "ms_policy_act", "ms_policy_act_common", "ms_offer_act_free", "ms_discounted_returns", "ms_unit_returns",
-    "ms_ppo_workspace_bytes", "ms_ppo_grad",
+    "ms_ppo_workspace_bytes", "ms_ppo_grad", "ms_adam_step",
 )
 
 

@@ -162,7 +162,22 @@ class MsPpoBatch(ct.Structure):
         ("U", ct.c_int32),
         ("E", ct.c_int64),
         ("common_row", ct.c_void_p),
+        ("returns_ld", ct.c_int32),
     ]
+
+
+class MsAdamTensor(ct.Structure):
+    _fields_ = [
+        ("param", ct.c_void_p),
+        ("grad", ct.c_void_p),
+        ("exp_avg", ct.c_void_p),
+        ("exp_avg_sq", ct.c_void_p),
+        ("numel", ct.c_int64),
+        ("lr_group", ct.c_int32),
+    ]
+
+
+ADAM_MAX_TENSORS = 16
 
 
 class MsPpoGrads(ct.Structure):

@@ -28,6 +28,7 @@ hipError_t launch_returns(const float*, int, int64_t, int64_t, double, float*, h
 hipError_t launch_unit_returns(const void*, int, int, int64_t, int, const int32_t*, int, double, float*, hipStream_t);
 hipError_t launch_ppo_grad(const PpoArgs&, const GradOut&, hipStream_t);
 int ppo_param_count(int D, int A);
+hipError_t launch_adam(const AdamTensor*, int, const double*, int, int64_t, double, double, double, hipStream_t);
 }  // namespace ms
 
 // work split of k_ppo_grad: ~8192 wave chunks over all groups (4 per block), >= 8 tiles of 16 rows each
@@ -521,6 +522,7 @@ int ms_ppo_grad(const ms_mlp_params* a, const ms_mlp_params* c, const ms_ppo_bat
     p.T = b->T;
     p.U = b->U;
     p.G = a->n_groups;
+    p.ret_ld = b->returns_ld > 0 ? b->returns_ld : p.G;
     p.E = b->E;
     p.R = R;
     ppo_split(R, p.G, &p.chunk_tiles, &p.n_chunks);
@@ -529,6 +531,25 @@ int ms_ppo_grad(const ms_mlp_params* a, const ms_mlp_params* c, const ms_ppo_bat
     p.inv_R = 1.0f / (float)R;
     ms::GradOut go{g->w1, g->b1, g->w2, g->b2, g->w3, g->b3, g->cw1, g->cb1, g->cw2, g->cb2, g->cw3, g->cb3, g->loss};
     HIP_TRY(ms::launch_ppo_grad(p, go, (hipStream_t)stream));
+    return MS_OK;
+}
+
+static_assert(sizeof(ms_adam_tensor) == sizeof(ms::AdamTensor), "ms_adam_tensor layout");
+static_assert(MS_ADAM_MAX_TENSORS == ms::kAdamMaxTensors, "ms_adam_tensor count");
+
+int ms_adam_step(const ms_adam_tensor* tensors, int32_t n_tensors, const double* lr, int32_t n_lr, int64_t step,
+                 double beta1, double beta2, double eps, void* stream) {
+    if (!tensors || !lr) return fail(MS_EINVAL, "NULL argument");
+    if (n_tensors < 1 || n_tensors > MS_ADAM_MAX_TENSORS) return fail(MS_EINVAL, "n_tensors must be in [1, %d]", MS_ADAM_MAX_TENSORS);
+    if (n_lr < 1 || n_lr > ms::kAdamMaxGroups) return fail(MS_EINVAL, "n_lr must be in [1, %d]", ms::kAdamMaxGroups);
+    if (step < 1) return fail(MS_EINVAL, "step must be >= 1");
+    for (int i = 0; i < n_tensors; i++) {
+        const ms_adam_tensor& t = tensors[i];
+        if (!t.param || !t.grad || !t.exp_avg || !t.exp_avg_sq || t.numel < 0) return fail(MS_EINVAL, "bad tensor %d", i);
+        if (t.lr_group < 0 || t.lr_group >= n_lr) return fail(MS_EINVAL, "tensor %d: lr_group out of range", i);
+    }
+    HIP_TRY(ms::launch_adam(reinterpret_cast<const ms::AdamTensor*>(tensors), n_tensors, lr, n_lr, step, beta1, beta2,
+                            eps, (hipStream_t)stream));
     return MS_OK;
 }
 

@@ -12,14 +12,24 @@ struct PpoArgs {
     const int8_t* states;                            // [R][U][stride]  (R = T*E rows, r = t*E + e)
     const int8_t* actions;                           // [R][U]
     const float* old_lp;                             // [R][U]
-    const float* ret;                                // [E][G][T] normalised returns
+    const float* ret;                                // [T][E][ret_ld] normalised returns
     const int32_t* unit_of_group;                    // [G]
     const int8_t* common;                            // [stride] rows equal to it share one forward, or NULL
     float* partials;                                 // [G][n_chunks][P]
-    int D, A, stride, T, U, G;
+    int D, A, stride, T, U, G, ret_ld;
     long long E, R;
     int chunk_tiles, n_chunks, P;
     float eps_clip, inv_R;
+};
+
+constexpr int kAdamMaxTensors = 16, kAdamMaxGroups = 4;
+struct AdamTensor {  // layout of ms_adam_tensor
+    float* param;
+    const float* grad;
+    float* exp_avg;
+    float* exp_avg_sq;
+    int64_t numel;
+    int32_t lr_group;
 };
 
 struct GradOut {

@@ -725,36 +725,66 @@ __global__ void __launch_bounds__(256) k_returns(const float* __restrict__ rewar
 // Returns of sequence (e, g) = unit unit_of_group[g] of replica e, gathered from the rollout
 // rewards [T][E][U] and written time-major [T][E][G] (coalesced: g is the fastest thread index).
 // Same arithmetic as k_returns: float64 scan, f32 values, mean and unbiased std over T.
-__global__ void __launch_bounds__(256) k_unit_returns(const void* __restrict__ rewards, int is_i32, int T, int64_t E,
-                                                      int U, const int32_t* __restrict__ unit_of_group, int G,
-                                                      double gamma, float* __restrict__ out) {
+// The thread's loads are issued kRetBatch at a time (they do not depend on the scan), so a
+// sequence costs ~3*T/kRetBatch memory round trips instead of 3*T. G may list the sub-units of
+// several update draws at once: the rollout row [t][e][0..U) is then read once for all of them.
+constexpr int kRetBatch = 16;
+
+template <bool I32>
+__global__ void __launch_bounds__(256) k_unit_returns(const void* __restrict__ rewards, int T, int64_t E, int U,
+                                                      const int32_t* __restrict__ unit_of_group, int G, double gamma,
+                                                      float* __restrict__ out) {
     const int64_t m = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (m >= E * G) return;
     const int64_t e = m / G;
     const int g = (int)(m - e * G);
     const int u = unit_of_group[g];
     const int64_t EG = E * G;
+    const int64_t EU = E * U;
+    const size_t src0 = (size_t)e * U + u;
     double Gs = 0.0, s = 0.0;
-    for (int t = T - 1; t >= 0; t--) {
-        const int64_t idx = ((int64_t)t * E + e) * U + u;
-        const double r = is_i32 ? (double)static_cast<const int32_t*>(rewards)[idx]
-                                : (double)static_cast<const float*>(rewards)[idx];
-        Gs = __dadd_rn(r, __dmul_rn(gamma, Gs));  // Python: two roundings, never an fma
-        const float f = (float)Gs;
-        out[(int64_t)t * EG + m] = f;
-        s += (double)f;
+    for (int t1 = T; t1 > 0; t1 -= kRetBatch) {
+        double r[kRetBatch];
+#pragma unroll
+        for (int k = 0; k < kRetBatch; k++) {
+            const int t = t1 - 1 - k;
+            const size_t idx = src0 + (size_t)(t < 0 ? 0 : t) * EU;
+            r[k] = I32 ? (double)static_cast<const int32_t*>(rewards)[idx] : (double)static_cast<const float*>(rewards)[idx];
+        }
+#pragma unroll
+        for (int k = 0; k < kRetBatch; k++) {
+            const int t = t1 - 1 - k;
+            if (t >= 0) {
+                Gs = __dadd_rn(r[k], __dmul_rn(gamma, Gs));  // Python: two roundings, never an fma
+                const float f = (float)Gs;
+                out[(int64_t)t * EG + m] = f;
+                s += (double)f;
+            }
+        }
     }
     const float mean = (float)(s / T);
     double v = 0.0;
-    for (int t = 0; t < T; t++) {
-        const double d = (double)out[(int64_t)t * EG + m] - (double)mean;
-        v += d * d;
+    for (int t0 = 0; t0 < T; t0 += kRetBatch) {
+        float f[kRetBatch];
+#pragma unroll
+        for (int k = 0; k < kRetBatch; k++) f[k] = out[(int64_t)min(t0 + k, T - 1) * EG + m];
+#pragma unroll
+        for (int k = 0; k < kRetBatch; k++) {
+            if (t0 + k < T) {
+                const double d = (double)f[k] - (double)mean;
+                v += d * d;
+            }
+        }
     }
     const float sd = T > 1 ? (float)sqrt(v / (T - 1)) : NAN;
     const float den = sd + 1e-7f;
-    for (int t = 0; t < T; t++) {
-        float* o = out + (int64_t)t * EG + m;
-        *o = (*o - mean) / den;
+    for (int t0 = 0; t0 < T; t0 += kRetBatch) {
+        float f[kRetBatch];
+#pragma unroll
+        for (int k = 0; k < kRetBatch; k++) f[k] = out[(int64_t)min(t0 + k, T - 1) * EG + m];
+#pragma unroll
+        for (int k = 0; k < kRetBatch; k++)
+            if (t0 + k < T) out[(int64_t)(t0 + k) * EG + m] = (f[k] - mean) / den;
     }
 }
 
@@ -762,8 +792,9 @@ hipError_t launch_unit_returns(const void* rewards, int is_i32, int T, int64_t E
                                int G, double gamma, float* out, hipStream_t st) {
     const int64_t M = E * G;
     if (M <= 0) return hipSuccess;
-    hipLaunchKernelGGL(k_unit_returns, dim3((unsigned)((M + 255) / 256)), dim3(256), 0, st, rewards, is_i32, T, E, U,
-                       unit_of_group, G, gamma, out);
+    auto kern = is_i32 ? k_unit_returns<true> : k_unit_returns<false>;
+    hipLaunchKernelGGL(kern, dim3((unsigned)((M + 255) / 256)), dim3(256), 0, st, rewards, T, E, U, unit_of_group, G,
+                       gamma, out);
     return hipGetLastError();
 }
 

@@ -576,7 +576,7 @@ __global__ void __launch_bounds__((64 * GradLds<NQ, NT, COMMON>::WPB), ((NQ * NT
             }
         pre_act = p.actions[(size_t)r * p.U + u];
         pre_olp = p.old_lp[(size_t)r * p.U + u];
-        pre_G = p.ret[(size_t)r * p.G + grp];
+        pre_G = p.ret[(size_t)r * p.ret_ld + grp];
     };
 
     if (!COMMON) {
@@ -662,7 +662,7 @@ __global__ void __launch_bounds__((64 * GradLds<NQ, NT, COMMON>::WPB), ((NQ * NT
             const int rr = r < lim ? r : rb;
             s_act[k] = p.actions[(size_t)rr * p.U + u];
             s_olp[k] = p.old_lp[(size_t)rr * p.U + u];
-            s_G[k] = p.ret[(size_t)rr * p.G + grp];
+            s_G[k] = p.ret[(size_t)rr * p.ret_ld + grp];
         };
         // the listed rows t0 .. t0 + 16*n - 1 (the last tile may be partial: cnt rows in all) in
         // 16-row tiles, the next tile's rows prefetched
@@ -927,5 +927,57 @@ reduce:
 }
 
 int ppo_param_count(int D, int A) { return poff(D, A).total; }
+
+// ---------------------------------------------------------------------------
+// Adam (torch.optim.Adam's foreach step, torch/optim/adam.py _multi_tensor_adam) over up to 16
+// tensors of one PPO group in one launch: blockIdx.y = tensor. Per element, each foreach op's
+// f32 rounding in turn:
+//   m = lerp(m, g, 1 - beta1);  v = v * beta2 + (1 - beta2) * g * g;
+//   p += (-lr / bc1) * m / (sqrt(v) / sqrt(bc2) + eps)
+struct AdamArgs {
+    AdamTensor t[kAdamMaxTensors];
+    float w1, beta2, one_m_beta2, eps;
+    float neg_step[kAdamMaxGroups], bc2_sqrt;
+};
+
+__global__ void __launch_bounds__(256) k_adam(AdamArgs a) {
+    const AdamTensor& t = a.t[blockIdx.y];
+    const float ns = a.neg_step[t.lr_group];
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < t.numel; i += (int64_t)gridDim.x * 256) {
+        const float g = t.grad[i];
+        float m = t.exp_avg[i], v = t.exp_avg_sq[i];
+        m = m + a.w1 * (g - m);                  // lerp, weight < 0.5
+        v = v * a.beta2;                         // mul_
+        v = v + a.one_m_beta2 * (g * g);         // addcmul_
+        const float den = sqrtf(v) / a.bc2_sqrt + a.eps;
+        t.param[i] = t.param[i] + ns * (m / den);  // addcdiv_
+        t.exp_avg[i] = m;
+        t.exp_avg_sq[i] = v;
+    }
+}
+
+hipError_t launch_adam(const AdamTensor* ts, int n, const double* lr, int n_lr, int64_t step, double beta1,
+                       double beta2, double eps, hipStream_t st) {
+    if (n < 1 || n > kAdamMaxTensors || n_lr < 1 || n_lr > kAdamMaxGroups || step < 1) return hipErrorInvalidValue;
+    AdamArgs a{};
+    int64_t mx = 1;
+    for (int i = 0; i < n; i++) {
+        if (ts[i].lr_group < 0 || ts[i].lr_group >= n_lr) return hipErrorInvalidValue;
+        a.t[i] = ts[i];
+        mx = ts[i].numel > mx ? ts[i].numel : mx;
+    }
+    // the scalars as torch computes them (Python floats) and passes them to the f32 foreach ops
+    const double bc1 = 1.0 - pow(beta1, (double)step), bc2 = 1.0 - pow(beta2, (double)step);
+    a.w1 = (float)(1.0 - beta1);
+    a.beta2 = (float)beta2;
+    a.one_m_beta2 = (float)(1.0 - beta2);
+    a.eps = (float)eps;
+    for (int k = 0; k < n_lr; k++) a.neg_step[k] = (float)((lr[k] / bc1) * -1.0);
+    a.bc2_sqrt = (float)sqrt(bc2);
+    int64_t bx = (mx + 255) / 256;
+    bx = bx > 1024 ? 1024 : bx;
+    hipLaunchKernelGGL(k_adam, dim3((unsigned)bx, (unsigned)n), dim3(256), 0, st, a);
+    return hipGetLastError();
+}
 
 }  // namespace ms

@@ -180,8 +180,50 @@ def unit_returns(rewards_teu: torch.Tensor, unit_of_group: torch.Tensor, gamma: 
     return out
 
 
+class HipAdam:
+    """torch.optim.Adam (defaults betas (0.9, 0.999), eps 1e-8, no weight decay) over the
+    parameters of one PPOGroup as one ``ms_adam_step`` launch per step: tensor i of
+    ``param_groups[k]["params"]`` uses ``param_groups[k]["lr"]`` like torch's param groups
+    (PPOmodules.py:100-105). The state (exp_avg, exp_avg_sq, step) mirrors torch's."""
+
+    def __init__(self, param_groups, betas=(0.9, 0.999), eps=1e-8):
+        self.param_groups = [dict(params=list(g["params"]), lr=float(g["lr"])) for g in param_groups]
+        self.betas, self.eps = betas, eps
+        self.step_count = 0
+        self.state = {}
+        for g in self.param_groups:
+            for p in g["params"]:
+                assert p.is_cuda and p.dtype == torch.float32 and p.is_contiguous()
+                self.state[p] = dict(exp_avg=torch.zeros_like(p), exp_avg_sq=torch.zeros_like(p))
+        n = sum(len(g["params"]) for g in self.param_groups)
+        assert n <= abi.ADAM_MAX_TENSORS and len(self.param_groups) <= 4
+
+    def zero_grad(self):
+        for g in self.param_groups:
+            for p in g["params"]:
+                p.grad = None
+
+    @torch.no_grad()
+    def step(self, stream=None):
+        self.step_count += 1
+        ts = []
+        for k, g in enumerate(self.param_groups):
+            for p in g["params"]:
+                if p.grad is None:  # torch skips parameters without a gradient
+                    continue
+                st = self.state[p]
+                ts.append(abi.MsAdamTensor(ptr(p), ptr(p.grad), ptr(st["exp_avg"]), ptr(st["exp_avg_sq"]), p.numel(), k))
+        if not ts:
+            return
+        arr = (abi.MsAdamTensor * len(ts))(*ts)
+        lrs = (ct.c_double * len(self.param_groups))(*[g["lr"] for g in self.param_groups])
+        check(lib.ms_adam_step(arr, len(ts), lrs, len(self.param_groups), self.step_count, self.betas[0],
+                               self.betas[1], self.eps, stream_ptr(stream)))
+
+
 class PPOGroup:
-    """Policy / policy_old pair + Adam for one unit type (PPOmodules.py:75-174)."""
+    """Policy / policy_old pair + Adam for one unit type (PPOmodules.py:75-174). The torch-autograd
+    ``update`` steps torch.optim.Adam; ``update_fused`` steps the HIP Adam (HipAdam)."""
 
     def __init__(self, n_groups, in_dim, n_actions, lr_actor, lr_critic, gamma, eps_clip, k_epochs, device,
                  allreduce=None, init_nets=None):
@@ -193,13 +235,28 @@ class PPOGroup:
         self.policy_old = GroupedActorCritic(n_groups, in_dim, n_actions, init=False).to(device)
         self.policy_old.requires_grad_(False)
         self.sync_old()
-        self.optimizer = torch.optim.Adam([
+        self.param_groups = [
             {"params": self.policy.actor_parameters(), "lr": lr_actor},
             {"params": self.policy.critic_parameters(), "lr": lr_critic},
-        ])
+        ]
+        self._torch_opt = self._hip_opt = None
         self.gamma, self.eps_clip, self.K = gamma, eps_clip, k_epochs
         self.allreduce = allreduce
         self.last_losses = []
+
+    @property
+    def optimizer(self):
+        """torch.optim.Adam of the torch-autograd path (created on first use)."""
+        if self._torch_opt is None:
+            self._torch_opt = torch.optim.Adam([dict(g) for g in self.param_groups])
+        return self._torch_opt
+
+    @property
+    def hip_optimizer(self):
+        """HipAdam of the fused path (created on first use)."""
+        if self._hip_opt is None:
+            self._hip_opt = HipAdam(self.param_groups)
+        return self._hip_opt
 
     @torch.no_grad()
     def sync_old(self):
@@ -234,7 +291,7 @@ class PPOGroup:
         return losses
 
     def update_fused(self, states_i8, actions_i8, old_logprobs, returns_teg, unit_of_group, T: int, E: int,
-                     stream=None, common_row=None):
+                     stream=None, common_row=None, returns_ld: int = 0):
         """The same K epochs with the gradient from the fused HIP kernel (ms_ppo_grad).
 
         states_i8 [R, U, stride] int8 rollout rows (R = T*E, row r = t*E + e), actions_i8 [R, U],
@@ -254,15 +311,16 @@ class PPOGroup:
         ws_bytes = lib.ms_ppo_workspace_bytes(ct.byref(a), R)
         ws = torch.empty(((ws_bytes + 3) // 4,), dtype=torch.float32, device=states_i8.device)
         batch = abi.MsPpoBatch(ptr(states_i8), ptr(actions_i8), ptr(old_logprobs), ptr(returns_teg),
-                               ptr(unit_of_group), stride, T, U, E, ptr(common_row))
+                               ptr(unit_of_group), stride, T, U, E, ptr(common_row), int(returns_ld))
         grads = abi.MsPpoGrads(*[ptr(getattr(pol, k).grad) for k in ACTOR_KEYS + CRITIC_KEYS], ptr(loss_buf))
         losses = []
+        opt = self.hip_optimizer
         for _ in range(self.K):
             check(lib.ms_ppo_grad(ct.byref(a), ct.byref(c), ct.byref(batch), ct.c_float(self.eps_clip), ptr(ws),
                                   ws_bytes, ct.byref(grads), stream_ptr(stream)))
             if self.allreduce is not None:
                 self.allreduce(pol.parameters())
-            self.optimizer.step()
+            opt.step(stream)
             losses.append(loss_buf[:, 0] + 0.5 * loss_buf[:, 1] - 0.01 * loss_buf[:, 2])
         self.last_losses = losses
         return losses

@@ -282,15 +282,21 @@ class Trainer:
             states = self.acc_obs if u is self.acc else (self.off_obs if u is self.off else self.price_obs)
             states = states[:T]
             ls = []
-            for u_sel in sel[u.name]:
-                if self.fused:
-                    sel32 = u_sel.to(torch.int32)
-                    ret = unit_returns(u.rewards, sel32, u.group.gamma)  # [T][E][G]
-                    common = self.acc_common if (u is self.acc and self.common_rows) else None
+            if self.fused:
+                # the returns of every draw's sub-units in one launch: [T][E][sum of G], draw d at
+                # column offset d*G (returns depend on the rewards only, not on earlier draws' updates)
+                all_sel = torch.cat(sel[u.name]).to(torch.int32)
+                ret_all = unit_returns(u.rewards, all_sel, u.group.gamma)
+                common = self.acc_common if (u is self.acc and self.common_rows) else None
+                col = 0
+                for u_sel in sel[u.name]:
                     ls += u.group.update_fused(states.reshape(T * E, u.U, u.stride), u.actions.view(T * E, u.U),
-                                               u.logprobs.view(T * E, u.U), ret, u_sel.to(torch.int32), T, E,
-                                               common_row=common)
-                else:
+                                               u.logprobs.view(T * E, u.U), ret_all.view(-1)[col:],
+                                               all_sel[col:col + u_sel.numel()], T, E, common_row=common,
+                                               returns_ld=all_sel.numel())
+                    col += u_sel.numel()
+            else:
+                for u_sel in sel[u.name]:
                     x, a, lp, ret = u.batch(states, u_sel)
                     ls += u.group.update(x, a, lp, ret)
             u.group.sync_old()

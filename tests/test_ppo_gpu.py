@@ -328,3 +328,58 @@ def test_trainer_graph_replay_matches_eager(ms):
         assert torch.equal(outs[0][k], outs[1][k]), k
     assert torch.equal(trs[0].acc_obs, trs[1].acc_obs)
     assert trs[0].env.round == trs[1].env.round == 48
+
+
+def test_hip_adam_matches_torch_adam(ms):
+    """ms_adam_step (HipAdam) against torch.optim.Adam with the actor / critic param groups of
+    PPO.__init__ (PPOmodules.py:100-105), over several steps with changing gradients."""
+    ppo = _ppo(ms)
+    gen = torch.Generator().manual_seed(3)
+    shapes = [(8, 16, 51), (8, 16), (8, 16, 16), (8, 25, 16), (8, 1, 16), (8, 1)]
+    init = [torch.randn(s, generator=gen) for s in shapes]
+    p_ref = [t.clone().cuda().requires_grad_(True) for t in init]
+    p_hip = [t.clone().cuda().requires_grad_(True) for t in init]
+    groups = lambda ps: [{"params": ps[:4], "lr": 0.003}, {"params": ps[4:], "lr": 0.01}]
+    ref = torch.optim.Adam(groups(p_ref))
+    hip = ppo.HipAdam(groups(p_hip))
+    for step in range(6):
+        grads = [torch.randn(s, generator=gen).cuda() * (10.0 ** (step - 3)) for s in shapes]
+        for p, g in zip(p_ref, grads):
+            p.grad = g.clone()
+        for p, g in zip(p_hip, grads):
+            p.grad = g.clone()
+        ref.step()
+        hip.step()
+        for i, (a, b) in enumerate(zip(p_hip, p_ref)):
+            np.testing.assert_allclose(a.detach().cpu().numpy(), b.detach().cpu().numpy(), rtol=2e-6, atol=1e-7,
+                                       err_msg="tensor %d step %d" % (i, step))
+        for i, (a, b) in enumerate(zip(p_hip, p_ref)):
+            st_h, st_r = hip.state[a], ref.state[b]
+            np.testing.assert_allclose(st_h["exp_avg_sq"].cpu().numpy(), st_r["exp_avg_sq"].cpu().numpy(), rtol=2e-6,
+                                       atol=0)
+
+
+def test_unit_returns_of_several_draws_feed_the_gradient(ms):
+    """One ms_unit_returns launch for two draws (unit_of_group concatenated) read through
+    ms_ppo_batch.returns_ld gives the same gradient as separate per-draw returns."""
+    ppo = _ppo(ms)
+    G, T, E, U, D, stride, A = 4, 12, 40, 12, 18, 20, 9
+    states, actions, old_lp, _ = _rand_batch(G, T, E, U, D, stride, A, 9)
+    gen = torch.Generator().manual_seed(5)
+    rew = torch.randint(-5, 9, (T, E, U), generator=gen).float().cuda()
+    draws = [torch.randint(0, U, (G,), generator=gen).to(torch.int32).cuda() for _ in range(2)]
+    both = torch.cat(draws)
+    ret_both = ppo.unit_returns(rew, both, 0.5)
+    for d, sel in enumerate(draws):
+        torch.manual_seed(7)
+        g1 = ppo.PPOGroup(G, D, A, 0.003, 0.01, 0.5, 0.2, 1, device="cuda")
+        torch.manual_seed(7)
+        g2 = ppo.PPOGroup(G, D, A, 0.003, 0.01, 0.5, 0.2, 1, device="cuda")
+        ret_one = ppo.unit_returns(rew, sel, 0.5)
+        torch.testing.assert_close(ret_both[:, :, d * G:(d + 1) * G], ret_one, rtol=0, atol=0)
+        l1 = g1.update_fused(states.cuda(), actions.cuda(), old_lp.cuda(), ret_one, sel, T, E)
+        l2 = g2.update_fused(states.cuda(), actions.cuda(), old_lp.cuda(), ret_both.view(-1)[d * G:], sel, T, E,
+                             returns_ld=2 * G)
+        torch.testing.assert_close(l1[0], l2[0], rtol=0, atol=0)
+        for k in ppo.ACTOR_KEYS + ppo.CRITIC_KEYS:
+            torch.testing.assert_close(getattr(g1.policy, k), getattr(g2.policy, k), rtol=0, atol=0)
