@@ -121,6 +121,12 @@ typedef struct ms_reward_out {
     int32_t* acceptor;      /* [E][N][C] acceptorNetRewards */
     int32_t* auctioneer;    /* [E][C]    auctioneerReward */
     int32_t* agent;         /* [E][N]    agentReward */
+    /* getAggregatedFixedPricesReward (Reward.py:92-143), for the aggregated agents:
+     * offerRewards[a] = sum of prio1 over a's accepted offers; acceptorRewards[a] = the
+     * rewards of a's terminating jobs minus what a pays along the liability chains (no
+     * recipient credit, unlike the divided acceptor rewards). */
+    int32_t* aggregated_offer;     /* [E][N] */
+    int32_t* aggregated_acceptor;  /* [E][N] */
 } ms_reward_out;
 
 /* One executed offer (world.acceptedOffers entry), stored at its core's index. */
@@ -309,6 +315,26 @@ typedef struct ms_ppo_grads {  /* device outputs, [G][...] like the weights */
 size_t ms_ppo_workspace_bytes(const ms_mlp_params* actor, int64_t rows);
 int ms_ppo_grad(const ms_mlp_params* actor, const ms_mlp_params* critic, const ms_ppo_batch* batch, float eps_clip,
                 void* workspace, size_t workspace_bytes, const ms_ppo_grads* grads, void* stream);
+
+/* ---- aggregated agents (AggregatedAgent Agent.py:73-140, AggregatedFixPricePPOAgent :359-391,
+ * FullyAggregatedFixPricePPOAgent :393-492) around ms_env_step ----
+ * Observations from the divided rows ms_env_step / ms_env_reset wrote (acc_obs
+ * [E][N][C][acc_obs_stride], off_obs [E][N][L][off_obs_stride]); any output may be NULL:
+ *   agg_acceptor [E][N][align4(C*D_acc)]        concat over cores of the acceptor rows (Agent.py:82-124)
+ *   agg_offer    [E][N][align4(2C+2L)]          cores' (prio, rem), then slots' (prio, rem) (Agent.py:126-134)
+ *   fully        [E][N][align4(2C+2L+C*D_acc)]  concat(offer, acceptor) (Agent.py:464)
+ * Pad bytes are zero. */
+int ms_aggregate_obs(const ms_config* cfg, int64_t n_envs, const int8_t* acc_obs, const int8_t* off_obs,
+                     int8_t* agg_acceptor, int8_t* agg_offer, int8_t* fully, void* stream);
+/* Agent action numbers -> the divided actions ms_env_step takes (numberToNDimensionalAction
+ * Agent.py:644-666: action of core c = digit c of the acceptor number in base O+1, of slot s =
+ * digit s of the offer number in base C+1). fully = 0: actions = acceptor numbers [E][N] then
+ * offer numbers [E][N]; fully = 1: actions [E][N], acceptor = a / (C+1)^L, offer = a % (C+1)^L
+ * (Agent.py:469-473). Out-of-range numbers (ValueError in the reference) decode as "reject all /
+ * offer nothing" and are counted into *n_bad (device int32, may be NULL). EINVAL when the
+ * action space exceeds int32. */
+int ms_decode_aggregated(const ms_config* cfg, int64_t n_envs, const int32_t* actions, int32_t fully,
+                         int8_t* acceptor, int8_t* offer_core, int32_t* n_bad, void* stream);
 
 /* ---- Adam step (torch.optim.Adam as PPO.__init__ builds it, PPOmodules.py:100-112) ----
  * One optimizer.step() over the tensors of one PPO group: tensor i uses lr[lr_group[i]] (actor

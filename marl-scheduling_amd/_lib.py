@@ -62,6 +62,8 @@ def _load():
         "ms_ppo_grad": (ct.c_int, [ct.POINTER(abi.MsMlpParams), ct.POINTER(abi.MsMlpParams),
                                    ct.POINTER(abi.MsPpoBatch), ct.c_float, P, ct.c_size_t,
                                    ct.POINTER(abi.MsPpoGrads), P]),
+        "ms_aggregate_obs": (ct.c_int, [ct.POINTER(abi.MsConfig), i64, P, P, P, P, P, P]),
+        "ms_decode_aggregated": (ct.c_int, [ct.POINTER(abi.MsConfig), i64, P, i32, P, P, P, P]),
         "ms_adam_step": (ct.c_int, [ct.POINTER(abi.MsAdamTensor), i32, ct.POINTER(ct.c_double), i32, i64, ct.c_double,
                                     ct.c_double, ct.c_double, P]),
     }
@@ -83,6 +85,7 @@ EXPORTED = (
     "ms_env_get_rng", "ms_env_set_rng", "ms_env_export",
     "ms_env_import", "ms_policy_act", "ms_policy_act_common", "ms_offer_act_free", "ms_discounted_returns", "ms_unit_returns",
     "ms_ppo_workspace_bytes", "ms_ppo_grad", "ms_adam_step",
+    "ms_aggregate_obs", "ms_decode_aggregated",
 )
 
 

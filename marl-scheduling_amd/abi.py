@@ -91,6 +91,8 @@ class MsRewardOut(ct.Structure):
         ("acceptor", ct.c_void_p),
         ("auctioneer", ct.c_void_p),
         ("agent", ct.c_void_p),
+        ("aggregated_offer", ct.c_void_p),
+        ("aggregated_acceptor", ct.c_void_p),
     ]
 
 

@@ -10,7 +10,7 @@ FLAGS=(-O3 -std=c++17 -fPIC --offload-arch="${ARCH}" -Wall -Wno-unused-function
 OBJDIR="${HERE}/build"
 mkdir -p "${OBJDIR}"
 objs=()
-for src in env_kernels.hip policy_kernels.hip ppo_kernels.hip capi.cpp; do
+for src in env_kernels.hip policy_kernels.hip ppo_kernels.hip agg_kernels.hip capi.cpp; do
   obj="${OBJDIR}/${src%.*}.o"
   if [[ ! -f "${obj}" || "${HERE}/csrc/${src}" -nt "${obj}" || "${HERE}/csrc/ms_layout.h" -nt "${obj}" || "${HERE}/csrc/ms_ppo.h" -nt "${obj}" || "${HERE}/../include/marlsched.h" -nt "${obj}" ]]; then
     # the env round reproduces Python's float64 arithmetic: no contraction there; the policy

@@ -28,6 +28,8 @@ hipError_t launch_returns(const float*, int, int64_t, int64_t, double, float*, h
 hipError_t launch_unit_returns(const void*, int, int, int64_t, int, const int32_t*, int, double, float*, hipStream_t);
 hipError_t launch_ppo_grad(const PpoArgs&, const GradOut&, hipStream_t);
 int ppo_param_count(int D, int A);
+hipError_t launch_aggregate_obs(const AggArgs&, hipStream_t);
+hipError_t launch_decode_aggregated(const int32_t*, long long, int, int, int, int, int8_t*, int8_t*, int*, hipStream_t);
 hipError_t launch_adam(const AdamTensor*, int, const double*, int, int64_t, double, double, double, hipStream_t);
 }  // namespace ms
 
@@ -220,6 +222,8 @@ int ms_env_step(ms_env* env, const ms_actions* act, const ms_obs_out* obs, const
         io.rew_acc = rew->acceptor;
         io.rew_auct = rew->auctioneer;
         io.rew_agent = rew->agent;
+        io.rew_agg_off = rew->aggregated_offer;
+        io.rew_agg_acc = rew->aggregated_acceptor;
     }
     if (ev) {
         io.ev_acc = ev->accepted;
@@ -531,6 +535,47 @@ int ms_ppo_grad(const ms_mlp_params* a, const ms_mlp_params* c, const ms_ppo_bat
     p.inv_R = 1.0f / (float)R;
     ms::GradOut go{g->w1, g->b1, g->w2, g->b2, g->w3, g->b3, g->cw1, g->cb1, g->cw2, g->cb2, g->cw3, g->cb3, g->loss};
     HIP_TRY(ms::launch_ppo_grad(p, go, (hipStream_t)stream));
+    return MS_OK;
+}
+
+int ms_aggregate_obs(const ms_config* cfg, int64_t E, const int8_t* acc_obs, const int8_t* off_obs,
+                     int8_t* agg_acceptor, int8_t* agg_offer, int8_t* fully, void* stream) {
+    int rc = validate_config(cfg);
+    if (rc) return rc;
+    if (E < 1 || !acc_obs || !off_obs) return fail(MS_EINVAL, "need E >= 1 and both divided observation arrays");
+    const ms::Params P = ms::make_params(*cfg, cap_of(cfg));
+    ms::AggArgs g{};
+    g.acc = acc_obs;
+    g.off = off_obs;
+    g.out_acc = agg_acceptor;
+    g.out_off = agg_offer;
+    g.out_full = fully;
+    g.N = P.N;
+    g.C = P.C;
+    g.L = P.L;
+    g.d_acc = P.d_acc;
+    g.acc_stride = P.acc_stride;
+    g.off_stride = P.off_stride;
+    g.agg_acc_stride = ms::align4(P.C * P.d_acc);
+    g.agg_off_stride = ms::align4(2 * P.C + 2 * P.L);
+    g.full_stride = ms::align4(2 * P.C + 2 * P.L + P.C * P.d_acc);
+    g.E = E;
+    HIP_TRY(ms::launch_aggregate_obs(g, (hipStream_t)stream));
+    return MS_OK;
+}
+
+int ms_decode_aggregated(const ms_config* cfg, int64_t E, const int32_t* actions, int32_t fully, int8_t* acceptor,
+                         int8_t* offer_core, int32_t* n_bad, void* stream) {
+    int rc = validate_config(cfg);
+    if (rc) return rc;
+    if (E < 1 || !actions || !acceptor || !offer_core) return fail(MS_EINVAL, "NULL argument or E < 1");
+    const ms::Params P = ms::make_params(*cfg, cap_of(cfg));
+    double space = 1.0;
+    for (int c = 0; c < P.C; c++) space *= (double)(P.O + 1);
+    for (int s = 0; s < P.L; s++) space *= (double)(P.C + 1);
+    if (space > 2147483647.0) return fail(MS_EINVAL, "aggregated action space (O+1)^C * (C+1)^L exceeds int32");
+    HIP_TRY(ms::launch_decode_aggregated(actions, (long long)E * P.N, P.C, P.L, P.O, fully ? 1 : 0, acceptor,
+                                         offer_core, n_bad, (hipStream_t)stream));
     return MS_OK;
 }
 

@@ -824,6 +824,7 @@ __device__ __forceinline__ void env_round(const Params& P, int64_t E, uint8_t* r
     int16_t* s_auct = reinterpret_cast<int16_t*>(smem + P.s_auct);  // auctioneer action per core
     int32_t* s_agent_r = reinterpret_cast<int32_t*>(smem + P.s_agentr);  // agentReward
     int32_t* s_auct_r = reinterpret_cast<int32_t*>(smem + P.s_auctr);    // auctioneerReward
+    int32_t* s_credit = reinterpret_cast<int32_t*>(smem + P.s_credit);   // chain credits per recipient
     uint32_t& s_flags = *reinterpret_cast<uint32_t*>(smem + P.s_misc);
     int& s_n_exec = *reinterpret_cast<int*>(smem + P.s_misc + 4);
 
@@ -892,7 +893,10 @@ __device__ __forceinline__ void env_round(const Params& P, int64_t E, uint8_t* r
         s_exec[i] = -1;
         s_fresh[i] = 0;
     }
-    for (int i = gl; i < N; i += LPE) s_agent_r[i] = 0;
+    for (int i = gl; i < N; i += LPE) {
+        s_agent_r[i] = 0;
+        s_credit[i] = 0;
+    }
     if (gl == 0) {
         s_flags = 0;
         s_n_exec = 0;
@@ -1116,6 +1120,7 @@ __device__ __forceinline__ void env_round(const Params& P, int64_t E, uint8_t* r
                     if (le.recipient > 0) {
                         atomicAdd(&s_agent_r[le.recipient - 1], traded);
                         acc_r[(le.recipient - 1) * C + c] += traded;
+                        if (io.rew_agg_acc) atomicAdd(&s_credit[le.recipient - 1], traded);
                     } else {
                         s_auct_r[c] = traded;
                     }
@@ -1243,6 +1248,23 @@ __device__ __forceinline__ void env_round(const Params& P, int64_t E, uint8_t* r
         rew(io.rew_price, NL, price_r);
         rew(io.rew_agent, N, s_agent_r);
         rew(io.rew_auct, C, s_auct_r);
+        // getAggregatedFixedPricesReward (Reward.py:92-143): offer = sum of the agent's slot rewards
+        // (prio1 of its accepted offers); acceptor = its divided acceptor rewards without the chain
+        // credits it received as a recipient
+        if (io.rew_agg_off || io.rew_agg_acc) {
+            for (int a = gl; a < N; a += LPE) {
+                if (io.rew_agg_off) {
+                    int v = 0;
+                    for (int j = 0; j < L; j++) v += (int)off_r[a * L + j];
+                    io.rew_agg_off[e * N + a] = v;
+                }
+                if (io.rew_agg_acc) {
+                    int v = -s_credit[a];
+                    for (int c = 0; c < C; c++) v += acc_r[a * C + c];
+                    io.rew_agg_acc[e * N + a] = v;
+                }
+            }
+        }
     }
     MS_MARK(10);
     build_masks<LPE>(R, P, s_mc, s_mr, gl);

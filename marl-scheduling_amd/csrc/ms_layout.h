@@ -52,7 +52,7 @@ struct Params {
     // small envs keep many waves per CU in flight
     int32_t s_rec, s_act_acc, s_act_off, s_act_price, s_act_auct, s_accr, s_offr, s_pricer,
         s_spawn_kind, s_scratch, s_total;
-    int32_t s_mc, s_mr, s_newle, s_exec, s_key, s_auct, s_agentr, s_auctr, s_rank, s_fresh, s_misc;
+    int32_t s_mc, s_mr, s_newle, s_exec, s_key, s_auct, s_agentr, s_credit, s_auctr, s_rank, s_fresh, s_misc;
     // observation scratch (offsets inside s_scratch): C owner rows + the foreign row
     // [C+1][acc_stride], the source-row dword offset of every acceptor row [N*C] u16, the
     // offer-row template [off_stride] and the slot pairs [NL] u16
@@ -75,8 +75,22 @@ struct StepIO {
     int32_t* rew_acc;
     int32_t* rew_auct;
     int32_t* rew_agent;
+    int32_t* rew_agg_off;
+    int32_t* rew_agg_acc;
     ms_accept_rec* ev_acc;
     ms_term_rec* ev_term;
+};
+
+// launch arguments of k_aggregate_obs (agg_kernels.hip): divided rows in, aggregated rows out
+struct AggArgs {
+    const int8_t* acc;  // [E][N][C][acc_stride]
+    const int8_t* off;  // [E][N][L][off_stride]
+    int8_t* out_acc;    // [E][N][agg_acc_stride] or NULL
+    int8_t* out_off;    // [E][N][agg_off_stride] or NULL
+    int8_t* out_full;   // [E][N][full_stride] or NULL
+    int N, C, L, d_acc, acc_stride, off_stride;
+    int agg_acc_stride, agg_off_stride, full_stride;
+    long long E;
 };
 
 inline int32_t align4(int32_t x) { return (x + 3) & ~3; }
@@ -141,6 +155,7 @@ inline Params make_params(const ms_config& c, int32_t cap) {
     p.s_mr = s; s += 16 * (p.N + 1);           // offer masks per recipient
     p.s_newle = s; s += 8 * p.C;               // this round's liability entry per core
     p.s_agentr = s; s += 4 * p.N;              // agentReward
+    p.s_credit = s; s += 4 * p.N;              // chain credits received (aggregated acceptor rewards)
     p.s_auctr = s; s += 4 * p.C;               // auctioneerReward
     p.s_exec = s; s += align4(2 * p.C);        // executed slot per core
     p.s_key = s; s += align4(2 * p.C);         // execution order key

@@ -54,15 +54,55 @@ class BatchedEnv:
         auct = torch.empty((E, self.C, s.acc_obs_stride), dtype=torch.int8, device=d) if auctioneer else None
         return dict(acceptor=acc, offer=off, auctioneer=auct)
 
-    def reward_buffers(self):
+    def reward_buffers(self, aggregated=False):
         E, d = self.E, self.device
-        return dict(
+        r = dict(
             offer=torch.empty((E, self.N, self.L), dtype=torch.float32, device=d),
             price=torch.empty((E, self.N, self.L), dtype=torch.float32, device=d) if self.free_prices else None,
             acceptor=torch.empty((E, self.N, self.C), dtype=torch.int32, device=d),
             auctioneer=torch.empty((E, self.C), dtype=torch.int32, device=d),
             agent=torch.empty((E, self.N), dtype=torch.int32, device=d),
         )
+        if aggregated:  # getAggregatedFixedPricesReward (Reward.py:92-143)
+            r["aggregated_offer"] = torch.empty((E, self.N), dtype=torch.int32, device=d)
+            r["aggregated_acceptor"] = torch.empty((E, self.N), dtype=torch.int32, device=d)
+        return r
+
+    # ---- aggregated agents (Agent.py:73-140, 359-492)
+    def aggregated_dims(self):
+        """(dim, stride) of the aggregated acceptor, offer and fully aggregated rows."""
+        N, C, L, d_acc = self.N, self.C, self.L, self.shape.acc_obs_dim
+        dims = dict(acceptor=C * d_acc, offer=2 * C + 2 * L, fully=2 * C + 2 * L + C * d_acc)
+        return {k: (v, (v + 3) // 4 * 4) for k, v in dims.items()}
+
+    def aggregated_action_counts(self):
+        """(O+1)^C acceptor and (C+1)^L offer actions per agent (PPOmodules.py:180, 198)."""
+        return (self.O + 1) ** self.C, (self.C + 1) ** self.L
+
+    def aggregate_obs(self, obs, out=None, kinds=("acceptor", "offer"), stream=None):
+        """Aggregated observations [E, N, stride] int8 from the divided ones (ms_aggregate_obs)."""
+        dims = self.aggregated_dims()
+        if out is None:
+            out = {k: torch.empty((self.E, self.N, dims[k][1]), dtype=torch.int8, device=self.device) for k in kinds}
+        for k, t in out.items():
+            assert t.dtype == torch.int8 and t.is_contiguous() and t.numel() == self.E * self.N * dims[k][1], k
+        check(lib.ms_aggregate_obs(ct.byref(self.cfg), self.E, ptr(obs["acceptor"]), ptr(obs["offer"]),
+                                   ptr(out.get("acceptor")), ptr(out.get("offer")), ptr(out.get("fully")),
+                                   stream_ptr(stream)))
+        return out
+
+    def decode_aggregated(self, numbers, fully: bool, acceptor=None, offer_core=None, n_bad=None, stream=None):
+        """Agent action numbers (int32: [2, E, N] acceptor/offer numbers, or [E, N] fully aggregated)
+        -> divided actions (int8 [E, N, C], [E, N, L]) for step (ms_decode_aggregated)."""
+        assert numbers.dtype == torch.int32 and numbers.is_contiguous()
+        assert numbers.numel() == self.E * self.N * (1 if fully else 2)
+        if acceptor is None:
+            acceptor = torch.empty((self.E, self.N, self.C), dtype=torch.int8, device=self.device)
+        if offer_core is None:
+            offer_core = torch.empty((self.E, self.N, self.L), dtype=torch.int8, device=self.device)
+        check(lib.ms_decode_aggregated(ct.byref(self.cfg), self.E, ptr(numbers), int(bool(fully)), ptr(acceptor),
+                                       ptr(offer_core), ptr(n_bad), stream_ptr(stream)))
+        return acceptor, offer_core
 
     def event_buffers(self):
         E, d = self.E, self.device
@@ -105,7 +145,8 @@ class BatchedEnv:
                           ptr(auctioneer))
         o = abi.MsObsOut(ptr(obs.get("acceptor")), ptr(obs.get("offer")), ptr(obs.get("auctioneer")))
         r = abi.MsRewardOut(ptr(rewards.get("offer")), ptr(rewards.get("price")), ptr(rewards.get("acceptor")),
-                            ptr(rewards.get("auctioneer")), ptr(rewards.get("agent")))
+                            ptr(rewards.get("auctioneer")), ptr(rewards.get("agent")),
+                            ptr(rewards.get("aggregated_offer")), ptr(rewards.get("aggregated_acceptor")))
         ev = abi.MsEventOut(ptr(events.get("accepted")), ptr(events.get("terminated"))) if events else None
         check(lib.ms_env_step(self._h, ct.byref(a), ct.byref(o), ct.byref(r), ct.byref(ev) if ev else None,
                               stream_ptr(stream)))

@@ -226,13 +226,13 @@ class PPOGroup:
     ``update`` steps torch.optim.Adam; ``update_fused`` steps the HIP Adam (HipAdam)."""
 
     def __init__(self, n_groups, in_dim, n_actions, lr_actor, lr_critic, gamma, eps_clip, k_epochs, device,
-                 allreduce=None, init_nets=None):
+                 allreduce=None, init_nets=None, hidden: int = HIDDEN):
         if init_nets is not None:  # per-group parameter dicts built by the caller, in reference order
             assert len(init_nets) == n_groups
-            self.policy = GroupedActorCritic.from_params(init_nets, in_dim, n_actions).to(device)
+            self.policy = GroupedActorCritic.from_params(init_nets, in_dim, n_actions, hidden).to(device)
         else:
-            self.policy = GroupedActorCritic(n_groups, in_dim, n_actions).to(device)
-        self.policy_old = GroupedActorCritic(n_groups, in_dim, n_actions, init=False).to(device)
+            self.policy = GroupedActorCritic(n_groups, in_dim, n_actions, hidden).to(device)
+        self.policy_old = GroupedActorCritic(n_groups, in_dim, n_actions, hidden, init=False).to(device)
         self.policy_old.requires_grad_(False)
         self.sync_old()
         self.param_groups = [
@@ -257,6 +257,16 @@ class PPOGroup:
         if self._hip_opt is None:
             self._hip_opt = HipAdam(self.param_groups)
         return self._hip_opt
+
+    @torch.no_grad()
+    def sample(self, x, generator=None):
+        """PPO.selectAction + ActorCritic.act (PPOmodules.py:53-63, 114-125) in PyTorch-ROCm for nets the
+        16-wide HIP kernels do not cover (the aggregated agents' 32 / 64 hidden units and (O+1)^C
+        actions): x [G, R, D] float on the device -> (actions [G, R] long, log-probs [G, R] f32) from
+        policy_old, torch's Categorical (probs renormalised, multinomial sampling)."""
+        dist = Categorical(self.policy_old.actor_probs(x))
+        a = dist.sample()
+        return a, dist.log_prob(a)
 
     @torch.no_grad()
     def sync_old(self):

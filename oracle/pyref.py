@@ -305,6 +305,20 @@ class PyWorld:
             for o in self.accepted:
                 off_r[o.offerer - 1][o.queue_pos] = o.prio1
             offer_rewards = off_r
+        # getAggregatedFixedPricesReward (Reward.py:92-143): the offer reward sums prio1 over the
+        # agent's accepted offers, the acceptor reward has no recipient credit
+        agg_off = np.zeros((N, 1), dtype=np.int64)
+        agg_acc = np.zeros((N, 1), dtype=np.int64)
+        for o in self.accepted:
+            agg_off[o.offerer - 1][0] += o.prio1
+        for c, owner, gen, ts in self.term:
+            agg_acc[owner - 1] += gen
+            last, tm = ts, 0
+            for e in self.liab[c]:
+                tm += last - e.round
+                last = e.round
+                agg_acc[e.offerer - 1] -= round(e.price / e.nec_time * tm)
+        self.last_aggregated = (agg_off, agg_acc)
         for c, owner, gen, ts in self.term:
             acc[owner - 1][c] = gen
             if not self.cfg.free_prices:
@@ -325,7 +339,16 @@ class PyWorld:
             self.liab[c] = deque()
         return offer_rewards, acc, auct, agent, term_rev
 
-    # ---- canonical state for comparisons (same fields as ms_state_host)
+    # ---- aggregated agents: AggregatedAgent (Agent.py:82-134), FullyAggregatedFixPricePPOAgent
+    #      (Agent.py:399-464) observations of the current state
+    def aggregated_obs(self):
+        acc = [[v for c in range(self.C) for v in self.acceptor_obs(a, c)] for a in range(self.N)]
+        cores = [v for c in range(self.C) for v in (self.core_job[c].prio, self.core_job[c].rem)]
+        off = [cores + [v for j in self.coll[a] for v in (j.prio, j.rem)] for a in range(self.N)]
+        fully = [off[a] + acc[a] for a in range(self.N)]  # torch.cat((offer, acceptor)) Agent.py:464
+        return acc, off, fully
+
+        # ---- canonical state for comparisons (same fields as ms_state_host)
     def state(self):
         N, C, L = self.N, self.C, self.L
         oc = [[-1] * L for _ in range(N)]
@@ -352,3 +375,19 @@ class PyWorld:
             liab=liab,
             mt_state=self.rng.getstate(),
         )
+
+
+def number_to_nd_action(number, base, dimensionality):
+    """numberToNDimensionalAction (Agent.py:644-666), restated."""
+    if number < 0 or number >= base ** dimensionality:
+        raise ValueError("Illegal Argument")
+    out = []
+    dim = dimensionality - 1
+    n = number
+    while len(out) < dimensionality:
+        d = n if dim == 0 else n // (base ** dim)
+        n -= (base ** dim) * d
+        dim -= 1
+        out.append(d)
+    out.reverse()
+    return out
