@@ -15,8 +15,10 @@ SchedulingEnvironment.py:21-348:
 * ``saveRewards(...)`` and ``updateAgents()`` follow the reference.
 
 Every round runs on libmarlsched at E = 1 (see ``marlsched_dropin``). The
-aggregated, fully-aggregated, hard-coded-agent and DQN envs are outside this
-build's hot path and raise ``NotImplementedError``.
+aggregated and fully-aggregated envs (``PPOAggregatedFixPriceEnv``,
+``PPOFullyAggregatedFixPriceEnv``) run the divided step with the aggregation
+kernels around it. The hard-coded-agent and DQN envs are outside this build's
+hot path and raise ``NotImplementedError``.
 
 ``LocallySharedParamsDividedFreePriceEnv`` is an addition. BASELINE cfg3 trains
 free prices with locally shared parameters, which the reference has no class
@@ -318,6 +320,168 @@ class LocallySharedParamsDividedFreePriceEnv(PPODividedFreePriceEnv):
     _arch = "local"
 
 
+class _AggUnits:
+    """ExperienceBuffer (PPOmodules.py:9-22) of one aggregated net per agent: per round the agents'
+    states [N, D] f32, actions [N] and log-probs [N] on the device, rewards [N] on the host."""
+
+    def __init__(self, group):
+        self.group = group
+        self.states, self.actions, self.logprobs, self.rewards = [], [], [], []
+
+    @property
+    def T(self):
+        return len(self.actions)
+
+    def clear(self):
+        self.states, self.actions, self.logprobs, self.rewards = [], [], [], []
+
+    def update(self):
+        """PPO.update (PPOmodules.py:127-174) of every agent's net: HIP returns + torch autograd / Adam."""
+        if not self.actions:
+            return []
+        if len(self.rewards) != len(self.actions):
+            raise RuntimeError("%d rewards saved for %d actions" % (len(self.rewards), len(self.actions)))
+        x = torch.stack(self.states, 1)            # [N, T, D]
+        a = torch.stack(self.actions, 1)           # [N, T]
+        lp = torch.stack(self.logprobs, 1)
+        r = torch.tensor(np.stack(self.rewards), dtype=torch.float32, device=x.device)  # [T, N]
+        ret = ppo.discounted_returns(r, self.group.gamma)  # [N, T]
+        losses = self.group.update(x, a, lp, ret)
+        self.group.sync_old()
+        self.clear()
+        return losses
+
+
+class _AggregatedPPOEnv(SchedulingEnv):
+    """PPOAggregatedFixPriceEnv / PPOFullyAggregatedFixPriceEnv (SchedulingEnvironment.py:213-250) at E = 1.
+
+    Observations per agent are the aggregated rows of AggregatedAgent (Agent.py:82-134): the acceptor
+    row as a 1-D float32 tensor (torch.cat onto torch.tensor([]) promotes it), the offer row as
+    int64. Actions are drawn as one number per net (PyTorch-ROCm: 32 / 64 hidden units) and decoded
+    on the device (ms_decode_aggregated, numberToNDimensionalAction Agent.py:644-666); rewards are
+    getAggregatedFixedPricesReward's (Reward.py:92-143) from the env step."""
+
+    _fully = False
+
+    def __init__(self, world, params):
+        super().__init__(world, params)
+        self.LR_ACTOR = params["LR_ACTOR"]
+        self.LR_CRITIC = params["LR_CRITIC"]
+        self.OFFER_GAMMA = params["OFFER_GAMMA"]
+        self.ACCEPTOR_GAMMA = params["ACCEPTOR_GAMMA"]
+        self.EPS_CLIP = params["EPS_CLIP"]
+        self.RAW_K_EPOCHS = params["RAW_K_EPOCHS"]
+        self.ACCEPTOR_K_EPOCHS = params["ACCEPTOR_K_EPOCHS"]
+        self.OFFER_K_EPOCHS = params["OFFER_K_EPOCHS"]
+        self.CENTRALISATION_SAMPLE = params["CENTRALISATION_SAMPLE"]
+        eng = self._eng
+        env = eng.env
+        if env.free_prices:
+            raise ValueError("the aggregated envs are fixed-price only (SchedulingEnvironment.py:213-248)")
+        eng.rew = env.reward_buffers(aggregated=True)
+        N = world.numberOfAgents
+        self._dims = env.aggregated_dims()
+        n_acc, n_off = env.aggregated_action_counts()
+        dev = eng.device
+        # nets in the reference's order: agent by agent (Agent.py:363-366 / 397), policy then policy_old
+        kinds = ["fully"] if self._fully else ["acc", "off"]
+        spec = dict(acc=(self._dims["acceptor"][0], n_acc, 32, self.ACCEPTOR_GAMMA, self.ACCEPTOR_K_EPOCHS),
+                    off=(self._dims["offer"][0], n_off, 32, self.OFFER_GAMMA, self.OFFER_K_EPOCHS),
+                    fully=(self._dims["fully"][0], n_acc * n_off, 64, self.ACCEPTOR_GAMMA, self.ACCEPTOR_K_EPOCHS))
+        nets = {k: [] for k in kinds}
+        for _ in range(N):
+            for k in kinds:
+                D, A, H = spec[k][:3]
+                nets[k].append(ppo.reference_actor_critic_params(D, A, H))
+                ppo.reference_actor_critic_params(D, A, H)
+        self._units = {}
+        for k in kinds:
+            D, A, H, gam, K = spec[k]
+            grp = ppo.PPOGroup(N, D, A, self.LR_ACTOR, self.LR_CRITIC, gam, self.EPS_CLIP, K, dev, init_nets=nets[k],
+                               hidden=H)
+            self._units[k] = _AggUnits(grp)
+        self._agg = {k: torch.zeros((1, N, self._dims[k][1]), dtype=torch.int8, device=dev)
+                     for k in ("acceptor", "offer")}
+        self._numbers = torch.zeros((1 if self._fully else 2, 1, N), dtype=torch.int32, device=dev)
+        self._bad = torch.zeros(1, dtype=torch.int32, device=dev)
+
+    def _aggregated_host(self):
+        eng = self._eng
+        eng.env.aggregate_obs(eng.obs, out=self._agg)
+        acc = self._agg["acceptor"][0, :, : self._dims["acceptor"][0]].cpu().float()
+        off = self._agg["offer"][0, :, : self._dims["offer"][0]].cpu().long()
+        N = acc.shape[0]
+        return [acc[a].clone() for a in range(N)], [off[a].clone() for a in range(N)]
+
+    def reset(self):
+        _, _, auct = self._eng.reset()
+        acc, off = self._aggregated_host()
+        return acc, off, auct
+
+    def step(self, offerActions, acceptorActions, auctioneer_action):
+        out = super().step(offerActions, acceptorActions, auctioneer_action)
+        acc, off = self._aggregated_host()
+        return (acc, off) + tuple(out[2:])
+
+    def _rewards(self, r, terms):
+        """getAggregatedFixedPricesReward (Reward.py:92-143) containers; it leaves
+        env.terminationRevenues alone."""
+        N, C = self.world.numberOfAgents, self.world.numberOfCores
+        off = r["aggregated_offer"].astype(np.int64).reshape(N, 1)
+        acc = r["aggregated_acceptor"].astype(np.int64).reshape(N, 1)
+        auct = r["auctioneer"].astype(np.int64).reshape(C)
+        agent = r["agent"].astype(np.int64).reshape(N)
+        return off, acc, auct, agent
+
+    def getActionForAllAgents(self, nestedAcceptorNetObservationTensors, nestedOfferNetObservationTensors):
+        eng, w = self._eng, self.world
+        N, C, L = w.numberOfAgents, w.numberOfCores, w.collectionLength
+        dev = eng.device
+        acc_x = torch.stack([torch.as_tensor(x).float() for x in nestedAcceptorNetObservationTensors]).to(dev)
+        off_x = torch.stack([torch.as_tensor(x).float() for x in nestedOfferNetObservationTensors]).to(dev)
+        if self._fully:  # torch.cat((offerObservations, acceptorObservations)) (Agent.py:464)
+            xs = dict(fully=torch.cat((off_x, acc_x), 1))
+        else:
+            xs = dict(acc=acc_x, off=off_x)
+        for i, (k, x) in enumerate(xs.items()):
+            u = self._units[k]
+            a, lp = u.group.sample(x.unsqueeze(1))  # [N, 1]
+            u.states.append(x)
+            u.actions.append(a[:, 0])
+            u.logprobs.append(lp[:, 0])
+            self._numbers[i, 0].copy_(a[:, 0])
+        acc, off = eng.env.decode_aggregated(self._numbers, self._fully, n_bad=self._bad)
+        acc_h, off_h = acc[0].cpu().tolist(), off[0].cpu().tolist()
+        if int(self._bad.item()):
+            raise ValueError("Illegal Argument")  # numberToNDimensionalAction (Agent.py:651-652)
+        return [[int(v) for v in acc_h[a]] for a in range(N)], [[int(v) for v in off_h[a]] for a in range(N)]
+
+    def saveRewards(self, offerUnitRewards, acceptorUnitRewards, agentReward):
+        """SchedulingEnvironment.py:223-225 / 243-247: the acceptor net saves agentReward, the offer
+        net offerUnitRewards[i][0]; the fully aggregated net their sum."""
+        off = np.asarray(offerUnitRewards, dtype=np.float64).reshape(-1)
+        agent = np.asarray(agentReward, dtype=np.float64).reshape(-1)
+        if self._fully:
+            self._units["fully"].rewards.append(agent + off)
+        else:
+            self._units["acc"].rewards.append(agent)
+            self._units["off"].rewards.append(off)
+
+    def updateAgents(self):
+        """Every agent's nets (Agent.py:384-386, 487-488)."""
+        self._last_losses = {k: u.update() for k, u in self._units.items()}
+
+
+class PPOAggregatedFixPriceEnv(_AggregatedPPOEnv):
+    """PPOAggregatedFixPriceEnv (SchedulingEnvironment.py:213-228)."""
+
+
+class PPOFullyAggregatedFixPriceEnv(_AggregatedPPOEnv):
+    """PPOFullyAggregatedFixPriceEnv (SchedulingEnvironment.py:231-250)."""
+
+    _fully = True
+
+
 def _out_of_scope(name):
     class _Env:
         def __init__(self, *a, **k):
@@ -327,7 +491,5 @@ def _out_of_scope(name):
     return _Env
 
 
-PPOAggregatedFixPriceEnv = _out_of_scope("PPOAggregatedFixPriceEnv")
-PPOFullyAggregatedFixPriceEnv = _out_of_scope("PPOFullyAggregatedFixPriceEnv")
 HardcodedFixPriceEnvironment = _out_of_scope("HardcodedFixPriceEnvironment")
 DQNDividedFixedPricesEnv = _out_of_scope("DQNDividedFixedPricesEnv")

@@ -50,7 +50,7 @@ def test_dropin_modules_keep_the_reference_names():
     assert w.round == 0 and w.maxAmountOfOffersToOneAgent == 6 and w.accProbabilities == [0.8, 1.0]
     assert w.acceptedOffers == [] and w.verweilzeiten == []
     with pytest.raises(NotImplementedError):
-        env_mod.PPOAggregatedFixPriceEnv(w, rl_params())
+        env_mod.HardcodedFixPriceEnvironment(w, rl_params())
     if not torch.cuda.is_available():  # no CPU fallback
         with pytest.raises(RuntimeError):
             env_mod.PPODividedFixedPriceEnv(w, rl_params())
@@ -235,7 +235,8 @@ def test_dropin_ppo_update_matches_reference(arch):
 @pytest.mark.parametrize("env_name", ["PPODividedFixedPriceEnv", "PPODividedFreePriceEnv",
                                       "GloballySharedParamsDividedFixedPriceEnv",
                                       "LocallySharedParamsDividedFixedPriceEnv",
-                                      "LocallySharedParamsDividedFreePriceEnv"])
+                                      "LocallySharedParamsDividedFreePriceEnv", "PPOAggregatedFixPriceEnv",
+                                      "PPOFullyAggregatedFixPriceEnv"])
 def test_dropin_runs_the_trainppo_loop(env_name):
     """The loop body of trainPPO.py:133-216, unchanged, for 3 episodes with updates."""
     world, env_mod, _ = _mods()
@@ -270,3 +271,53 @@ def test_dropin_runs_the_trainppo_loop(env_name):
     assert updates == 1 and w.round == 30
     for u in env._units.values():
         assert u.T == 10 and all(torch.isfinite(p).all() for p in u.group.policy.parameters())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("fully", [False, True])
+def test_dropin_aggregated_env_matches_object_restatement(fully):
+    """PPOAggregatedFixPriceEnv / PPOFullyAggregatedFixPriceEnv: observation containers (float32
+    acceptor rows, int64 offer rows per agent) and getAggregatedFixedPricesReward arrays against the
+    restatement, with the global random stream shared, and the nets in the reference's init order."""
+    from oracle.pyref import PyWorld
+
+    world, env_mod, _ = _mods()
+    wp = world_params(N=2, C=2, L=2)
+    seed = 99
+    random.seed(seed)
+    torch.manual_seed(3)
+    w = world.World(wp)
+    cls = env_mod.PPOFullyAggregatedFixPriceEnv if fully else env_mod.PPOAggregatedFixPriceEnv
+    env = cls(w, rl_params())
+    torch.manual_seed(3)
+    ppo = __import__("marlsched_dropin").ppo
+    O, N, C = 4, 2, 2
+    da, do = C * (3 + 2 * O), 2 * C + 2 * 2
+    first = ppo.reference_actor_critic_params(do + da, 25 * 9, 64) if fully else \
+        ppo.reference_actor_critic_params(da, 25, 32)
+    unit = env._units["fully" if fully else "acc"]
+    for name, v in first.items():
+        torch.testing.assert_close(getattr(unit.group.policy, name)[0].cpu(), v.detach(), rtol=0, atol=0)
+    pw = PyWorld(_pyref_config(wp, False), seed)
+    acc_obs, off_obs, auct_obs = env.reset()
+    for t in range(120):
+        pa, po, _ = pw.aggregated_obs()
+        assert all(x.dtype == torch.float32 for x in acc_obs) and all(x.dtype == torch.int64 for x in off_obs)
+        assert [x.tolist() for x in acc_obs] == pa and [x.tolist() for x in off_obs] == po, t
+        acc_l, off_l = env.getActionForAllAgents(acc_obs, off_obs)
+        auct = w.auctioneer.getAuctioneerAction(auct_obs)
+        assert auct == pw.auctioneer_actions()
+        out = env.step(off_l, acc_l, auct)
+        _, (_, _, auct_r, agent_r, _), _, _ = pw.step(acc_l, off_l, auct)
+        w_off, w_acc = pw.last_aggregated
+        assert out[3].dtype == np.int64 and out[3].shape == (N, 1) and out[4].shape == (N, 1)
+        np.testing.assert_array_equal(out[3], w_off)
+        np.testing.assert_array_equal(out[4], w_acc)
+        np.testing.assert_array_equal(out[5], auct_r)
+        np.testing.assert_array_equal(out[6], agent_r)
+        assert random.getstate() == pw.rng.getstate(), t
+        env.saveRewards(out[3], out[4], out[6])
+        acc_obs, off_obs, auct_obs = out[0], out[1], out[2]
+    env.updateAgents()
+    for u in env._units.values():
+        assert u.T == 0 and all(torch.isfinite(p).all() for p in u.group.policy.parameters())
