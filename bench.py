@@ -200,6 +200,27 @@ def main():
     tr.iteration()
     torch.cuda.synchronize(device)
     tr.env.step, tr.use_graph = orig_step, graph_mode
+    # The same launches as the rollout graph replays them: the UPDATE_STEP env steps of one
+    # rollout (same ring buffers) captured into a HIP graph of their own, events around its replay.
+    graph_step_us = None
+    if tr.use_graph:
+        E, N, C, L = args.envs, tr.N, tr.C, tr.L
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            for t in range(tr.T):
+                obs = dict(acceptor=tr.acc_obs[t + 1], offer=tr.off_obs[t + 1])
+                rew = dict(offer=tr.off.rewards[t].view(E, N, L), acceptor=tr.acc.rewards[t].view(E, N, C),
+                           agent=tr.agent_reward, auctioneer=tr.auct_reward,
+                           price=tr.price.rewards[t].view(E, N, L) if tr.free else None)
+                orig_step(tr.acc.actions[t].view(E, N, C), tr.off.actions[t].view(E, N, L),
+                          tr.env_price.view(E, N, L) if tr.free else None, obs=obs, rewards=rew)
+        g.replay()  # warm
+        s_ev, e_ev = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s_ev.record(stream)
+        g.replay()
+        e_ev.record(stream)
+        torch.cuda.synchronize(device)
+        graph_step_us = s_ev.elapsed_time(e_ev) * 1e3 / tr.T
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=device)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -212,7 +233,11 @@ def main():
     agent_steps = world * args.envs * shape.n_agents * rounds
     value = agent_steps / elapsed
     step_ms = [s.elapsed_time(e) for s, e in step_events]
-    avg_step_s = sum(step_ms) / len(step_ms) / 1e3
+    eager_step_s = sum(step_ms) / len(step_ms) / 1e3
+    # the roofline figure: HIP events around each launch of one eager training iteration (fresh
+    # policy actions on the evolving state). The replay of the captured env steps re-applies the
+    # last rollout's actions to a later state and is reported beside it (rocprof: profiles/)
+    avg_step_s = eager_step_s
     b_round = env_round_bytes(shape, tr.cfg.new_jobs_per_round, tr.free)
     achieved = b_round * args.envs / avg_step_s / 1e9
     result = {
@@ -246,6 +271,8 @@ def main():
             "traffic": None,
             "bytes_per_env_round": b_round,
             "avg_launch_us": avg_step_s * 1e6,
+            "launch_timing": "HIP events around each env-step launch of one eager training iteration",
+            "graph_replay_launch_us": graph_step_us,
         },
         "breakdown_ms_per_step": {
             "rollout": timings["rollout"] / args.steps * 1e3,

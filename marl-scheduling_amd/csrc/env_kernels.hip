@@ -130,6 +130,17 @@ __device__ void mt_twist_into_successor(uint32_t* mt_env, uint32_t sel, uint8_t*
 // successor (bit 1). An env whose stream crossed into the successor block in the previous round
 // gets the next successor at the start of the round: the whole wave twists it in LDS (the LDS is
 // not staged yet), once per ~40 rounds of an env.
+// successor := twist(current) for every group whose leader lane is set in the wave-uniform mask
+// `need` (sel = that leader's mt_sel); the whole wave twists each env in turn in `lds`
+template <int LPE>
+__device__ void mt_refill_groups(uint32_t* mt, int64_t e0, uint64_t need, uint32_t sel, uint8_t* lds, int lane) {
+    while (need) {
+        const int src = __ffsll((unsigned long long)need) - 1;
+        need &= need - 1;
+        mt_twist_into_successor(mt + (e0 + src / LPE) * 2 * kMtN, (uint32_t)__shfl((int)sel, src), lds, lane);
+    }
+}
+
 template <int LPE>
 __device__ void mt_refill_next(uint32_t* mt, const uint8_t* recs, const Params& P, int64_t slot, bool active,
                                uint8_t* lds, int lane) {
@@ -137,12 +148,7 @@ __device__ void mt_refill_next(uint32_t* mt, const uint8_t* recs, const Params& 
     const int64_t e0 = slot * (kWave / LPE);
     uint32_t sel = 0;
     if (active && gl == 0) sel = *reinterpret_cast<const uint32_t*>(recs + (e0 + lane / LPE) * P.rec_bytes + 12);
-    uint64_t need = __ballot(active && gl == 0 && !(sel & 2u));
-    while (need) {
-        const int src = __ffsll((unsigned long long)need) - 1;
-        need &= need - 1;
-        mt_twist_into_successor(mt + (e0 + src / LPE) * 2 * kMtN, (uint32_t)__shfl((int)sel, src), lds, lane);
-    }
+    mt_refill_groups<LPE>(mt, e0, __ballot(active && gl == 0 && !(sel & 2u)), sel, lds, lane);
 }
 
 // New (mt_sel, mti) after a round whose draws ended at stream index fin (relative to the current
@@ -204,7 +210,8 @@ struct MtStream {
     int p;            // next unconsumed stream position
     bool fell_back;   // cur was overwritten with twist(nxt)
     bool store;       // false for a padding group: never write (its draws are discarded)
-    uint32_t v;       // this lane's tempered word (position wb + gl)
+    uint32_t v;       // this lane's raw state word (position wb + gl); tempered where it is used, so
+                      // the load's wait lands at the first draw, not at the load
 
     __device__ void init(uint32_t* mt_env, uint32_t sel, int mti, bool active) {
         cur = mt_env + (sel & 1u) * kMtN;
@@ -231,7 +238,7 @@ struct MtStream {
             raw = nxt[g - kMtN];
         else if (g < 3 * kMtN)
             raw = mt_ld(cur + g - 2 * kMtN);
-        v = mt_temper(raw);
+        v = raw;
         wb = pos;
         wend = fell_back ? pos + LPE : min(pos + LPE, 2 * kMtN - mti0);
     }
@@ -243,11 +250,12 @@ struct MtStream {
         for (;;) {
             if (p >= wend) load(p, 1, L);
             const int pos = wb + L.gl;
-            const bool ok = pos >= p && pos < wend && ((v >> sh) < n);
+            const uint32_t tv = mt_temper(v);
+            const bool ok = pos >= p && pos < wend && ((tv >> sh) < n);
             const uint64_t m = L.ballot(ok);
             if (m) {
                 const int q = __ffsll((unsigned long long)m) - 1;
-                const uint32_t r = L.shfl(v, q) >> sh;
+                const uint32_t r = L.shfl(tv, q) >> sh;
                 p = wb + q + 1;
                 return r;
             }
@@ -661,29 +669,34 @@ __device__ void hardcoded_auctioneer(Rec& R, const Params& P, const M128* s_mc, 
     const int8_t* c_owner = R.core_owner();
     const int8_t* o_price = R.offer_price();
     const int8_t* s_rem = R.slot_rem();
-    // per core: the max ratio over the auctioneer's offers (the padded list's -1 entries and the
-    // own empty job bound it from below) and how many offers attain it
+    // per core, in one pass over the auctioneer's offers: the max ratio (the padded list's -1
+    // entries and the own empty job bound it from below), how many offers attain it and their
+    // positions in the padded list (a new maximum restarts the count)
     int mn = -1, md = 1, nt = 0;
+    M128 ties{0, 0};
     if (gl < C) {
         if (c_owner[gl] == 0) {
-            const M128 cand = mand(s_mc[gl], s_mr[0]);
-            for (MaskIter it(cand); it.more();) {
+            int k = 0;
+            for (MaskIter it(mand(s_mc[gl], s_mr[0])); it.more(); k++) {
                 const int i = it.next();
                 int num, den;
                 ratio_of(o_price[i], s_rem[i], num, den);
-                if (num * md > mn * den) {
-                    mn = num;
-                    md = den;
+                const int lhs = num * md, rhs = mn * den;
+                if (lhs >= rhs) {
+                    if (lhs > rhs) {
+                        mn = num;
+                        md = den;
+                        nt = 0;
+                        ties = M128{0, 0};
+                    }
+                    nt++;
+                    if (k < 64)
+                        ties.lo |= 1ull << k;
+                    else
+                        ties.hi |= 1ull << (k - 64);
                 }
             }
-            if (mn > -md) {  // max(ratios) > own ratio (-1, the auctioneer's empty job)
-                for (MaskIter it(cand); it.more();) {
-                    const int i = it.next();
-                    int num, den;
-                    ratio_of(o_price[i], s_rem[i], num, den);
-                    nt += (num * md == mn * den);
-                }
-            }
+            if (!(mn > -md)) nt = 0;  // max(ratios) must exceed the own ratio (-1, the empty job)
         }
         s_auct[gl] = (int16_t)O;
     }
@@ -697,18 +710,7 @@ __device__ void hardcoded_auctioneer(Rec& R, const Params& P, const M128* s_mc, 
         if (gl == c) my_pick = (int)pick;
     }
     // the pick-th maximal candidate's position in the padded list
-    if (gl < C && nt > 0) {
-        int k = 0, t = 0;
-        for (MaskIter it(mand(s_mc[gl], s_mr[0])); it.more(); k++) {
-            const int i = it.next();
-            int num, den;
-            ratio_of(o_price[i], s_rem[i], num, den);
-            if (num * md == mn * den) {
-                if (t == my_pick) s_auct[gl] = (int16_t)k;
-                t++;
-            }
-        }
-    }
+    if (gl < C && nt > 0) s_auct[gl] = (int16_t)kth_bit(ties, my_pick);
 }
 
 // ---------------------------------------------------------------------------
@@ -1183,8 +1185,9 @@ __device__ __forceinline__ void env_round(const Params& P, int64_t E, uint8_t* r
             const int avail = (rs.wend - rs.p) / 2;
             const int cnt = min(avail, total_pairs - done);
             const int off0 = rs.p - rs.wb;
-            const uint32_t wa = Lg.shfl(rs.v, (off0 + 2 * gl) & (LPE - 1));
-            const uint32_t wb2 = Lg.shfl(rs.v, (off0 + 2 * gl + 1) & (LPE - 1));
+            const uint32_t tv = mt_temper(rs.v);
+            const uint32_t wa = Lg.shfl(tv, (off0 + 2 * gl) & (LPE - 1));
+            const uint32_t wb2 = Lg.shfl(tv, (off0 + 2 * gl + 1) & (LPE - 1));
             if (gl < cnt) {
                 // random(): (a>>5 * 2^26 + b>>6) / 2^53 (Modules/_randommodule.c)
                 const double u = ((double)(wa >> 5) * 67108864.0 + (double)(wb2 >> 6)) * (1.0 / 9007199254740992.0);
