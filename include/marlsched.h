@@ -49,15 +49,22 @@ extern "C" {
 #define MS_EINVAL 22      /* bad argument / shape / config */
 #define MS_ENOMEM 12      /* device or host allocation failed */
 #define MS_EHIP 1001      /* a HIP runtime call failed */
-#define MS_EOVERFLOW 75   /* a per-env error flag is set (see MS_FLAG_*) */
+#define MS_EOVERFLOW 75   /* a fatal per-env error flag is set (see MS_FLAG_*) */
 
-/* per-env error flags (ORed over envs by ms_env_flags) */
+/* per-env error flags (ORed over envs by ms_env_flags; sticky in each env's record). All but
+ * SPAWN_EDGE are "fatal": the reference raises there, so once a completed round has set one, the
+ * next ms_env_step returns MS_EOVERFLOW without launching (the round that set it cannot report
+ * it: a step is asynchronous; the check reads a host-coherent word the kernel sets, no sync).
+ * SPAWN_EDGE marks a documented deviation (the build clamps where the reference raises
+ * UnboundLocalError) and does not stop stepping. ms_env_import clears them. */
 #define MS_FLAG_LIABILITY_OVERFLOW 0x01u /* a core's liability chain exceeded liability_cap */
 #define MS_FLAG_BAD_ACTION 0x02u         /* acceptor action outside [0, O] (reference asserts, world.py:389,404) */
 #define MS_FLAG_COLLECTION_FULL 0x04u    /* insertJob into a full collection (reference raises, world.py:133) */
 #define MS_FLAG_SPAWN_EDGE 0x08u         /* u >= accProbabilities[-1]; clamped to last kind (Agent.py:53-56) */
-#define MS_FLAG_RNG_WINDOW 0x10u         /* more random words requested in one step than the stream window holds */
+#define MS_FLAG_RNG_WINDOW 0x10u         /* a round drew past the 3 MT blocks it can reach (> 1248 words) */
 #define MS_FLAG_GUARD 0x20u              /* offer recipient != core owner at execution (world.py:266) */
+#define MS_FATAL_FLAGS (MS_FLAG_LIABILITY_OVERFLOW | MS_FLAG_BAD_ACTION | MS_FLAG_COLLECTION_FULL | \
+                        MS_FLAG_RNG_WINDOW | MS_FLAG_GUARD)
 
 /* RNG modes */
 #define MS_RNG_CPYTHON_MT19937 0 /* per-env MT19937 with CPython random.seed/random/_randbelow semantics */
@@ -194,14 +201,15 @@ int ms_config_shape(const ms_config* cfg, ms_shape* out);
 int ms_env_reset(ms_env* env, const ms_obs_out* obs, void* stream);
 
 /* One round for all E envs (SchedulingEnvironment.py:32-83). Rewards/events are
- * fully written (zeros where nothing happened). */
+ * fully written (zeros where nothing happened). Returns MS_EOVERFLOW (and launches nothing)
+ * once an earlier completed round has raised a fatal flag (MS_FATAL_FLAGS). */
 int ms_env_step(ms_env* env, const ms_actions* act, const ms_obs_out* obs,
                 const ms_reward_out* rew, const ms_event_out* ev, void* stream);
 
 /* Host round counter (all replicas advance together). */
 int64_t ms_env_round(const ms_env* env);
 
-/* Synchronises the stream and returns the OR of all env flags in *flags. */
+/* Synchronises the stream and returns the OR of all env flags in *flags (MS_OK either way). */
 int ms_env_flags(ms_env* env, uint32_t* flags, void* stream);
 
 /* CPython random._randbelow(n) drawn on env e's stream (n >= 1); synchronous. */

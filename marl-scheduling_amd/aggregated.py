@@ -130,6 +130,8 @@ class AggregatedTrainer:
         else:
             self.numbers[0].copy_(self.units["acceptor"].actions[t])
             self.numbers[1].copy_(self.units["offer"].actions[t])
+        # n_bad counts illegal action numbers over the iteration (reset at its start); the reference
+        # raises on one (Agent.py:651-652): iteration() checks the count after the rollout
         acc, off = self.env.decode_aggregated(self.numbers, self.fully, n_bad=self.n_bad)
         self.env.step(acc, off, obs=self.div_obs, rewards=self.rew)
         agent = self.rew["agent"].float()
@@ -149,8 +151,12 @@ class AggregatedTrainer:
         return losses
 
     def iteration(self):
+        self.n_bad.zero_()
         for t in range(self.T):
             self.round(t)
+        if int(self.n_bad.item()):
+            raise ValueError("Illegal Argument: %d action numbers outside the action space (Agent.py:651-652)"
+                             % int(self.n_bad.item()))
         self.iterations += 1
         return self.update()
 

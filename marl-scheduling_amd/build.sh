@@ -1,5 +1,8 @@
 #!/usr/bin/env bash
 # Builds libmarlsched.so (gfx950) in-tree: the HIP kernels + the C ABI.
+# An object is rebuilt when the sha256 of its source, the headers it includes, the compiler
+# version and the flags differs from the key stored beside it (not by mtime: a restored or
+# copied tree keeps no trustworthy timestamps). MS_CLEAN=1 rebuilds everything.
 set -euo pipefail
 HERE="$(cd "$(dirname "${BASH_SOURCE[0]}")" && pwd)"
 OUT="${HERE}/libmarlsched.so"
@@ -8,22 +11,30 @@ ARCH="${MS_OFFLOAD_ARCH:-gfx950}"
 FLAGS=(-O3 -std=c++17 -fPIC --offload-arch="${ARCH}" -Wall -Wno-unused-function
        -I"${HERE}/../include")
 OBJDIR="${HERE}/build"
+[[ "${MS_CLEAN:-0}" == 1 ]] && rm -rf "${OBJDIR}"
 mkdir -p "${OBJDIR}"
+HEADERS=("${HERE}/csrc/ms_layout.h" "${HERE}/csrc/ms_ppo.h" "${HERE}/csrc/ms_common.h" "${HERE}/../include/marlsched.h")
+CCVER="$("${HIPCC}" --version 2>/dev/null | head -3 | tr '\n' ' ')"
 objs=()
+pids=()
 for src in env_kernels.hip policy_kernels.hip ppo_kernels.hip agg_kernels.hip capi.cpp; do
   obj="${OBJDIR}/${src%.*}.o"
-  if [[ ! -f "${obj}" || "${HERE}/csrc/${src}" -nt "${obj}" || "${HERE}/csrc/ms_layout.h" -nt "${obj}" || "${HERE}/csrc/ms_ppo.h" -nt "${obj}" || "${HERE}/../include/marlsched.h" -nt "${obj}" ]]; then
-    # the env round reproduces Python's float64 arithmetic: no contraction there; the policy
-    # and PPO kernels follow torch's f32 (which fuses freely) within tolerance: fma allowed
-    contract=(-ffp-contract=off)
-    [[ "${src}" == policy_kernels.hip || "${src}" == ppo_kernels.hip ]] && contract=(-ffp-contract=fast)
-    if [[ "${src}" == *.cpp ]]; then
-      "${HIPCC}" "${FLAGS[@]}" "${contract[@]}" -x hip -c "${HERE}/csrc/${src}" -o "${obj}"
-    else
-      "${HIPCC}" "${FLAGS[@]}" "${contract[@]}" -c "${HERE}/csrc/${src}" -o "${obj}"
-    fi
+  # the env round reproduces Python's float64 arithmetic: no contraction there; the policy
+  # and PPO kernels follow torch's f32 (which fuses freely) within tolerance: fma allowed
+  contract=(-ffp-contract=off)
+  [[ "${src}" == policy_kernels.hip || "${src}" == ppo_kernels.hip ]] && contract=(-ffp-contract=fast)
+  key="$( { cat "${HERE}/csrc/${src}" "${HEADERS[@]}"; echo "${CCVER} ${FLAGS[*]} ${contract[*]}"; } | sha256sum | cut -d' ' -f1)"
+  if [[ ! -f "${obj}" || "$(cat "${obj}.key" 2>/dev/null)" != "${key}" ]]; then
+    rm -f "${obj}.key"
+    lang=()
+    [[ "${src}" == *.cpp ]] && lang=(-x hip)
+    # the objects compile in parallel; a key is written only after its object built
+    ( "${HIPCC}" "${FLAGS[@]}" "${contract[@]}" "${lang[@]}" -c "${HERE}/csrc/${src}" -o "${obj}" &&
+      echo "${key}" > "${obj}.key" ) &
+    pids+=($!)
   fi
   objs+=("${obj}")
 done
+for p in "${pids[@]}"; do wait "${p}"; done
 "${HIPCC}" -shared -fPIC --offload-arch="${ARCH}" -o "${OUT}" "${objs[@]}"
 echo "${OUT}"

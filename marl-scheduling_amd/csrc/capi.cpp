@@ -53,6 +53,8 @@ struct ms_env {
     uint32_t* mt;
     ms::Liab* liab;
     uint32_t* scratch_u32;  // device word for randbelow
+    uint32_t* err_host;     // sticky error word in host-coherent memory: set by a round that raised a
+                            // fatal per-env flag (ms_layout.h kFatalFlags), read by ms_env_step without a sync
     int64_t round;
 };
 
@@ -150,6 +152,7 @@ void ms_env_destroy(ms_env* env) {
     if (env->mt) (void)hipFree(env->mt);
     if (env->liab) (void)hipFree(env->liab);
     if (env->scratch_u32) (void)hipFree(env->scratch_u32);
+    if (env->err_host) (void)hipHostFree(env->err_host);
     if (cur != env->device) (void)hipSetDevice(cur);
     delete env;
 }
@@ -170,10 +173,12 @@ int ms_env_create(const ms_config* cfg, int64_t n_envs, uint64_t seed, ms_env** 
     size_t mt_b = (size_t)n_envs * 2 * ms::kMtN * sizeof(uint32_t);  // current block + successor
     size_t liab_b = (size_t)n_envs * env->P.C * env->P.cap * sizeof(ms::Liab);
     if (hipMalloc(&env->recs, rec_b) != hipSuccess || hipMalloc(&env->mt, mt_b) != hipSuccess ||
-        hipMalloc(&env->liab, liab_b) != hipSuccess || hipMalloc(&env->scratch_u32, 16) != hipSuccess) {
+        hipMalloc(&env->liab, liab_b) != hipSuccess || hipMalloc(&env->scratch_u32, 16) != hipSuccess ||
+        hipHostMalloc(&env->err_host, 16, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess) {
         ms_env_destroy(env);
         return fail(MS_ENOMEM, "device allocation of %zu bytes failed", rec_b + mt_b + liab_b);
     }
+    *env->err_host = 0;
     hipError_t e = ms::launch_env_init(env->P, n_envs, env->recs, env->mt, env->liab, seed, nullptr);
     if (e == hipSuccess) e = hipDeviceSynchronize();
     if (e != hipSuccess) {
@@ -206,7 +211,12 @@ int ms_env_step(ms_env* env, const ms_actions* act, const ms_obs_out* obs, const
     if (!env || !act) return fail(MS_EINVAL, "env/actions is NULL");
     if (!act->acceptor || !act->offer_core) return fail(MS_EINVAL, "acceptor and offer_core actions are required");
     if (env->cfg.free_prices && !act->offer_price) return fail(MS_EINVAL, "free prices need offer_price actions");
+    // a completed earlier round raised a flag on which the reference raises (assert / TypeError):
+    // stop stepping, as the reference would (which replica and flag: ms_env_flags)
+    if (__atomic_load_n(env->err_host, __ATOMIC_ACQUIRE))
+        return fail(MS_EOVERFLOW, "an earlier round raised a per-env error flag (see ms_env_flags)");
     ms::StepIO io{};
+    io.err_word = env->err_host;
     io.act_acc = act->acceptor;
     io.act_off = act->offer_core;
     io.act_price = env->cfg.free_prices ? act->offer_price : nullptr;
@@ -428,6 +438,9 @@ int ms_env_import(ms_env* env, const ms_state_host* in, void* stream) {
                         hipMemcpyHostToDevice));
     HIP_TRY(hipMemcpy(env->liab, lb.data(), lb.size() * sizeof(ms::Liab), hipMemcpyHostToDevice));
     env->round = in->round[0];
+    *env->err_host = 0;
+    for (int64_t e = 0; e < env->E; e++)
+        if (in->flags && (in->flags[e] & MS_FATAL_FLAGS)) *env->err_host = 1;
     return MS_OK;
 }
 

@@ -79,6 +79,7 @@ struct StepIO {
     int32_t* rew_agg_acc;
     ms_accept_rec* ev_acc;
     ms_term_rec* ev_term;
+    uint32_t* err_word;  // host-coherent sticky word: set to 1 by a round raising a fatal flag
 };
 
 // launch arguments of k_aggregate_obs (agg_kernels.hip): divided rows in, aggregated rows out

@@ -150,16 +150,14 @@ class PPOSchedulingEnv(SchedulingEnv):
         s = eng.env.shape
         dims = dict(acc=(s.acc_obs_dim, s.acc_actions), off=(s.off_obs_dim, s.off_actions),
                     price=(4, s.price_actions))
-        off_units = ["off", "price"] if self._free else ["off"]
         if self._arch == "divided":  # Agent.py:495-502, 589-596 (FreePriceOfferPPO: coreChooser, priceChooser)
-            order = [u for _ in range(N) for u in ["acc"] * C + off_units * L]
             groups = dict(acc=N * C, off=N * L, price=N * L)
         elif self._arch == "local":  # Agent.py:669-680: LocallySharedAcceptorPPO, then the offer net
-            order = [u for _ in range(N) for u in ["acc"] + off_units]
             groups = dict(acc=N, off=N, price=N)
         else:  # SchedulingEnvironment.py:269-275: sharedAcceptorNet, sharedOfferNet
-            order = ["acc"] + off_units
             groups = dict(acc=1, off=1, price=1)
+        off_units = ["off", "price"] if self._free else ["off"]
+        order = ppo.reference_init_order(self._arch, N, C, L, self._free)
         nets = reference_nets(order, {k: dims[k] for k in set(order)})
         if self._free:
             k_off = self.RAW_K_EPOCHS if self._arch == "divided" else self.OFFER_K_EPOCHS
@@ -450,6 +448,7 @@ class _AggregatedPPOEnv(SchedulingEnv):
             u.actions.append(a[:, 0])
             u.logprobs.append(lp[:, 0])
             self._numbers[i, 0].copy_(a[:, 0])
+        self._bad.zero_()  # per call: one illegal number raises for that call only
         acc, off = eng.env.decode_aggregated(self._numbers, self._fully, n_bad=self._bad)
         acc_h, off_h = acc[0].cpu().tolist(), off[0].cpu().tolist()
         if int(self._bad.item()):

@@ -265,13 +265,4 @@ class Units:
         return self.group.update_fused(self.states[:T], self.actions[:T], self.logprobs[:T], ret, sel, T, 1)
 
 
-def reference_nets(order, dims):
-    """Build ActorCritic parameter dicts in the reference's construction order: each PPO object makes
-    policy then policy_old (PPOmodules.py:99,107) on torch's CPU generator. order: list of unit-type
-    names in construction order; dims: name -> (in_dim, n_actions). Returns name -> [dict, ...]."""
-    nets = {k: [] for k in dims}
-    for name in order:
-        D, A = dims[name]
-        nets[name].append(ppo.reference_actor_critic_params(D, A))
-        ppo.reference_actor_critic_params(D, A)  # policy_old: same init stream, then overwritten
-    return nets
+reference_nets = ppo.reference_nets  # kept importable from here (SchedulingEnvironment.py)

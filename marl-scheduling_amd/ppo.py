@@ -40,6 +40,32 @@ def reference_actor_critic_params(in_dim: int, n_actions: int, hidden: int = HID
                 cw1=c1.weight, cb1=c1.bias, cw2=c2.weight, cb2=c2.bias, cw3=c3.weight, cb3=c3.bias)
 
 
+def reference_nets(order, dims):
+    """ActorCritic parameter dicts in the reference's construction order: each PPO object makes
+    policy then policy_old (PPOmodules.py:99,107) on torch's CPU generator. order: list of unit-type
+    names in construction order; dims: name -> (in_dim, n_actions). Returns name -> [dict, ...]."""
+    nets = {k: [] for k in dims}
+    for name in order:
+        D, A = dims[name]
+        nets[name].append(reference_actor_critic_params(D, A))
+        reference_actor_critic_params(D, A)  # policy_old: same init stream, then overwritten
+    return nets
+
+
+def reference_init_order(arch: str, N: int, C: int, L: int, free: bool):
+    """Unit types in the order the reference's agents construct their PPO objects:
+    divided — per agent C acceptors then L offer units (Agent.py:495-502; free prices: coreChooser,
+    priceChooser per slot, Agent.py:589-596, PPOmodules.py:277-306); locally shared — per agent the
+    shared acceptor then the shared offer unit(s) (Agent.py:669-680); globally shared — one acceptor
+    then the offer unit(s) (SchedulingEnvironment.py:269-275)."""
+    off_units = ["off", "price"] if free else ["off"]
+    if arch == "divided":
+        return [u for _ in range(N) for u in ["acc"] * C + off_units * L]
+    if arch == "local":
+        return [u for _ in range(N) for u in ["acc"] + off_units]
+    return ["acc"] + off_units
+
+
 ACTOR_KEYS = ("w1", "b1", "w2", "b2", "w3", "b3")
 CRITIC_KEYS = ("cw1", "cb1", "cw2", "cb2", "cw3", "cb3")
 

@@ -27,7 +27,7 @@ import torch
 
 from . import abi
 from .env import BatchedEnv
-from .ppo import PPOGroup, discounted_returns, offer_act_free, unit_returns
+from .ppo import PPOGroup, discounted_returns, offer_act_free, reference_init_order, reference_nets, unit_returns
 
 
 @dataclass
@@ -135,18 +135,23 @@ class Trainer:
             ga, go, k_acc, k_off = 1, 1, _k_epochs(hp.raw_k_epochs, N * C), _k_epochs(hp.raw_k_epochs, N * L)
         self.k_acc, self.k_off = k_acc, k_off
         allreduce = self._allreduce if world_size > 1 else None
-        torch.manual_seed(seed)  # same initial weights on every rank
+        # initial weights: the reference's construction order on torch's CPU generator, so a seeded
+        # Trainer starts from the weights the reference's agents would draw (same on every rank)
+        torch.manual_seed(seed)
+        dims = dict(acc=(s.acc_obs_dim, s.acc_actions), off=(s.off_obs_dim, s.off_actions), price=(4, s.price_actions))
+        order = reference_init_order(arch, N, C, L, self.free)
+        nets = reference_nets(order, {k: dims[k] for k in set(order)})
         dev = self.device
-        mk = lambda G, D, A, gamma, K: PPOGroup(G, D, A, hp.lr_actor, hp.lr_critic, gamma, hp.eps_clip, K, dev,
-                                                allreduce)
+        mk = lambda G, D, A, gamma, K, init: PPOGroup(G, D, A, hp.lr_actor, hp.lr_critic, gamma, hp.eps_clip, K, dev,
+                                                      allreduce, init_nets=init)
         self.acc = _Unit("acceptor", self.E, T, N * C, (N * C) // ga, s.acc_obs_dim, s.acc_obs_stride, s.acc_actions,
-                         mk(ga, s.acc_obs_dim, s.acc_actions, acc_gamma, k_acc), dev, torch.int32)
+                         mk(ga, s.acc_obs_dim, s.acc_actions, acc_gamma, k_acc, nets["acc"]), dev, torch.int32)
         self.off = _Unit("offer", self.E, T, N * L, (N * L) // go, s.off_obs_dim, s.off_obs_stride, s.off_actions,
-                         mk(go, s.off_obs_dim, s.off_actions, hp.offer_gamma, k_off), dev, torch.float32)
+                         mk(go, s.off_obs_dim, s.off_actions, hp.offer_gamma, k_off, nets["off"]), dev, torch.float32)
         self.price = None
         if self.free:
             self.price = _Unit("price", self.E, T, N * L, (N * L) // go, 4, 4, s.price_actions,
-                               mk(go, 4, s.price_actions, hp.offer_gamma, k_off), dev, torch.float32)
+                               mk(go, 4, s.price_actions, hp.offer_gamma, k_off, nets["price"]), dev, torch.float32)
         if world_size > 1:
             self._broadcast_params()
         # observation ring: slot t holds the state acted on at round t; slot T the next state
