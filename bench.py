@@ -132,6 +132,28 @@ def cpu_baseline(seconds_budget: float = 20.0):
                       "one locally-shared PPO update (K=1, 2 sub-units per agent and unit type)" % (E, rounds, cores)}
 
 
+ROLLOUT_STREAMS = 1   # replica parts on separate HIP streams in the rollout (Trainer rollout_streams)
+SAMPLE_EVERY = 8      # rounds between timed env launches
+
+
+def committed_traffic(alg_bytes_per_launch):
+    """HBM bytes per k_env_step launch from the committed PMC passes of this workload
+    (profiles/*/traffic.json, written by profiles/run_profile.sh: FETCH_SIZE doubled per the
+    gfx950 correction + WRITE_SIZE, per launch), newest profile first; None if absent."""
+    import glob
+    paths = sorted(glob.glob(os.path.join(REPO, "profiles", "*", "traffic.json")), key=os.path.getmtime, reverse=True)
+    for p in paths:
+        try:
+            with open(p) as f:
+                d = json.load(f)
+        except (OSError, ValueError):
+            continue
+        if d.get("kernel") == "k_env_step" and d.get("bytes"):
+            return {"bytes": d["bytes"], "source": os.path.relpath(p, REPO),
+                    "vs_algorithmic": d["bytes"] / alg_bytes_per_launch}
+    return None
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -141,6 +163,8 @@ def main():
     ap.add_argument("--update-step", type=int, default=200)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-graph", action="store_true", help="eager rollout instead of HIP-graph replay")
+    ap.add_argument("--rollout-streams", type=int, default=ROLLOUT_STREAMS,
+                    help="replica parts stepped on separate HIP streams (env of one part beside act of another)")
     args = ap.parse_args()
 
     import torch
@@ -158,11 +182,19 @@ def main():
     ms = importlib.import_module("marl-scheduling_amd")
     trainer_mod = importlib.import_module("marl-scheduling_amd.trainer")
     tr = trainer_mod.Trainer.from_named("cfg3", n_envs=args.envs, update_step=args.update_step, seed=0,
-                                        device=device, rank=rank, world_size=world)
+                                        device=device, rank=rank, world_size=world,
+                                        rollout_streams=args.rollout_streams)
     shape = tr.env.shape
 
+    # Per-launch duration of k_env_step inside the timed region: every SAMPLE_EVERY-th round's env
+    # launches record their span (first wave start -> last wave end, s_memrealtime at 100 MHz, two
+    # atomics per wave) into a device buffer that the captured rollout graph re-initialises on every
+    # replay; the last timed iteration's spans are read after the timed region. (HIP timing events
+    # cannot be captured into the graph on ROCm 7.2, neither torch's Event.record nor
+    # hipEventRecordWithFlags(hipEventRecordExternal): tools/graph_event_probe.py.)
+    tr.record_launch_spans(SAMPLE_EVERY)
+
     tr.use_graph = not args.no_graph
-    stream = torch.cuda.current_stream(device)
     for _ in range(max(args.warmup, 1 if tr.use_graph else 0)):
         tr.iteration()  # the first rollout also captures the HIP graph
     torch.cuda.synchronize(device)
@@ -179,48 +211,7 @@ def main():
     torch.cuda.synchronize(device)
     elapsed = time.perf_counter() - t0
     timings = dict(tr.timings)
-
-    # Per-launch duration of the env-step kernel with HIP events on its stream. Timing
-    # events cannot be captured into a HIP graph on ROCm 7.2 (hipErrorInvalidHandle,
-    # tools/graph_event_probe.py), so this is one eager rollout right after the timed
-    # region on the same buffers and evolving state; rocprofv3 cross-checks it (profiles/).
-    step_events = []
-    orig_step = tr.env.step
-
-    def timed_step(*a, **kw):
-        s_ev, e_ev = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        s_ev.record(stream)
-        out = orig_step(*a, **kw)
-        e_ev.record(stream)
-        step_events.append((s_ev, e_ev))
-        return out
-
-    tr.env.step = timed_step
-    graph_mode, tr.use_graph = tr.use_graph, False
-    tr.iteration()
-    torch.cuda.synchronize(device)
-    tr.env.step, tr.use_graph = orig_step, graph_mode
-    # The same launches as the rollout graph replays them: the UPDATE_STEP env steps of one
-    # rollout (same ring buffers) captured into a HIP graph of their own, events around its replay.
-    graph_step_us = None
-    if tr.use_graph:
-        E, N, C, L = args.envs, tr.N, tr.C, tr.L
-        g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
-            for t in range(tr.T):
-                obs = dict(acceptor=tr.acc_obs[t + 1], offer=tr.off_obs[t + 1])
-                rew = dict(offer=tr.off.rewards[t].view(E, N, L), acceptor=tr.acc.rewards[t].view(E, N, C),
-                           agent=tr.agent_reward, auctioneer=tr.auct_reward,
-                           price=tr.price.rewards[t].view(E, N, L) if tr.free else None)
-                orig_step(tr.acc.actions[t].view(E, N, C), tr.off.actions[t].view(E, N, L),
-                          tr.env_price.view(E, N, L) if tr.free else None, obs=obs, rewards=rew)
-        g.replay()  # warm
-        s_ev, e_ev = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        s_ev.record(stream)
-        g.replay()
-        e_ev.record(stream)
-        torch.cuda.synchronize(device)
-        graph_step_us = s_ev.elapsed_time(e_ev) * 1e3 / tr.T
+    launch_us = tr.launch_spans_us()
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=device)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -232,14 +223,11 @@ def main():
     rounds = args.update_step * args.steps
     agent_steps = world * args.envs * shape.n_agents * rounds
     value = agent_steps / elapsed
-    step_ms = [s.elapsed_time(e) for s, e in step_events]
-    eager_step_s = sum(step_ms) / len(step_ms) / 1e3
-    # the roofline figure: HIP events around each launch of one eager training iteration (fresh
-    # policy actions on the evolving state). The replay of the captured env steps re-applies the
-    # last rollout's actions to a later state and is reported beside it (rocprof: profiles/)
-    avg_step_s = eager_step_s
+    avg_step_s = sum(launch_us) / len(launch_us) / 1e6
+    part_envs = args.envs // args.rollout_streams
     b_round = env_round_bytes(shape, tr.cfg.new_jobs_per_round, tr.free)
-    achieved = b_round * args.envs / avg_step_s / 1e9
+    achieved = b_round * part_envs / avg_step_s / 1e9
+    traffic = committed_traffic(b_round * part_envs)
     result = {
         "metric": METRIC,
         "value": value,
@@ -268,17 +256,20 @@ def main():
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS,
-            "traffic": None,
+            "traffic": traffic["bytes"] if traffic else None,
+            "traffic_source": traffic["source"] if traffic else None,
             "bytes_per_env_round": b_round,
+            "envs_per_launch": part_envs,
             "avg_launch_us": avg_step_s * 1e6,
-            "launch_timing": "HIP events around each env-step launch of one eager training iteration",
-            "graph_replay_launch_us": graph_step_us,
+            "launches_timed": len(launch_us),
+            "launch_timing": "first-wave-start to last-wave-end span (s_memrealtime, 100 MHz) of every %d-th "
+                             "round's env launches in the last timed iteration (graph replay)" % SAMPLE_EVERY,
         },
         "breakdown_ms_per_step": {
             "rollout": timings["rollout"] / args.steps * 1e3,
             "update": timings["update"] / args.steps * 1e3,
-            "rollout_mode": "hip-graph replay" if not args.no_graph else "eager",
-            "env_step_kernels": sum(step_ms),
+            "rollout_mode": ("hip-graph replay" if not args.no_graph else "eager")
+                            + (", %d streams" % args.rollout_streams if args.rollout_streams > 1 else ""),
         },
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

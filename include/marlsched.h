@@ -163,6 +163,11 @@ typedef struct ms_term_rec {
 typedef struct ms_event_out {
     ms_accept_rec* accepted; /* [E][C] or NULL */
     ms_term_rec* terminated; /* [E][C] or NULL */
+    /* [E][2] device u64 or NULL: per wave of the launch, its start and end on the s_memrealtime
+     * clock (100 MHz), wave b at [b][0..1] (a wave steps 64 / lanes_per_env envs, so the first
+     * ceil(E * lanes_per_env / 64) entries are written); min start to max end is the launch's span.
+     * Measurement only: two plain stores per wave. */
+    uint64_t* launch_span;
 } ms_event_out;
 
 /* Host-side canonical state (export/import for parity tests and KAT scenarios).

@@ -123,7 +123,7 @@ class MsTermRec(ct.Structure):
 
 
 class MsEventOut(ct.Structure):
-    _fields_ = [("accepted", ct.c_void_p), ("terminated", ct.c_void_p)]
+    _fields_ = [("accepted", ct.c_void_p), ("terminated", ct.c_void_p), ("launch_span", ct.c_void_p)]
 
 
 class MsStateHost(ct.Structure):

@@ -6,6 +6,7 @@
 
 #include <stdarg.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <vector>
@@ -238,6 +239,7 @@ int ms_env_step(ms_env* env, const ms_actions* act, const ms_obs_out* obs, const
     if (ev) {
         io.ev_acc = ev->accepted;
         io.ev_term = ev->terminated;
+        io.span = reinterpret_cast<unsigned long long*>(ev->launch_span);
     }
     HIP_TRY(ms::launch_env_step(env->P, env->E, env->recs, env->mt, env->liab, io, (hipStream_t)stream));
     env->round += 1;

@@ -209,6 +209,7 @@ struct MtStream {
     int wb, wend;     // window covers stream positions [wb, wend)
     int p;            // next unconsumed stream position
     bool fell_back;   // cur was overwritten with twist(nxt)
+    bool overrun;     // a draw needed words past the third block (MS_FLAG_RNG_WINDOW)
     bool store;       // false for a padding group: never write (its draws are discarded)
     uint32_t v;       // this lane's raw state word (position wb + gl); tempered where it is used, so
                       // the load's wait lands at the first draw, not at the load
@@ -219,9 +220,12 @@ struct MtStream {
         mti0 = mti;
         wb = wend = p = 0;
         fell_back = false;
+        overrun = false;
         store = active;
         v = 0;
     }
+
+    __device__ __forceinline__ uint32_t word() const { return mt_temper(v); }  // the window's tempered word
 
     // Window at stream position pos. need = words the caller is about to consume; need == 0
     // only peeks (never falls back; the window may be empty).
@@ -230,15 +234,16 @@ struct MtStream {
             if (store) mt_twist_from<LPE>(cur, nxt, L.gl);
             fell_back = true;
         }
+        if (need > 0 && mti0 + pos + need > 3 * kMtN) overrun = true;
         const int g = mti0 + pos + L.gl;
-        uint32_t raw = 0;
+        uint32_t w = 0;
         if (g < kMtN)
-            raw = cur[g];
+            w = cur[g];
         else if (g < 2 * kMtN)
-            raw = nxt[g - kMtN];
+            w = nxt[g - kMtN];
         else if (g < 3 * kMtN)
-            raw = mt_ld(cur + g - 2 * kMtN);
-        v = raw;
+            w = mt_ld(cur + g - 2 * kMtN);
+        v = w;
         wb = pos;
         wend = fell_back ? pos + LPE : min(pos + LPE, 2 * kMtN - mti0);
     }
@@ -250,7 +255,7 @@ struct MtStream {
         for (;;) {
             if (p >= wend) load(p, 1, L);
             const int pos = wb + L.gl;
-            const uint32_t tv = mt_temper(v);
+            const uint32_t tv = word();
             const bool ok = pos >= p && pos < wend && ((tv >> sh) < n);
             const uint64_t m = L.ballot(ok);
             if (m) {
@@ -847,11 +852,9 @@ __device__ __forceinline__ void env_round(const Params& P, int64_t E, uint8_t* r
     int8_t* spawn_kind = reinterpret_cast<int8_t*>(smem + P.s_spawn_kind);
     uint8_t* scratch = smem + P.s_scratch;
 
-    // ---- successor MT blocks of the envs that crossed into theirs last round (whole wave, LDS
-    //      not staged yet), then stage state and actions in LDS
-    mt_refill_next<LPE>(mt, recs, P, slot, active, smem_all, lane);
+    // ---- stage state and actions in LDS; the successor MT blocks of the envs that crossed into
+    //      theirs last round are made while the staged words wait in registers (whole wave in LDS)
     __shared__ int32_t s_kt[48];
-    load_kind_tables(P, s_kt, lane);
     {
         // the record and the dword-aligned action arrays: one batch of loads, then the LDS stores
         const uint32_t* src_rec = reinterpret_cast<const uint32_t*>(recs + e * (int64_t)P.rec_bytes);
@@ -873,6 +876,12 @@ __device__ __forceinline__ void env_round(const Params& P, int64_t E, uint8_t* r
         br.load(src_rec, rec_dw, gl);
 #pragma unroll
         for (int i = 0; i < 4; i++) ba[i].load(reinterpret_cast<const uint32_t*>(a_src[i]), a_dw[i], gl);
+        // record dword 3 (mt_sel) is group lane 3's first staged word: the refill test costs no load
+        // round trip of its own (the LDS is not written yet, so the twist may use all of it)
+        const uint32_t sel = Lg.shfl(br.v[0], 3);
+        const uint64_t need = __ballot(active && gl == 0 && !(sel & 2u));
+        if (need) mt_refill_groups<LPE>(mt, slot * (kWave / LPE), need, sel, smem_all, lane);
+        load_kind_tables(P, s_kt, lane);
         br.store(reinterpret_cast<uint32_t*>(rec), rec_dw, gl);
 #pragma unroll
         for (int i = 0; i < 4; i++) ba[i].store(reinterpret_cast<uint32_t*>(a_dst[i]), a_dw[i], gl);
@@ -952,6 +961,9 @@ __device__ __forceinline__ void env_round(const Params& P, int64_t E, uint8_t* r
     } else {
         for (int c = gl; c < C; c += LPE) s_auct[c] = a_auct[c];
     }
+    // the spawn's words, peeked now at the stream position the tie-breaks left: the load's latency
+    // hides behind the executions and the tick (a window short of the spawn reloads there)
+    if (rs.wend - rs.p < 2 * P.new_jobs * N) rs.load(rs.p, 0, Lg);
     wave_sync();
     MS_MARK(3);
 
@@ -993,6 +1005,7 @@ __device__ __forceinline__ void env_round(const Params& P, int64_t E, uint8_t* r
             const int i = s_exec[c];
             const int offerer = i / L + 1, slot = i - (offerer - 1) * L;
             const int recip = o_recip[i];
+            if (recip != c_owner[c]) s_flags |= MS_FLAG_GUARD;  // executeAnOffer's ownership check (world.py:266)
             const int nk = s_kind[i], nrem = s_rem[i], nbirth = s_birth[i];
             const int price = o_price[i];
             // removeAndReturnEntry (world.py:135-141); newJob.wait = False (world.py:276)
@@ -1141,6 +1154,8 @@ __device__ __forceinline__ void env_round(const Params& P, int64_t E, uint8_t* r
     wave_sync();
     MS_MARK(6);
 
+    // ---- ownership is final for the round: stream every acceptor chunk with no owner-row dword
+    //      now (the stores drain while the offers, spawn, outputs and owner rows are computed)
     // ---- offers from offer actions (createFixPriceOfferObjectsFromActions world.py:406-443,
     //      createFreePriceOfferObjectsFromActions world.py:445-478); IDs = slot order
     for (int i = gl; i < NL; i += LPE) {
@@ -1185,7 +1200,7 @@ __device__ __forceinline__ void env_round(const Params& P, int64_t E, uint8_t* r
             const int avail = (rs.wend - rs.p) / 2;
             const int cnt = min(avail, total_pairs - done);
             const int off0 = rs.p - rs.wb;
-            const uint32_t tv = mt_temper(rs.v);
+            const uint32_t tv = rs.word();
             const uint32_t wa = Lg.shfl(tv, (off0 + 2 * gl) & (LPE - 1));
             const uint32_t wb2 = Lg.shfl(tv, (off0 + 2 * gl + 1) & (LPE - 1));
             if (gl < cnt) {
@@ -1229,17 +1244,21 @@ __device__ __forceinline__ void env_round(const Params& P, int64_t E, uint8_t* r
     wave_sync();
     MS_MARK(8);
     if (gl == 0) {
+        if (rs.overrun) s_flags |= MS_FLAG_RNG_WINDOW;
         R.round() = round + 1;
         mt_commit(rs.end_index(), &R.mti(), &R.mt_sel());
         R.flags() |= s_flags;
+        // the host sees a fatal flag at its next ms_env_step without synchronising (plain store to
+        // host-coherent memory; any nonzero value will do, so racing groups need no atomic)
+        if ((s_flags & MS_FATAL_FLAGS) && io.err_word && active) *io.err_word = 1u;
     }
     wave_sync();
     MS_MARK(9);
 
     // ---- outputs: state record, rewards, observations of the new offer set
     if (active) {
-        copy_dwords<LPE>(reinterpret_cast<uint32_t*>(recs + e * (int64_t)P.rec_bytes), reinterpret_cast<uint32_t*>(rec),
-                         P.rec_bytes / 4, gl);
+        copy_out<LPE>(WtOut(recs, E * P.rec_bytes), e * P.rec_bytes, reinterpret_cast<uint32_t*>(recs + e * (int64_t)P.rec_bytes),
+                      reinterpret_cast<const uint32_t*>(rec), P.rec_bytes / 4, gl);
         // rewards: write-through (consumed by the update, rounds later)
         auto rew = [&](void* base, int per_env, const void* src) {
             if (!base) return;
@@ -1284,12 +1303,16 @@ __device__ __forceinline__ void env_round(const Params& P, int64_t E, uint8_t* r
 // per wave would let one slot's observation stores drain under the next slot's compute, but the
 // compiler then keeps the whole round's state live across iterations: 3x the VGPRs.)
 template <int LPE>
-__global__ void __launch_bounds__(64) k_env_step(Params P, int64_t E, uint8_t* recs, uint32_t* mt, Liab* liab,
+__global__ void __launch_bounds__(64, 4) k_env_step(Params P, int64_t E, uint8_t* recs, uint32_t* mt, Liab* liab,
                                                  StepIO io) {
 #ifdef MS_PHASE_TIMING
     const uint64_t rt_start = __builtin_amdgcn_s_memrealtime();
 #endif
+    // per-wave start / end for the bench's launch span (optional; plain stores, no shared address,
+    // nothing held across the round: the kernel sits at 4 waves per SIMD with no register to spare)
+    if (io.span && threadIdx.x == 0) io.span[2 * blockIdx.x] = __builtin_amdgcn_s_memrealtime();
     env_round<LPE>(P, E, recs, mt, liab, io, blockIdx.x);
+    if (io.span && threadIdx.x == 0) io.span[2 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime();
 #ifdef MS_PHASE_TIMING
     if (threadIdx.x == 0) {
         g_wave_span[blockIdx.x % kProbeSlots][0] = rt_start;

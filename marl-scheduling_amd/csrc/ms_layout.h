@@ -80,6 +80,7 @@ struct StepIO {
     ms_accept_rec* ev_acc;
     ms_term_rec* ev_term;
     uint32_t* err_word;  // host-coherent sticky word: set to 1 by a round raising a fatal flag
+    unsigned long long* span;  // [waves][2] or NULL: each wave's start / end (s_memrealtime)
 };
 
 // launch arguments of k_aggregate_obs (agg_kernels.hip): divided rows in, aggregated rows out

@@ -147,7 +147,8 @@ class BatchedEnv:
         r = abi.MsRewardOut(ptr(rewards.get("offer")), ptr(rewards.get("price")), ptr(rewards.get("acceptor")),
                             ptr(rewards.get("auctioneer")), ptr(rewards.get("agent")),
                             ptr(rewards.get("aggregated_offer")), ptr(rewards.get("aggregated_acceptor")))
-        ev = abi.MsEventOut(ptr(events.get("accepted")), ptr(events.get("terminated"))) if events else None
+        ev = abi.MsEventOut(ptr(events.get("accepted")), ptr(events.get("terminated")),
+                            ptr(events.get("launch_span"))) if events else None
         check(lib.ms_env_step(self._h, ct.byref(a), ct.byref(o), ct.byref(r), ct.byref(ev) if ev else None,
                               stream_ptr(stream)))
         return obs, rewards, events

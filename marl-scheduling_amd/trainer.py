@@ -103,10 +103,33 @@ def broadcast_params(groups, group=None):
         grp.sync_old()
 
 
+class EnvParts:
+    """The rank's E replicas as P contiguous parts [e0, e1), each its own BatchedEnv (replica e keeps
+    random.seed(base + e) whatever the split). One part per rollout stream (Trainer.round)."""
+
+    def __init__(self, cfg, E: int, base_seed: int, n_parts: int, device):
+        assert E % n_parts == 0
+        w = E // n_parts
+        self.parts = [(BatchedEnv(cfg, w, seed=base_seed + k * w, device=device), k * w, (k + 1) * w)
+                      for k in range(n_parts)]
+        self.E = E
+        self.shape = self.parts[0][0].shape
+
+    @property
+    def round(self) -> int:
+        return self.parts[0][0].round
+
+    def flags(self) -> int:
+        f = 0
+        for env, _, _ in self.parts:
+            f |= env.flags()
+        return f
+
+
 class Trainer:
     def __init__(self, cfg: abi.MsConfig, n_envs: int, arch: str = "local", hyper: Hyper | None = None, seed: int = 0,
                  device=None, rank: int = 0, world_size: int = 1, process_group=None, fused: bool = True,
-                 use_graph: bool = True, common_rows: bool = True):
+                 use_graph: bool = True, common_rows: bool = True, rollout_streams: int = 1):
         assert arch in ("divided", "local", "global")
         self.fused = fused  # fused HIP gradient (ms_ppo_grad) vs torch autograd
         self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
@@ -115,7 +138,12 @@ class Trainer:
         self.hp = hyper or Hyper()
         self.rank, self.world_size, self.pg = rank, world_size, process_group
         self.seed = seed
-        self.env = BatchedEnv(cfg, self.E, seed=env_seed(seed, rank, self.E), device=self.device)
+        # rollout_streams > 1: the replicas split into that many parts, each stepped on its own HIP
+        # stream, so one part's env round (latency-bound) runs beside another part's act kernels
+        # (VALU-bound); the parts share the rollout rings and the nets
+        assert rollout_streams >= 1 and self.E % rollout_streams == 0
+        self.env = EnvParts(cfg, self.E, env_seed(seed, rank, self.E), rollout_streams, self.device)
+        self.streams = [None] + [torch.cuda.Stream(device=self.device) for _ in range(rollout_streams - 1)]
         s = self.env.shape
         N, C, L = s.n_agents, s.n_cores, s.collection_length
         self.N, self.C, self.L = N, C, L
@@ -173,7 +201,10 @@ class Trainer:
         self.graph = None
         self.rounds_done = 0
         self.iterations = 0
-        self.env.reset(dict(acceptor=self.acc_obs[0], offer=self.off_obs[0]))
+        for env, e0, e1 in self.env.parts:
+            env.reset(dict(acceptor=self.acc_obs[0][e0:e1], offer=self.off_obs[0][e0:e1]))
+        self.span_every = 0  # > 0: every span_every-th round's env launches record their span (bench)
+        self.spans = None
         self.timings = dict(rollout=0.0, update=0.0)
 
     @classmethod
@@ -200,35 +231,71 @@ class Trainer:
     # ---- rollout
     def round(self, t: int):
         """getActionForAllAgents + env.step + saveRewards for round t of the iteration
-        (trainPPO.py:160-167)."""
-        E, N, C, L = self.E, self.N, self.C, self.L
-        seed = self.seed * 7919 + self.rank
-        base = 8 * t  # Philox offsets: static per round + the device counter (advanced per rollout)
+        (trainPPO.py:160-167), part by part: part k's launches go to stream k."""
+        for k in range(len(self.env.parts)):
+            self._round_part(t, k)
+
+    def _round_part(self, t: int, k: int):
+        env, e0, e1 = self.env.parts[k]
+        st = self.streams[k]
+        E, N, C, L = e1 - e0, self.N, self.C, self.L
+        # Philox key per rank and part (part 0 keeps the unsplit key); offsets: static per round +
+        # the device counter (advanced per rollout)
+        seed = self.seed * 7919 + self.rank + k * 0x9E3779B1
+        base = 8 * t
+        sl = lambda x: x[e0:e1]
         # per agent: offer units then acceptors (Agent.py:504-515); separate streams per unit type
         if self.free:
             # FreePriceOfferPPO.selectAction (PPOmodules.py:312-332): core chooser, then the price
             # chooser on [obs[2a:2a+2], obs[-2:]] or the dummy [-5,-5,-5,-5] when a == 0, one launch
-            out = dict(core_action=self.off.actions[t], core_logprob=self.off.logprobs[t],
-                       price_state=self.price_obs[t], price_action=self.price.actions[t],
-                       price_logprob=self.price.logprobs[t], env_price=self.env_price)
-            offer_act_free(self.off.group.policy_old, self.price.group.policy_old, self.off_obs[t], C, seed, base + 1,
-                           out, offset_dev=self.rng_ctr)
+            out = dict(core_action=sl(self.off.actions[t]), core_logprob=sl(self.off.logprobs[t]),
+                       price_state=sl(self.price_obs[t]), price_action=sl(self.price.actions[t]),
+                       price_logprob=sl(self.price.logprobs[t]), env_price=sl(self.env_price))
+            offer_act_free(self.off.group.policy_old, self.price.group.policy_old, sl(self.off_obs[t]), C, seed,
+                           base + 1, out, offset_dev=self.rng_ctr, stream=st)
         else:
-            self.off.group.policy_old.act(self.off_obs[t], N * L, seed, base + 1, action=self.off.actions[t],
-                                          logprob=self.off.logprobs[t], offset_dev=self.rng_ctr)
-        self.acc.group.policy_old.act(self.acc_obs[t], N * C, seed, base + 3, action=self.acc.actions[t],
-                                      logprob=self.acc.logprobs[t], offset_dev=self.rng_ctr,
-                                      common_row=self.acc_common if self.common_rows else None)
-        obs = dict(acceptor=self.acc_obs[t + 1], offer=self.off_obs[t + 1])
-        rew = dict(offer=self.off.rewards[t].view(E, N, L), acceptor=self.acc.rewards[t].view(E, N, C),
-                   agent=self.agent_reward, auctioneer=self.auct_reward,
-                   price=self.price.rewards[t].view(E, N, L) if self.free else None)
-        self.env.step(self.acc.actions[t].view(E, N, C), self.off.actions[t].view(E, N, L),
-                      self.env_price.view(E, N, L) if self.free else None, obs=obs, rewards=rew)
+            self.off.group.policy_old.act(sl(self.off_obs[t]), N * L, seed, base + 1, action=sl(self.off.actions[t]),
+                                          logprob=sl(self.off.logprobs[t]), offset_dev=self.rng_ctr, stream=st)
+        self.acc.group.policy_old.act(sl(self.acc_obs[t]), N * C, seed, base + 3, action=sl(self.acc.actions[t]),
+                                      logprob=sl(self.acc.logprobs[t]), offset_dev=self.rng_ctr,
+                                      common_row=self.acc_common if self.common_rows else None, stream=st)
+        obs = dict(acceptor=sl(self.acc_obs[t + 1]), offer=sl(self.off_obs[t + 1]))
+        rew = dict(offer=sl(self.off.rewards[t]).view(E, N, L), acceptor=sl(self.acc.rewards[t]).view(E, N, C),
+                   agent=sl(self.agent_reward), auctioneer=sl(self.auct_reward),
+                   price=sl(self.price.rewards[t]).view(E, N, L) if self.free else None)
+        ev = dict(launch_span=self.spans[t, k]) if self.span_every and t % self.span_every == 0 else None
+        env.step(sl(self.acc.actions[t]).view(E, N, C), sl(self.off.actions[t]).view(E, N, L),
+                 sl(self.env_price).view(E, N, L) if self.free else None, obs=obs, rewards=rew, events=ev, stream=st)
+
+    def record_launch_spans(self, every: int):
+        """Every `every`-th round's env launches record their span (first wave start, last wave end
+        on the 100 MHz s_memrealtime clock) into self.spans [T][parts][2]; read with launch_spans_us().
+        Set before the first rollout (the HIP graph captures it)."""
+        self.span_every = int(every)
+        w = self.env.parts[0][2] - self.env.parts[0][1]
+        self.spans = torch.zeros((self.T, len(self.env.parts), w, 2), dtype=torch.int64, device=self.device)
+
+    def launch_spans_us(self):
+        """Durations (us) of the recorded env launches of the last rollout."""
+        sp = self.spans[:: self.span_every].cpu().numpy()  # [rounds][parts][waves][2]
+        out = []
+        for r in range(sp.shape[0]):
+            for k in range(sp.shape[1]):
+                w = sp[r, k]
+                w = w[w[:, 1] > 0]  # the waves of the launch
+                out.append(float(w[:, 1].max() - w[:, 0].min()) / 100.0)
+        return out
 
     def _rollout_body(self):
+        cur = torch.cuda.current_stream(self.device)
+        if self.span_every:
+            self.spans[:: self.span_every].zero_()
+        for s in self.streams[1:]:  # fork: the side streams start after everything queued so far
+            s.wait_stream(cur)
         for t in range(self.T):
             self.round(t)
+        for s in self.streams[1:]:  # join
+            cur.wait_stream(s)
         self.rng_ctr.add_(8 * self.T)
 
     def rollout(self):

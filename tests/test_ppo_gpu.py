@@ -330,6 +330,40 @@ def test_trainer_graph_replay_matches_eager(ms):
     assert trs[0].env.round == trs[1].env.round == 48
 
 
+def test_trainer_two_stream_rollout(ms):
+    """rollout_streams=2: the replicas split in two parts stepped on two HIP streams. Part 0 keeps
+    the unsplit Philox key, so its half of the rollout is bit-identical to the unsplit trainer's;
+    part 1 draws from its own key. The split graph replay equals the split eager rollout."""
+    tr_mod = importlib.import_module("marl-scheduling_amd.trainer")
+    E, T = 64, 12
+    mk = lambda streams, g: tr_mod.Trainer.from_named("cfg3", n_envs=E, update_step=T, seed=4, device="cuda:0",
+                                                      use_graph=g, rollout_streams=streams)
+    one, two_g, two_e = mk(1, False), mk(2, True), mk(2, False)
+    one.rollout()
+    two_g.rollout()
+    two_e.rollout()
+    torch.cuda.synchronize()
+    h = E // 2
+    assert torch.equal(one.acc_obs[:, :h], two_e.acc_obs[:, :h])
+    assert torch.equal(one.off_obs[:, :h], two_e.off_obs[:, :h])
+    assert torch.equal(one.acc.actions[:, :h], two_e.acc.actions[:, :h])
+    assert torch.equal(one.acc.rewards[:, :h], two_e.acc.rewards[:, :h])
+    assert not torch.equal(one.acc.actions[:, h:], two_e.acc.actions[:, h:])  # part 1: its own key
+    for _ in range(2):  # graph capture happened in the first rollout; replays from here
+        two_g.rollout()
+        two_e.rollout()
+    for name in ("acc_obs", "off_obs", "price_obs"):
+        assert torch.equal(getattr(two_g, name), getattr(two_e, name)), name
+    for u in ("acc", "off", "price"):
+        assert torch.equal(getattr(two_g, u).actions, getattr(two_e, u).actions), u
+        assert torch.equal(getattr(two_g, u).rewards, getattr(two_e, u).rewards), u
+    assert two_g.env.round == two_e.env.round == 3 * T
+    assert two_g.flags() == 0 and two_e.flags() == 0
+    losses = [t.update() for t in (two_g, two_e)]
+    for k in losses[0]:
+        assert torch.equal(losses[0][k], losses[1][k]), k
+
+
 def test_hip_adam_matches_torch_adam(ms):
     """ms_adam_step (HipAdam) against torch.optim.Adam with the actor / critic param groups of
     PPO.__init__ (PPOmodules.py:100-105), over several steps with changing gradients."""

@@ -13,9 +13,10 @@ import torch
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 abi = importlib.import_module("marl-scheduling_amd.abi")
-NAMES = {1: "stage", 2: "MT peek + masks + liab prefetch", 3: "auctioneer", 4: "exec select + rank",
-         5: "leader executions", 6: "tick + settlement", 7: "offers", 8: "spawn", 9: "record round/mti",
-         10: "write record + rewards", 11: "rebuild masks", 12: "emit observations", 13: "successor MT twist"}
+NAMES = {1: "stage (+ successor MT twist)", 2: "MT peek + masks + liab prefetch", 3: "auctioneer + spawn peek",
+         4: "exec select + rank", 5: "executions", 6: "tick + settlement", 7: "offers", 8: "spawn",
+         9: "record round/mti", 10: "write record + rewards", 11: "rebuild masks", 12: "emit observations"}
+ORDER = list(range(1, 13))
 
 
 def main(E=16384, steps=20, min_lpe=None):
@@ -71,10 +72,10 @@ def main(E=16384, steps=20, min_lpe=None):
         lpe *= 2
     waves = (E + 64 // lpe - 1) // (64 // lpe)
     n_blocks = waves
-    tot = sum(buf[k] for k in range(1, 14))
+    tot = sum(buf[k] for k in ORDER)
     print("k_env_step (probe build, %d lanes/env) %.1f us/step; per wave: %.0f cycles" % (lpe, ev[0].elapsed_time(ev[1]) * 1e3 / steps,
                                                                         tot / waves / steps))
-    for k in range(1, 14):
+    for k in ORDER:
         print("  %2d %-34s %8.0f cycles/wave  %5.1f%%" % (k, NAMES[k], buf[k] / waves / steps, 100.0 * buf[k] / tot))
     # entry / exit times of every wave of the last launch (s_memrealtime, 100 MHz)
     import numpy as np
