@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define MS_ABI_VERSION 3
+#define MS_ABI_VERSION 4
 
 #define MS_MAX_KINDS 16
 #define MS_MAX_AGENTS 64
@@ -160,6 +160,30 @@ typedef struct ms_term_rec {
     int32_t dwell;    /* Verweilzeit = round - birthDate (world.py:350-357) */
 } ms_term_rec;
 
+/* Per-replica episode accumulators of the training driver's metrics (trainPPO.py:172-226,
+ * trainDQN.py:187-259): every ms_env_step that is given them adds its round into the slot of the
+ * round's episode. The caller reads a slot once its episode is done (world.round % episodeLength
+ * == 0, SchedulingEnvironment.py:64-67) and zeroes it before the slot is reused. Updated with
+ * no-return device atomics, one env per group of lanes, so the order per replica is fixed. */
+typedef struct ms_env_metrics {
+    int64_t acceptor_reward;     /* sum over rounds and units of acceptorNetRewards */
+    int64_t offer_reward;        /* sum of offerNetRewards / coreChooserRewards (prio1, integers) */
+    double price_reward;         /* sum of priceChooserRewards (free prices) */
+    int64_t auctioneer_reward;   /* sum over rounds of sum(auctioneerReward) (trainPPO.py:183) */
+    int64_t termination_revenue; /* env.terminationRevenues (Reward.py:193; fixed prices) */
+    double quality_sum;          /* sum over rounds with an acception of the round's mean
+                                    acception quality (SchedulingEnvironment.py:174-192) */
+    int32_t quality_rounds;      /* rounds counted in quality_sum */
+    int32_t acception_amount;    /* sum over rounds of the number of non-auctioneer acceptions */
+    int32_t rounds;              /* rounds added */
+    int32_t pad;
+    int32_t price_sum[MS_MAX_KINDS];   /* offeredReward of accepted offers, by jobKind (trainPPO.py:172-174) */
+    int32_t price_count[MS_MAX_KINDS];
+    int32_t dwell_sum[MS_MAX_KINDS];   /* round - birthDate - 1 of terminated jobs, by kind (world.py:350-357) */
+    int32_t dwell_count[MS_MAX_KINDS];
+    int64_t agent_reward[MS_MAX_AGENTS]; /* sum of agentReward */
+} ms_env_metrics;
+
 typedef struct ms_event_out {
     ms_accept_rec* accepted; /* [E][C] or NULL */
     ms_term_rec* terminated; /* [E][C] or NULL */
@@ -168,6 +192,10 @@ typedef struct ms_event_out {
      * ceil(E * lanes_per_env / 64) entries are written); min start to max end is the launch's span.
      * Measurement only: two plain stores per wave. */
     uint64_t* launch_span;
+    /* [metrics_slots][E] or NULL: round r (world.round before the step) adds into slot
+     * (r / episode_length) % metrics_slots */
+    ms_env_metrics* metrics;
+    int32_t metrics_slots;
 } ms_event_out;
 
 /* Host-side canonical state (export/import for parity tests and KAT scenarios).

@@ -71,7 +71,7 @@ def _load():
         fn = getattr(L, name)
         fn.restype = res
         fn.argtypes = args
-    if L.ms_abi_version() != 3:
+    if L.ms_abi_version() != 4:
         raise ImportError("libmarlsched.so ABI version mismatch")
     return L
 

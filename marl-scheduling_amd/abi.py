@@ -123,7 +123,50 @@ class MsTermRec(ct.Structure):
 
 
 class MsEventOut(ct.Structure):
-    _fields_ = [("accepted", ct.c_void_p), ("terminated", ct.c_void_p), ("launch_span", ct.c_void_p)]
+    _fields_ = [("accepted", ct.c_void_p), ("terminated", ct.c_void_p), ("launch_span", ct.c_void_p),
+                ("metrics", ct.c_void_p), ("metrics_slots", ct.c_int32)]
+
+
+class MsEnvMetrics(ct.Structure):
+    """ms_env_metrics: one replica's episode accumulators (include/marlsched.h)."""
+    _fields_ = [
+        ("acceptor_reward", ct.c_int64),
+        ("offer_reward", ct.c_int64),
+        ("price_reward", ct.c_double),
+        ("auctioneer_reward", ct.c_int64),
+        ("termination_revenue", ct.c_int64),
+        ("quality_sum", ct.c_double),
+        ("quality_rounds", ct.c_int32),
+        ("acception_amount", ct.c_int32),
+        ("rounds", ct.c_int32),
+        ("pad", ct.c_int32),
+        ("price_sum", ct.c_int32 * MAX_KINDS),
+        ("price_count", ct.c_int32 * MAX_KINDS),
+        ("dwell_sum", ct.c_int32 * MAX_KINDS),
+        ("dwell_count", ct.c_int32 * MAX_KINDS),
+        ("agent_reward", ct.c_int64 * MAX_AGENTS),
+    ]
+
+
+METRICS_BYTES = ct.sizeof(MsEnvMetrics)
+
+
+# numpy view of an [.., E] array of ms_env_metrics (field offsets from the ctypes struct)
+def metrics_dtype():
+    import numpy as np
+    f = MsEnvMetrics
+    names, formats, offsets = [], [], []
+    for name, ctype in f._fields_:
+        names.append(name)
+        off = getattr(f, name).offset
+        offsets.append(off)
+        if name in ("price_sum", "price_count", "dwell_sum", "dwell_count"):
+            formats.append((np.int32, MAX_KINDS))
+        elif name == "agent_reward":
+            formats.append((np.int64, MAX_AGENTS))
+        else:
+            formats.append({ct.c_int64: np.int64, ct.c_double: np.float64, ct.c_int32: np.int32}[ctype])
+    return np.dtype(dict(names=names, formats=formats, offsets=offsets, itemsize=ct.sizeof(f)))
 
 
 class MsStateHost(ct.Structure):

@@ -240,6 +240,9 @@ int ms_env_step(ms_env* env, const ms_actions* act, const ms_obs_out* obs, const
         io.ev_acc = ev->accepted;
         io.ev_term = ev->terminated;
         io.span = reinterpret_cast<unsigned long long*>(ev->launch_span);
+        io.metrics = ev->metrics;
+        io.metrics_slots = ev->metrics_slots;
+        if (io.metrics && io.metrics_slots < 1) return fail(MS_EINVAL, "ms_env_step: metrics_slots must be >= 1");
     }
     HIP_TRY(ms::launch_env_step(env->P, env->E, env->recs, env->mt, env->liab, io, (hipStream_t)stream));
     env->round += 1;

@@ -442,6 +442,20 @@ __device__ __forceinline__ void mask_set(M128* m, int i) {
     atomicOr(w, 1ull << (i & 63));
 }
 
+// Episode metrics (ms_env_metrics): no-return device atomics on the env's own accumulators (one
+// group per env, so nothing contends across envs and each replica's order is fixed). The vector
+// atomics leave no wait in the round's chain; the adds land before the kernel ends.
+__device__ __forceinline__ void m_add(int32_t* p, int v) {
+    if (v) __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void m_add(int64_t* p, long long v) {
+    if (v) __hip_atomic_fetch_add(reinterpret_cast<unsigned long long*>(p), (unsigned long long)v, __ATOMIC_RELAXED,
+                                  __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void m_add(double* p, double v) {
+    if (v != 0.0) unsafeAtomicAdd(p, v);
+}
+
 // Masks of the current offers: mc[c] = offers to core c, mr[r] = offers to
 // recipient r (0 = auctioneer). Ends with a phase boundary.
 template <int LPE>
@@ -929,6 +943,9 @@ __device__ __forceinline__ void env_round(const Params& P, int64_t E, uint8_t* r
     int8_t* o_recip = R.offer_recip();
     int8_t* o_price = R.offer_price();
     Liab* my_liab = liab + e * (int64_t)C * P.cap;
+    // this round's episode accumulators (trainPPO.py:172-187): slot of episode round / episodeLength
+    ms_env_metrics* mx = (io.metrics && active) ? io.metrics + (int64_t)((round / P.ep_len) % io.metrics_slots) * E + e
+                                                : nullptr;
 
     // ---- issue the dependent loads early: the MT window at mti (a peek: no twist
     //      yet) and the newest liability entries of every core that may terminate
@@ -1000,6 +1017,8 @@ __device__ __forceinline__ void env_round(const Params& P, int64_t E, uint8_t* r
     //      groups' leaders run their envs' loops side by side
     if (gl == 0) {
         const int n_exec = s_n_exec;
+        double q_sum = 0.0;  // calculateAverageAcceptionQuality (SchedulingEnvironment.py:174-192)
+        int n_q = 0;
         for (int r = 0; r < n_exec; r++) {
             const int c = s_by_rank[r];
             const int i = s_exec[c];
@@ -1063,6 +1082,15 @@ __device__ __forceinline__ void env_round(const Params& P, int64_t E, uint8_t* r
                 off_r[i] = (float)prio1;
                 price_r[i] = pc;
             }
+            if (mx) {
+                m_add(&mx->price_sum[nk], price);  // prices.append((offeredReward, jobKind)) trainPPO.py:172-174
+                m_add(&mx->price_count[nk], 1);
+                if (recip != 0) {  // formerCore* = the core's job before this round's execution
+                    const double former = ok >= 0 ? (double)R.prio(ok) / (double)orem : 0.0;
+                    q_sum += ((double)price / (double)nrem - former) * 10.0;
+                    n_q++;
+                }
+            }
             if (io.ev_acc && active) {
                 ms_accept_rec ar;
                 ar.valid = 1;
@@ -1078,6 +1106,11 @@ __device__ __forceinline__ void env_round(const Params& P, int64_t E, uint8_t* r
                 ar.round = round;
                 io.ev_acc[e * C + c] = ar;
             }
+        }
+        if (mx && n_q > 0) {  // statistics.mean of the round's qualities, then collected per round
+            m_add(&mx->quality_sum, q_sum / n_q);
+            m_add(&mx->quality_rounds, 1);
+            m_add(&mx->acception_amount, n_q);
         }
     }
     wave_sync();
@@ -1101,6 +1134,11 @@ __device__ __forceinline__ void env_round(const Params& P, int64_t E, uint8_t* r
                 tr.prio = (int8_t)R.prio(kind);
                 tr.init_len = (int8_t)R.len(kind);
                 tr.dwell = round - c_birth[c];
+                if (mx) {  // verweilzeiten (world.py:350-357); env.terminationRevenues (Reward.py:193)
+                    m_add(&mx->dwell_sum[kind], tr.dwell - 1);
+                    m_add(&mx->dwell_count[kind], 1);
+                    if (!P.free_prices) m_add(&mx->termination_revenue, (long long)gen);
+                }
                 // Core.assignCoreToAuctioneer (world.py:57-59)
                 c_kind[c] = -1;
                 c_rem[c] = -1;
@@ -1265,6 +1303,23 @@ __device__ __forceinline__ void env_round(const Params& P, int64_t E, uint8_t* r
             copy_out<LPE>(WtOut(base, E * per_env * 4), e * per_env * 4, reinterpret_cast<uint32_t*>(base) + e * per_env,
                           reinterpret_cast<const uint32_t*>(src), per_env, gl);
         };
+        if (mx) {  // the driver's reward accumulators (trainPPO.py:176-183)
+            if (gl < N) {
+                int ar = 0, orw = 0;
+                float pr = 0.f;
+                for (int c = 0; c < C; c++) ar += acc_r[gl * C + c];
+                for (int j = 0; j < L; j++) {
+                    orw += (int)off_r[gl * L + j];
+                    pr += price_r[gl * L + j];
+                }
+                m_add(&mx->agent_reward[gl], (long long)s_agent_r[gl]);
+                m_add(&mx->acceptor_reward, (long long)ar);
+                m_add(&mx->offer_reward, (long long)orw);
+                if (P.free_prices) m_add(&mx->price_reward, (double)pr);
+            }
+            if (gl < C) m_add(&mx->auctioneer_reward, (long long)s_auct_r[gl]);
+            if (gl == 0) m_add(&mx->rounds, 1);
+        }
         rew(io.rew_acc, N * C, acc_r);
         rew(io.rew_offer, NL, off_r);
         rew(io.rew_price, NL, price_r);

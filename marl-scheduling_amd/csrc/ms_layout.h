@@ -47,6 +47,7 @@ struct Params {
     int32_t fix[MS_MAX_KINDS];
     int32_t n_fix;
     int32_t free_prices, commercial, new_jobs, mult;
+    int32_t ep_len;  // episodeLength (world.py:243): the metrics slot of a round
     float net_zero;
     // LDS carve-up (byte offsets into dynamic shared memory), sized to the config so that
     // small envs keep many waves per CU in flight
@@ -81,6 +82,8 @@ struct StepIO {
     ms_term_rec* ev_term;
     uint32_t* err_word;  // host-coherent sticky word: set to 1 by a round raising a fatal flag
     unsigned long long* span;  // [waves][2] or NULL: each wave's start / end (s_memrealtime)
+    ms_env_metrics* metrics;   // [slots][E] episode accumulators or NULL
+    int32_t metrics_slots;
 };
 
 // launch arguments of k_aggregate_obs (agg_kernels.hip): divided rows in, aggregated rows out
@@ -140,6 +143,7 @@ inline Params make_params(const ms_config& c, int32_t cap) {
     p.commercial = c.commercial_reward;
     p.new_jobs = c.new_jobs_per_round;
     p.mult = c.reward_multiplier;
+    p.ep_len = c.episode_length > 0 ? c.episode_length : 1;
     p.net_zero = (float)c.net_zero_offer_reward;
     // LDS plan
     int32_t s = 0;

@@ -111,6 +111,11 @@ class BatchedEnv:
             terminated=torch.empty((E, self.C, abi.TERM_REC_BYTES), dtype=torch.int8, device=d),
         )
 
+    def metrics_buffer(self, slots: int = 1):
+        """Episode accumulators [slots][E] of ms_env_metrics (zeroed), for events["metrics"]:
+        round r adds into slot (r // episode_length) % slots."""
+        return torch.zeros((slots, self.E, abi.METRICS_BYTES), dtype=torch.uint8, device=self.device)
+
     # ---- API
     @property
     def round(self) -> int:
@@ -147,8 +152,13 @@ class BatchedEnv:
         r = abi.MsRewardOut(ptr(rewards.get("offer")), ptr(rewards.get("price")), ptr(rewards.get("acceptor")),
                             ptr(rewards.get("auctioneer")), ptr(rewards.get("agent")),
                             ptr(rewards.get("aggregated_offer")), ptr(rewards.get("aggregated_acceptor")))
-        ev = abi.MsEventOut(ptr(events.get("accepted")), ptr(events.get("terminated")),
-                            ptr(events.get("launch_span"))) if events else None
+        ev = None
+        if events:
+            m = events.get("metrics")
+            if m is not None:
+                assert m.dtype == torch.uint8 and m.is_contiguous() and m.shape[1:] == (self.E, abi.METRICS_BYTES)
+            ev = abi.MsEventOut(ptr(events.get("accepted")), ptr(events.get("terminated")),
+                                ptr(events.get("launch_span")), ptr(m), 0 if m is None else m.shape[0])
         check(lib.ms_env_step(self._h, ct.byref(a), ct.byref(o), ct.byref(r), ct.byref(ev) if ev else None,
                               stream_ptr(stream)))
         return obs, rewards, events

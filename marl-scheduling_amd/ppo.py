@@ -8,11 +8,13 @@ nets of one unit type are stacked into groups ``[G, ...]``:
 * locally shared   — one group per agent (``LocallySharedPPO``, PPOmodules.py:490-597),
 * globally shared  — one group (``GloballySharedPPO``, PPOmodules.py:335-449).
 
-Action selection runs in the fused HIP kernel (``ms_policy_act``); the
-update runs as batched torch ops (bmm over groups) with ``torch.optim.Adam``
-on two parameter groups (actor / critic learning rates, PPOmodules.py:100-105).
-All groups step in lockstep, which equals independent per-net optimizers
-because Adam is elementwise. With E replicas a sub-unit's batch holds its
+Action selection runs in the fused HIP kernel (``ms_policy_act``). The update's
+gradient comes from the fused HIP kernel (``ms_ppo_grad``: forward, loss and
+backward of every group in one launch) and the HIP Adam step (``ms_adam_step``)
+applies it on two parameter groups (actor / critic learning rates,
+PPOmodules.py:100-105); ``PPOGroup.update`` keeps a torch-autograd twin with
+``torch.optim.Adam`` as the numerical reference. All groups step in lockstep,
+which equals independent per-net optimizers because Adam is elementwise. With E replicas a sub-unit's batch holds its
 E*T transitions; returns are normalised per replica over T so that E = 1 is
 exactly the reference.
 """
@@ -335,6 +337,24 @@ class PPOGroup:
         (device). Adam (torch) applies the gradient; with several ranks the gradient is
         all-reduced first. common_row (int8 [stride], device, optional): rows equal to it share one
         forward and one backward pass (same gradient up to f32 summation order)."""
+        epoch = self.fused_epoch(states_i8, actions_i8, old_logprobs, returns_teg, unit_of_group, T, E, stream,
+                                 common_row, returns_ld)
+        losses = []
+        for _ in range(self.K):
+            loss = epoch()
+            if self.allreduce is not None:
+                self.allreduce(self.policy.parameters())
+            self.hip_optimizer.step(stream)
+            losses.append(loss)
+        self.last_losses = losses
+        return losses
+
+    def fused_epoch(self, states_i8, actions_i8, old_logprobs, returns_teg, unit_of_group, T: int, E: int,
+                    stream=None, common_row=None, returns_ld: int = 0):
+        """The gradient half of one K-epoch step of ``update_fused``, for callers that all-reduce
+        several groups' gradients in one call (Trainer.update): returns a function that writes this
+        epoch's gradient into ``policy``'s .grad tensors (ms_ppo_grad) and returns the per-group loss
+        (the Adam step is ``hip_optimizer.step``)."""
         pol = self.policy
         R, U, stride = states_i8.shape
         assert R == T * E and states_i8.is_contiguous() and actions_i8.is_contiguous()
@@ -349,14 +369,14 @@ class PPOGroup:
         batch = abi.MsPpoBatch(ptr(states_i8), ptr(actions_i8), ptr(old_logprobs), ptr(returns_teg),
                                ptr(unit_of_group), stride, T, U, E, ptr(common_row), int(returns_ld))
         grads = abi.MsPpoGrads(*[ptr(getattr(pol, k).grad) for k in ACTOR_KEYS + CRITIC_KEYS], ptr(loss_buf))
-        losses = []
-        opt = self.hip_optimizer
-        for _ in range(self.K):
+        # the structs above hold raw device pointers: the closure keeps every tensor they point into
+        # alive until its last launch (a caller's temporaries would otherwise be freed and reused)
+        keep = (states_i8, actions_i8, old_logprobs, returns_teg, unit_of_group, common_row, ws, loss_buf)
+
+        def run():
+            assert keep
             check(lib.ms_ppo_grad(ct.byref(a), ct.byref(c), ct.byref(batch), ct.c_float(self.eps_clip), ptr(ws),
                                   ws_bytes, ct.byref(grads), stream_ptr(stream)))
-            if self.allreduce is not None:
-                self.allreduce(pol.parameters())
-            opt.step(stream)
-            losses.append(loss_buf[:, 0] + 0.5 * loss_buf[:, 1] - 0.01 * loss_buf[:, 2])
-        self.last_losses = losses
-        return losses
+            return loss_buf[:, 0] + 0.5 * loss_buf[:, 1] - 0.01 * loss_buf[:, 2]
+
+        return run

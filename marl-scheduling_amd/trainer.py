@@ -129,13 +129,17 @@ class EnvParts:
 class Trainer:
     def __init__(self, cfg: abi.MsConfig, n_envs: int, arch: str = "local", hyper: Hyper | None = None, seed: int = 0,
                  device=None, rank: int = 0, world_size: int = 1, process_group=None, fused: bool = True,
-                 use_graph: bool = True, common_rows: bool = True, rollout_streams: int = 1):
+                 use_graph: bool = True, common_rows: bool = True, rollout_streams: int = 1, metrics: bool = False,
+                 episode_length: int | None = None):
         assert arch in ("divided", "local", "global")
         self.fused = fused  # fused HIP gradient (ms_ppo_grad) vs torch autograd
         self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
         torch.cuda.set_device(self.device)
-        self.cfg, self.arch, self.E = cfg, arch, int(n_envs)
         self.hp = hyper or Hyper()
+        if episode_length is not None:  # episodeLength (world.py:243): the env's `done` cadence
+            cfg = abi.MsConfig.from_buffer_copy(cfg)
+            cfg.episode_length = int(episode_length)
+        self.cfg, self.arch, self.E = cfg, arch, int(n_envs)
         self.rank, self.world_size, self.pg = rank, world_size, process_group
         self.seed = seed
         # rollout_streams > 1: the replicas split into that many parts, each stepped on its own HIP
@@ -203,6 +207,13 @@ class Trainer:
         self.iterations = 0
         for env, e0, e1 in self.env.parts:
             env.reset(dict(acceptor=self.acc_obs[0][e0:e1], offer=self.off_obs[0][e0:e1]))
+        # episode metrics (trainPPO.py:153-226): the env kernel adds every round into per-replica
+        # accumulators, slot (round // episodeLength) % slots; finished episodes are read after each
+        # rollout (metrics.py) and their slots zeroed before reuse
+        self.ep_len = int(self.cfg.episode_length)
+        self.metric_slots = -(-T // self.ep_len) + 1
+        self.metric_bufs = [env.metrics_buffer(self.metric_slots) for env, _, _ in self.env.parts] if metrics else None
+        self.episode_log = []
         self.span_every = 0  # > 0: every span_every-th round's env launches record their span (bench)
         self.spans = None
         self.timings = dict(rollout=0.0, update=0.0)
@@ -264,6 +275,8 @@ class Trainer:
                    agent=sl(self.agent_reward), auctioneer=sl(self.auct_reward),
                    price=sl(self.price.rewards[t]).view(E, N, L) if self.free else None)
         ev = dict(launch_span=self.spans[t, k]) if self.span_every and t % self.span_every == 0 else None
+        if self.metric_bufs is not None:
+            ev = dict(ev or {}, metrics=self.metric_bufs[k])
         env.step(sl(self.acc.actions[t]).view(E, N, C), sl(self.off.actions[t]).view(E, N, L),
                  sl(self.env_price).view(E, N, L) if self.free else None, obs=obs, rewards=rew, events=ev, stream=st)
 
@@ -350,29 +363,48 @@ class Trainer:
         sel = self._draws()
         losses = {}
         T, E = self.T, self.E
-        for u in self.units():
-            states = self.acc_obs if u is self.acc else (self.off_obs if u is self.off else self.price_obs)
-            states = states[:T]
-            ls = []
-            if self.fused:
+        states_of = lambda u: (self.acc_obs if u is self.acc else (self.off_obs if u is self.off else self.price_obs))[:T]
+        if self.fused:
+            # Each unit type's draws update its nets in sequence (draw d trains on the weights draw
+            # d-1 left), but the unit types are independent nets: step s of the update = epoch k of
+            # draw d of every unit type that has one, with ONE all-reduce of all their gradients
+            # (one flattened RCCL call per step) before each type's Adam step.
+            steps = {}
+            for u in self.units():
                 # the returns of every draw's sub-units in one launch: [T][E][sum of G], draw d at
                 # column offset d*G (returns depend on the rewards only, not on earlier draws' updates)
                 all_sel = torch.cat(sel[u.name]).to(torch.int32)
                 ret_all = unit_returns(u.rewards, all_sel, u.group.gamma)
                 common = self.acc_common if (u is self.acc and self.common_rows) else None
-                col = 0
+                col, seq = 0, []
                 for u_sel in sel[u.name]:
-                    ls += u.group.update_fused(states.reshape(T * E, u.U, u.stride), u.actions.view(T * E, u.U),
-                                               u.logprobs.view(T * E, u.U), ret_all.view(-1)[col:],
-                                               all_sel[col:col + u_sel.numel()], T, E, common_row=common,
-                                               returns_ld=all_sel.numel())
+                    ep = u.group.fused_epoch(states_of(u).reshape(T * E, u.U, u.stride), u.actions.view(T * E, u.U),
+                                             u.logprobs.view(T * E, u.U), ret_all.view(-1)[col:],
+                                             all_sel[col:col + u_sel.numel()], T, E, common_row=common,
+                                             returns_ld=all_sel.numel())
+                    seq += [ep] * u.group.K
                     col += u_sel.numel()
-            else:
+                steps[u.name] = (u, seq, [])
+            for s in range(max(len(v[1]) for v in steps.values())):
+                live = [(u, seq, ls) for u, seq, ls in steps.values() if s < len(seq)]
+                for u, seq, ls in live:
+                    ls.append(seq[s]())
+                if self.world_size > 1:
+                    self._allreduce([p for u, _, _ in live for p in u.group.policy.parameters()])
+                for u, _, _ in live:
+                    u.group.hip_optimizer.step()
+            for u, _, ls in steps.values():
+                u.group.last_losses = ls
+                u.group.sync_old()
+                losses[u.name] = torch.stack(ls)
+        else:
+            for u in self.units():
+                ls = []
                 for u_sel in sel[u.name]:
-                    x, a, lp, ret = u.batch(states, u_sel)
+                    x, a, lp, ret = u.batch(states_of(u), u_sel)
                     ls += u.group.update(x, a, lp, ret)
-            u.group.sync_old()
-            losses[u.name] = torch.stack(ls)
+                u.group.sync_old()
+                losses[u.name] = torch.stack(ls)
         # next iteration starts from the last observation
         self.acc_obs[0].copy_(self.acc_obs[self.T])
         self.off_obs[0].copy_(self.off_obs[self.T])
@@ -388,7 +420,34 @@ class Trainer:
         ev[2].record()
         self._pending_events.append(ev)
         self.iterations += 1
+        if self.metric_bufs is not None:
+            self._harvest_episodes()
         return losses
+
+    # ---- metrics
+    def _harvest_episodes(self):
+        """Per-replica values of every episode finished by now (trainPPO.py:200-226), appended to
+        self.episode_log; their accumulator slots are zeroed for reuse."""
+        from . import metrics as mx
+        s = self.env.shape
+        done = self.rounds_done // self.ep_len
+        while len(self.episode_log) < done:
+            slot = len(self.episode_log) % self.metric_slots
+            raw = torch.cat([b[slot] for b in self.metric_bufs]).cpu().numpy()
+            for b in self.metric_bufs:
+                b[slot].zero_()
+            self.episode_log.append(mx.episode_values(mx.view(raw), self.cfg, self.ep_len, s.n_agents, s.n_cores,
+                                                      s.collection_length))
+
+    def args_dict(self, replica="mean", params=None):
+        """argsDict of the finished episodes (trainPPO.py:229-243): replica = "mean" averages the
+        replicas' values per episode, an int picks one replica."""
+        from . import metrics as mx
+        p = dict(params or {})
+        p.setdefault("episodeLength", self.ep_len)
+        p.setdefault("UPDATE_STEP", self.T)
+        p.setdefault("n_envs", self.E * self.world_size)
+        return mx.args_dict(self.episode_log, self.cfg, p, replica=replica)
 
     @property
     def timings(self):

@@ -271,6 +271,22 @@ def test_trainer_fused_matches_torch_update(ms):
                                        getattr(u1.group.policy, k).detach().cpu().numpy(), rtol=1e-4, atol=1e-5)
 
 
+def test_trainer_one_allreduce_per_update_step(ms):
+    """The unit types' gradients of one (draw, epoch) step share one flattened all-reduce (§8(e)):
+    cfg3 locally shared has 2 draws x K=1 for acceptor, core chooser and price chooser -> 2 calls
+    carrying all three types' parameters, and the same result as the per-type order."""
+    tr_mod = importlib.import_module("marl-scheduling_amd.trainer")
+    trs = [tr_mod.Trainer.from_named("cfg3", n_envs=32, update_step=10, seed=6, device="cuda:0") for _ in range(2)]
+    calls = []
+    trs[0].world_size = 2  # route through the all-reduce hook without a process group
+    trs[0]._allreduce = lambda ps: calls.append(sum(p.numel() for p in ps))
+    out = [t.iteration() for t in trs]
+    n_params = sum(p.numel() for u in trs[0].units() for p in u.group.policy.parameters())
+    assert calls == [n_params, n_params]
+    for name in out[0]:
+        assert torch.equal(out[0][name], out[1][name])
+
+
 @pytest.mark.parametrize("G,per_group,C,A2", [(8, 3, 8, 13), (2, 3, 2, 11), (1, 48, 16, 11)])
 def test_offer_act_free_matches_reference(ms, G, per_group, C, A2):
     """FreePriceOfferPPO.selectAction (PPOmodules.py:312-332) fused: core chooser, price input, price chooser."""
