@@ -395,6 +395,54 @@ typedef struct ms_adam_tensor {
 int ms_adam_step(const ms_adam_tensor* tensors, int32_t n_tensors, const double* lr, int32_t n_lr, int64_t step,
                  double beta1, double beta2, double eps, void* stream);
 
+/* ---- DQN units: DQNEntity (DQNmodules.py:34-94) and optimize_model (DQNmodules.py:97-154) for the
+ * DQN env (DQNDividedFixedPricesEnv SchedulingEnvironment.py:351-436, DividedFixPriceDQNAgent
+ * Agent.py:303-356), G nets of one unit type batched over groups and replicas ----
+ * Nets: nn.Sequential(Linear(D, 16), Tanh, Linear(16, A)), stacked over groups (nn.Linear layouts). */
+typedef struct ms_qnet_params {
+    const float *w1, *b1, *w2, *b2; /* [G][16][D], [G][16], [G][A][16], [G][A] */
+    int32_t in_dim;                 /* D (<= 256) */
+    int32_t hidden;                 /* must be 16 */
+    int32_t n_actions;              /* A (<= 127) */
+    int32_t n_groups;               /* G */
+} ms_qnet_params;
+
+/* selectAction (DQNmodules.py:56-70) for rows obs[e][u][stride] (unit u uses group
+ * u / units_per_group): greedy[e*U+u] = the first argmax of Q; action = greedy when the row's first
+ * uniform u1 > eps_threshold (RUN_END + (RUN_START - RUN_END) * exp(-round / RUN_DECAY)), else
+ * floor(u2 * A) (random.randrange). uniforms: [2][E*U] doubles in [0, 1) or NULL = Philox4x32-10
+ * keyed by seed, counter (row, offset + *offset_dev). greedy may be NULL. */
+int ms_dqn_act(const ms_qnet_params* q, const int8_t* obs, int32_t obs_stride, int64_t n_envs, int32_t n_units,
+               int32_t units_per_group, double eps_threshold, const double* uniforms, uint64_t seed, uint64_t offset,
+               const uint64_t* offset_dev, int8_t* action, int8_t* greedy, void* stream);
+
+/* A minibatch of every group: the replay memories of all (replica, unit) pairs, [E][U][capacity] transitions
+ * (ReplayMemory DQNmodules.py:13-31, Transition(state, action, next_state, reward)), and for each pair
+ * `batch` sampled memory indices (np.random.choice(memory[:nextFreeIndex], BATCH_SIZE) in the reference). */
+typedef struct ms_dqn_batch {
+    const int8_t* states;      /* [E][U][capacity][stride] */
+    const int8_t* next_states; /* [E][U][capacity][stride] */
+    const int8_t* actions;     /* [E][U][capacity] */
+    const float* rewards;      /* [E][U][capacity] */
+    const int32_t* samples;    /* [E][U][batch], each in [0, capacity) */
+    int32_t stride, n_units, units_per_group, capacity, batch;
+    int64_t n_envs;
+    float gamma;               /* GAMMA of the unit type (OFFER_GAMMA / ACCEPTOR_GAMMA) */
+} ms_dqn_batch;
+
+typedef struct ms_qnet_grads { /* device outputs [G][...] like the weights */
+    float *w1, *b1, *w2, *b2;
+    float* loss;               /* [G] SmoothL1 loss, mean over the group's rows */
+} ms_qnet_grads;
+
+/* Gradient of mean SmoothL1(Q(s)[a], r + gamma * max Q_target(s')) over each group's
+ * units_per_group * E * batch rows (one minibatch per replica: the replicas' mean loss), written
+ * clamped to [-grad_clip, grad_clip] (grad_clip <= 0: none); the Adam step is ms_adam_step.
+ * Deterministic (fixed summation order). */
+size_t ms_dqn_workspace_bytes(const ms_qnet_params* q, int64_t rows_per_group);
+int ms_dqn_grad(const ms_qnet_params* policy, const ms_qnet_params* target, const ms_dqn_batch* batch, float grad_clip,
+                void* workspace, size_t workspace_bytes, const ms_qnet_grads* grads, void* stream);
+
 const char* ms_last_error(void);
 int ms_abi_version(void);
 

@@ -66,6 +66,12 @@ def _load():
         "ms_decode_aggregated": (ct.c_int, [ct.POINTER(abi.MsConfig), i64, P, i32, P, P, P, P]),
         "ms_adam_step": (ct.c_int, [ct.POINTER(abi.MsAdamTensor), i32, ct.POINTER(ct.c_double), i32, i64, ct.c_double,
                                     ct.c_double, ct.c_double, P]),
+        "ms_dqn_act": (ct.c_int, [ct.POINTER(abi.MsQnetParams), P, i32, i64, i32, i32, ct.c_double, P, u64, u64, P,
+                                  P, P, P]),
+        "ms_dqn_workspace_bytes": (ct.c_size_t, [ct.POINTER(abi.MsQnetParams), i64]),
+        "ms_dqn_grad": (ct.c_int, [ct.POINTER(abi.MsQnetParams), ct.POINTER(abi.MsQnetParams),
+                                   ct.POINTER(abi.MsDqnBatch), ct.c_float, P, ct.c_size_t,
+                                   ct.POINTER(abi.MsQnetGrads), P]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)
@@ -85,7 +91,7 @@ EXPORTED = (
     "ms_env_get_rng", "ms_env_set_rng", "ms_env_export",
     "ms_env_import", "ms_policy_act", "ms_policy_act_common", "ms_offer_act_free", "ms_discounted_returns", "ms_unit_returns",
     "ms_ppo_workspace_bytes", "ms_ppo_grad", "ms_adam_step",
-    "ms_aggregate_obs", "ms_decode_aggregated",
+    "ms_aggregate_obs", "ms_decode_aggregated", "ms_dqn_act", "ms_dqn_workspace_bytes", "ms_dqn_grad",
 )
 
 

@@ -195,6 +195,23 @@ class MsMlpParams(ct.Structure):
     ]
 
 
+class MsQnetParams(ct.Structure):
+    _fields_ = [("w1", ct.c_void_p), ("b1", ct.c_void_p), ("w2", ct.c_void_p), ("b2", ct.c_void_p),
+                ("in_dim", ct.c_int32), ("hidden", ct.c_int32), ("n_actions", ct.c_int32), ("n_groups", ct.c_int32)]
+
+
+class MsDqnBatch(ct.Structure):
+    _fields_ = [("states", ct.c_void_p), ("next_states", ct.c_void_p), ("actions", ct.c_void_p),
+                ("rewards", ct.c_void_p), ("samples", ct.c_void_p), ("stride", ct.c_int32), ("n_units", ct.c_int32),
+                ("units_per_group", ct.c_int32), ("capacity", ct.c_int32), ("batch", ct.c_int32),
+                ("n_envs", ct.c_int64), ("gamma", ct.c_float)]
+
+
+class MsQnetGrads(ct.Structure):
+    _fields_ = [("w1", ct.c_void_p), ("b1", ct.c_void_p), ("w2", ct.c_void_p), ("b2", ct.c_void_p),
+                ("loss", ct.c_void_p)]
+
+
 class MsPpoBatch(ct.Structure):
     _fields_ = [
         ("states", ct.c_void_p),

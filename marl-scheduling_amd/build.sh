@@ -13,11 +13,11 @@ FLAGS=(-O3 -std=c++17 -fPIC --offload-arch="${ARCH}" -Wall -Wno-unused-function
 OBJDIR="${HERE}/build"
 [[ "${MS_CLEAN:-0}" == 1 ]] && rm -rf "${OBJDIR}"
 mkdir -p "${OBJDIR}"
-HEADERS=("${HERE}/csrc/ms_layout.h" "${HERE}/csrc/ms_ppo.h" "${HERE}/csrc/ms_common.h" "${HERE}/../include/marlsched.h")
+HEADERS=("${HERE}/csrc/ms_layout.h" "${HERE}/csrc/ms_ppo.h" "${HERE}/csrc/ms_dqn.h" "${HERE}/csrc/ms_common.h" "${HERE}/../include/marlsched.h")
 CCVER="$("${HIPCC}" --version 2>/dev/null | head -3 | tr '\n' ' ')"
 objs=()
 pids=()
-for src in env_kernels.hip policy_kernels.hip ppo_kernels.hip agg_kernels.hip capi.cpp; do
+for src in env_kernels.hip policy_kernels.hip ppo_kernels.hip agg_kernels.hip dqn_kernels.hip capi.cpp; do
   obj="${OBJDIR}/${src%.*}.o"
   # the env round reproduces Python's float64 arithmetic: no contraction there; the policy
   # and PPO kernels follow torch's f32 (which fuses freely) within tolerance: fma allowed

@@ -12,6 +12,7 @@
 #include <vector>
 
 #include "ms_layout.h"
+#include "ms_dqn.h"
 #include "ms_ppo.h"
 
 namespace ms {
@@ -32,6 +33,8 @@ int ppo_param_count(int D, int A);
 hipError_t launch_aggregate_obs(const AggArgs&, hipStream_t);
 hipError_t launch_decode_aggregated(const int32_t*, long long, int, int, int, int, int8_t*, int8_t*, int*, hipStream_t);
 hipError_t launch_adam(const AdamTensor*, int, const double*, int, int64_t, double, double, double, hipStream_t);
+hipError_t launch_dqn_act(const DqnActArgs&, hipStream_t);
+hipError_t launch_dqn_grad(const DqnGradArgs&, const DqnReduceArgs&, hipStream_t);
 }  // namespace ms
 
 // work split of k_ppo_grad: ~8192 wave chunks over all groups (4 per block), >= 8 tiles of 16 rows each
@@ -634,3 +637,116 @@ int ms_discounted_returns(const float* rewards, int32_t T, int64_t M, int64_t ro
 }
 
 }  // extern "C"
+
+// ---- DQN units
+
+static int qnet_check(const ms_qnet_params* q, const char* who) {
+    if (!q || !q->w1 || !q->b1 || !q->w2 || !q->b2) return fail(MS_EINVAL, "%s: null net parameter", who);
+    if (q->hidden != ms::kQH) return fail(MS_EINVAL, "%s: hidden must be %d", who, ms::kQH);
+    if (q->in_dim < 1 || q->in_dim > 256 || q->n_actions < 1 || q->n_actions > 127 || q->n_groups < 1)
+        return fail(MS_EINVAL, "%s: bad net shape", who);
+    return MS_OK;
+}
+
+static ms::QArgs qargs(const ms_qnet_params* q, int upg) {
+    ms::QArgs a;
+    a.w1 = q->w1;
+    a.b1 = q->b1;
+    a.w2 = q->w2;
+    a.b2 = q->b2;
+    a.D = q->in_dim;
+    a.A = q->n_actions;
+    a.G = q->n_groups;
+    a.upg = upg;
+    return a;
+}
+
+static int dqn_param_count(int D, int A) { return ms::kQH * D + ms::kQH + A * ms::kQH + A; }
+
+int ms_dqn_act(const ms_qnet_params* q, const int8_t* obs, int32_t obs_stride, int64_t n_envs, int32_t n_units,
+               int32_t units_per_group, double eps_threshold, const double* uniforms, uint64_t seed, uint64_t offset,
+               const uint64_t* offset_dev, int8_t* action, int8_t* greedy, void* stream) {
+    if (int rc = qnet_check(q, "ms_dqn_act")) return rc;
+    if (!obs || !action || n_envs < 1 || n_units < 1 || units_per_group < 1 ||
+        units_per_group * q->n_groups != n_units || obs_stride < q->in_dim || (obs_stride & 3))
+        return fail(MS_EINVAL, "ms_dqn_act: bad rows / units (units_per_group * n_groups must equal n_units)");
+    if (n_units > 65535) return fail(MS_EINVAL, "ms_dqn_act: at most 65535 units");
+    ms::DqnActArgs a{};
+    a.q = qargs(q, units_per_group);
+    a.obs = obs;
+    a.stride = obs_stride;
+    a.U = n_units;
+    a.E = n_envs;
+    a.eps = eps_threshold;
+    a.uniforms = uniforms;
+    a.seed = seed;
+    a.offset = offset;
+    a.offset_dev = offset_dev;
+    a.action = action;
+    a.greedy = greedy;
+    HIP_TRY(ms::launch_dqn_act(a, (hipStream_t)stream));
+    return MS_OK;
+}
+
+static int dqn_xpitch(int D) { return 4 * ((((D + 3) / 4)) | 1); }
+
+size_t ms_dqn_workspace_bytes(const ms_qnet_params* q, int64_t rows_per_group) {
+    if (!q || rows_per_group < 1) return 0;
+    const int64_t nblk = (rows_per_group + 255) / 256;
+    return sizeof(float) * (size_t)q->n_groups * (size_t)nblk * (size_t)(dqn_param_count(q->in_dim, q->n_actions) + 1);
+}
+
+int ms_dqn_grad(const ms_qnet_params* policy, const ms_qnet_params* target, const ms_dqn_batch* b, float grad_clip,
+                void* workspace, size_t workspace_bytes, const ms_qnet_grads* g, void* stream) {
+    if (int rc = qnet_check(policy, "ms_dqn_grad (policy)")) return rc;
+    if (int rc = qnet_check(target, "ms_dqn_grad (target)")) return rc;
+    if (policy->in_dim != target->in_dim || policy->n_actions != target->n_actions ||
+        policy->n_groups != target->n_groups)
+        return fail(MS_EINVAL, "ms_dqn_grad: policy and target shapes differ");
+    if (!b || !g || !b->states || !b->next_states || !b->actions || !b->rewards || !b->samples || !g->w1 || !g->b1 ||
+        !g->w2 || !g->b2 || !g->loss)
+        return fail(MS_EINVAL, "ms_dqn_grad: null batch / gradient pointer");
+    if (b->n_envs < 1 || b->batch < 1 || b->capacity < 1 || b->units_per_group < 1 ||
+        b->units_per_group * policy->n_groups != b->n_units || b->stride < policy->in_dim || (b->stride & 3))
+        return fail(MS_EINVAL, "ms_dqn_grad: bad batch shape");
+    const int64_t rows = (int64_t)b->units_per_group * b->n_envs * b->batch;
+    const size_t need = ms_dqn_workspace_bytes(policy, rows);
+    if (!workspace || workspace_bytes < need) return fail(MS_EINVAL, "ms_dqn_grad: workspace too small (%zu < %zu)",
+                                                          workspace_bytes, need);
+    ms::DqnGradArgs a{};
+    a.q = qargs(policy, b->units_per_group);
+    a.t = qargs(target, b->units_per_group);
+    a.states = b->states;
+    a.next_states = b->next_states;
+    a.actions = b->actions;
+    a.rewards = b->rewards;
+    a.samples = b->samples;
+    a.stride = b->stride;
+    a.U = b->n_units;
+    a.cap = b->capacity;
+    a.B = b->batch;
+    a.xpitch = dqn_xpitch(policy->in_dim);
+    a.P = dqn_param_count(policy->in_dim, policy->n_actions) + 1;
+    a.E = b->n_envs;
+    a.rows = rows;
+    a.gamma = b->gamma;
+    a.inv_rows = (float)(1.0 / (double)rows);
+    a.partials = static_cast<float*>(workspace);
+    if (ms::dqn_grad_lds(a.q, a.xpitch) > 160 * 1024) return fail(MS_EINVAL, "ms_dqn_grad: net too wide for LDS");
+    ms::DqnReduceArgs r{};
+    r.partials = a.partials;
+    r.nblk = (int)((rows + 255) / 256);
+    r.P = a.P;
+    r.D = a.q.D;
+    r.A = a.q.A;
+    r.clip = grad_clip;
+    r.inv_rows = a.inv_rows;
+    r.w1 = g->w1;
+    r.b1 = g->b1;
+    r.w2 = g->w2;
+    r.b2 = g->b2;
+    r.loss = g->loss;
+    if (r.nblk > 65535 * 64) return fail(MS_EINVAL, "ms_dqn_grad: too many rows per group");
+    HIP_TRY(ms::launch_dqn_grad(a, r, (hipStream_t)stream));
+    return MS_OK;
+}
