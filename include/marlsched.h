@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define MS_ABI_VERSION 4
+#define MS_ABI_VERSION 5
 
 #define MS_MAX_KINDS 16
 #define MS_MAX_AGENTS 64
@@ -119,6 +119,12 @@ typedef struct ms_obs_out {
     int8_t* acceptor;   /* [E][N][C][acc_obs_stride]  Agent.py:167-212 (pad bytes zero) */
     int8_t* offer;      /* [E][N][L][off_obs_stride]  Agent.py:271-300 */
     int8_t* auctioneer; /* [E][C][acc_obs_stride]     Auctioneer.py:34-77 */
+    /* Compact acceptor observations (the [E][N][C] acceptor rows regenerated on demand): core_rows[e][c]
+     * is the acceptor row core c's owner sees ([1, prio, rem, offers to c in ID order, pads]), core_owner
+     * [E][C] its ownerID. Acceptor row (a, c) equals core_rows[e][c] when core_owner[e][c] == a + 1 and
+     * the constant [0, -1, -1, (-2, -2) * O] otherwise (Agent.py:167-212; see ms_regen_acceptor_rows). */
+    int8_t* core_rows;  /* [E][C][acc_obs_stride] */
+    int8_t* core_owner; /* [E][C] */
 } ms_obs_out;
 
 /* Reward outputs (device pointers; any may be NULL to skip). */
@@ -376,6 +382,19 @@ int ms_aggregate_obs(const ms_config* cfg, int64_t n_envs, const int8_t* acc_obs
  * action space exceeds int32. */
 int ms_decode_aggregated(const ms_config* cfg, int64_t n_envs, const int32_t* actions, int32_t fully,
                          int8_t* acceptor, int8_t* offer_core, int32_t* n_bad, void* stream);
+
+/* Agent rows regenerated from compact observations (ms_obs_out.core_rows / core_owner, kept per
+ * record in a replay memory of M records): for b < n_rows, record frame[b] seen by agent agent[b]
+ * (0-based):
+ *   acceptor [n_rows][align4(C * D_acc)]  the aggregated acceptor row (Agent.py:82-124): concat over
+ *            cores c of core_rows[m][c][0:D_acc] if core_owner[m][c] == agent + 1, else the foreign
+ *            row [0, -1, -1, (-2, -2) * O];
+ *   offer    [n_rows][align4(2C + 2L)]    the aggregated offer row (Agent.py:126-134): the cores'
+ *            (prio, rem) = core_rows[m][c][1:3], then slot_pairs[m][agent][s][0:2] ([M][N][L][2]).
+ * Either output may be NULL; pad bytes are zero. */
+int ms_regen_agent_rows(const ms_config* cfg, const int8_t* core_rows, const int8_t* core_owner,
+                        const int8_t* slot_pairs, const int64_t* frame, const int32_t* agent, int64_t n_rows,
+                        int8_t* acceptor, int8_t* offer, void* stream);
 
 /* ---- Adam step (torch.optim.Adam as PPO.__init__ builds it, PPOmodules.py:100-112) ----
  * One optimizer.step() over the tensors of one PPO group: tensor i uses lr[lr_group[i]] (actor

@@ -68,6 +68,7 @@ def _load():
                                     ct.c_double, ct.c_double, P]),
         "ms_dqn_act": (ct.c_int, [ct.POINTER(abi.MsQnetParams), P, i32, i64, i32, i32, ct.c_double, P, u64, u64, P,
                                   P, P, P]),
+        "ms_regen_agent_rows": (ct.c_int, [ct.POINTER(abi.MsConfig), P, P, P, P, P, i64, P, P, P]),
         "ms_dqn_workspace_bytes": (ct.c_size_t, [ct.POINTER(abi.MsQnetParams), i64]),
         "ms_dqn_grad": (ct.c_int, [ct.POINTER(abi.MsQnetParams), ct.POINTER(abi.MsQnetParams),
                                    ct.POINTER(abi.MsDqnBatch), ct.c_float, P, ct.c_size_t,
@@ -77,7 +78,7 @@ def _load():
         fn = getattr(L, name)
         fn.restype = res
         fn.argtypes = args
-    if L.ms_abi_version() != 4:
+    if L.ms_abi_version() != 5:
         raise ImportError("libmarlsched.so ABI version mismatch")
     return L
 
@@ -92,6 +93,7 @@ EXPORTED = (
     "ms_env_import", "ms_policy_act", "ms_policy_act_common", "ms_offer_act_free", "ms_discounted_returns", "ms_unit_returns",
     "ms_ppo_workspace_bytes", "ms_ppo_grad", "ms_adam_step",
     "ms_aggregate_obs", "ms_decode_aggregated", "ms_dqn_act", "ms_dqn_workspace_bytes", "ms_dqn_grad",
+    "ms_regen_agent_rows",
 )
 
 

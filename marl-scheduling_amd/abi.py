@@ -81,7 +81,8 @@ class MsActions(ct.Structure):
 
 
 class MsObsOut(ct.Structure):
-    _fields_ = [("acceptor", ct.c_void_p), ("offer", ct.c_void_p), ("auctioneer", ct.c_void_p)]
+    _fields_ = [("acceptor", ct.c_void_p), ("offer", ct.c_void_p), ("auctioneer", ct.c_void_p),
+                ("core_rows", ct.c_void_p), ("core_owner", ct.c_void_p)]
 
 
 class MsRewardOut(ct.Structure):

@@ -130,4 +130,57 @@ hipError_t launch_decode_aggregated(const int32_t* actions, long long EN, int C,
     return hipGetLastError();
 }
 
+
+// Agent rows regenerated from the compact observations of a replay memory (ms_regen_agent_rows):
+// sample b reads compact record frame[b] (core rows [C][acc_stride], owners [C], slot pairs
+// [N][L][2]) as agent agent[b]. Acceptor byte k = byte k % D_acc of core k / D_acc's row if the
+// agent owns that core, else of the constant foreign row [0, -1, -1, (-2, -2) * O] (Agent.py:167-212);
+// offer bytes = the cores' (prio, rem) (bytes 1, 2 of every core row) then the agent's slot pairs.
+__global__ void __launch_bounds__(256) k_regen_agent_rows(RegenArgs g) {
+    const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+    const int wa = g.acc ? g.acc_ld / 4 : 0, wo = g.off ? g.off_ld / 4 : 0;
+    const int per = wa + wo;
+    const long long b = i / per;
+    if (b >= g.n) return;
+    int w = (int)(i - b * per);
+    const long long m = g.frame[b];
+    const int a = g.agent[b];
+    const int8_t* rows = g.core_rows + (size_t)m * g.C * g.acc_stride;
+    const int8_t* own = g.core_owner + (size_t)m * g.C;
+    uint32_t v = 0;
+    int8_t* dst;
+    if (w < wa) {
+        for (int q = 0; q < 4; q++) {
+            const int k = 4 * w + q;
+            if (k >= g.C * g.d_acc) break;
+            const int c = k / g.d_acc, col = k - c * g.d_acc;
+            int8_t x;
+            if (own[c] == a + 1)
+                x = rows[(size_t)c * g.acc_stride + col];
+            else
+                x = col == 0 ? 0 : (col < 3 ? -1 : -2);
+            v |= (uint32_t)(uint8_t)x << (8 * q);
+        }
+        dst = g.acc + (size_t)b * g.acc_ld + 4 * w;
+    } else {
+        w -= wa;
+        const int8_t* sp = g.slot_pairs + ((size_t)m * g.N + a) * g.L * 2;
+        for (int q = 0; q < 4; q++) {
+            const int k = 4 * w + q;
+            if (k >= 2 * g.C + 2 * g.L) break;
+            const int8_t x = k < 2 * g.C ? rows[(size_t)(k >> 1) * g.acc_stride + 1 + (k & 1)] : sp[k - 2 * g.C];
+            v |= (uint32_t)(uint8_t)x << (8 * q);
+        }
+        dst = g.off + (size_t)b * g.off_ld + 4 * w;
+    }
+    *reinterpret_cast<uint32_t*>(dst) = v;
+}
+
+hipError_t launch_regen_agent_rows(const RegenArgs& g, hipStream_t s) {
+    const int per = (g.acc ? g.acc_ld / 4 : 0) + (g.off ? g.off_ld / 4 : 0);
+    const long long n = g.n * per;
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_regen_agent_rows, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, g);
+    return hipGetLastError();
+}
 }  // namespace ms

@@ -17,7 +17,8 @@
 
 namespace ms {
 hipError_t launch_env_init(const Params&, int64_t, uint8_t*, uint32_t*, Liab*, uint64_t, hipStream_t);
-hipError_t launch_env_reset(const Params&, int64_t, const uint8_t*, int8_t*, int8_t*, int8_t*, hipStream_t);
+hipError_t launch_env_reset(const Params&, int64_t, const uint8_t*, int8_t*, int8_t*, int8_t*, int8_t*, int8_t*,
+                            hipStream_t);
 hipError_t launch_env_step(const Params&, int64_t, uint8_t*, uint32_t*, Liab*, const StepIO&, hipStream_t);
 hipError_t launch_env_randbelow(const Params&, uint8_t*, uint32_t*, int64_t, uint32_t, uint32_t*, hipStream_t);
 hipError_t launch_env_auctioneer(const Params&, int64_t, uint8_t*, uint32_t*, int8_t*, hipStream_t);
@@ -34,6 +35,7 @@ hipError_t launch_aggregate_obs(const AggArgs&, hipStream_t);
 hipError_t launch_decode_aggregated(const int32_t*, long long, int, int, int, int, int8_t*, int8_t*, int*, hipStream_t);
 hipError_t launch_adam(const AdamTensor*, int, const double*, int, int64_t, double, double, double, hipStream_t);
 hipError_t launch_dqn_act(const DqnActArgs&, hipStream_t);
+hipError_t launch_regen_agent_rows(const RegenArgs&, hipStream_t);
 hipError_t launch_dqn_grad(const DqnGradArgs&, const DqnReduceArgs&, hipStream_t);
 }  // namespace ms
 
@@ -205,7 +207,8 @@ int64_t ms_env_round(const ms_env* env) {
 
 int ms_env_reset(ms_env* env, const ms_obs_out* obs, void* stream) {
     if (!env || !obs) return fail(MS_EINVAL, "env/obs is NULL");
-    HIP_TRY(ms::launch_env_reset(env->P, env->E, env->recs, obs->acceptor, obs->offer, obs->auctioneer,
+    HIP_TRY(ms::launch_env_reset(env->P, env->E, env->recs, obs->acceptor, obs->offer, obs->auctioneer, obs->core_rows,
+                                 obs->core_owner,
                                  (hipStream_t)stream));
     return MS_OK;
 }
@@ -229,6 +232,8 @@ int ms_env_step(ms_env* env, const ms_actions* act, const ms_obs_out* obs, const
         io.obs_acc = obs->acceptor;
         io.obs_off = obs->offer;
         io.obs_auct = obs->auctioneer;
+        io.obs_crow = obs->core_rows;
+        io.obs_cown = obs->core_owner;
     }
     if (rew) {
         io.rew_offer = rew->offer;
@@ -748,5 +753,35 @@ int ms_dqn_grad(const ms_qnet_params* policy, const ms_qnet_params* target, cons
     r.loss = g->loss;
     if (r.nblk > 65535 * 64) return fail(MS_EINVAL, "ms_dqn_grad: too many rows per group");
     HIP_TRY(ms::launch_dqn_grad(a, r, (hipStream_t)stream));
+    return MS_OK;
+}
+
+int ms_regen_agent_rows(const ms_config* cfg, const int8_t* core_rows, const int8_t* core_owner,
+                        const int8_t* slot_pairs, const int64_t* frame, const int32_t* agent, int64_t n_rows,
+                        int8_t* acceptor, int8_t* offer, void* stream) {
+    int rc = validate_config(cfg);
+    if (rc) return rc;
+    if (n_rows < 0 || !frame || !agent || !core_rows) return fail(MS_EINVAL, "ms_regen_agent_rows: NULL argument");
+    if (!acceptor && !offer) return MS_OK;
+    if (acceptor && !core_owner) return fail(MS_EINVAL, "ms_regen_agent_rows: acceptor rows need core_owner");
+    if (offer && !slot_pairs) return fail(MS_EINVAL, "ms_regen_agent_rows: offer rows need slot_pairs");
+    const ms::Params P = ms::make_params(*cfg, cap_of(cfg));
+    ms::RegenArgs g{};
+    g.core_rows = core_rows;
+    g.core_owner = core_owner;
+    g.slot_pairs = slot_pairs;
+    g.frame = frame;
+    g.agent = agent;
+    g.acc = acceptor;
+    g.off = offer;
+    g.n = n_rows;
+    g.N = P.N;
+    g.C = P.C;
+    g.L = P.L;
+    g.d_acc = P.d_acc;
+    g.acc_stride = P.acc_stride;
+    g.acc_ld = ms::align4(P.C * P.d_acc);
+    g.off_ld = ms::align4(2 * P.C + 2 * P.L);
+    HIP_TRY(ms::launch_regen_agent_rows(g, (hipStream_t)stream));
     return MS_OK;
 }

@@ -649,8 +649,10 @@ __device__ __forceinline__ void emit_rows(uint32_t* base, int64_t e, int64_t E, 
 // All observations of env e (dst == NULL skips a kind; a padding group passes write = false).
 template <int LPE>
 __device__ void emit_obs(Rec& R, const Params& P, const M128* mc, const M128* mr, uint8_t* scratch, int8_t* acc,
-                         int8_t* off, int8_t* auct, int64_t e, int64_t E, bool write, int gl) {
-    build_obs_sources<LPE>(R, P, mc, mr, scratch, acc != nullptr, auct != nullptr, off != nullptr, gl);
+                         int8_t* off, int8_t* auct, int8_t* crows, int8_t* cown, int64_t e, int64_t E, bool write,
+                         int gl) {
+    build_obs_sources<LPE>(R, P, mc, mr, scratch, acc != nullptr, auct != nullptr || crows != nullptr, off != nullptr,
+                           gl);
     if (!write) return;
     const int C = P.C, nw = P.acc_stride / 4, nwo = P.off_stride / 4;
     const uint32_t* crow = reinterpret_cast<const uint32_t*>(scratch);
@@ -663,6 +665,14 @@ __device__ void emit_obs(Rec& R, const Params& P, const M128* mc, const M128* mr
         const int8_t* owner = R.core_owner();
         emit_rows<LPE>(reinterpret_cast<uint32_t*>(auct), e, E, C, nw, P.mag_acc, gl,
                        [&](int c, int col, int) { return crow[(owner[c] == 0 ? c : C) * nw + col]; });
+    }
+    // compact acceptor observations: the owner row of every core and the owners; acceptor row (a, c)
+    // is core row c when a + 1 == owner[c], else the constant foreign row (regenerated on demand)
+    if (crows) emit_rows<LPE>(reinterpret_cast<uint32_t*>(crows), e, E, C, nw, P.mag_acc, gl,
+                              [&](int c, int col, int) { return crow[c * nw + col]; });
+    if (cown) {
+        const int8_t* owner = R.core_owner();
+        for (int c = gl; c < C; c += LPE) cown[e * C + c] = owner[c];
     }
     if (off) {
         const uint32_t* otmpl = reinterpret_cast<const uint32_t*>(scratch + P.s_otmpl);
@@ -803,7 +813,7 @@ __global__ void __launch_bounds__(64) k_env_init(Params P, uint8_t* recs, uint32
 }
 
 __global__ void __launch_bounds__(64) k_env_reset(Params P, const uint8_t* recs, int8_t* obs_acc, int8_t* obs_off,
-                                                  int8_t* obs_auct) {
+                                                  int8_t* obs_auct, int8_t* obs_crow, int8_t* obs_cown) {
     extern __shared__ __align__(16) uint8_t smem[];
     M128* s_mc = reinterpret_cast<M128*>(smem + P.s_mc);
     M128* s_mr = reinterpret_cast<M128*>(smem + P.s_mr);
@@ -817,7 +827,8 @@ __global__ void __launch_bounds__(64) k_env_reset(Params P, const uint8_t* recs,
     wave_sync();
     Rec R{rec, &P, s_kt};
     build_masks<kWave>(R, P, s_mc, s_mr, lane);
-    emit_obs<kWave>(R, P, s_mc, s_mr, smem + P.s_scratch, obs_acc, obs_off, obs_auct, e, gridDim.x, true, lane);
+    emit_obs<kWave>(R, P, s_mc, s_mr, smem + P.s_scratch, obs_acc, obs_off, obs_auct, obs_crow, obs_cown, e, gridDim.x,
+                    true, lane);
 }
 
 constexpr int kLiabPrefetch = 4;  // newest chain entries loaded ahead per core that may terminate
@@ -1346,7 +1357,8 @@ __device__ __forceinline__ void env_round(const Params& P, int64_t E, uint8_t* r
     MS_MARK(10);
     build_masks<LPE>(R, P, s_mc, s_mr, gl);
     MS_MARK(11);
-    emit_obs<LPE>(R, P, s_mc, s_mr, scratch, io.obs_acc, io.obs_off, io.obs_auct, e, E, active, gl);
+    emit_obs<LPE>(R, P, s_mc, s_mr, scratch, io.obs_acc, io.obs_off, io.obs_auct, io.obs_crow, io.obs_cown, e, E, active,
+                  gl);
     MS_MARK(12);
 #ifdef MS_PHASE_TIMING
     if (lane == 0)
@@ -1466,8 +1478,8 @@ hipError_t launch_env_init(const Params& P, int64_t E, uint8_t* recs, uint32_t* 
     return hipGetLastError();
 }
 hipError_t launch_env_reset(const Params& P, int64_t E, const uint8_t* recs, int8_t* a, int8_t* o, int8_t* u,
-                            hipStream_t s) {
-    hipLaunchKernelGGL(k_env_reset, dim3((unsigned)E), dim3(kWave), P.s_total, s, P, recs, a, o, u);
+                            int8_t* crow, int8_t* cown, hipStream_t s) {
+    hipLaunchKernelGGL(k_env_reset, dim3((unsigned)E), dim3(kWave), P.s_total, s, P, recs, a, o, u, crow, cown);
     return hipGetLastError();
 }
 

@@ -71,6 +71,8 @@ struct StepIO {
     int8_t* obs_acc;
     int8_t* obs_off;
     int8_t* obs_auct;
+    int8_t* obs_crow;  // [E][C][acc_stride] owner row of every core, or NULL
+    int8_t* obs_cown;  // [E][C] core owners, or NULL
     float* rew_offer;
     float* rew_price;
     int32_t* rew_acc;
@@ -96,6 +98,19 @@ struct AggArgs {
     int N, C, L, d_acc, acc_stride, off_stride;
     int agg_acc_stride, agg_off_stride, full_stride;
     long long E;
+};
+
+// launch arguments of k_regen_agent_rows (agg_kernels.hip)
+struct RegenArgs {
+    const int8_t* core_rows;   // [M][C][acc_stride]
+    const int8_t* core_owner;  // [M][C]
+    const int8_t* slot_pairs;  // [M][N][L][2] (offer rows) or NULL
+    const int64_t* frame;      // [n] record index
+    const int32_t* agent;      // [n] 0-based agent
+    int8_t* acc;               // [n][acc_ld] or NULL
+    int8_t* off;               // [n][off_ld] or NULL
+    long long n;
+    int N, C, L, d_acc, acc_stride, acc_ld, off_ld;
 };
 
 inline int32_t align4(int32_t x) { return (x + 3) & ~3; }

@@ -54,6 +54,13 @@ class BatchedEnv:
         auct = torch.empty((E, self.C, s.acc_obs_stride), dtype=torch.int8, device=d) if auctioneer else None
         return dict(acceptor=acc, offer=off, auctioneer=auct)
 
+    def compact_obs_buffers(self):
+        """Compact acceptor observations (ms_obs_out.core_rows / core_owner) + the offer rows."""
+        s, E, d = self.shape, self.E, self.device
+        return dict(core_rows=torch.empty((E, self.C, s.acc_obs_stride), dtype=torch.int8, device=d),
+                    core_owner=torch.empty((E, self.C), dtype=torch.int8, device=d),
+                    offer=torch.empty((E, self.N, self.L, s.off_obs_stride), dtype=torch.int8, device=d))
+
     def reward_buffers(self, aggregated=False):
         E, d = self.E, self.device
         r = dict(
@@ -104,6 +111,20 @@ class BatchedEnv:
                                        ptr(offer_core), ptr(n_bad), stream_ptr(stream)))
         return acceptor, offer_core
 
+    def regen_agent_rows(self, core_rows, core_owner, slot_pairs, frame, agent, acceptor=None, offer=None,
+                         stream=None):
+        """ms_regen_agent_rows: aggregated acceptor / offer rows of (record frame[b], agent[b]) from compact
+        records core_rows [M, C, acc_stride], core_owner [M, C], slot_pairs [M, N, L, 2] (int8)."""
+        n = frame.numel()
+        assert frame.dtype == torch.int64 and agent.dtype == torch.int32 and agent.numel() == n
+        d = self.aggregated_dims()
+        if acceptor is None and offer is None:
+            acceptor = torch.empty((n, d["acceptor"][1]), dtype=torch.int8, device=self.device)
+            offer = torch.empty((n, d["offer"][1]), dtype=torch.int8, device=self.device)
+        check(lib.ms_regen_agent_rows(ct.byref(self.cfg), ptr(core_rows), ptr(core_owner), ptr(slot_pairs), ptr(frame),
+                                      ptr(agent), n, ptr(acceptor), ptr(offer), stream_ptr(stream)))
+        return acceptor, offer
+
     def event_buffers(self):
         E, d = self.E, self.device
         return dict(
@@ -124,7 +145,8 @@ class BatchedEnv:
     def reset(self, obs=None, stream=None):
         """SchedulingEnv.reset (SchedulingEnvironment.py:85-109): observations only."""
         obs = obs or self.obs_buffers()
-        o = abi.MsObsOut(ptr(obs.get("acceptor")), ptr(obs.get("offer")), ptr(obs.get("auctioneer")))
+        o = abi.MsObsOut(ptr(obs.get("acceptor")), ptr(obs.get("offer")), ptr(obs.get("auctioneer")),
+                         ptr(obs.get("core_rows")), ptr(obs.get("core_owner")))
         check(lib.ms_env_reset(self._h, ct.byref(o), stream_ptr(stream)))
         return obs
 
@@ -148,7 +170,8 @@ class BatchedEnv:
         rewards = self.reward_buffers() if rewards is None else rewards
         a = abi.MsActions(ptr(acceptor), ptr(offer_core), ptr(offer_price if self.free_prices else None),
                           ptr(auctioneer))
-        o = abi.MsObsOut(ptr(obs.get("acceptor")), ptr(obs.get("offer")), ptr(obs.get("auctioneer")))
+        o = abi.MsObsOut(ptr(obs.get("acceptor")), ptr(obs.get("offer")), ptr(obs.get("auctioneer")),
+                         ptr(obs.get("core_rows")), ptr(obs.get("core_owner")))
         r = abi.MsRewardOut(ptr(rewards.get("offer")), ptr(rewards.get("price")), ptr(rewards.get("acceptor")),
                             ptr(rewards.get("auctioneer")), ptr(rewards.get("agent")),
                             ptr(rewards.get("aggregated_offer")), ptr(rewards.get("aggregated_acceptor")))
