@@ -154,18 +154,100 @@ def committed_traffic(alg_bytes_per_launch):
     return None
 
 
+OTHER = {  # BASELINE configs[1], [3], [4]: per-GPU replicas of the 1-GPU / 8-GPU sharded workloads
+    "cfg2": dict(envs=4096, what="4096 env replicas x 4 agents x 4 cores, fixPrices, PPO globallySharedParameters"),
+    "cfg4": dict(envs=8192, what="16 agents x 16 cores x 3 slots, freePrices, divided PPO (the aggregated acceptor's "
+                                 "(O+1)^C actions are infeasible, DESIGN.md), 65536 replicas / 8 GPUs = 8192 per GPU"),
+    "cfg5": dict(envs=8192, what="32 agents x 32 cores x 3 slots, freePrices, Branching DQN on compact observations, "
+                                 "65536 replicas / 8 GPUs = 8192 per GPU"),
+}
+
+
+def bench_other(args):
+    """The other BASELINE workloads on this rank (informational lines; the headline is cfg3):
+    cfg2 / cfg4 = PPO iterations of the batched trainer; cfg5 = Branching DQN frames (one step =
+    --update-step frames: act, env step, replay, one update per role per frame)."""
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    device = torch.device("cuda", local_rank)
+    torch.cuda.set_device(device)
+    importlib.import_module("marl-scheduling_amd")
+    spec = OTHER[args.config]
+    E = args.envs or spec["envs"]
+    T = args.update_step
+    if args.config == "cfg5":
+        bdqn = importlib.import_module("marl-scheduling_amd.bdqn")
+        abi = importlib.import_module("marl-scheduling_amd.abi")
+        tr = bdqn.BDQNTrainer(abi.named_config("cfg5"), n_envs=E, bcfg=bdqn.BDQNConfig(memory_frames=64,
+                                                                                      learning_starts=8),
+                              seed=rank, device=device)
+        run = lambda: [tr.step() for _ in range(T)]
+        N = tr.N
+    else:
+        trainer_mod = importlib.import_module("marl-scheduling_amd.trainer")
+        tr = trainer_mod.Trainer.from_named(args.config, n_envs=E, update_step=T, seed=0, device=device, rank=rank,
+                                            world_size=world)
+        tr.use_graph = not args.no_graph
+        run = tr.iteration
+        N = tr.N
+    for _ in range(max(args.warmup, 1)):
+        run()
+    torch.cuda.synchronize(device)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(device)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        run()
+    torch.cuda.synchronize(device)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(device)
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    if tr.flags():
+        raise SystemExit("env error flags set: 0x%x" % tr.flags())
+    value = world * E * N * T * args.steps / elapsed
+    result = {"metric": "agent-env-steps/sec (whole node), %s" % args.config, "value": value,
+              "unit": "agent-env-steps/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+              "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
+              "vs_baseline": None, "dtype": "int8/f32", "data": "synthetic (reference spawn sampler, random-init nets)",
+              "config": {"workload": "%s: %s; one step = %d rounds%s" % (args.config, spec["what"], T,
+                                                                       " + update" if args.config != "cfg5" else ""),
+                         "replicas_per_gpu": E, "rounds_per_step": T}}
+    if rank == 0:
+        print(json.dumps(result))
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=2)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--envs", type=int, default=16384, help="env replicas per GPU")
+    ap.add_argument("--envs", type=int, default=None, help="env replicas per GPU (default: the config's per-GPU share)")
     ap.add_argument("--update-step", type=int, default=200)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-graph", action="store_true", help="eager rollout instead of HIP-graph replay")
     ap.add_argument("--rollout-streams", type=int, default=ROLLOUT_STREAMS,
                     help="replica parts stepped on separate HIP streams (env of one part beside act of another)")
+    ap.add_argument("--config", default="cfg3", choices=["cfg2", "cfg3", "cfg4", "cfg5"],
+                    help="BASELINE config (cfg3 = the headline; cfg2/cfg4/cfg5 are the other BASELINE workloads)")
     args = ap.parse_args()
+    if args.config != "cfg3":
+        return bench_other(args)
 
     import torch
     import torch.distributed as dist
@@ -181,6 +263,7 @@ def main():
     torch.cuda.set_device(device)
     ms = importlib.import_module("marl-scheduling_amd")
     trainer_mod = importlib.import_module("marl-scheduling_amd.trainer")
+    args.envs = args.envs or 16384
     tr = trainer_mod.Trainer.from_named("cfg3", n_envs=args.envs, update_step=args.update_step, seed=0,
                                         device=device, rank=rank, world_size=world,
                                         rollout_streams=args.rollout_streams)

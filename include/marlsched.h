@@ -106,7 +106,10 @@ typedef struct ms_shape {
     int64_t env_record_bytes;  /* packed per-env state record on the device */
 } ms_shape;
 
-/* Actions for one step of all E envs (device pointers). */
+/* Actions for one step of all E envs (device pointers). acceptor and offer_core both NULL = the
+ * hard-coded agents of HardcodedFixPriceEnvironment (SchedulingEnvironment.py:439-456,
+ * DividedHardcodedAgent Agent.py:622-641, HardcodedModules.py:16-45, 81-109) act in-kernel on the env
+ * stream (fixed prices only), before the auctioneer. */
 typedef struct ms_actions {
     const int8_t* acceptor;    /* [E][N][C] in [0, O]; O = reject (world.py:391-404) */
     const int8_t* offer_core;  /* [E][N][L] core action a: core a+1 if a < C else no offer (world.py:412,450) */

@@ -68,13 +68,20 @@ class BranchingQ(nn.Module):
         advs = F_.linear(out, self.wa, self.ba).view(-1, self.ac_dim, self.n)
         return value.unsqueeze(2) + advs - advs.mean(2, keepdim=True)
 
+    def greedy(self, h1_pre):
+        """get_action's argmax (BranchingDQNModules.py:117-123) without materialising q: value and the
+        advantage mean are constant along a branch, so argmax q = argmax advantage (torch.argmax's
+        first-maximum rule may differ from q's only on exact float ties)."""
+        out = torch.relu(F_.linear(torch.relu(h1_pre), self.w2, self.b2))
+        return torch.argmax(F_.linear(out, self.wa, self.ba).view(-1, self.ac_dim, self.n), dim=2)
+
     def forward(self, x):
         """x [B, obs] float -> q [B, ac_dim, n]."""
         return self.head(F_.linear(x, self.w1, self.b1))
 
-    def forward_compact(self, core_rows, core_owner, n_agents: int, d_acc: int):
-        """Acceptor q of every agent of every replica from the compact observations (module doc):
-        core_rows [E, C, stride] int8, core_owner [E, C] int8 -> q [E * N, C, n] (row e * N + a)."""
+    def layer1_compact(self, core_rows, core_owner, n_agents: int, d_acc: int):
+        """Layer-1 pre-activations of every agent's acceptor row from the compact observations (module doc):
+        core_rows [E, C, stride] int8, core_owner [E, C] int8 -> [E * N, 128] (row e * N + a)."""
         E, C, _ = core_rows.shape
         O = (d_acc - 3) // 2
         foreign = torch.tensor([0.0, -1.0, -1.0] + [-2.0] * (2 * O), device=core_rows.device)
@@ -87,7 +94,11 @@ class BranchingQ(nn.Module):
         mask = own > 0
         rows = (torch.arange(E, device=own.device).unsqueeze(1) * n_agents + own - 1)[mask]
         h1 = h1.index_add(0, rows, part.transpose(0, 1)[mask])
-        return self.head(h1)
+        return h1
+
+    def forward_compact(self, core_rows, core_owner, n_agents: int, d_acc: int):
+        """q [E * N, C, n] of every agent from the compact observations (layer1_compact + head)."""
+        return self.head(self.layer1_compact(core_rows, core_owner, n_agents, d_acc))
 
 
 @dataclass
@@ -218,16 +229,19 @@ class BDQNTrainer:
     def _actions(self, slot, eps):
         """get_action (BranchingDQNModules.py:117-123) of every agent, epsilon-greedy per agent (:181-186)."""
         E, N = self.E, self.N
-        q_acc = self.roles["acc"].q.forward_compact(self.core_rows[slot], self.core_owner[slot], N, self.d_acc)
+        qa = self.roles["acc"].q
+        h1 = dict(acc=qa.layer1_compact(self.core_rows[slot], self.core_owner[slot], N, self.d_acc))
         x_off = self._offer_rows(slot)
-        qs = dict(acc=q_acc, off=self.roles["off"].q(x_off))
-        if self.free:
-            qs["price"] = self.roles["price"].q(x_off)
+        for k in ("off", "price"):
+            if k in self.roles:
+                q = self.roles[k].q
+                h1[k] = F_.linear(x_off, q.w1, q.b1)
         explore = torch.rand((E * N,), generator=self.gen, device=self.device) <= eps
         out = {}
-        for k, q in qs.items():
-            greedy = torch.argmax(q, dim=2)
-            rnd = torch.randint(0, q.shape[2], greedy.shape, generator=self.gen, device=self.device)
+        for k, h in h1.items():
+            q = self.roles[k].q
+            greedy = q.greedy(h)
+            rnd = torch.randint(0, q.n, greedy.shape, generator=self.gen, device=self.device)
             out[k] = torch.where(explore.unsqueeze(1), rnd, greedy).to(torch.int8).view(E, N, -1)
         return out
 

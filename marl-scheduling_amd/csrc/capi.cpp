@@ -216,7 +216,10 @@ int ms_env_reset(ms_env* env, const ms_obs_out* obs, void* stream) {
 int ms_env_step(ms_env* env, const ms_actions* act, const ms_obs_out* obs, const ms_reward_out* rew,
                 const ms_event_out* ev, void* stream) {
     if (!env || !act) return fail(MS_EINVAL, "env/actions is NULL");
-    if (!act->acceptor || !act->offer_core) return fail(MS_EINVAL, "acceptor and offer_core actions are required");
+    if (!act->acceptor != !act->offer_core)
+        return fail(MS_EINVAL, "acceptor and offer_core actions are given together (both NULL: hard-coded agents)");
+    if (!act->acceptor && env->cfg.free_prices)
+        return fail(MS_EINVAL, "the hard-coded agents are fixed-price only (HardcodedFixPriceEnvironment)");
     if (env->cfg.free_prices && !act->offer_price) return fail(MS_EINVAL, "free prices need offer_price actions");
     // a completed earlier round raised a flag on which the reference raises (assert / TypeError):
     // stop stepping, as the reference would (which replica and flag: ms_env_flags)

@@ -742,6 +742,106 @@ __device__ void hardcoded_auctioneer(Rec& R, const Params& P, const M128* s_mc, 
     if (gl < C && nt > 0) s_auct[gl] = (int16_t)kth_bit(ties, my_pick);
 }
 
+// The hard-coded agents of HardcodedFixPriceEnvironment (SchedulingEnvironment.py:439-456):
+// DividedHardcodedAgent.getActions (Agent.py:630-641) asks, per agent, its HardcodedOfferer of
+// every slot (HardcodedModules.py:81-109: a core of minimal ratio, random.sample over the tied
+// cores) and then its HardcodedAcceptor of every core (:16-45: reject unless the agent owns the core
+// and the best offered ratio beats its own job's; random.sample over the tied maxima), all on the
+// env stream before the auctioneer draws. The offer rows of all slots hold the same core pairs, so
+// one candidate mask serves every offerer. Writes the staged action arrays (LDS). Needs LPE >= C.
+template <int LPE>
+__device__ void hardcoded_agents(Rec& R, const Params& P, const M128* s_mc, const M128* s_mr, MtStream<LPE>& rs,
+                                 int8_t* a_acc, int8_t* a_off, const Lanes<LPE>& L) {
+    const int C = P.C, N = P.N, NL = P.NL, O = P.O, gl = L.gl;
+    const int8_t* c_owner = R.core_owner();
+    const int8_t* c_kind = R.core_kind();
+    const int8_t* c_rem = R.core_rem();
+    const int8_t* o_price = R.offer_price();
+    const int8_t* s_rem = R.slot_rem();
+    // offerers: the cores of minimal calculateRewardRatio(prio, rem) (empty cores: -1)
+    uint64_t cand = 0;
+    int mn = 0, md = 1;
+    for (int c = 0; c < C; c++) {
+        const int k = c_kind[c];
+        int num, den;
+        ratio_of(k >= 0 ? R.prio(k) : -1, c_rem[c], num, den);
+        const int lhs = num * md, rhs = mn * den;
+        if (c == 0 || lhs < rhs) {
+            mn = num;
+            md = den;
+            cand = 1ull << c;
+        } else if (lhs == rhs) {
+            cand |= 1ull << c;
+        }
+    }
+    const uint32_t nc = (uint32_t)__popcll(cand);
+    // acceptors: group lane c evaluates core c for its owner (an agent's own job is never empty)
+    int nt = 0;
+    M128 ties{0, 0};
+    if (gl < C && c_owner[gl] > 0) {
+        const int k = c_kind[gl];
+        int on, od;
+        ratio_of(R.prio(k), c_rem[gl], on, od);
+        int bn = 0, bd = 1, kk = 0;
+        bool any = false;
+        for (MaskIter it(mand(s_mc[gl], s_mr[c_owner[gl]])); it.more(); kk++) {
+            const int i = it.next();
+            int num, den;
+            ratio_of(o_price[i], s_rem[i], num, den);
+            const int lhs = num * bd, rhs = bn * den;
+            if (!any || lhs > rhs) {
+                bn = num;
+                bd = den;
+                nt = 0;
+                ties = M128{0, 0};
+                any = true;
+            }
+            if (lhs >= rhs || nt == 0) {
+                nt++;
+                if (kk < 64)
+                    ties.lo |= 1ull << kk;
+                else
+                    ties.hi |= 1ull << (kk - 64);
+            }
+        }
+        // the (-2, -2) pads of the padded list rate -1 (calculateRewardRatio)
+        if (kk < O && (!any || -bd >= bn)) {
+            if (!any || -bd > bn) {
+                bn = -1;
+                bd = 1;
+                nt = 0;
+                ties = M128{0, 0};
+            }
+            for (int q = kk; q < O; q++) {
+                nt++;
+                if (q < 64)
+                    ties.lo |= 1ull << q;
+                else
+                    ties.hi |= 1ull << (q - 64);
+            }
+        }
+        if (!(bn * od > on * bd)) nt = 0;  // max(listOfOfferdRatios) > ownRewardRatio
+    }
+    for (int i = gl; i < N * C; i += LPE) a_acc[i] = (int8_t)O;
+    wave_sync();
+    // the draws, in getActions order
+    for (int a = 0; a < N; a++) {
+        for (int j = 0; j < P.L; j++) {
+            const uint32_t pick = rs.randbelow(nc, L);
+            uint64_t m = cand;
+            for (uint32_t q = 0; q < pick; q++) m &= m - 1;
+            if (gl == 0) a_off[a * P.L + j] = (int8_t)(__ffsll((unsigned long long)m) - 1);
+        }
+        const uint64_t mine = L.ballot(gl < C && nt > 0 && c_owner[gl] == a + 1);
+        for (uint64_t m = mine; m; m &= m - 1) {
+            const int c = __ffsll((unsigned long long)m) - 1;
+            const uint32_t pick = rs.randbelow(L.shfl((uint32_t)nt, c), L);
+            if (gl == c) a_acc[a * C + c] = (int8_t)kth_bit(ties, (int)pick);
+        }
+    }
+    (void)NL;
+}
+
 // ---------------------------------------------------------------------------
 // kernels (the host picks LPE; init / reset / auctioneer / randbelow run one env per wave)
 
@@ -884,7 +984,7 @@ __device__ __forceinline__ void env_round(const Params& P, int64_t E, uint8_t* r
         // the record and the dword-aligned action arrays: one batch of loads, then the LDS stores
         const uint32_t* src_rec = reinterpret_cast<const uint32_t*>(recs + e * (int64_t)P.rec_bytes);
         const int rec_dw = P.rec_bytes / 4;
-        const int8_t* a_src[4] = {io.act_acc + e * N * C, io.act_off + e * NL,
+        const int8_t* a_src[4] = {io.act_acc ? io.act_acc + e * N * C : nullptr, io.act_off ? io.act_off + e * NL : nullptr,
                                   io.act_price ? io.act_price + e * NL : nullptr,
                                   io.act_auct ? io.act_auct + e * C : nullptr};
         int8_t* a_dst[4] = {a_acc, a_off, a_price, a_auct};
@@ -984,6 +1084,10 @@ __device__ __forceinline__ void env_round(const Params& P, int64_t E, uint8_t* r
     MS_MARK(2);
     // ---- auctioneer actions: HardcodedAuctioneerAcceptor (HardcodedModules.py:54-78), asked by the
     //      driver before env.step (trainPPO.py:162); ties broken with random.sample -> _randbelow
+    if (!io.act_acc) {  // HardcodedFixPriceEnvironment: the agents' actions come from the kernel
+        hardcoded_agents<LPE>(R, P, s_mc, s_mr, rs, a_acc, a_off, Lg);
+        wave_sync();
+    }
     if (!io.act_auct) {
         hardcoded_auctioneer<LPE>(R, P, s_mc, s_mr, rs, s_auct, Lg);
     } else {

@@ -20,8 +20,9 @@ aggregated and fully-aggregated envs (``PPOAggregatedFixPriceEnv``,
 kernels around it. ``DQNDividedFixedPricesEnv`` runs the DQN units on the HIP
 kernels of ``dqn.py`` (selectAction, ReplayMemory, optimize_model) with the
 reference's random streams (Python's ``random`` for exploration and memory
-replacement, numpy's global RandomState for the minibatches). The hard-coded-agent
-env is outside this build's hot path and raises ``NotImplementedError``.
+replacement, numpy's global RandomState for the minibatches).
+``HardcodedFixPriceEnvironment`` applies the hard-coded agents' rules on the host at
+E = 1 (the batched env runs them in the kernel).
 
 ``LocallySharedParamsDividedFreePriceEnv`` is an addition. BASELINE cfg3 trains
 free prices with locally shared parameters, which the reference has no class
@@ -495,7 +496,52 @@ def _out_of_scope(name):
     return _Env
 
 
-HardcodedFixPriceEnvironment = _out_of_scope("HardcodedFixPriceEnvironment")
+def _ratio(priority, length):
+    """calculateRewardRatio (HardcodedModules.py:5-13): -1 for the empty (-1) and pad (-2) entries."""
+    return -1 if priority in (-1, -2) or length in (-1, -2) else priority / length
+
+
+class HardcodedFixPriceEnvironment(SchedulingEnv):
+    """HardcodedFixPriceEnvironment (SchedulingEnvironment.py:439-456) at E = 1: the world steps on the device;
+    the agents are DividedHardcodedAgent's (Agent.py:622-641) rules on the returned observations, drawing
+    their tie-breaks (random.sample) from Python's global stream, which is the env's stream. The
+    batched twin runs the same agents inside the env kernel (ms_actions acceptor = offer_core = NULL)."""
+
+    def __init__(self, world, params):
+        super().__init__(world, params)
+
+    def getActionForAllAgents(self, nestedAcceptorNetObservationTensors, nestedOfferNetObservationTensors):
+        w = self.world
+        reject = w.numberOfAgents * w.collectionLength
+        acc_l, off_l = [], []
+        for acc_rows, off_rows in zip(nestedAcceptorNetObservationTensors, nestedOfferNetObservationTensors):
+            offers = []
+            for row in off_rows:  # HardcodedOfferer: a core of lowest ratio (HardcodedModules.py:89-109)
+                v = row.tolist()[:-2]
+                ratios = [_ratio(v[i], v[i + 1]) for i in range(0, len(v), 2)]
+                low = min(ratios)
+                offers.append(random.sample([(c, r) for c, r in enumerate(ratios) if r == low], 1)[0][0])
+            accepts = []
+            for row in acc_rows:  # HardcodedAcceptor (HardcodedModules.py:22-45)
+                v = row.tolist()
+                if v[0] == 0:
+                    accepts.append(reject)
+                    continue
+                offered = [_ratio(v[i], v[i + 1]) for i in range(3, len(v), 2)]
+                best = max(offered)
+                if best > _ratio(v[1], v[2]):
+                    accepts.append(random.sample([(k, r) for k, r in enumerate(offered) if r == best], 1)[0][0])
+                else:
+                    accepts.append(reject)
+            off_l.append(offers)
+            acc_l.append(accepts)
+        return acc_l, off_l
+
+    def saveRewards(self, offerNetRewards, acceptorNetRewards, agentReward):
+        pass
+
+    def updateAgents(self):
+        pass
 
 
 class _DQNAgentHandle(_AgentHandle):

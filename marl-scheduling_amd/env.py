@@ -161,7 +161,10 @@ class BatchedEnv:
         for t in (acceptor, offer_core, offer_price, auctioneer):
             if t is not None:
                 assert t.dtype == torch.int8 and t.is_contiguous() and t.device == self.device
-        assert acceptor.numel() == self.E * self.N * self.C and offer_core.numel() == self.E * self.N * self.L
+        # acceptor and offer_core both None: the hard-coded agents act in the kernel (fixed prices)
+        assert (acceptor is None) == (offer_core is None)
+        if acceptor is not None:
+            assert acceptor.numel() == self.E * self.N * self.C and offer_core.numel() == self.E * self.N * self.L
         if self.free_prices:
             assert offer_price is not None and offer_price.numel() == self.E * self.N * self.L
         if auctioneer is not None:

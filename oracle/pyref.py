@@ -151,6 +151,38 @@ class PyWorld:
                 out.append(self.O)
         return out
 
+    # ---- DividedHardcodedAgent.getActions (Agent.py:630-641) of every agent on the env stream:
+    #      per agent its HardcodedOfferers (HardcodedModules.py:81-109), then its HardcodedAcceptors (:16-45)
+    def hardcoded_agent_actions(self):
+        acc_obs = [[self.acceptor_obs(a, c) for c in range(self.C)] for a in range(self.N)]
+        off_obs = [[self.offer_obs(a, s) for s in range(self.L)] for a in range(self.N)]
+        acc_act, off_act = [], []
+        for a in range(self.N):
+            offers = []
+            for s in range(self.L):
+                row = off_obs[a][s]
+                core_ratios = [ratio(row[2 * c], row[2 * c + 1]) for c in range(self.C)]
+                low = min(core_ratios)
+                cands = [(i, r) for i, r in enumerate(core_ratios) if r == low]
+                offers.append(self.rng.sample(cands, 1)[0][0])
+            accs = []
+            for c in range(self.C):
+                row = acc_obs[a][c]
+                if row[0] == 0:
+                    accs.append(self.O)
+                    continue
+                own = ratio(row[1], row[2])
+                offered = [ratio(row[3 + 2 * k], row[4 + 2 * k]) for k in range(self.O)]
+                best = max(offered)
+                if best > own:
+                    cands = [(i, r) for i, r in enumerate(offered) if r == best]
+                    accs.append(self.rng.sample(cands, 1)[0][0])
+                else:
+                    accs.append(self.O)
+            off_act.append(offers)
+            acc_act.append(accs)
+        return acc_act, off_act
+
     # ---- world.step1 (world.py:295-334) + SchedulingEnv.step (SchedulingEnvironment.py:32-83)
     def step(self, acc_act, off_act, auct_act=None):
         if auct_act is None:

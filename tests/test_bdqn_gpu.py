@@ -152,3 +152,16 @@ def test_bdqn_trainer_cfg5(ms):
     assert tr.flags() == 0 and tr.env.round == 9 and tr.stored == 6
     assert set(tr.last_losses) >= {"acc", "off"}
     assert all(torch.isfinite(v) for v in tr.last_losses.values())
+
+
+def test_greedy_is_the_argmax_of_q(ms):
+    bdqn = _bdqn()
+    torch.manual_seed(9)
+    net = bdqn.BranchingQ(70, 3, 33).cuda()
+    x = torch.randint(-5, 13, (4096, 70), device="cuda").float()
+    with torch.no_grad():
+        q = net(x)
+        g = net.greedy(torch.nn.functional.linear(x, net.w1, net.b1))
+    top2 = q.topk(2, dim=2).values
+    clear = (top2[..., 0] - top2[..., 1]) > 1e-4
+    assert torch.equal(g[clear], q.argmax(2)[clear])

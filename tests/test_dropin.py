@@ -49,8 +49,6 @@ def test_dropin_modules_keep_the_reference_names():
     w = world.World(world_params())
     assert w.round == 0 and w.maxAmountOfOffersToOneAgent == 6 and w.accProbabilities == [0.8, 1.0]
     assert w.acceptedOffers == [] and w.verweilzeiten == []
-    with pytest.raises(NotImplementedError):
-        env_mod.HardcodedFixPriceEnvironment(w, rl_params())
     if not torch.cuda.is_available():  # no CPU fallback
         with pytest.raises(RuntimeError):
             env_mod.PPODividedFixedPriceEnv(w, rl_params())
@@ -321,3 +319,31 @@ def test_dropin_aggregated_env_matches_object_restatement(fully):
     env.updateAgents()
     for u in env._units.values():
         assert u.T == 0 and all(torch.isfinite(p).all() for p in u.group.policy.parameters())
+
+
+@pytest.mark.gpu
+def test_dropin_hardcoded_env_matches_restatement():
+    """trainPPO.py's loop with hardcodedAgents (SchedulingEnvironment.py:439-456) against the restatement's
+    hard-coded agents on the same global stream."""
+    from oracle.pyref import PyWorld
+
+    world, env_mod, _ = _mods()
+    wp = world_params(N=3, C=4, L=2, ep=25)
+    seed = 77
+    random.seed(seed)
+    w = world.World(wp)
+    env = env_mod.HardcodedFixPriceEnvironment(w, rl_params())
+    pw = PyWorld(_pyref_config(wp, False), seed)
+    acc_obs, off_obs, auct_obs = env.reset()
+    for t in range(100):
+        acc, off = env.getActionForAllAgents(acc_obs, off_obs)
+        r_acc, r_off = pw.hardcoded_agent_actions()
+        assert (acc, off) == (r_acc, r_off), t
+        auct = w.auctioneer.getAuctioneerAction(auct_obs)
+        out = env.step(off, acc, auct)
+        (r_obs, _, _, _) = pw.step(r_acc, r_off, pw.auctioneer_actions())
+        acc_obs, off_obs, auct_obs = out[0], out[1], out[2]
+        assert _as_lists(acc_obs) == r_obs[0], t
+        assert random.getstate() == pw.rng.getstate(), t
+        env.saveRewards(out[3], out[4], out[6])
+        env.updateAgents()
