@@ -15,7 +15,8 @@ import torch  # noqa: F401  (load torch's HIP runtime before the library)
 from . import abi
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libmarlsched.so")
+# MARLSCHED_LIB: an experiment variant built by tools/build_variant.sh (profiling runs only)
+LIB_PATH = os.environ.get("MARLSCHED_LIB") or os.path.join(HERE, "libmarlsched.so")
 
 
 class MarlSchedError(RuntimeError):

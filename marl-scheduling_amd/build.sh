@@ -5,12 +5,12 @@
 # copied tree keeps no trustworthy timestamps). MS_CLEAN=1 rebuilds everything.
 set -euo pipefail
 HERE="$(cd "$(dirname "${BASH_SOURCE[0]}")" && pwd)"
-OUT="${HERE}/libmarlsched.so"
+OUT="${MS_OUT:-${HERE}/libmarlsched.so}"   # MS_OUT / MS_OBJDIR / MS_EXTRA_FLAGS: experiment variants (tools/)
 HIPCC="${HIPCC:-/opt/rocm/bin/hipcc}"
 ARCH="${MS_OFFLOAD_ARCH:-gfx950}"
 FLAGS=(-O3 -std=c++17 -fPIC --offload-arch="${ARCH}" -Wall -Wno-unused-function
-       -I"${HERE}/../include")
-OBJDIR="${HERE}/build"
+       -I"${HERE}/../include" ${MS_EXTRA_FLAGS:-})
+OBJDIR="${MS_OBJDIR:-${HERE}/build}"
 [[ "${MS_CLEAN:-0}" == 1 ]] && rm -rf "${OBJDIR}"
 mkdir -p "${OBJDIR}"
 HEADERS=("${HERE}/csrc/ms_layout.h" "${HERE}/csrc/ms_ppo.h" "${HERE}/csrc/ms_dqn.h" "${HERE}/csrc/ms_common.h" "${HERE}/../include/marlsched.h")
