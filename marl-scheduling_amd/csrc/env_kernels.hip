@@ -934,8 +934,11 @@ __global__ void __launch_bounds__(64) k_env_reset(Params P, const uint8_t* recs,
 constexpr int kLiabPrefetch = 4;  // newest chain entries loaded ahead per core that may terminate
 
 // One round of SchedulingEnv.step (SchedulingEnvironment.py:32-83): group g of block b steps env
-// b * (64 / LPE) + g. Each group owns a P.s_total-byte slice of the block's LDS.
-template <int LPE>
+// b * (64 / LPE) + g. Each group owns a P.s_total-byte slice of the block's LDS. EXT: the kernel
+// variant with the optional features (hard-coded agents when io.act_acc == NULL, episode metrics,
+// compact acceptor observations); the plain training round is compiled without them, so it carries
+// none of their registers (the compact emission alone costs ~90 spilled SGPRs).
+template <int LPE, bool EXT>
 __device__ __forceinline__ void env_round(const Params& P, int64_t E, uint8_t* recs, uint32_t* mt, Liab* liab,
                                           const StepIO& io, int64_t slot) {
     extern __shared__ __align__(16) uint8_t smem_all[];
@@ -1055,8 +1058,11 @@ __device__ __forceinline__ void env_round(const Params& P, int64_t E, uint8_t* r
     int8_t* o_price = R.offer_price();
     Liab* my_liab = liab + e * (int64_t)C * P.cap;
     // this round's episode accumulators (trainPPO.py:172-187): slot of episode round / episodeLength
-    ms_env_metrics* mx = (io.metrics && active) ? io.metrics + (int64_t)((round / P.ep_len) % io.metrics_slots) * E + e
-                                                : nullptr;
+    const bool HC = EXT && io.act_acc == nullptr;
+    constexpr bool MX = EXT;
+    ms_env_metrics* mx = (MX && io.metrics && active)
+                             ? io.metrics + (int64_t)((round / P.ep_len) % io.metrics_slots) * E + e
+                             : nullptr;
 
     // ---- issue the dependent loads early: the MT window at mti (a peek: no twist
     //      yet) and the newest liability entries of every core that may terminate
@@ -1084,7 +1090,7 @@ __device__ __forceinline__ void env_round(const Params& P, int64_t E, uint8_t* r
     MS_MARK(2);
     // ---- auctioneer actions: HardcodedAuctioneerAcceptor (HardcodedModules.py:54-78), asked by the
     //      driver before env.step (trainPPO.py:162); ties broken with random.sample -> _randbelow
-    if (!io.act_acc) {  // HardcodedFixPriceEnvironment: the agents' actions come from the kernel
+    if (HC) {  // HardcodedFixPriceEnvironment: the agents' actions come from the kernel
         hardcoded_agents<LPE>(R, P, s_mc, s_mr, rs, a_acc, a_off, Lg);
         wave_sync();
     }
@@ -1197,7 +1203,7 @@ __device__ __forceinline__ void env_round(const Params& P, int64_t E, uint8_t* r
                 off_r[i] = (float)prio1;
                 price_r[i] = pc;
             }
-            if (mx) {
+            if (MX && mx) {
                 m_add(&mx->price_sum[nk], price);  // prices.append((offeredReward, jobKind)) trainPPO.py:172-174
                 m_add(&mx->price_count[nk], 1);
                 if (recip != 0) {  // formerCore* = the core's job before this round's execution
@@ -1222,7 +1228,7 @@ __device__ __forceinline__ void env_round(const Params& P, int64_t E, uint8_t* r
                 io.ev_acc[e * C + c] = ar;
             }
         }
-        if (mx && n_q > 0) {  // statistics.mean of the round's qualities, then collected per round
+        if (MX && mx && n_q > 0) {  // statistics.mean of the round's qualities, then collected per round
             m_add(&mx->quality_sum, q_sum / n_q);
             m_add(&mx->quality_rounds, 1);
             m_add(&mx->acception_amount, n_q);
@@ -1249,7 +1255,7 @@ __device__ __forceinline__ void env_round(const Params& P, int64_t E, uint8_t* r
                 tr.prio = (int8_t)R.prio(kind);
                 tr.init_len = (int8_t)R.len(kind);
                 tr.dwell = round - c_birth[c];
-                if (mx) {  // verweilzeiten (world.py:350-357); env.terminationRevenues (Reward.py:193)
+                if (MX && mx) {  // verweilzeiten (world.py:350-357); env.terminationRevenues (Reward.py:193)
                     m_add(&mx->dwell_sum[kind], tr.dwell - 1);
                     m_add(&mx->dwell_count[kind], 1);
                     if (!P.free_prices) m_add(&mx->termination_revenue, (long long)gen);
@@ -1418,7 +1424,7 @@ __device__ __forceinline__ void env_round(const Params& P, int64_t E, uint8_t* r
             copy_out<LPE>(WtOut(base, E * per_env * 4), e * per_env * 4, reinterpret_cast<uint32_t*>(base) + e * per_env,
                           reinterpret_cast<const uint32_t*>(src), per_env, gl);
         };
-        if (mx) {  // the driver's reward accumulators (trainPPO.py:176-183)
+        if (MX && mx) {  // the driver's reward accumulators (trainPPO.py:176-183)
             if (gl < N) {
                 int ar = 0, orw = 0;
                 float pr = 0.f;
@@ -1461,8 +1467,8 @@ __device__ __forceinline__ void env_round(const Params& P, int64_t E, uint8_t* r
     MS_MARK(10);
     build_masks<LPE>(R, P, s_mc, s_mr, gl);
     MS_MARK(11);
-    emit_obs<LPE>(R, P, s_mc, s_mr, scratch, io.obs_acc, io.obs_off, io.obs_auct, io.obs_crow, io.obs_cown, e, E, active,
-                  gl);
+    emit_obs<LPE>(R, P, s_mc, s_mr, scratch, io.obs_acc, io.obs_off, io.obs_auct, EXT ? io.obs_crow : nullptr,
+                  EXT ? io.obs_cown : nullptr, e, E, active, gl);
     MS_MARK(12);
 #ifdef MS_PHASE_TIMING
     if (lane == 0)
@@ -1473,7 +1479,7 @@ __device__ __forceinline__ void env_round(const Params& P, int64_t E, uint8_t* r
 // One round for the 64 / LPE envs of wave slot blockIdx.x. (A persistent loop over several slots
 // per wave would let one slot's observation stores drain under the next slot's compute, but the
 // compiler then keeps the whole round's state live across iterations: 3x the VGPRs.)
-template <int LPE>
+template <int LPE, bool EXT>
 __global__ void __launch_bounds__(64, 4) k_env_step(Params P, int64_t E, uint8_t* recs, uint32_t* mt, Liab* liab,
                                                  StepIO io) {
 #ifdef MS_PHASE_TIMING
@@ -1482,7 +1488,7 @@ __global__ void __launch_bounds__(64, 4) k_env_step(Params P, int64_t E, uint8_t
     // per-wave start / end for the bench's launch span (optional; plain stores, no shared address,
     // nothing held across the round: the kernel sits at 4 waves per SIMD with no register to spare)
     if (io.span && threadIdx.x == 0) io.span[2 * blockIdx.x] = __builtin_amdgcn_s_memrealtime();
-    env_round<LPE>(P, E, recs, mt, liab, io, blockIdx.x);
+    env_round<LPE, EXT>(P, E, recs, mt, liab, io, blockIdx.x);
     if (io.span && threadIdx.x == 0) io.span[2 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime();
 #ifdef MS_PHASE_TIMING
     if (threadIdx.x == 0) {
@@ -1605,14 +1611,18 @@ static hipError_t launch_step_t(const Params& P, int64_t E, uint8_t* recs, uint3
     constexpr int G = kWave / LPE;
     const int64_t blocks = (E + G - 1) / G;
     const size_t lds = (size_t)P.s_total * G > 4 * kMtN ? (size_t)P.s_total * G : 4 * kMtN;  // >= one MT block
-    hipLaunchKernelGGL((k_env_step<LPE>), dim3((unsigned)blocks), dim3(kWave), lds, s, P, E, recs, mt, liab, io);
+    const bool ext = io.act_acc == nullptr || io.metrics != nullptr || io.obs_crow != nullptr || io.obs_cown != nullptr;
+    auto kern = ext ? k_env_step<LPE, true> : k_env_step<LPE, false>;
+    hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(kWave), lds, s, P, E, recs, mt, liab, io);
     return hipGetLastError();
 }
 
 hipError_t launch_env_step(const Params& P, int64_t E, uint8_t* recs, uint32_t* mt, Liab* liab, const StepIO& io,
                            hipStream_t s) {
     switch (lanes_per_env(P)) {
+#if MS_MIN_LPE <= 8
         case 8: return launch_step_t<8>(P, E, recs, mt, liab, io, s);
+#endif
         case 16: return launch_step_t<16>(P, E, recs, mt, liab, io, s);
         case 32: return launch_step_t<32>(P, E, recs, mt, liab, io, s);
         default: return launch_step_t<64>(P, E, recs, mt, liab, io, s);

@@ -41,8 +41,12 @@ def main(E=16384, steps=30):
         p = torch.randint(0, 13, (E, N, L), device="cuda", generator=g, dtype=torch.int32).to(torch.int8)
         acts.append((a, o, p))
     full = env.obs_buffers()
+    comp = env.compact_obs_buffers()
     rew = env.reward_buffers()  # preallocated: the loop must not be host-bound
     for name, obs in [("acceptor+offer obs", full), ("offer obs only", dict(offer=full["offer"])),
+                      ("offer + compact acceptor", dict(offer=full["offer"], core_rows=comp["core_rows"],
+                                                        core_owner=comp["core_owner"])),
+                      ("compact acceptor only", dict(core_rows=comp["core_rows"], core_owner=comp["core_owner"])),
                       ("no obs", dict(acceptor=None)), ("acceptor+offer obs", full)]:
         print("%-22s %7.1f us/step" % (name, timed(env, acts, obs, rew, steps)))
 
