@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define MS_ABI_VERSION 5
+#define MS_ABI_VERSION 6
 
 #define MS_MAX_KINDS 16
 #define MS_MAX_AGENTS 64
@@ -354,6 +354,10 @@ typedef struct ms_ppo_batch {
     const int8_t* common_row;
     /* row pitch of returns in floats (0 = the number of groups): returns[(t*E + e)*ld + g] */
     int32_t returns_ld;
+    /* 0: rows of 4 bytes (stride 4, nets of <= 4 inputs and <= 32 actions, no common_row) are keyed:
+     * each group's distinct rows get one forward and one backward pass, and each row adds its loss
+     * derivatives to its distinct row's int64 fixed-point sums (2^-28); -1: every row on its own */
+    int32_t row_keys;
 } ms_ppo_batch;
 
 typedef struct ms_ppo_grads {  /* device outputs, [G][...] like the weights */

@@ -79,7 +79,7 @@ def _load():
         fn = getattr(L, name)
         fn.restype = res
         fn.argtypes = args
-    if L.ms_abi_version() != 5:
+    if L.ms_abi_version() != 6:
         raise ImportError("libmarlsched.so ABI version mismatch")
     return L
 

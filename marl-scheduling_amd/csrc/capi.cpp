@@ -9,6 +9,8 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <algorithm>
+#include <cmath>
 #include <vector>
 
 #include "ms_layout.h"
@@ -31,6 +33,7 @@ hipError_t launch_returns(const float*, int, int64_t, int64_t, double, float*, h
 hipError_t launch_unit_returns(const void*, int, int, int64_t, int, const int32_t*, int, double, float*, hipStream_t);
 hipError_t launch_ppo_grad(const PpoArgs&, const GradOut&, hipStream_t);
 int ppo_param_count(int D, int A);
+int ppo_partial_rows(int n_chunks, bool keyed);
 hipError_t launch_aggregate_obs(const AggArgs&, hipStream_t);
 hipError_t launch_decode_aggregated(const int32_t*, long long, int, int, int, int, int8_t*, int8_t*, int*, hipStream_t);
 hipError_t launch_adam(const AdamTensor*, int, const double*, int, int64_t, double, double, double, hipStream_t);
@@ -518,11 +521,37 @@ int ms_offer_act_free(const ms_mlp_params* core, const ms_mlp_params* price, con
     return MS_OK;
 }
 
-size_t ms_ppo_workspace_bytes(const ms_mlp_params* a, int64_t rows) {
-    if (!a || rows < 1 || a->n_groups < 1) return 0;
+// keyed rows (ppo_kernels.hip) for nets of at most 4 inputs and 32 actions: the byte sizes of the
+// table arrays that follow the partial vectors in the workspace
+static bool ppo_keyable(const ms_mlp_params* a) { return a->in_dim <= 4 && a->n_actions <= 32; }
+struct KeyWs {
+    size_t mark, idx, act, olp, ret, rank, sorted, n, flag, part, pcnt, ploss, fwd;
+    size_t total() const {
+        return align256(mark) + align256(idx) + align256(act) + align256(olp) + align256(ret) + align256(rank) +
+               align256(sorted) + align256(n) + align256(flag) + align256(part) + align256(pcnt) + align256(ploss) +
+               align256(fwd);
+    }
+    static size_t align256(size_t b) { return (b + 255) & ~(size_t)255; }
+};
+static KeyWs key_ws(const ms_mlp_params* a, int64_t rows) {
+    const size_t G = (size_t)a->n_groups, nt16 = 16 * (size_t)((a->n_actions + 15) / 16), gr = G * (size_t)rows;
+    const size_t dense = G * ms::kKeyDense, ranks = G * ms::kKeyMaxRanks, pr = ranks * ms::kKeyScanBlocks;
+    return KeyWs{dense, gr * 4, gr, gr * 4, gr * 4, dense * 4, ranks * 4, G * 4, G * 4, pr * (nt16 + 1) * 8, pr * 4,
+                 G * ms::kKeyScanBlocks * 16, ranks * (nt16 + 4) * 4};
+}
+static size_t align256(size_t b) { return (b + 255) & ~(size_t)255; }
+static size_t ppo_partials_bytes(const ms_mlp_params* a, int64_t rows) {
     int ct, nc;
     ppo_split(rows, a->n_groups, &ct, &nc);
-    return (size_t)a->n_groups * (nc / 4) * ms::ppo_param_count(a->in_dim, a->n_actions) * sizeof(float);  // per block
+    return align256((size_t)a->n_groups * ms::ppo_partial_rows(nc, ppo_keyable(a)) *
+                    ms::ppo_param_count(a->in_dim, a->n_actions) * sizeof(float));  // one vector per block
+}
+
+size_t ms_ppo_workspace_bytes(const ms_mlp_params* a, int64_t rows) {
+    if (!a || rows < 1 || a->n_groups < 1) return 0;
+    size_t b = ppo_partials_bytes(a, rows);
+    if (ppo_keyable(a)) b += key_ws(a, rows).total();
+    return b;
 }
 
 int ms_ppo_grad(const ms_mlp_params* a, const ms_mlp_params* c, const ms_ppo_batch* b, float eps_clip, void* ws,
@@ -562,6 +591,33 @@ int ms_ppo_grad(const ms_mlp_params* a, const ms_mlp_params* c, const ms_ppo_bat
     p.P = ms::ppo_param_count(p.D, p.A);
     p.eps_clip = eps_clip;
     p.inv_R = 1.0f / (float)R;
+    if (ppo_keyable(a) && b->row_keys == 0) {
+        const KeyWs k = key_ws(a, R);
+        uint8_t* w = (uint8_t*)ws + ppo_partials_bytes(a, R);
+        auto take = [&w](size_t bytes) {
+            uint8_t* q = w;
+            w += KeyWs::align256(bytes);
+            return q;
+        };
+        p.key_mark = take(k.mark);
+        p.key_idx = (uint32_t*)take(k.idx);
+        p.key_act = (int8_t*)take(k.act);
+        p.key_olp = (float*)take(k.olp);
+        p.key_ret = (float*)take(k.ret);
+        p.key_rank = (int32_t*)take(k.rank);
+        p.key_sorted = (uint32_t*)take(k.sorted);
+        p.key_n = (int32_t*)take(k.n);
+        p.key_flag = (int32_t*)take(k.flag);
+        p.key_part = (long long*)take(k.part);
+        p.key_pcnt = (uint32_t*)take(k.pcnt);
+        p.key_ploss = (float*)take(k.ploss);
+        p.key_fwd = (float*)take(k.fwd);
+        p.key_nbs = ms::kKeyScanBlocks;
+        // ranks per scan pass: the LDS sums (int64 per action + V - G, a uint32 count) in 147 KB
+        p.key_cap = (147 * 1024) / ((16 * ((a->n_actions + 15) / 16) + 1) * 8 + 4);
+        // |term| * 2^28 * R < 2^62: a slot's int64 sum cannot overflow
+        p.key_bound = (float)std::min(1e30, std::ldexp(1.0, 62) / ms::kKeyFx / (double)R);
+    }
     ms::GradOut go{g->w1, g->b1, g->w2, g->b2, g->w3, g->b3, g->cw1, g->cb1, g->cw2, g->cb2, g->cw3, g->cb3, g->loss};
     HIP_TRY(ms::launch_ppo_grad(p, go, (hipStream_t)stream));
     return MS_OK;

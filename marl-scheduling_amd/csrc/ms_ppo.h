@@ -20,7 +20,35 @@ struct PpoArgs {
     long long E, R;
     int chunk_tiles, n_chunks, P;
     float eps_clip, inv_R;
+    int part_rows, part_off;  // partial vectors per group, this launch's first one
+    // keyed rows (rows of <= 4 bytes whose values lie in [-8, 24), ppo_kernels.hip): a row's dense
+    // index packs its bytes 5 bits each; the distinct rows of a group, ranked by dense index, get
+    // one forward and one backward pass, and every row adds its loss derivatives to its rank's
+    // int64 fixed-point sums (per scan block, in LDS)
+    uint8_t* key_mark;     // [G][kKeyDense] dense index occurs
+    uint32_t* key_idx;     // [G][R] the rows' dense indices, actions, old log-probs, returns (contiguous)
+    int8_t* key_act;
+    float* key_olp;
+    float* key_ret;
+    int32_t* key_rank;     // [G][kKeyDense] dense index -> rank
+    uint32_t* key_sorted;  // [G][kKeyMaxRanks] rank -> row word
+    int32_t* key_n;        // [G] distinct rows, -1: the group takes the tile path
+    int32_t* key_flag;     // [G] set when a row is out of range or its terms too large (tile path)
+    long long* key_part;   // [G][scan blocks][kKeyMaxRanks][16*NT + 1] per scan block: sums of
+                           //   d min(surr) / d ratio * ratio per action, of V - G
+    uint32_t* key_pcnt;    // [G][scan blocks][kKeyMaxRanks] rows per rank
+    float* key_ploss;      // [G][scan blocks][4] the scan blocks' loss sums
+    float* key_fwd;        // [G][kKeyMaxRanks][16*NT + 4] clamped log-probs, V, entropy per rank
+    float key_bound;       // a larger |term| sends the group to the tile path (keeps the sums in int64)
+    int key_nbs;           // scan blocks per group
+    int key_cap;           // ranks per scan pass (LDS)
 };
+
+constexpr int kKeyDense = 1 << 20;   // 4 bytes x 5 bits
+constexpr int kKeyMaxRanks = 4096;   // distinct rows per group, more: tile path
+constexpr int kKeyBlocks = 32;       // blocks per group of the rank passes (forward, backward)
+constexpr int kKeyScanBlocks = 32;   // blocks per group of the row scan
+constexpr double kKeyFx = 268435456.0;           // 2^28: fixed-point scale of the keyed sums
 
 constexpr int kAdamMaxTensors = 16, kAdamMaxGroups = 4;
 struct AdamTensor {  // layout of ms_adam_tensor

@@ -26,6 +26,8 @@
 #include <hip/hip_runtime.h>
 #include <math.h>
 
+#include <algorithm>
+
 #include "../../include/marlsched.h"
 #include "ms_common.h"
 #include "ms_ppo.h"
@@ -118,8 +120,13 @@ struct BoolC {
     static constexpr bool value = B;
 };
 
-template <int NQ, int NT, bool CM>
+// kernel modes: every row on its own; rows equal to one common row; keyed rows (the backward and
+// the forward of a group's distinct rows, k_key_scan sums the rows' loss derivatives in between)
+enum GradMode { kPlain = 0, kCommonRow = 1, kKeyBack = 3, kKeyFwd = 4 };
+
+template <int NQ, int NT, int MODE>
 struct GradLds {
+    static constexpr bool CM = MODE == kCommonRow;
     static constexpr int S1 = (NQ + 1) / 2;           // 32-input k-steps of layer 1 (16*NQ inputs)
     static constexpr int W1B = 32 * S1 + 8;           // bf16 pitch of a split W1 row (+16 B: no conflicts)
     static constexpr int XPD = (NQ & 1) ? 4 * NQ + 6 : 4 * NQ + 2;  // staged input row pitch (dwords)
@@ -141,15 +148,14 @@ struct GradLds {
 
 // NQ = 16-wide input tiles with 16*NQ > D, NT = ceil(A/16) action tiles. A block owns 4 chunks
 // of one group and has L::WPB waves.
-template <int NQ, int NT, bool COMMON>
-__global__ void __launch_bounds__((64 * GradLds<NQ, NT, COMMON>::WPB), ((NQ * NT >= 32) ? 1 : 2)) k_ppo_grad(PpoArgs p) {
-    using L = GradLds<NQ, NT, COMMON>;
+template <int NQ, int NT, int MODE>
+__global__ void __launch_bounds__((64 * GradLds<NQ, NT, MODE>::WPB), ((NQ * NT >= 32) ? 1 : 2)) k_ppo_grad(PpoArgs p) {
+    using L = GradLds<NQ, NT, MODE>;
     constexpr int TP = L::TP, TP2 = L::TP2, XPD = L::XPD, S1 = L::S1, W1B = L::W1B;
     constexpr int NTH = 64 * L::WPB, CPW = 4 / L::WPB;  // threads per block, chunks per wave
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int g4 = lane >> 4;  // MFMA k-group / C-row group
     const int j = lane & 15;   // batch row within the tile (C column)
-    const int blocks_per_group = p.n_chunks >> 2;
     // groups interleaved over the block index: the G groups' blocks of the same rows run at the
     // same time, so the rollout lines they share (rows [r][0..U) of states, actions, log-probs)
     // come from HBM once and hit in the Infinity Cache for the other groups
@@ -579,7 +585,96 @@ __global__ void __launch_bounds__((64 * GradLds<NQ, NT, COMMON>::WPB), ((NQ * NT
         pre_G = p.ret[(size_t)r * p.ret_ld + grp];
     };
 
-    if (!COMMON) {
+    if constexpr (MODE == kKeyFwd || MODE == kKeyBack) {
+        // ---- keyed rows, the passes over one group's distinct rows in rank order (16 ranks per
+        //      tile, a contiguous range of tiles per wave). Fwd: the forward values of every rank.
+        //      Back: the ranks' summed loss derivatives (k_key_scan's block sums, added in block
+        //      order) through one backward pass per rank, exactly as the common row's virtual tile
+        //      (the backward is linear in them)
+        constexpr int KA = 16 * NT + 1, KF = 16 * NT + 4;
+        const bool keyed = p.key_n[grp] >= 0 && p.key_flag[grp] == 0;
+        const int n = keyed ? p.key_n[grp] : 0;
+        const int tiles = (n + 15) / 16;
+        const int wpg = (int)(gridDim.x / p.G) * L::WPB;
+        const int tpw = (tiles + wpg - 1) / wpg;
+        const int st0 = (blk * L::WPB + wave) * tpw, st1 = min(st0 + tpw, tiles);
+        const size_t gr = (size_t)grp * kKeyMaxRanks;
+        const double fx_lp = -(double)p.inv_R / kKeyFx, fx_v = (double)p.inv_R / kKeyFx;
+        int otile = 0;
+        for (int tile = st0; tile < st1; tile++) {
+            const int rank = 16 * tile + j;
+            const bool occ = rank < n;
+            const uint32_t kw = occ ? p.key_sorted[gr + rank] : 0u;
+            uint32_t xr[S1][2];
+#pragma unroll
+            for (int s = 0; s < S1; s++) xr[s][0] = xr[s][1] = 0u;
+            xr[0][0] = g4 == 0 ? kw : 0u;  // a stride-4 row is dword 0 of k-step 0
+            if constexpr (MODE == kKeyFwd) {
+                Fwd f;
+                forward(xr, f);
+                if (occ) {
+                    float* dst = p.key_fwd + (gr + rank) * KF;
+#pragma unroll
+                    for (int t = 0; t < NT; t++)
+#pragma unroll
+                        for (int q = 0; q < 4; q++) dst[16 * t + 4 * g4 + q] = f.cl[t][q];
+                    if (g4 == 0) {
+                        dst[16 * NT] = f.V;
+                        dst[16 * NT + 1] = f.ent;
+                    }
+                }
+            } else {
+                long long acc[NT][4], accv = 0;
+                uint32_t cnt = 0;
+#pragma unroll
+                for (int t = 0; t < NT; t++) acc[t][0] = acc[t][1] = acc[t][2] = acc[t][3] = 0;
+                if (occ) {
+                    for (int b = 0; b < p.key_nbs; b++) {
+                        const size_t pr = ((size_t)grp * p.key_nbs + b) * kKeyMaxRanks + rank;
+                        const long long* ac = p.key_part + pr * KA;
+#pragma unroll
+                        for (int t = 0; t < NT; t++)
+#pragma unroll
+                            for (int q = 0; q < 4; q++)
+                                if (16 * t + 4 * g4 + q < A) acc[t][q] += ac[16 * t + 4 * g4 + q];
+                        accv += ac[16 * NT];
+                        cnt += p.key_pcnt[pr];
+                    }
+                }
+                float vsum[NT][4];
+#pragma unroll
+                for (int t = 0; t < NT; t++)
+#pragma unroll
+                    for (int q = 0; q < 4; q++) vsum[t][q] = (float)((double)acc[t][q] * fx_lp);
+                const float gv = (float)((double)accv * fx_v);
+                const float gh = -0.01f * p.inv_R * (float)cnt;
+                const int half = otile & 1;
+                tile_step(BoolC<true>{}, xr, 0, 0.f, 0.f, true, half, half == 1, vsum, gh, gv);
+                otile++;
+            }
+        }
+        if constexpr (MODE == kKeyFwd) {
+            return;
+        } else {
+            if (otile & 1) {  // the last pair's second half: a tile of zero derivatives
+                uint32_t xr[S1][2];
+#pragma unroll
+                for (int s = 0; s < S1; s++) xr[s][0] = xr[s][1] = 0u;
+                tile_step(BoolC<true>{}, xr, 0, 0.f, 0.f, true, 1, true, zero_vs, 0.f, 0.f);
+            }
+            if (keyed && blk == 0 && wave == 0 && lane == 0) {  // the scan blocks' loss sums, in block order
+                for (int b = 0; b < p.key_nbs; b++) {
+                    const float* ls = p.key_ploss + ((size_t)grp * p.key_nbs + b) * 4;
+                    l_min += ls[0];
+                    l_mse += ls[1];
+                    l_ent += ls[2];
+                }
+            }
+        }
+    } else if constexpr (MODE == kPlain) {
+        // behind the keyed passes (key_n set): only the groups they could not take
+        const int tile_end_g = (p.key_n && p.key_n[grp] >= 0 && p.key_flag[grp] == 0) ? tile0 : tile_end;
+        const int tile_end = tile_end_g;
         // rows past the end load row 0's values: their loss weight is 0, so every derivative of
         // theirs is exactly 0 (all inputs finite)
         auto row_of_tile = [&](int tile) { return tile * 16 + j < R ? tile * 16 + j : 0; };
@@ -833,7 +928,7 @@ __global__ void __launch_bounds__((64 * GradLds<NQ, NT, COMMON>::WPB), ((NQ * NT
         }
         __syncthreads();
     }
-    float* outp = p.partials + ((size_t)grp * blocks_per_group + blk) * p.P;
+    float* outp = p.partials + ((size_t)grp * p.part_rows + p.part_off + blk) * p.P;
     for (int i = tid; i < p.P; i += NTH) outp[i] = acc[i];
 }
 
@@ -873,33 +968,271 @@ __global__ void __launch_bounds__(256) k_ppo_reduce(const float* __restrict__ pa
     if (dst) dst[(size_t)grp * k + (i - base)] = s;
 }
 
-template <int NQ, int NT, bool CM>
-static hipError_t launch_grad_cm(const PpoArgs& a, hipStream_t st) {
-    using L = GradLds<NQ, NT, CM>;
+template <int NQ, int NT, int MODE>
+static hipError_t launch_grad_cm(const PpoArgs& a, unsigned blocks_per_group, hipStream_t st) {
+    using L = GradLds<NQ, NT, MODE>;
     const size_t lds = sizeof(float) * L::lds_floats;
     if (lds > 160 * 1024 || (size_t)a.P > (size_t)L::lds_floats) return hipErrorInvalidValue;  // partial in LDS
-    hipLaunchKernelGGL((k_ppo_grad<NQ, NT, CM>), dim3((unsigned)(a.G * (a.n_chunks / 4))), dim3(64 * L::WPB), lds, st,
+    hipLaunchKernelGGL((k_ppo_grad<NQ, NT, MODE>), dim3((unsigned)a.G * blocks_per_group), dim3(64 * L::WPB), lds, st,
                        a);
     return hipGetLastError();
 }
 
-// the common-row path for inputs up to 128 bytes (its scan holds a row per lane in registers)
-template <int NQ, int NT>
-static hipError_t launch_grad_t(const PpoArgs& a, hipStream_t st) {
-    if constexpr (NQ <= 8) {
-        if (a.common && a.stride >= 16) {
-            using L = GradLds<NQ, NT, true>;
-            if (sizeof(float) * L::lds_floats <= 160 * 1024) return launch_grad_cm<NQ, NT, true>(a, st);
+// ---- keyed rows (nets of <= 4 inputs on 4-byte rows, e.g. the price chooser PPOmodules.py:327-330:
+//      a few hundred distinct rows among millions). A row's dense index packs its bytes + 8, 5 bits
+//      each; a group with a byte outside [-8, 24) takes the tile path.
+__device__ __forceinline__ bool key_index(uint32_t w, int D, uint32_t& idx) {
+    bool ok = true;
+    idx = 0;
+#pragma unroll
+    for (int b = 0; b < 4; b++) {
+        if (b < D) {
+            const int v = (int)(int8_t)(w >> (8 * b)) + 8;
+            ok &= (unsigned)v < 32u;
+            idx |= (uint32_t)(v & 31) << (5 * b);
         }
     }
-    return launch_grad_cm<NQ, NT, false>(a, st);
+    return ok;
 }
+
+// one pass over the rows: every group's (dense index, action, old log-prob, return) to contiguous
+// per-group arrays (so the scan reads whole lines instead of one unit's bytes of [R][U] rows), and
+// every row's dense index marked (a load first: the frequent rows' marks are set early; every writer
+// of a mark writes the same byte). Thread = row, all groups.
+__global__ void __launch_bounds__(256) k_key_gather(PpoArgs p) {
+    const uint32_t kmask = p.D >= 4 ? 0xffffffffu : ((1u << (8 * p.D)) - 1u);
+    constexpr int GB = 8;  // groups per batch: all their loads are issued before any store
+    for (long long r = (long long)blockIdx.x * 256 + threadIdx.x; r < p.R; r += (long long)gridDim.x * 256) {
+        for (int g0 = 0; g0 < p.G; g0 += GB) {
+            uint32_t w[GB], idx[GB];
+            int8_t act[GB];
+            float olp[GB], ret[GB];
+            uint8_t mk[GB];
+#pragma unroll
+            for (int k = 0; k < GB; k++) {
+                const int grp = min(g0 + k, p.G - 1);
+                const int u = p.unit_of_group[grp];
+                w[k] = *reinterpret_cast<const uint32_t*>(p.states + (r * p.U + u) * p.stride) & kmask;
+                act[k] = p.actions[(size_t)r * p.U + u];
+                olp[k] = p.old_lp[(size_t)r * p.U + u];
+                ret[k] = p.ret[(size_t)r * p.ret_ld + grp];
+            }
+#pragma unroll
+            for (int k = 0; k < GB; k++) {
+                const int grp = min(g0 + k, p.G - 1);
+                if (!key_index(w[k], p.D, idx[k]))
+                    __hip_atomic_store(p.key_flag + grp, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                mk[k] = p.key_mark[(size_t)grp * kKeyDense + idx[k]];
+            }
+#pragma unroll
+            for (int k = 0; k < GB; k++) {
+                if (g0 + k >= p.G) break;
+                const int grp = g0 + k;
+                if (mk[k] == 0) p.key_mark[(size_t)grp * kKeyDense + idx[k]] = 1;
+                const size_t c = (size_t)grp * p.R + r;
+                p.key_idx[c] = idx[k];
+                p.key_act[c] = act[k];
+                p.key_olp[c] = olp[k];
+                p.key_ret[c] = ret[k];
+            }
+        }
+    }
+}
+
+// the row word of a dense index
+__device__ __forceinline__ uint32_t key_word_of(uint32_t idx, int D) {
+    uint32_t w = 0;
+#pragma unroll
+    for (int b = 0; b < 4; b++)
+        if (b < D) w |= (uint32_t)(uint8_t)(int8_t)((int)((idx >> (5 * b)) & 31u) - 8) << (8 * b);
+    return w;
+}
+
+// ranks = the occurring dense indices in ascending order (a block-wide scan per group), so every
+// later pass runs in an order that depends only on the set of distinct rows: deterministic
+__global__ void __launch_bounds__(1024) k_key_rank(PpoArgs p) {
+    __shared__ int part[1024];
+    const int grp = blockIdx.x, tid = threadIdx.x;
+    if (p.key_flag[grp]) {
+        if (tid == 0) p.key_n[grp] = -1;
+        return;
+    }
+    constexpr int PER = kKeyDense / 1024;  // contiguous indices per thread
+    const size_t o = (size_t)grp * kKeyDense + (size_t)tid * PER;
+    const uint4* m4 = reinterpret_cast<const uint4*>(p.key_mark + o);
+    int c = 0;
+    for (int k = 0; k < PER / 16; k++) {
+        const uint4 v = m4[k];
+        c += __popc(v.x) + __popc(v.y) + __popc(v.z) + __popc(v.w);  // marks are 0 or 1
+    }
+    part[tid] = c;
+    __syncthreads();
+    for (int d = 1; d < 1024; d <<= 1) {  // inclusive scan
+        const int x = tid >= d ? part[tid - d] : 0;
+        __syncthreads();
+        part[tid] += x;
+        __syncthreads();
+    }
+    const int n = part[1023];
+    int rk = part[tid] - c;
+    if (n <= kKeyMaxRanks) {
+        for (int k = 0; k < PER / 16 && c > 0; k++) {
+            const uint4 v = m4[k];
+            if ((v.x | v.y | v.z | v.w) == 0u) continue;
+            const uint32_t wv[4] = {v.x, v.y, v.z, v.w};
+            for (int b = 0; b < 16; b++) {
+                if ((wv[b >> 2] >> (8 * (b & 3))) & 0xffu) {
+                    const size_t d = o + 16 * k + b;
+                    p.key_rank[d] = rk;
+                    p.key_sorted[(size_t)grp * kKeyMaxRanks + rk] = key_word_of((uint32_t)(16 * k + b + tid * PER), p.D);
+                    rk++;
+                }
+            }
+        }
+    }
+    if (tid == 0) p.key_n[grp] = n <= kKeyMaxRanks ? n : -1;
+}
+
+// the row scan: every row of the group looks up its rank and forward values and adds
+// d min(surr) / d ratio * ratio (at its action), V - G and 1 to its rank's int64 sums in LDS (the
+// sums do not depend on the order of the adds); ranks in passes of key_cap; then the block's sums
+// and loss terms go to its own slice of key_part / key_pcnt / key_ploss with plain stores
+template <int NT>
+__global__ void __launch_bounds__(1024) k_key_scan(PpoArgs p) {
+    constexpr int KA = 16 * NT + 1, KF = 16 * NT + 4;
+    extern __shared__ __align__(16) long long sacc[];  // [cap][KA], then uint32 cnt[cap]
+    __shared__ float red[3][1024];
+    const int grp = blockIdx.x % p.G, blk = blockIdx.x / p.G, tid = threadIdx.x;
+    const int n = p.key_n[grp];
+    if (n < 0) return;
+    uint32_t* scnt = reinterpret_cast<uint32_t*>(sacc + (size_t)p.key_cap * KA);
+    const long long r_lo = p.R * blk / p.key_nbs, r_hi = p.R * (blk + 1) / p.key_nbs;
+    const size_t gd = (size_t)grp * kKeyDense, gr = (size_t)grp * kKeyMaxRanks, gc = (size_t)grp * p.R;
+    const size_t pb = (size_t)grp * p.key_nbs + blk;
+    const float fx = (float)kKeyFx;
+    float l_min = 0.f, l_mse = 0.f, l_ent = 0.f;
+    bool bad = false;
+    constexpr int UN = 4;  // rows in flight per thread
+    for (int lo = 0; lo < n; lo += p.key_cap) {
+        const int hi = min(lo + p.key_cap, n), nr = hi - lo;
+        for (int i = tid; i < nr * KA; i += 1024) sacc[i] = 0;
+        for (int i = tid; i < nr; i += 1024) scnt[i] = 0u;
+        __syncthreads();
+        for (long long r0 = r_lo; r0 < r_hi; r0 += 1024 * UN) {
+            uint32_t w[UN];
+            int act[UN];
+            float olp[UN], G[UN];
+#pragma unroll
+            for (int k = 0; k < UN; k++) {
+                const size_t c = gc + (size_t)min(r0 + 1024 * k + tid, r_hi - 1);
+                w[k] = p.key_idx[c];
+                act[k] = p.key_act[c];
+                olp[k] = p.key_olp[c];
+                G[k] = p.key_ret[c];
+            }
+            int rank[UN];
+#pragma unroll
+            for (int k = 0; k < UN; k++) rank[k] = p.key_rank[gd + w[k]];
+#pragma unroll
+            for (int k = 0; k < UN; k++) {
+                const long long r = r0 + 1024 * k + tid;
+                if (r >= r_hi || rank[k] < lo || rank[k] >= hi) continue;
+                const float* fw = p.key_fwd + (gr + rank[k]) * KF;
+                const bool av = (unsigned)act[k] < (unsigned)p.A;
+                const float lp = av ? fw[act[k]] : 0.f;
+                const float V = fw[16 * NT], ent = fw[16 * NT + 1];
+                // the tile path's per-row derivatives with the rank's forward values
+                const float ratio = fast_exp(lp - olp[k]);
+                const float adv = G[k] - V;
+                const float sur1 = ratio * adv;
+                const float rc = fminf(fmaxf(ratio, 1.f - p.eps_clip), 1.f + p.eps_clip);
+                const float sur2 = rc * adv;
+                const float inr = (ratio >= 1.f - p.eps_clip && ratio <= 1.f + p.eps_clip) ? 1.f : 0.f;
+                const float dmin = sur1 < sur2 ? adv : (sur2 < sur1 ? adv * inr : 0.5f * adv + 0.5f * adv * inr);
+                const float qd = dmin * ratio, dv = V - G[k];
+                if (!(fabsf(qd) <= p.key_bound && fabsf(dv) <= p.key_bound)) {  // NaN included
+                    bad = true;
+                    continue;
+                }
+                long long* a = sacc + (size_t)(rank[k] - lo) * KA;
+                if (av) atomicAdd(reinterpret_cast<unsigned long long*>(a + act[k]), (unsigned long long)__float2ll_rn(qd * fx));
+                atomicAdd(reinterpret_cast<unsigned long long*>(a + 16 * NT), (unsigned long long)__float2ll_rn(dv * fx));
+                atomicAdd(scnt + (rank[k] - lo), 1u);
+                l_min += -fminf(sur1, sur2);
+                l_mse += dv * dv;
+                l_ent += ent;
+            }
+        }
+        __syncthreads();
+        long long* dst = p.key_part + (pb * kKeyMaxRanks + lo) * KA;
+        for (int i = tid; i < nr * KA; i += 1024) dst[i] = sacc[i];
+        uint32_t* dc = p.key_pcnt + pb * kKeyMaxRanks + lo;
+        for (int i = tid; i < nr; i += 1024) dc[i] = scnt[i];
+        __syncthreads();
+    }
+    if (bad) __hip_atomic_store(p.key_flag + grp, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // the block's loss sums (fixed tree order)
+    red[0][tid] = l_min;
+    red[1][tid] = l_mse;
+    red[2][tid] = l_ent;
+    __syncthreads();
+    for (int d = 512; d > 0; d >>= 1) {
+        if (tid < d)
+            for (int c = 0; c < 3; c++) red[c][tid] += red[c][tid + d];
+        __syncthreads();
+    }
+    if (tid < 3) p.key_ploss[pb * 4 + tid] = red[tid][0];
+}
+
+// the common-row path for inputs up to 128 bytes (its scan holds a row per lane in registers)
+template <int NQ, int NT>
+static hipError_t launch_grad_t(const PpoArgs& a0, hipStream_t st) {
+    PpoArgs a = a0;
+    const unsigned nb = (unsigned)(a.n_chunks / 4);
+    a.part_off = 0;
+    if constexpr (NQ == 1 && NT <= 2) {
+        if (a.key_mark && a.stride == 4 && !a.common) {
+            // keyed rows: mark -> rank -> forward of the ranks -> row scan -> backward of the ranks,
+            // then the tile path for the groups the keyed passes could not take
+            hipError_t e;
+            if ((e = hipMemsetAsync(a.key_mark, 0, (size_t)a.G * kKeyDense, st)) != hipSuccess) return e;
+            if ((e = hipMemsetAsync(a.key_flag, 0, a.G * sizeof(int32_t), st)) != hipSuccess) return e;
+            const unsigned ib = (unsigned)std::min<long long>((a.R + 255) / 256, 16384);
+            hipLaunchKernelGGL(k_key_gather, dim3(ib), dim3(256), 0, st, a);
+            if ((e = hipGetLastError()) != hipSuccess) return e;
+            hipLaunchKernelGGL(k_key_rank, dim3(a.G), dim3(1024), 0, st, a);
+            if ((e = hipGetLastError()) != hipSuccess) return e;
+            a.part_rows = kKeyBlocks + (int)nb;
+            if ((e = launch_grad_cm<NQ, NT, kKeyFwd>(a, kKeyBlocks, st)) != hipSuccess) return e;
+            constexpr int KA = 16 * NT + 1;
+            const size_t lds = (size_t)a.key_cap * (KA * 8 + 4);
+            hipLaunchKernelGGL(k_key_scan<NT>, dim3((unsigned)(a.G * a.key_nbs)), dim3(1024), lds, st, a);
+            if ((e = hipGetLastError()) != hipSuccess) return e;
+            if ((e = launch_grad_cm<NQ, NT, kKeyBack>(a, kKeyBlocks, st)) != hipSuccess) return e;
+            a.part_off = kKeyBlocks;
+            return launch_grad_cm<NQ, NT, kPlain>(a, nb, st);
+        }
+    }
+    a.key_n = nullptr;
+    a.part_rows = (int)nb;
+    if constexpr (NQ <= 8) {
+        if (a.common && a.stride >= 16) {
+            using L = GradLds<NQ, NT, kCommonRow>;
+            if (sizeof(float) * L::lds_floats <= 160 * 1024) return launch_grad_cm<NQ, NT, kCommonRow>(a, nb, st);
+        }
+    }
+    return launch_grad_cm<NQ, NT, kPlain>(a, nb, st);
+}
+
+// partial vectors per group that launch_ppo_grad writes (the keyed path adds its slot blocks)
+int ppo_partial_rows(int n_chunks, bool keyed) { return n_chunks / 4 + (keyed ? kKeyBlocks : 0); }
 
 hipError_t launch_ppo_grad(const PpoArgs& a, const GradOut& go, hipStream_t st) {
     const int nq = a.D / 16 + 1;  // 16*NQ > D leaves room for the ones column
     const int nt = (a.A + 15) / 16;
     if (a.n_chunks % 4 != 0) return hipErrorInvalidValue;
     hipError_t e;
+    const bool keyed = a.key_mark && a.stride == 4 && !a.common && nq == 1 && nt <= 2;
 #define MS_PPO_CASE(Q, T)                \
     if (nq <= Q && nt <= T) {            \
         e = launch_grad_t<Q, T>(a, st);  \
@@ -920,8 +1253,8 @@ reduce:
     if (e != hipSuccess) return e;
     {
         const int P = poff(a.D, a.A).total;
-        hipLaunchKernelGGL(k_ppo_reduce, dim3((P + 63) / 64, a.G), dim3(256), 0, st, a.partials, a.G, a.n_chunks / 4,
-                           P, a.D, a.A, go);
+        hipLaunchKernelGGL(k_ppo_reduce, dim3((P + 63) / 64, a.G), dim3(256), 0, st, a.partials, a.G,
+                           ppo_partial_rows(a.n_chunks, keyed), P, a.D, a.A, go);
     }
     return hipGetLastError();
 }

@@ -367,7 +367,8 @@ class PPOGroup:
         ws_bytes = lib.ms_ppo_workspace_bytes(ct.byref(a), R)
         ws = torch.empty(((ws_bytes + 3) // 4,), dtype=torch.float32, device=states_i8.device)
         batch = abi.MsPpoBatch(ptr(states_i8), ptr(actions_i8), ptr(old_logprobs), ptr(returns_teg),
-                               ptr(unit_of_group), stride, T, U, E, ptr(common_row), int(returns_ld))
+                               ptr(unit_of_group), stride, T, U, E, ptr(common_row), int(returns_ld),
+                               int(getattr(self, "row_keys", 0)))
         grads = abi.MsPpoGrads(*[ptr(getattr(pol, k).grad) for k in ACTOR_KEYS + CRITIC_KEYS], ptr(loss_buf))
         # the structs above hold raw device pointers: the closure keeps every tensor they point into
         # alive until its last launch (a caller's temporaries would otherwise be freed and reused)

@@ -258,6 +258,62 @@ def test_fused_grad_common_rows_matches_autograd(ms, G, T, E, U, O, A, K, frac):
         assert err <= 1e-4 * scale + 1e-7, (k, err, scale)
 
 
+@pytest.mark.parametrize("G,T,E,U,A,K,n_keys", [(8, 20, 300, 24, 16, 2, 40), (4, 13, 700, 6, 13, 1, 3000),
+                                                 (2, 50, 2000, 3, 9, 1, 0), (2, 9, 400, 3, 20, 1, -1)])
+def test_fused_grad_keyed_rows_matches_autograd(ms, G, T, E, U, A, K, n_keys):
+    """ms_ppo_grad on 4-byte rows (the price chooser's input, PPOmodules.py:327-330): each group's
+    distinct rows get one forward and one backward, every row adds its loss derivatives to its
+    distinct row's fixed-point sums. n_keys distinct rows per batch (3000: more than one scan pass
+    of ranks; 0: bytes uniform in [-8, 24), more distinct rows than ranks, and -1: bytes over the
+    whole int8 range, outside the dense index: both send the groups to the tile path);
+    checked against torch autograd and against the same kernel with keying off (row_keys = -1),
+    and twice in a row for bit-identical gradients."""
+    ppo = _ppo(ms)
+    D, stride = 4, 4
+    gen = torch.Generator().manual_seed(8)
+    R = T * E
+    if n_keys > 0:
+        pool = torch.randint(-5, 13, (n_keys, 4), generator=gen, dtype=torch.int8)
+        pool[0] = -5  # the price chooser's [-5, -5, -5, -5] row (no offer), a tenth of all rows
+        idx = torch.randint(0, n_keys, (R, U), generator=gen)
+        idx[torch.rand((R, U), generator=gen) < 0.1] = 0
+        states = pool[idx]
+    elif n_keys == 0:
+        states = torch.randint(-8, 24, (R, U, 4), generator=gen, dtype=torch.int8)
+    else:
+        states = torch.randint(-128, 127, (R, U, 4), generator=gen, dtype=torch.int8)
+    actions = torch.randint(0, A, (R, U), generator=gen).to(torch.int8)
+    old_lp = -torch.rand((R, U), generator=gen) * 3
+    ret = torch.randn((E, G, T), generator=gen)
+    u_sel = torch.randint(0, U, (G,), generator=torch.Generator().manual_seed(3))
+    x = states[:, u_sel, :D].permute(1, 0, 2).float().cuda()
+    a = actions[:, u_sel].T.long().cuda()
+    lp = old_lp[:, u_sel].T.contiguous().cuda()
+    rt = ret.permute(1, 2, 0).reshape(G, R).cuda()
+    torch.manual_seed(23)
+    ref = ppo.PPOGroup(G, D, A, 0.003, 0.01, 0.9, 0.2, K, device="cuda")
+    ref_losses = ref.update(x, a, lp, rt)
+    ref_grads = {k: getattr(ref.policy, k).grad.clone() for k in ppo.ACTOR_KEYS + ppo.CRITIC_KEYS}
+    args = (states.cuda(), actions.cuda(), old_lp.cuda(), ret.permute(2, 0, 1).contiguous().cuda(),
+            u_sel.to(torch.int32).cuda(), T, E)
+    runs = []
+    for keys in (0, 0, -1):
+        torch.manual_seed(23)
+        fus = ppo.PPOGroup(G, D, A, 0.003, 0.01, 0.9, 0.2, K, device="cuda")
+        fus.row_keys = keys
+        losses = fus.update_fused(*args)
+        runs.append((losses, {k: getattr(fus.policy, k).grad.clone() for k in ref_grads}))
+    for losses, grads in runs:
+        for rl, fl in zip(ref_losses, losses):
+            np.testing.assert_allclose(fl.cpu().numpy(), rl.cpu().numpy(), rtol=1e-5, atol=1e-6)
+        for k, g in ref_grads.items():
+            scale = g.abs().max().item() + 1e-12
+            err = (grads[k] - g).abs().max().item()
+            assert err <= 1e-4 * scale + 1e-7, (k, err, scale)
+    for k in ref_grads:  # integer sums: the keyed gradient does not depend on the atomics' order
+        assert torch.equal(runs[0][1][k], runs[1][1][k]), k
+
+
 def test_trainer_fused_matches_torch_update(ms):
     tr_mod = importlib.import_module("marl-scheduling_amd.trainer")
     trs = [tr_mod.Trainer.from_named("cfg3", n_envs=32, update_step=20, seed=4, device="cuda:0", fused=f)
