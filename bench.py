@@ -29,15 +29,17 @@ METRIC = "agent-env-steps/sec (whole node), 8 agents×8 cores×16384 envs, 1/2/4
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
 
 
-def env_round_bytes(shape, k_new_jobs: int, free: bool) -> int:
+def env_round_bytes(shape, k_new_jobs: int, free: bool, compact: bool = False) -> int:
     """Algorithmic HBM bytes of one env replica's round in k_env_step:
-    state record read+write, actions read, observations written, rewards written,
-    and the MT19937 words the spawn draws consume (tie-break words and liability
-    entries are data dependent and not counted: this is a lower bound)."""
+    state record read+write, actions read, observations written (compact: the C core rows and
+    owners instead of the N*C acceptor rows), rewards written, and the MT19937 words the spawn
+    draws consume (tie-break words and liability entries are data dependent and not counted: this
+    is a lower bound)."""
     N, C, L = shape.n_agents, shape.n_cores, shape.collection_length
     rec = shape.env_record_bytes
     acts = N * C + N * L * (2 if free else 1)
-    obs = N * C * shape.acc_obs_stride + N * L * shape.off_obs_stride
+    acc_obs = C * (shape.acc_obs_stride + 1) if compact else N * C * shape.acc_obs_stride
+    obs = acc_obs + N * L * shape.off_obs_stride
     rew = 4 * (N * C + N * L * (2 if free else 1) + N + C)
     rng = 4 * 2 * k_new_jobs * N
     return 2 * rec + acts + obs + rew + rng
@@ -139,16 +141,17 @@ SAMPLE_EVERY = 8      # rounds between timed env launches
 def committed_traffic(alg_bytes_per_launch):
     """HBM bytes per k_env_step launch from the committed PMC passes of this workload
     (profiles/*/traffic.json, written by profiles/run_profile.sh: FETCH_SIZE doubled per the
-    gfx950 correction + WRITE_SIZE, per launch), newest profile first; None if absent."""
+    gfx950 correction + WRITE_SIZE, per launch), newest round first; None if absent."""
     import glob
-    paths = sorted(glob.glob(os.path.join(REPO, "profiles", "*", "traffic.json")), key=os.path.getmtime, reverse=True)
+    paths = sorted(glob.glob(os.path.join(REPO, "profiles", "*", "traffic.json")), reverse=True)  # newest round first
     for p in paths:
         try:
             with open(p) as f:
                 d = json.load(f)
         except (OSError, ValueError):
             continue
-        if d.get("kernel") == "k_env_step" and d.get("bytes"):
+        # the passes of this workload's kernel: same algorithmic bytes per launch
+        if d.get("kernel") == "k_env_step" and d.get("bytes") and d.get("algorithmic_bytes") == alg_bytes_per_launch:
             return {"bytes": d["bytes"], "source": os.path.relpath(p, REPO),
                     "vs_algorithmic": d["bytes"] / alg_bytes_per_launch}
     return None
@@ -308,7 +311,7 @@ def main():
     value = agent_steps / elapsed
     avg_step_s = sum(launch_us) / len(launch_us) / 1e6
     part_envs = args.envs // args.rollout_streams
-    b_round = env_round_bytes(shape, tr.cfg.new_jobs_per_round, tr.free)
+    b_round = env_round_bytes(shape, tr.cfg.new_jobs_per_round, tr.free, tr.compact)
     achieved = b_round * part_envs / avg_step_s / 1e9
     traffic = committed_traffic(b_round * part_envs)
     result = {

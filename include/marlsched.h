@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define MS_ABI_VERSION 6
+#define MS_ABI_VERSION 7
 
 #define MS_MAX_KINDS 16
 #define MS_MAX_AGENTS 64
@@ -307,6 +307,15 @@ int ms_policy_act_common(const ms_mlp_params* p, const int8_t* obs, int32_t obs_
                          uint64_t seed, uint64_t offset, const uint64_t* offset_dev, const float* uniforms,
                          int8_t* action, float* logprob, void* stream);
 
+/* ms_policy_act_common on compact acceptor observations (ms_obs_out.core_rows / core_owner):
+ * core_rows [E][C][obs_stride], core_owner [E][C]; unit u = a*C + c of replica e acts on core row
+ * (e, c) when core_owner[e][c] == a + 1 and on common_row otherwise (Agent.py:167-212). Outputs are
+ * bit-identical to ms_policy_act_common on the [E][N*C] rows those regenerate. */
+int ms_policy_act_compact(const ms_mlp_params* p, const int8_t* core_rows, const int8_t* core_owner,
+                          int32_t obs_stride, int64_t n_envs, int32_t n_units, int32_t units_per_group, int32_t n_cores,
+                          const int8_t* common_row, uint64_t seed, uint64_t offset, const uint64_t* offset_dev,
+                          const float* uniforms, int8_t* action, float* logprob, void* stream);
+
 /* FreePriceOfferPPO.selectAction (PPOmodules.py:312-332) in one launch: the core
  * chooser acts on the offer observation (D_off = 2C+2); the price chooser acts on
  * price_state = [obs[2a], obs[2a+1], obs[2C], obs[2C+1]] or [-5,-5,-5,-5] when a == 0
@@ -354,6 +363,11 @@ typedef struct ms_ppo_batch {
     const int8_t* common_row;
     /* row pitch of returns in floats (0 = the number of groups): returns[(t*E + e)*ld + g] */
     int32_t returns_ld;
+    /* compact acceptor observations (with common_row): states = core rows [R][n_cores][stride] and
+     * core_owner [R][n_cores] (ms_obs_out.core_rows / core_owner per round); unit u = a*C + c of row r
+     * reads core row (r, c) when core_owner[r][c] == a + 1, else common_row. NULL: states [R][U][stride] */
+    const int8_t* core_owner;
+    int32_t n_cores;
     /* 0: rows of 4 bytes (stride 4, nets of <= 4 inputs and <= 32 actions, no common_row) are keyed:
      * each group's distinct rows get one forward and one backward pass, and each row adds its loss
      * derivatives to its distinct row's int64 fixed-point sums (2^-28); -1: every row on its own */

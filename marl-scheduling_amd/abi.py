@@ -226,6 +226,8 @@ class MsPpoBatch(ct.Structure):
         ("E", ct.c_int64),
         ("common_row", ct.c_void_p),
         ("returns_ld", ct.c_int32),
+        ("core_owner", ct.c_void_p),
+        ("n_cores", ct.c_int32),
         ("row_keys", ct.c_int32),
     ]
 

@@ -22,7 +22,10 @@ for src in env_kernels.hip policy_kernels.hip ppo_kernels.hip agg_kernels.hip dq
   # the env round reproduces Python's float64 arithmetic: no contraction there; the policy
   # and PPO kernels follow torch's f32 (which fuses freely) within tolerance: fma allowed
   contract=(-ffp-contract=off)
-  [[ "${src}" == policy_kernels.hip || "${src}" == ppo_kernels.hip ]] && contract=(-ffp-contract=fast)
+  [[ "${src}" == policy_kernels.hip ]] && contract=(-ffp-contract=fast)
+  # the gradient kernel's variants (common rows by bytes or by owners) must agree bit for bit: fma only
+  # where an expression asks for it, never across statements (fast contraction depends on the code around)
+  [[ "${src}" == ppo_kernels.hip ]] && contract=(-ffp-contract=on)
   key="$( { cat "${HERE}/csrc/${src}" "${HEADERS[@]}"; echo "${CCVER} ${FLAGS[*]} ${contract[*]}"; } | sha256sum | cut -d' ' -f1)"
   if [[ ! -f "${obj}" || "$(cat "${obj}.key" 2>/dev/null)" != "${key}" ]]; then
     rm -f "${obj}.key"

@@ -26,6 +26,9 @@ hipError_t launch_env_randbelow(const Params&, uint8_t*, uint32_t*, int64_t, uin
 hipError_t launch_env_auctioneer(const Params&, int64_t, uint8_t*, uint32_t*, int8_t*, hipStream_t);
 hipError_t launch_policy_act(const ms_mlp_params*, const int8_t*, int, int64_t, int, int, const int8_t*, uint64_t,
                              uint64_t, const uint64_t*, const float*, int8_t*, float*, hipStream_t);
+hipError_t launch_policy_act_compact(const ms_mlp_params*, const int8_t*, const int8_t*, int, int64_t, int, int, int,
+                                     const int8_t*, uint64_t, uint64_t, const uint64_t*, const float*, int8_t*, float*,
+                                     hipStream_t);
 hipError_t launch_offer_act_free(const ms_mlp_params*, const ms_mlp_params*, const int8_t*, int, int64_t, int, int, int,
                                  uint64_t, uint64_t, const uint64_t*, const float*, int8_t*, float*, int8_t*, int8_t*,
                                  float*, int8_t*, hipStream_t);
@@ -500,6 +503,22 @@ int ms_policy_act_common(const ms_mlp_params* p, const int8_t* obs, int32_t obs_
     return MS_OK;
 }
 
+int ms_policy_act_compact(const ms_mlp_params* p, const int8_t* core_rows, const int8_t* core_owner,
+                          int32_t obs_stride, int64_t n_envs, int32_t n_units, int32_t units_per_group, int32_t n_cores,
+                          const int8_t* common_row, uint64_t seed, uint64_t offset, const uint64_t* offset_dev,
+                          const float* uniforms, int8_t* action, float* logprob, void* stream) {
+    if (!core_rows || !core_owner || !action || !logprob || !common_row) return fail(MS_EINVAL, "NULL argument");
+    int rc = check_mlp(p, obs_stride, n_units, units_per_group);
+    if (rc) return rc;
+    if (n_envs < 1) return fail(MS_EINVAL, "n_envs must be >= 1");
+    if (n_cores < 1 || n_units % n_cores != 0) return fail(MS_EINVAL, "n_units must be n_agents * n_cores");
+    if (obs_stride < 16) return fail(MS_EINVAL, "obs_stride must be >= 16");
+    HIP_TRY(ms::launch_policy_act_compact(p, core_rows, core_owner, obs_stride, n_envs, n_units, units_per_group,
+                                          n_cores, common_row, seed, offset, offset_dev, uniforms, action, logprob,
+                                          (hipStream_t)stream));
+    return MS_OK;
+}
+
 int ms_offer_act_free(const ms_mlp_params* core, const ms_mlp_params* price, const int8_t* obs, int32_t obs_stride,
                       int64_t n_envs, int32_t n_units, int32_t units_per_group, int32_t n_cores, uint64_t seed,
                       uint64_t offset, const uint64_t* offset_dev, const float* uniforms, int8_t* core_action,
@@ -566,6 +585,8 @@ int ms_ppo_grad(const ms_mlp_params* a, const ms_mlp_params* c, const ms_ppo_bat
         return fail(MS_EINVAL, "bad batch shape");
     if (!b->states || !b->actions || !b->old_logprobs || !b->returns || !b->unit_of_group)
         return fail(MS_EINVAL, "NULL batch pointer");
+    if (b->core_owner && (!b->common_row || b->n_cores < 1 || b->U % b->n_cores != 0 || b->stride < 16))
+        return fail(MS_EINVAL, "compact rows need common_row, stride >= 16 and U = n_agents * n_cores");
     const int64_t R = (int64_t)b->T * b->E;
     if (ws_bytes < ms_ppo_workspace_bytes(a, R)) return fail(MS_EINVAL, "workspace too small");
     ms::PpoArgs p{};
@@ -577,6 +598,8 @@ int ms_ppo_grad(const ms_mlp_params* a, const ms_mlp_params* c, const ms_ppo_bat
     p.ret = b->returns;
     p.unit_of_group = b->unit_of_group;
     p.common = b->common_row;
+    p.owner = b->core_owner;
+    p.owner_C = b->n_cores;
     p.partials = (float*)ws;
     p.D = a->in_dim;
     p.A = a->n_actions;

@@ -937,8 +937,10 @@ constexpr int kLiabPrefetch = 4;  // newest chain entries loaded ahead per core 
 // b * (64 / LPE) + g. Each group owns a P.s_total-byte slice of the block's LDS. EXT: the kernel
 // variant with the optional features (hard-coded agents when io.act_acc == NULL, episode metrics,
 // compact acceptor observations); the plain training round is compiled without them, so it carries
-// none of their registers (the compact emission alone costs ~90 spilled SGPRs).
-template <int LPE, bool EXT>
+// none of their registers (the compact emission beside the full rows costs ~90 spilled SGPRs). CMP:
+// the plain round that emits the compact acceptor observations instead of the [N][C] rows (the
+// training loop's form: its act and gradient kernels read core rows + owners).
+template <int LPE, bool EXT, bool CMP>
 __device__ __forceinline__ void env_round(const Params& P, int64_t E, uint8_t* recs, uint32_t* mt, Liab* liab,
                                           const StepIO& io, int64_t slot) {
     extern __shared__ __align__(16) uint8_t smem_all[];
@@ -1467,8 +1469,8 @@ __device__ __forceinline__ void env_round(const Params& P, int64_t E, uint8_t* r
     MS_MARK(10);
     build_masks<LPE>(R, P, s_mc, s_mr, gl);
     MS_MARK(11);
-    emit_obs<LPE>(R, P, s_mc, s_mr, scratch, io.obs_acc, io.obs_off, io.obs_auct, EXT ? io.obs_crow : nullptr,
-                  EXT ? io.obs_cown : nullptr, e, E, active, gl);
+    emit_obs<LPE>(R, P, s_mc, s_mr, scratch, CMP ? nullptr : io.obs_acc, io.obs_off, io.obs_auct,
+                  (EXT || CMP) ? io.obs_crow : nullptr, (EXT || CMP) ? io.obs_cown : nullptr, e, E, active, gl);
     MS_MARK(12);
 #ifdef MS_PHASE_TIMING
     if (lane == 0)
@@ -1479,7 +1481,7 @@ __device__ __forceinline__ void env_round(const Params& P, int64_t E, uint8_t* r
 // One round for the 64 / LPE envs of wave slot blockIdx.x. (A persistent loop over several slots
 // per wave would let one slot's observation stores drain under the next slot's compute, but the
 // compiler then keeps the whole round's state live across iterations: 3x the VGPRs.)
-template <int LPE, bool EXT>
+template <int LPE, bool EXT, bool CMP>
 __global__ void __launch_bounds__(64, 4) k_env_step(Params P, int64_t E, uint8_t* recs, uint32_t* mt, Liab* liab,
                                                  StepIO io) {
 #ifdef MS_PHASE_TIMING
@@ -1488,7 +1490,7 @@ __global__ void __launch_bounds__(64, 4) k_env_step(Params P, int64_t E, uint8_t
     // per-wave start / end for the bench's launch span (optional; plain stores, no shared address,
     // nothing held across the round: the kernel sits at 4 waves per SIMD with no register to spare)
     if (io.span && threadIdx.x == 0) io.span[2 * blockIdx.x] = __builtin_amdgcn_s_memrealtime();
-    env_round<LPE, EXT>(P, E, recs, mt, liab, io, blockIdx.x);
+    env_round<LPE, EXT, CMP>(P, E, recs, mt, liab, io, blockIdx.x);
     if (io.span && threadIdx.x == 0) io.span[2 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime();
 #ifdef MS_PHASE_TIMING
     if (threadIdx.x == 0) {
@@ -1611,8 +1613,9 @@ static hipError_t launch_step_t(const Params& P, int64_t E, uint8_t* recs, uint3
     constexpr int G = kWave / LPE;
     const int64_t blocks = (E + G - 1) / G;
     const size_t lds = (size_t)P.s_total * G > 4 * kMtN ? (size_t)P.s_total * G : 4 * kMtN;  // >= one MT block
-    const bool ext = io.act_acc == nullptr || io.metrics != nullptr || io.obs_crow != nullptr || io.obs_cown != nullptr;
-    auto kern = ext ? k_env_step<LPE, true> : k_env_step<LPE, false>;
+    const bool compact = io.obs_crow != nullptr || io.obs_cown != nullptr;
+    const bool ext = io.act_acc == nullptr || io.metrics != nullptr || (compact && io.obs_acc != nullptr);
+    auto kern = ext ? k_env_step<LPE, true, false> : (compact ? k_env_step<LPE, false, true> : k_env_step<LPE, false, false>);
     hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(kWave), lds, s, P, E, recs, mt, liab, io);
     return hipGetLastError();
 }

@@ -15,6 +15,8 @@ struct PpoArgs {
     const float* ret;                                // [T][E][ret_ld] normalised returns
     const int32_t* unit_of_group;                    // [G]
     const int8_t* common;                            // [stride] rows equal to it share one forward, or NULL
+    const int8_t* owner;                             // compact acceptor rows: states [R][owner_C][stride],
+    int owner_C;                                     //   owner [R][owner_C] (unit u = a*C + c), or NULL
     float* partials;                                 // [G][n_chunks][P]
     int D, A, stride, T, U, G, ret_ld;
     long long E, R;

@@ -302,6 +302,9 @@ struct ActArgs {
     int8_t* env_price;
     const int8_t* common;  // [stride] or NULL (k_act_common)
     int items_per_wave;    // k_act_common
+    // compact acceptor observations (k_act_common<.., OWN>): obs = core rows [E][C][stride], owner
+    // [E][C]; row (e, u = a*C + c) is core row (e, c) if owner[e][c] == a + 1, else the common row
+    const int8_t* owner;
 };
 
 // One wave = a contiguous range of 16-row tiles of one group; no LDS. Layer 1 runs on the bf16 MFMA
@@ -442,7 +445,7 @@ __global__ void __launch_bounds__(256) k_act(ActArgs a) {
 // MFMA tiles as in k_act. Outputs are bit-identical to k_act's.
 constexpr int kCommonSeg = 512;  // most rows per wave = capacity of the wave's LDS row list
 
-template <int S1, int NT, bool EXT_U>
+template <int S1, int NT, bool EXT_U, bool OWN>
 __global__ void __launch_bounds__(256) k_act_common(ActArgs a) {
     __shared__ int32_t s_list[4][kCommonSeg];
     __shared__ float s_cum[4][16 * NT], s_lp[4][16 * NT], s_S[4];
@@ -488,7 +491,7 @@ __global__ void __launch_bounds__(256) k_act_common(ActArgs a) {
     for (int k = 0; k < 16 * NT; k++) cum[k] = __uint_as_float(__builtin_amdgcn_readfirstlane(__float_as_uint(s_cum[wid][k])));
     constexpr int LPR = S1 <= 2 ? 4 : (S1 <= 4 ? 8 : 16);
     CommonScan<LPR> cs;
-    cs.init(crow, stride4, lane);
+    if (!OWN) cs.init(crow, stride4, lane);
     const float S = s_S[wid];
     const int last_nz = s_lnz[wid];
     const uint32_t s_magic = 0xffffffffu / (uint32_t)a.S;
@@ -511,20 +514,36 @@ __global__ void __launch_bounds__(256) k_act_common(ActArgs a) {
     //      from the table, the others listed
     int n_row = 0;
     bool n_in = false;
+    int8_t n_own = 0, n_agent1 = 0;
+    // compact rows: the core row of (e, u) and whether agent u / C + 1 owns core u % C
+    auto core_row_of = [&](int row, int& c_out) -> size_t {
+        const int e = row / a.U, u = row - e * a.U;
+        const int ag = u / a.n_cores;
+        c_out = ag;
+        return (size_t)e * a.n_cores + (u - ag * a.n_cores);
+    };
     auto load_step = [&](int i0) {
-        cs.load([&](int k) {
-            const int i = i0 + k;
-            return reinterpret_cast<const uint32_t*>(a.obs + (size_t)(i < i_end ? row_of_item(i) : 0) * a.stride);
-        }, lane);
+        if constexpr (!OWN) {
+            cs.load([&](int k) {
+                const int i = i0 + k;
+                return reinterpret_cast<const uint32_t*>(a.obs + (size_t)(i < i_end ? row_of_item(i) : 0) * a.stride);
+            }, lane);
+        }
         const int i = i0 + lane;
         n_in = i < i_end;
         n_row = n_in ? row_of_item(i) : 0;
+        if constexpr (OWN) {
+            int ag;
+            const size_t cr = core_row_of(n_row, ag);
+            n_own = a.owner[cr];
+            n_agent1 = (int8_t)(ag + 1);
+        }
     };
     if (i_begin < i_end) load_step(i_begin);
     for (int i0 = i_begin; i0 < i_end; i0 += 64) {
         const int row = n_row;
         const bool in = n_in;
-        const bool common = cs.lane_row_common(lane) && in;
+        const bool common = (OWN ? n_own != n_agent1 : cs.lane_row_common(lane)) && in;
         if (i0 + 64 < i_end) load_step(i0 + 64);
         if (common) {
             const float target = uniform_of(row) * S;
@@ -549,7 +568,12 @@ __global__ void __launch_bounds__(256) k_act_common(ActArgs a) {
     auto load_tile = [&](int t0) {
         const int k = t0 + j;
         t_row = list[k < n_list ? k : t0];
-        const uint32_t* src = reinterpret_cast<const uint32_t*>(a.obs + (size_t)t_row * a.stride);
+        size_t sr = (size_t)t_row;
+        if constexpr (OWN) {
+            int ag;
+            sr = core_row_of(t_row, ag);
+        }
+        const uint32_t* src = reinterpret_cast<const uint32_t*>(a.obs + sr * a.stride);
 #pragma unroll
         for (int s = 0; s < S1; s++) {
             const int c0 = 8 * s + 2 * g4;
@@ -582,7 +606,8 @@ __global__ void __launch_bounds__(256) k_act_common(ActArgs a) {
 
 template <int S1, int NT>
 static hipError_t launch_act_common_t(ActArgs& a, hipStream_t st) {
-    auto kern = a.uniforms ? k_act_common<S1, NT, true> : k_act_common<S1, NT, false>;
+    auto kern = a.owner ? (a.uniforms ? k_act_common<S1, NT, true, true> : k_act_common<S1, NT, false, true>)
+                        : (a.uniforms ? k_act_common<S1, NT, true, false> : k_act_common<S1, NT, false, false>);
     const int G = a.n1.n_groups;
     // ~3072 waves over all groups (measured best for cfg3), whole 64-row scan steps each, at most
     // one LDS list of rows
@@ -654,6 +679,32 @@ hipError_t launch_policy_act(const ms_mlp_params* p, const int8_t* obs, int stri
     a.n1 = *p;
     a.n2.n_groups = 0;
     a.obs = obs;
+    a.stride = stride;
+    a.U = U;
+    a.S = S;
+    a.E = (int)E;
+    a.n_items = (int)(E * S);
+    a.seed = seed;
+    a.offset = offset;
+    a.offset_dev = offset_dev;
+    a.uniforms = uniforms;
+    a.action = action;
+    a.logprob = logprob;
+    return dispatch_act(a, st);
+}
+
+hipError_t launch_policy_act_compact(const ms_mlp_params* p, const int8_t* core_rows, const int8_t* core_owner,
+                                     int stride, int64_t E, int U, int S, int n_cores, const int8_t* common,
+                                     uint64_t seed, uint64_t offset, const uint64_t* offset_dev, const float* uniforms,
+                                     int8_t* action, float* logprob, hipStream_t st) {
+    if (!common || stride < 16 || n_cores < 1 || U % n_cores != 0) return hipErrorInvalidValue;
+    ActArgs a{};
+    a.common = common;
+    a.owner = core_owner;
+    a.n_cores = n_cores;
+    a.n1 = *p;
+    a.n2.n_groups = 0;
+    a.obs = core_rows;
     a.stride = stride;
     a.U = U;
     a.S = S;

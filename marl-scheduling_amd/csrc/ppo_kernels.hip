@@ -120,13 +120,14 @@ struct BoolC {
     static constexpr bool value = B;
 };
 
-// kernel modes: every row on its own; rows equal to one common row; keyed rows (the backward and
-// the forward of a group's distinct rows, k_key_scan sums the rows' loss derivatives in between)
-enum GradMode { kPlain = 0, kCommonRow = 1, kKeyBack = 3, kKeyFwd = 4 };
+// kernel modes: every row on its own; rows equal to one common row (found by comparing the rows, or
+// from the core owners of compact acceptor observations); keyed rows (the backward and the forward
+// of a group's distinct rows, k_key_scan sums the rows' loss derivatives in between)
+enum GradMode { kPlain = 0, kCommonRow = 1, kOwnerRow = 2, kKeyBack = 3, kKeyFwd = 4 };
 
 template <int NQ, int NT, int MODE>
 struct GradLds {
-    static constexpr bool CM = MODE == kCommonRow;
+    static constexpr bool CM = MODE == kCommonRow || MODE == kOwnerRow;
     static constexpr int S1 = (NQ + 1) / 2;           // 32-input k-steps of layer 1 (16*NQ inputs)
     static constexpr int W1B = 32 * S1 + 8;           // bf16 pitch of a split W1 row (+16 B: no conflicts)
     static constexpr int XPD = (NQ & 1) ? 4 * NQ + 6 : 4 * NQ + 2;  // staged input row pitch (dwords)
@@ -238,8 +239,14 @@ __global__ void __launch_bounds__((64 * GradLds<NQ, NT, MODE>::WPB), ((NQ * NT >
     // input byte D of every staged row reads 1 (the bias column of dW1)
     const int one_dw = D >> 2;
     const uint32_t one_bit = 1u << (8 * (D & 3));
+    // compact acceptor rows: unit u = agent u / C, core u % C reads core row (r, u % C)
+    const int own_c = MODE == kOwnerRow ? u % p.owner_C : 0;
+    const int8_t own_me = MODE == kOwnerRow ? (int8_t)(u / p.owner_C + 1) : 0;
     auto row_src = [&](int r) {
-        return reinterpret_cast<const uint32_t*>(p.states + ((size_t)r * p.U + u) * p.stride);
+        if constexpr (MODE == kOwnerRow)
+            return reinterpret_cast<const uint32_t*>(p.states + ((size_t)r * p.owner_C + own_c) * p.stride);
+        else
+            return reinterpret_cast<const uint32_t*>(p.states + ((size_t)r * p.U + u) * p.stride);
     };
     const float zero_vs[NT][4] = {};
 
@@ -709,7 +716,7 @@ __global__ void __launch_bounds__((64 * GradLds<NQ, NT, MODE>::WPB), ((NQ * NT >
             }
         constexpr int LPR = S1 <= 2 ? 4 : (S1 <= 4 ? 8 : 16);
         CommonScan<LPR> cs;
-        cs.init(crow, stride4, lane);
+        if constexpr (MODE == kCommonRow) cs.init(crow, stride4, lane);
         {
             uint32_t xw[S1][2];
 #pragma unroll
@@ -748,13 +755,16 @@ __global__ void __launch_bounds__((64 * GradLds<NQ, NT, MODE>::WPB), ((NQ * NT >
         // scan registers, kScanDepth 64-row steps in flight: the rows' chunks (cooperative 16-byte
         // loads) and row r0 + lane's scalars
         constexpr int PF = kScanDepth;
-        u4a sc[PF][LPR];
+        u4a sc[MODE == kCommonRow ? PF : 1][MODE == kCommonRow ? LPR : 1];
         int s_act[PF];
+        int8_t s_own[PF];
         float s_olp[PF], s_G[PF];
         auto load_slot = [&](int k, int r0, int lim) {
-            cs.load_into(sc[k], [&](int q) { return row_src(r0 + q < lim ? r0 + q : rb); }, lane);
+            if constexpr (MODE == kCommonRow)
+                cs.load_into(sc[k], [&](int q) { return row_src(r0 + q < lim ? r0 + q : rb); }, lane);
             const int r = r0 + lane;
             const int rr = r < lim ? r : rb;
+            if constexpr (MODE == kOwnerRow) s_own[k] = p.owner[(size_t)rr * p.owner_C + own_c];
             s_act[k] = p.actions[(size_t)rr * p.U + u];
             s_olp[k] = p.old_lp[(size_t)rr * p.U + u];
             s_G[k] = p.ret[(size_t)rr * p.ret_ld + grp];
@@ -789,7 +799,11 @@ __global__ void __launch_bounds__((64 * GradLds<NQ, NT, MODE>::WPB), ((NQ * NT >
                     if (r0 >= seg_end) break;
                     const int r = r0 + lane;
                     const bool in = r < seg_end;
-                    const bool common = cs.common_of(sc[k], lane) && in;
+                    bool common;
+                    if constexpr (MODE == kOwnerRow)
+                        common = s_own[k] != own_me && in;
+                    else
+                        common = cs.common_of(sc[k], lane) && in;
                     const int act = s_act[k];
                     const float olp = s_olp[k], G = s_G[k];
                     if (r0 + 64 * PF < seg_end) load_slot(k, r0 + 64 * PF, seg_end);
@@ -1218,9 +1232,13 @@ static hipError_t launch_grad_t(const PpoArgs& a0, hipStream_t st) {
     if constexpr (NQ <= 8) {
         if (a.common && a.stride >= 16) {
             using L = GradLds<NQ, NT, kCommonRow>;
-            if (sizeof(float) * L::lds_floats <= 160 * 1024) return launch_grad_cm<NQ, NT, kCommonRow>(a, nb, st);
+            if (sizeof(float) * L::lds_floats <= 160 * 1024) {
+                if (a.owner) return launch_grad_cm<NQ, NT, kOwnerRow>(a, nb, st);
+                return launch_grad_cm<NQ, NT, kCommonRow>(a, nb, st);
+            }
         }
     }
+    if (a.owner) return hipErrorInvalidValue;  // compact rows need the common-row path
     return launch_grad_cm<NQ, NT, kPlain>(a, nb, st);
 }
 

@@ -166,6 +166,37 @@ class GroupedActorCritic(nn.Module):
                                 stream_ptr(stream)))
         return action, logprob
 
+    @torch.no_grad()
+    def act_compact(self, core_rows, core_owner, n_units: int, seed: int, offset: int, common_row, uniforms=None,
+                    action=None, logprob=None, stream=None, offset_dev=None):
+        """``act`` with common_row on compact acceptor observations (ms_policy_act_compact):
+        core_rows [E, C, stride], core_owner [E, C] int8; unit u = a*C + c acts on core row c when
+        core_owner == a + 1, else on common_row. Same outputs as ``act`` on the regenerated rows."""
+        E, C, stride = core_rows.shape
+        assert core_rows.dtype == torch.int8 and core_rows.is_contiguous() and core_owner.is_contiguous()
+        assert core_owner.shape == (E, C) and n_units % C == 0 and n_units % self.G == 0
+        dev = core_rows.device
+        if action is None:
+            action = torch.empty((E, n_units), dtype=torch.int8, device=dev)
+        if logprob is None:
+            logprob = torch.empty((E, n_units), dtype=torch.float32, device=dev)
+        p = self.mlp_params()
+        check(lib.ms_policy_act_compact(ct.byref(p), ptr(core_rows), ptr(core_owner), stride, E, n_units,
+                                        n_units // self.G, C, ptr(common_row), ct.c_uint64(seed), ct.c_uint64(offset),
+                                        ptr(offset_dev), ptr(uniforms), ptr(action), ptr(logprob), stream_ptr(stream)))
+        return action, logprob
+
+
+def regen_acceptor_rows(core_rows, core_owner, common_row, n_agents: int):
+    """The [..., N*C, stride] acceptor rows of compact observations (core_rows [..., C, stride],
+    core_owner [..., C]): row (a, c) = core_rows[c] if core_owner[c] == a + 1 else common_row
+    (Agent.py:167-212). Torch ops, for the reference update path and tests."""
+    C = core_rows.shape[-2]
+    agents = torch.arange(1, n_agents + 1, device=core_rows.device, dtype=core_owner.dtype)
+    own = core_owner.unsqueeze(-2) == agents.view(n_agents, 1)                  # [..., N, C]
+    rows = torch.where(own.unsqueeze(-1), core_rows.unsqueeze(-3), common_row)  # [..., N, C, stride]
+    return rows.reshape(rows.shape[:-3] + (n_agents * C, rows.shape[-1]))
+
 
 @torch.no_grad()
 def offer_act_free(core: GroupedActorCritic, price: GroupedActorCritic, obs_i8, n_cores: int, seed: int, offset: int,
@@ -329,16 +360,17 @@ class PPOGroup:
         return losses
 
     def update_fused(self, states_i8, actions_i8, old_logprobs, returns_teg, unit_of_group, T: int, E: int,
-                     stream=None, common_row=None, returns_ld: int = 0):
+                     stream=None, common_row=None, returns_ld: int = 0, core_owner=None):
         """The same K epochs with the gradient from the fused HIP kernel (ms_ppo_grad).
 
         states_i8 [R, U, stride] int8 rollout rows (R = T*E, row r = t*E + e), actions_i8 [R, U],
         old_logprobs [R, U] f32, returns_teg [T, E, G] f32 normalised (unit_returns), unit_of_group [G] int32
-        (device). Adam (torch) applies the gradient; with several ranks the gradient is
+        (device). Adam (HIP, ms_adam_step) applies the gradient; with several ranks the gradient is
         all-reduced first. common_row (int8 [stride], device, optional): rows equal to it share one
-        forward and one backward pass (same gradient up to f32 summation order)."""
+        forward and one backward pass (same gradient up to f32 summation order). core_owner [R, C]
+        (with common_row): states_i8 are compact acceptor rows [R, C, stride] (regen_acceptor_rows)."""
         epoch = self.fused_epoch(states_i8, actions_i8, old_logprobs, returns_teg, unit_of_group, T, E, stream,
-                                 common_row, returns_ld)
+                                 common_row, returns_ld, core_owner)
         losses = []
         for _ in range(self.K):
             loss = epoch()
@@ -350,13 +382,19 @@ class PPOGroup:
         return losses
 
     def fused_epoch(self, states_i8, actions_i8, old_logprobs, returns_teg, unit_of_group, T: int, E: int,
-                    stream=None, common_row=None, returns_ld: int = 0):
+                    stream=None, common_row=None, returns_ld: int = 0, core_owner=None):
         """The gradient half of one K-epoch step of ``update_fused``, for callers that all-reduce
         several groups' gradients in one call (Trainer.update): returns a function that writes this
         epoch's gradient into ``policy``'s .grad tensors (ms_ppo_grad) and returns the per-group loss
         (the Adam step is ``hip_optimizer.step``)."""
         pol = self.policy
+        # compact acceptor rows (core_owner [R, C]): states are the core rows [R, C, stride], and U
+        # (= N*C units) comes from the actions
         R, U, stride = states_i8.shape
+        n_cores = 0
+        if core_owner is not None:
+            n_cores, U = U, actions_i8.shape[1]
+            assert common_row is not None and core_owner.shape == (R, n_cores) and core_owner.is_contiguous()
         assert R == T * E and states_i8.is_contiguous() and actions_i8.is_contiguous()
         for prm in pol.parameters():
             if prm.grad is None:
@@ -368,11 +406,11 @@ class PPOGroup:
         ws = torch.empty(((ws_bytes + 3) // 4,), dtype=torch.float32, device=states_i8.device)
         batch = abi.MsPpoBatch(ptr(states_i8), ptr(actions_i8), ptr(old_logprobs), ptr(returns_teg),
                                ptr(unit_of_group), stride, T, U, E, ptr(common_row), int(returns_ld),
-                               int(getattr(self, "row_keys", 0)))
+                               ptr(core_owner), n_cores, int(getattr(self, "row_keys", 0)))
         grads = abi.MsPpoGrads(*[ptr(getattr(pol, k).grad) for k in ACTOR_KEYS + CRITIC_KEYS], ptr(loss_buf))
         # the structs above hold raw device pointers: the closure keeps every tensor they point into
         # alive until its last launch (a caller's temporaries would otherwise be freed and reused)
-        keep = (states_i8, actions_i8, old_logprobs, returns_teg, unit_of_group, common_row, ws, loss_buf)
+        keep = (states_i8, actions_i8, old_logprobs, returns_teg, unit_of_group, common_row, core_owner, ws, loss_buf)
 
         def run():
             assert keep

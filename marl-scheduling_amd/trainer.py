@@ -130,7 +130,7 @@ class Trainer:
     def __init__(self, cfg: abi.MsConfig, n_envs: int, arch: str = "local", hyper: Hyper | None = None, seed: int = 0,
                  device=None, rank: int = 0, world_size: int = 1, process_group=None, fused: bool = True,
                  use_graph: bool = True, common_rows: bool = True, rollout_streams: int = 1, metrics: bool = False,
-                 episode_length: int | None = None):
+                 episode_length: int | None = None, compact: bool = True):
         assert arch in ("divided", "local", "global")
         self.fused = fused  # fused HIP gradient (ms_ppo_grad) vs torch autograd
         self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
@@ -186,8 +186,17 @@ class Trainer:
                                mk(go, 4, s.price_actions, hp.offer_gamma, k_off, nets["price"]), dev, torch.float32)
         if world_size > 1:
             self._broadcast_params()
-        # observation ring: slot t holds the state acted on at round t; slot T the next state
-        self.acc_obs = torch.zeros((T + 1, self.E, N * C, s.acc_obs_stride), dtype=torch.int8, device=dev)
+        # observation ring: slot t holds the state acted on at round t; slot T the next state. With
+        # compact (and common_rows) the acceptor observations are kept as the env emits them
+        # compactly: the owner row of every core + the owners (C rows per replica instead of N*C;
+        # Agent.py:167-212), which the act and gradient kernels read directly
+        self.compact = bool(compact and common_rows and s.acc_obs_stride >= 16)  # the common-row kernels' range
+        if self.compact:
+            self.acc_rows = torch.zeros((T + 1, self.E, C, s.acc_obs_stride), dtype=torch.int8, device=dev)
+            self.acc_owner = torch.zeros((T + 1, self.E, C), dtype=torch.int8, device=dev)
+            self.acc_obs = None
+        else:
+            self.acc_obs = torch.zeros((T + 1, self.E, N * C, s.acc_obs_stride), dtype=torch.int8, device=dev)
         self.off_obs = torch.zeros((T + 1, self.E, N * L, s.off_obs_stride), dtype=torch.int8, device=dev)
         self.price_obs = torch.zeros((T, self.E, N * L, 4), dtype=torch.int8, device=dev) if self.free else None
         self.env_price = torch.zeros((self.E, N * L), dtype=torch.int8, device=dev)
@@ -206,7 +215,7 @@ class Trainer:
         self.rounds_done = 0
         self.iterations = 0
         for env, e0, e1 in self.env.parts:
-            env.reset(dict(acceptor=self.acc_obs[0][e0:e1], offer=self.off_obs[0][e0:e1]))
+            env.reset(dict(self._acc_out(0, e0, e1), offer=self.off_obs[0][e0:e1]))
         # episode metrics (trainPPO.py:153-226): the env kernel adds every round into per-replica
         # accumulators, slot (round // episodeLength) % slots; finished episodes are read after each
         # rollout (metrics.py) and their slots zeroed before reuse
@@ -228,6 +237,21 @@ class Trainer:
             hp.acceptor_gamma = -((1 - 5) / 5) + 0.15
         return cls(cfg, n_envs or abi.NAMED_ENVS[name], arch=kw.pop("arch", arch), hyper=hp, seed=seed, device=device,
                    **kw)
+
+    def _acc_out(self, t, e0, e1):
+        """The env's acceptor observation outputs for ring slot t, replicas [e0, e1)."""
+        if self.compact:
+            return dict(core_rows=self.acc_rows[t][e0:e1], core_owner=self.acc_owner[t][e0:e1])
+        return dict(acceptor=self.acc_obs[t][e0:e1])
+
+    def acceptor_rows(self, t0: int = 0, t1: int | None = None):
+        """The [t1 - t0, E, N*C, stride] acceptor rows of ring slots t0..t1-1 (regenerated from the
+        compact form when the ring is compact)."""
+        t1 = self.T + 1 if t1 is None else t1
+        if not self.compact:
+            return self.acc_obs[t0:t1]
+        from .ppo import regen_acceptor_rows
+        return regen_acceptor_rows(self.acc_rows[t0:t1], self.acc_owner[t0:t1], self.acc_common, self.N)
 
     # ---- distributed helpers
     def _allreduce(self, params):
@@ -267,10 +291,15 @@ class Trainer:
         else:
             self.off.group.policy_old.act(sl(self.off_obs[t]), N * L, seed, base + 1, action=sl(self.off.actions[t]),
                                           logprob=sl(self.off.logprobs[t]), offset_dev=self.rng_ctr, stream=st)
-        self.acc.group.policy_old.act(sl(self.acc_obs[t]), N * C, seed, base + 3, action=sl(self.acc.actions[t]),
-                                      logprob=sl(self.acc.logprobs[t]), offset_dev=self.rng_ctr,
-                                      common_row=self.acc_common if self.common_rows else None, stream=st)
-        obs = dict(acceptor=sl(self.acc_obs[t + 1]), offer=sl(self.off_obs[t + 1]))
+        if self.compact:
+            self.acc.group.policy_old.act_compact(sl(self.acc_rows[t]), sl(self.acc_owner[t]), N * C, seed, base + 3,
+                                                  self.acc_common, action=sl(self.acc.actions[t]),
+                                                  logprob=sl(self.acc.logprobs[t]), offset_dev=self.rng_ctr, stream=st)
+        else:
+            self.acc.group.policy_old.act(sl(self.acc_obs[t]), N * C, seed, base + 3, action=sl(self.acc.actions[t]),
+                                          logprob=sl(self.acc.logprobs[t]), offset_dev=self.rng_ctr,
+                                          common_row=self.acc_common if self.common_rows else None, stream=st)
+        obs = dict(self._acc_out(t + 1, e0, e1), offer=sl(self.off_obs[t + 1]))
         rew = dict(offer=sl(self.off.rewards[t]).view(E, N, L), acceptor=sl(self.acc.rewards[t]).view(E, N, C),
                    agent=sl(self.agent_reward), auctioneer=sl(self.auct_reward),
                    price=sl(self.price.rewards[t]).view(E, N, L) if self.free else None)
@@ -363,7 +392,10 @@ class Trainer:
         sel = self._draws()
         losses = {}
         T, E = self.T, self.E
-        states_of = lambda u: (self.acc_obs if u is self.acc else (self.off_obs if u is self.off else self.price_obs))[:T]
+        def states_of(u):
+            if u is self.acc:
+                return self.acc_rows[:T] if self.compact else self.acc_obs[:T]
+            return (self.off_obs if u is self.off else self.price_obs)[:T]
         if self.fused:
             # Each unit type's draws update its nets in sequence (draw d trains on the weights draw
             # d-1 left), but the unit types are independent nets: step s of the update = epoch k of
@@ -376,12 +408,14 @@ class Trainer:
                 all_sel = torch.cat(sel[u.name]).to(torch.int32)
                 ret_all = unit_returns(u.rewards, all_sel, u.group.gamma)
                 common = self.acc_common if (u is self.acc and self.common_rows) else None
+                owner = self.acc_owner[:T].reshape(T * E, self.C) if (u is self.acc and self.compact) else None
+                st_u = states_of(u)
                 col, seq = 0, []
                 for u_sel in sel[u.name]:
-                    ep = u.group.fused_epoch(states_of(u).reshape(T * E, u.U, u.stride), u.actions.view(T * E, u.U),
+                    ep = u.group.fused_epoch(st_u.reshape(T * E, -1, u.stride), u.actions.view(T * E, u.U),
                                              u.logprobs.view(T * E, u.U), ret_all.view(-1)[col:],
                                              all_sel[col:col + u_sel.numel()], T, E, common_row=common,
-                                             returns_ld=all_sel.numel())
+                                             returns_ld=all_sel.numel(), core_owner=owner)
                     seq += [ep] * u.group.K
                     col += u_sel.numel()
                 steps[u.name] = (u, seq, [])
@@ -400,13 +434,18 @@ class Trainer:
         else:
             for u in self.units():
                 ls = []
+                st_u = self.acceptor_rows(0, T) if (u is self.acc and self.compact) else states_of(u)
                 for u_sel in sel[u.name]:
-                    x, a, lp, ret = u.batch(states_of(u), u_sel)
+                    x, a, lp, ret = u.batch(st_u, u_sel)
                     ls += u.group.update(x, a, lp, ret)
                 u.group.sync_old()
                 losses[u.name] = torch.stack(ls)
         # next iteration starts from the last observation
-        self.acc_obs[0].copy_(self.acc_obs[self.T])
+        if self.compact:
+            self.acc_rows[0].copy_(self.acc_rows[self.T])
+            self.acc_owner[0].copy_(self.acc_owner[self.T])
+        else:
+            self.acc_obs[0].copy_(self.acc_obs[self.T])
         self.off_obs[0].copy_(self.off_obs[self.T])
         return losses
 

@@ -314,6 +314,89 @@ def test_fused_grad_keyed_rows_matches_autograd(ms, G, T, E, U, A, K, n_keys):
         assert torch.equal(runs[0][1][k], runs[1][1][k]), k
 
 
+@pytest.mark.parametrize("G,per_group,N,C,O,E", [(8, 8, 8, 8, 24, 1001), (1, 16, 4, 4, 12, 333),
+                                                 (32, 32, 32, 32, 96, 65), (3, 4, 3, 4, 9, 200)])
+@pytest.mark.parametrize("ext_u", [False, True])
+def test_act_compact_bit_identical(ms, G, per_group, N, C, O, E, ext_u):
+    """ms_policy_act_compact on (core rows, owners) == ms_policy_act_common on the [E][N*C] rows they
+    regenerate (Agent.py:167-212), bit for bit; owners include the auctioneer (0)."""
+    ppo = _ppo(ms)
+    D, A = 3 + 2 * O, O + 1
+    stride = (D + 3) // 4 * 4
+    U = N * C
+    assert U == G * per_group
+    torch.manual_seed(7)
+    net = ppo.GroupedActorCritic(G, D, A).cuda()
+    gen = torch.Generator().manual_seed(8)
+    rows = torch.zeros((E, C, stride), dtype=torch.int8)
+    rows[..., :D] = torch.randint(-5, 13, (E, C, D), generator=gen, dtype=torch.int8)
+    owner = torch.randint(0, N + 1, (E, C), generator=gen, dtype=torch.int8)
+    crow = _common_row(D, stride, O).cuda()
+    rows, owner = rows.cuda(), owner.cuda()
+    full = ppo.regen_acceptor_rows(rows, owner, crow, N).contiguous()
+    assert full.shape == (E, U, stride)
+    u = torch.rand((E, U), generator=gen).cuda() if ext_u else None
+    a0, l0 = net.act(full, U, seed=3, offset=11, uniforms=u, common_row=crow)
+    a1, l1 = net.act_compact(rows, owner, U, 3, 11, crow, uniforms=u)
+    assert torch.equal(a0, a1)
+    assert torch.equal(l0.view(torch.int32), l1.view(torch.int32))
+
+
+@pytest.mark.parametrize("G,T,E,N,C,O,K", [(8, 20, 37, 8, 8, 24, 1), (2, 9, 301, 4, 4, 12, 2), (1, 41, 250, 2, 3, 6, 1)])
+def test_fused_grad_compact_rows_bit_identical(ms, G, T, E, N, C, O, K):
+    """ms_ppo_grad on compact acceptor rows (core rows + owners) == ms_ppo_grad with common_row on
+    the regenerated [R][N*C] rows, bit for bit (same rows in the same order through the same
+    arithmetic), and within tolerance of torch autograd."""
+    ppo = _ppo(ms)
+    D, A = 3 + 2 * O, O + 1
+    stride = (D + 3) // 4 * 4
+    R, U = T * E, N * C
+    gen = torch.Generator().manual_seed(9)
+    rows = torch.zeros((R, C, stride), dtype=torch.int8)
+    rows[..., :D] = torch.randint(-5, 13, (R, C, D), generator=gen, dtype=torch.int8)
+    owner = torch.randint(0, N + 1, (R, C), generator=gen, dtype=torch.int8)
+    actions = torch.randint(0, A, (R, U), generator=gen).to(torch.int8)
+    old_lp = -torch.rand((R, U), generator=gen) * 3
+    ret = torch.randn((T, E, G), generator=gen)
+    u_sel = torch.randint(0, U, (G,), generator=torch.Generator().manual_seed(4)).to(torch.int32)
+    crow = _common_row(D, stride, O).cuda()
+    rows, owner = rows.cuda(), owner.cuda()
+    full = ppo.regen_acceptor_rows(rows, owner, crow, N).contiguous()
+    args = (actions.cuda(), old_lp.cuda(), ret.cuda(), u_sel.cuda(), T, E)
+    res = []
+    for compact in (False, True):
+        torch.manual_seed(24)
+        grp = ppo.PPOGroup(G, D, A, 0.003, 0.01, 0.9, 0.2, K, device="cuda")
+        if compact:
+            losses = grp.update_fused(rows, *args, common_row=crow, core_owner=owner)
+        else:
+            losses = grp.update_fused(full, *args, common_row=crow)
+        res.append((losses, {k: getattr(grp.policy, k).detach().clone() for k in ppo.ACTOR_KEYS + ppo.CRITIC_KEYS}))
+    for l0, l1 in zip(res[0][0], res[1][0]):
+        assert torch.equal(l0, l1)
+    for k in res[0][1]:
+        assert torch.equal(res[0][1][k], res[1][1][k]), k
+
+
+def test_trainer_compact_matches_materialised(ms):
+    """The trainer on compact acceptor rings (the env emits core rows + owners, the act and gradient
+    kernels read them) == the trainer on the materialised [N*C] rows, bit for bit over two PPO
+    iterations (rings, actions, losses, weights)."""
+    tr_mod = importlib.import_module("marl-scheduling_amd.trainer")
+    trs = [tr_mod.Trainer.from_named("cfg3", n_envs=64, update_step=12, seed=5, device="cuda:0", compact=c)
+           for c in (True, False)]
+    assert trs[0].compact and not trs[1].compact
+    for _ in range(2):
+        outs = [t.iteration() for t in trs]
+        for k in outs[0]:
+            assert torch.equal(outs[0][k], outs[1][k]), k
+    assert torch.equal(trs[0].acceptor_rows(), trs[1].acceptor_rows())
+    assert torch.equal(trs[0].acc.actions, trs[1].acc.actions)
+    for u0, u1 in zip(trs[0].units(), trs[1].units()):
+        for k in importlib.import_module("marl-scheduling_amd.ppo").ACTOR_KEYS:
+            assert torch.equal(getattr(u0.group.policy, k), getattr(u1.group.policy, k)), (u0.name, k)
+
+
 def test_trainer_fused_matches_torch_update(ms):
     tr_mod = importlib.import_module("marl-scheduling_amd.trainer")
     trs = [tr_mod.Trainer.from_named("cfg3", n_envs=32, update_step=20, seed=4, device="cuda:0", fused=f)
@@ -398,7 +481,7 @@ def test_trainer_graph_replay_matches_eager(ms):
         outs = [t.iteration() for t in trs]
     for k in outs[0]:
         assert torch.equal(outs[0][k], outs[1][k]), k
-    assert torch.equal(trs[0].acc_obs, trs[1].acc_obs)
+    assert torch.equal(trs[0].acceptor_rows(), trs[1].acceptor_rows())
     assert trs[0].env.round == trs[1].env.round == 48
 
 
@@ -416,7 +499,7 @@ def test_trainer_two_stream_rollout(ms):
     two_e.rollout()
     torch.cuda.synchronize()
     h = E // 2
-    assert torch.equal(one.acc_obs[:, :h], two_e.acc_obs[:, :h])
+    assert torch.equal(one.acceptor_rows()[:, :h], two_e.acceptor_rows()[:, :h])
     assert torch.equal(one.off_obs[:, :h], two_e.off_obs[:, :h])
     assert torch.equal(one.acc.actions[:, :h], two_e.acc.actions[:, :h])
     assert torch.equal(one.acc.rewards[:, :h], two_e.acc.rewards[:, :h])
@@ -424,7 +507,8 @@ def test_trainer_two_stream_rollout(ms):
     for _ in range(2):  # graph capture happened in the first rollout; replays from here
         two_g.rollout()
         two_e.rollout()
-    for name in ("acc_obs", "off_obs", "price_obs"):
+    assert torch.equal(two_g.acceptor_rows(), two_e.acceptor_rows())
+    for name in ("off_obs", "price_obs"):
         assert torch.equal(getattr(two_g, name), getattr(two_e, name)), name
     for u in ("acc", "off", "price"):
         assert torch.equal(getattr(two_g, u).actions, getattr(two_e, u).actions), u

@@ -13,7 +13,7 @@ tr_mod = importlib.import_module("marl-scheduling_amd.trainer")
 tr = tr_mod.Trainer.from_named("cfg3", n_envs=int(os.environ.get("E", 16384)), update_step=50, seed=1, device="cuda:0")
 tr.iteration()
 torch.cuda.synchronize()
-obs = tr.acc_obs[10]
+obs = tr.acceptor_rows(10, 11)[0].contiguous()
 crow = tr.acc_common
 eq = (obs == crow).all(-1)
 print("common fraction", eq.float().mean().item(), "per agent-core:", eq.float().mean(0).view(8, 8).mean(1).tolist())
