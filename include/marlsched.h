@@ -328,6 +328,18 @@ int ms_offer_act_free(const ms_mlp_params* core_chooser, const ms_mlp_params* pr
                       float* core_logprob, int8_t* price_state, int8_t* price_action,
                       float* price_logprob, int8_t* env_price, void* stream);
 
+/* getActionForAllAgents of a free-price round (SchedulingEnvironment.py:150-172) in one launch:
+ * ms_offer_act_free on off_obs (Philox offset off_offset) and ms_policy_act_compact on (core_rows,
+ * core_owner) (offset acc_offset), same seed and offset_dev; outputs identical to the two calls.
+ * The offer and acceptor waves share the CUs, so neither launch waits out its own latency alone. */
+int ms_act_round_free(const ms_mlp_params* core_chooser, const ms_mlp_params* price_chooser, const int8_t* off_obs,
+                      int32_t off_stride, int32_t off_units, int32_t off_units_per_group, const ms_mlp_params* acceptor,
+                      const int8_t* core_rows, const int8_t* core_owner, int32_t acc_stride, int32_t acc_units,
+                      int32_t acc_units_per_group, int32_t n_cores, const int8_t* common_row, int64_t n_envs,
+                      uint64_t seed, uint64_t off_offset, uint64_t acc_offset, const uint64_t* offset_dev,
+                      int8_t* core_action, float* core_logprob, int8_t* price_state, int8_t* price_action,
+                      float* price_logprob, int8_t* env_price, int8_t* acc_action, float* acc_logprob, void* stream);
+
 /* Discounted Monte-Carlo returns + per-sequence normalisation (PPOmodules.py:128-137):
  * rewards [T][M] (f32, as stored per round), for each sequence m:
  * G_t = r_t + gamma*G_{t+1} in float64, cast to f32, then

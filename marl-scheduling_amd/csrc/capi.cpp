@@ -29,6 +29,10 @@ hipError_t launch_policy_act(const ms_mlp_params*, const int8_t*, int, int64_t, 
 hipError_t launch_policy_act_compact(const ms_mlp_params*, const int8_t*, const int8_t*, int, int64_t, int, int, int,
                                      const int8_t*, uint64_t, uint64_t, const uint64_t*, const float*, int8_t*, float*,
                                      hipStream_t);
+hipError_t launch_act_round(const ms_mlp_params*, const ms_mlp_params*, const int8_t*, int, int, int,
+                            const ms_mlp_params*, const int8_t*, const int8_t*, int, int, int, int, const int8_t*,
+                            int64_t, uint64_t, uint64_t, uint64_t, const uint64_t*, int8_t*, float*, int8_t*, int8_t*,
+                            float*, int8_t*, int8_t*, float*, hipStream_t);
 hipError_t launch_offer_act_free(const ms_mlp_params*, const ms_mlp_params*, const int8_t*, int, int64_t, int, int, int,
                                  uint64_t, uint64_t, const uint64_t*, const float*, int8_t*, float*, int8_t*, int8_t*,
                                  float*, int8_t*, hipStream_t);
@@ -516,6 +520,36 @@ int ms_policy_act_compact(const ms_mlp_params* p, const int8_t* core_rows, const
     HIP_TRY(ms::launch_policy_act_compact(p, core_rows, core_owner, obs_stride, n_envs, n_units, units_per_group,
                                           n_cores, common_row, seed, offset, offset_dev, uniforms, action, logprob,
                                           (hipStream_t)stream));
+    return MS_OK;
+}
+
+int ms_act_round_free(const ms_mlp_params* core, const ms_mlp_params* price, const int8_t* off_obs, int32_t off_stride,
+                      int32_t off_units, int32_t off_units_per_group, const ms_mlp_params* acc, const int8_t* core_rows,
+                      const int8_t* core_owner, int32_t acc_stride, int32_t acc_units, int32_t acc_units_per_group,
+                      int32_t n_cores, const int8_t* common_row, int64_t n_envs, uint64_t seed, uint64_t off_offset,
+                      uint64_t acc_offset, const uint64_t* offset_dev, int8_t* core_action, float* core_logprob,
+                      int8_t* price_state, int8_t* price_action, float* price_logprob, int8_t* env_price,
+                      int8_t* acc_action, float* acc_logprob, void* stream) {
+    if (!off_obs || !core_rows || !core_owner || !common_row || !core_action || !core_logprob || !price_state ||
+        !price_action || !price_logprob || !env_price || !acc_action || !acc_logprob)
+        return fail(MS_EINVAL, "NULL argument");
+    if (n_envs < 1) return fail(MS_EINVAL, "n_envs must be >= 1");
+    int rc = check_mlp(core, off_stride, off_units, off_units_per_group);
+    if (rc) return rc;
+    rc = check_mlp(price, 4, off_units, off_units_per_group);
+    if (rc) return rc;
+    rc = check_mlp(acc, acc_stride, acc_units, acc_units_per_group);
+    if (rc) return rc;
+    if (price->in_dim != 4 || price->n_groups != core->n_groups) return fail(MS_EINVAL, "price chooser must be 4 -> A");
+    if (core->in_dim != 2 * n_cores + 2 || core->n_actions != n_cores + 1)
+        return fail(MS_EINVAL, "core chooser must be (2C+2) -> C+1");
+    if (n_cores < 1 || acc_units % n_cores != 0 || acc_stride < 16)
+        return fail(MS_EINVAL, "acceptor units must be n_agents * n_cores with obs_stride >= 16");
+    HIP_TRY(ms::launch_act_round(core, price, off_obs, off_stride, off_units, off_units_per_group, acc, core_rows,
+                                 core_owner, acc_stride, acc_units, acc_units_per_group, n_cores, common_row, n_envs,
+                                 seed, off_offset, acc_offset, offset_dev, core_action, core_logprob, price_state,
+                                 price_action, price_logprob, env_price, acc_action, acc_logprob,
+                                 (hipStream_t)stream));
     return MS_OK;
 }
 

@@ -12,6 +12,58 @@
 
 namespace ms {
 
+// ---- the four 16-lane rows of a wave without LDS: v_permlane16_swap / v_permlane32_swap (gfx950).
+// With both operands the same register, permlane16_swap returns rows (0, 0, 2, 2) and (1, 1, 3, 3)
+// and permlane32_swap halves (lo, lo) and (hi, hi): each lane gets its partner's value beside its
+// own. The reductions below equal the __shfl_xor(16) / (32) forms bit for bit (add and max are
+// commutative), without the LDS crossbar round trips.
+__device__ __forceinline__ void swap16(uint32_t v, uint32_t& a, uint32_t& b) {
+    const auto r = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+    a = r[0];
+    b = r[1];
+}
+__device__ __forceinline__ void swap32(uint32_t v, uint32_t& a, uint32_t& b) {
+    const auto r = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+    a = r[0];
+    b = r[1];
+}
+// v(l) + v(l ^ 16), then + the same of l ^ 32: the sum over lanes j, j+16, j+32, j+48 (j = l % 16)
+__device__ __forceinline__ float rows_sum(float v) {
+    uint32_t a, b;
+    swap16(__float_as_uint(v), a, b);
+    const float s = __uint_as_float(a) + __uint_as_float(b);
+    swap32(__float_as_uint(s), a, b);
+    return __uint_as_float(a) + __uint_as_float(b);
+}
+__device__ __forceinline__ float rows_max(float v) {
+    uint32_t a, b;
+    swap16(__float_as_uint(v), a, b);
+    const float s = fmaxf(__uint_as_float(a), __uint_as_float(b));
+    swap32(__float_as_uint(s), a, b);
+    return fmaxf(__uint_as_float(a), __uint_as_float(b));
+}
+__device__ __forceinline__ int rows_sum_i(int v) {
+    uint32_t a, b;
+    swap16((uint32_t)v, a, b);
+    const int s = (int)a + (int)b;
+    swap32((uint32_t)s, a, b);
+    return (int)a + (int)b;
+}
+__device__ __forceinline__ int rows_max_i(int v) {
+    uint32_t a, b;
+    swap16((uint32_t)v, a, b);
+    const int s = max((int)a, (int)b);
+    swap32((uint32_t)s, a, b);
+    return max((int)a, (int)b);
+}
+// r[k] = v of lane l % 16 + 16 k (= __shfl(v, l % 16 + 16 k)) for k = 0..3
+__device__ __forceinline__ void rows_bcast(uint32_t v, uint32_t (&r)[4]) {
+    uint32_t a, b;
+    swap16(v, a, b);          // a: rows (0, 0, 2, 2), b: rows (1, 1, 3, 3)
+    swap32(a, r[0], r[2]);    // rows 0 and 2 everywhere
+    swap32(b, r[1], r[3]);    // rows 1 and 3
+}
+
 typedef uint32_t u4a __attribute__((ext_vector_type(4), aligned(4)));  // 4-byte aligned 16-byte load
 
 template <int LPR>

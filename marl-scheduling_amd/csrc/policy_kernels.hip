@@ -19,6 +19,7 @@
 // float64, cast to f32 and normalised per sequence.
 #include <hip/hip_runtime.h>
 #include <math.h>
+#include <stdlib.h>
 
 #include "../../include/marlsched.h"
 #include "ms_common.h"
@@ -56,11 +57,7 @@ __device__ __forceinline__ void philox2(uint32_t c0, uint32_t c1, uint32_t c2, u
 
 __device__ __forceinline__ float u24(uint32_t r) { return (float)(r >> 8) * (1.0f / 16777216.0f); }
 
-__device__ __forceinline__ float xsum4g(float v) {
-    v += __shfl_xor(v, 16);
-    v += __shfl_xor(v, 32);
-    return v;
-}
+__device__ __forceinline__ float xsum4g(float v) { return rows_sum(v); }
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef uint32_t u4v __attribute__((ext_vector_type(4)));
@@ -180,8 +177,7 @@ struct Head {
                 m = fmaxf(m, z[t][q]);
             }
         }
-        m = fmaxf(m, __shfl_xor(m, 16));
-        m = fmaxf(m, __shfl_xor(m, 32));
+        m = rows_max(m);
         float bs[NT];
         const float m_l2e = m * 1.4426950408889634f;
 #pragma unroll
@@ -200,8 +196,10 @@ struct Head {
         float cum = 0.f;
 #pragma unroll
         for (int t = 0; t < NT; t++) {
-            const float gs0 = __shfl(bs[t], j), gs1 = __shfl(bs[t], j + 16), gs2 = __shfl(bs[t], j + 32),
-                        gs3 = __shfl(bs[t], j + 48);
+            uint32_t gsr[4];
+            rows_bcast(__float_as_uint(bs[t]), gsr);
+            const float gs0 = __uint_as_float(gsr[0]), gs1 = __uint_as_float(gsr[1]), gs2 = __uint_as_float(gsr[2]),
+                        gs3 = __uint_as_float(gsr[3]);
             float cc = cum + (g4 > 0 ? gs0 : 0.f) + (g4 > 1 ? gs1 : 0.f) + (g4 > 2 ? gs2 : 0.f);
 #pragma unroll
             for (int q = 0; q < 4; q++) {
@@ -226,8 +224,7 @@ struct Head {
         for (int t = 0; t < NT; t++)
 #pragma unroll
             for (int q = 0; q < 4; q++) cnt += (c[t][q] <= target) ? 1 : 0;
-        cnt += __shfl_xor(cnt, 16);
-        cnt += __shfl_xor(cnt, 32);
+        cnt = rows_sum_i(cnt);
         int a_sel = cnt;
         if (__builtin_expect(__ballot(a_sel >= A) != 0, 0)) {
             // u * S at or beyond the rounded total: the last action with nonzero probability
@@ -250,8 +247,7 @@ struct Head {
 #pragma unroll
             for (int q = 0; q < 4; q++)
                 if (z[t][q] > 0.f) last_nz = 16 * t + 4 * g4 + q;
-        last_nz = max(last_nz, __shfl_xor(last_nz, 16));
-        last_nz = max(last_nz, __shfl_xor(last_nz, 32));
+        last_nz = rows_max_i(last_nz);
         return last_nz;
     }
 
@@ -312,9 +308,9 @@ struct ActArgs {
 // lane (j, g) loads dwords 8s + 2g, 8s + 2g + 1 of tile row j, which are exactly its B fragment of
 // k-step s. S1 = ceil(stride / 32) k-steps.
 template <int S1, int NT, int NT2, bool EXT_U>
-__global__ void __launch_bounds__(256) k_act(ActArgs a) {
+__device__ __forceinline__ void act_tiles(const ActArgs& a, int block) {
     const int tid = threadIdx.x, lane = tid & 63;
-    const int gw = blockIdx.x * 4 + (tid >> 6);  // global wave index
+    const int gw = block * 4 + (tid >> 6);  // global wave index
     const int grp = gw / a.waves_per_group;
     const int wv = gw - grp * a.waves_per_group;
     if (grp >= a.n1.n_groups) return;
@@ -348,12 +344,15 @@ __global__ void __launch_bounds__(256) k_act(ActArgs a) {
     auto row_of = [&](int tile) -> int { return row_of_lane(tile, j); };
     // Philox uniforms, computed for 4 tiles at a time: lane (j, g4) draws for row j of tile
     // base + g4 (counter = the obs row index, so the values do not depend on the tiling)
-    uint32_t rnd0 = 0, rnd1 = 0;
+    uint32_t rnd0 = 0, rnd1 = 0, rb0[4] = {0, 0, 0, 0}, rb1[4] = {0, 0, 0, 0};
     auto draw4 = [&](int base) {
         const int r = base + g4 < t1 ? row_of_lane(base + g4, j) : -1;
         philox2((uint32_t)r, 0u, (uint32_t)off, (uint32_t)(off >> 32), (uint32_t)a.seed, (uint32_t)(a.seed >> 32), rnd0,
                 rnd1);
+        rows_bcast(rnd0, rb0);  // tile base + k takes row k's draws
+        rows_bcast(rnd1, rb1);
     };
+    auto pick4 = [](const uint32_t (&v)[4], int k) { return k == 0 ? v[0] : (k == 1 ? v[1] : (k == 2 ? v[2] : v[3])); };
     uint32_t pre[S1][2];
     // unconditional loads from clamped addresses, used as loaded: the rows past the end are never
     // written and the dwords past the row meet zero weights (so the wait lands at the use)
@@ -386,8 +385,8 @@ __global__ void __launch_bounds__(256) k_act(ActArgs a) {
         } else {
             const int k = (tile - t0) & 3;
             if (k == 0) draw4(tile);
-            u1 = u24((uint32_t)__shfl((int)rnd0, j + 16 * k));
-            u2 = u24((uint32_t)__shfl((int)rnd1, j + 16 * k));
+            u1 = u24(pick4(rb0, k));
+            u2 = u24(pick4(rb1, k));
         }
         f4 acc = {0, 0, 0, 0};
 #pragma unroll
@@ -445,14 +444,19 @@ __global__ void __launch_bounds__(256) k_act(ActArgs a) {
 // MFMA tiles as in k_act. Outputs are bit-identical to k_act's.
 constexpr int kCommonSeg = 512;  // most rows per wave = capacity of the wave's LDS row list
 
+template <int S1, int NT, int NT2, bool EXT_U>
+__global__ void __launch_bounds__(256) k_act(ActArgs a) {
+    act_tiles<S1, NT, NT2, EXT_U>(a, blockIdx.x);
+}
+
 template <int S1, int NT, bool EXT_U, bool OWN>
-__global__ void __launch_bounds__(256) k_act_common(ActArgs a) {
+__device__ __forceinline__ void act_common_rows(const ActArgs& a, int block) {
     __shared__ int32_t s_list[4][kCommonSeg];
     __shared__ float s_cum[4][16 * NT], s_lp[4][16 * NT], s_S[4];
     __shared__ int s_lnz[4];
     __shared__ uint32_t s_tmpl[4][8 * S1];
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    const int gw = blockIdx.x * 4 + wid;
+    const int gw = block * 4 + wid;
     const int grp = gw / a.waves_per_group;
     const int wv = gw - grp * a.waves_per_group;
     if (grp >= a.n1.n_groups) return;  // whole waves only: the kernel has no block barrier
@@ -514,7 +518,6 @@ __global__ void __launch_bounds__(256) k_act_common(ActArgs a) {
     //      from the table, the others listed
     int n_row = 0;
     bool n_in = false;
-    int8_t n_own = 0, n_agent1 = 0;
     // compact rows: the core row of (e, u) and whether agent u / C + 1 owns core u % C
     auto core_row_of = [&](int row, int& c_out) -> size_t {
         const int e = row / a.U, u = row - e * a.U;
@@ -532,19 +535,9 @@ __global__ void __launch_bounds__(256) k_act_common(ActArgs a) {
         const int i = i0 + lane;
         n_in = i < i_end;
         n_row = n_in ? row_of_item(i) : 0;
-        if constexpr (OWN) {
-            int ag;
-            const size_t cr = core_row_of(n_row, ag);
-            n_own = a.owner[cr];
-            n_agent1 = (int8_t)(ag + 1);
-        }
     };
-    if (i_begin < i_end) load_step(i_begin);
-    for (int i0 = i_begin; i0 < i_end; i0 += 64) {
-        const int row = n_row;
-        const bool in = n_in;
-        const bool common = (OWN ? n_own != n_agent1 : cs.lane_row_common(lane)) && in;
-        if (i0 + 64 < i_end) load_step(i0 + 64);
+    // one 64-row step: common rows sample from the table, the others are listed
+    auto scan_step = [&](int row, bool in, bool common) {
         if (common) {
             const float target = uniform_of(row) * S;
             int cnt = 0;
@@ -558,6 +551,35 @@ __global__ void __launch_bounds__(256) k_act_common(ActArgs a) {
         const uint64_t m = __ballot(other);
         if (other) list[n_list + __popcll(m & below)] = row;
         n_list += __popcll(m);
+    };
+    if constexpr (OWN) {
+        // compact rows: every step's owner byte is loaded up front (one memory round trip per wave)
+        constexpr int MS = kCommonSeg / 64;
+        int8_t own_st[MS], me_st[MS];
+        int row_st[MS];
+#pragma unroll
+        for (int st = 0; st < MS; st++) {
+            const int i = i_begin + 64 * st + lane;
+            row_st[st] = i < i_end ? row_of_item(i) : -1;
+            int ag;
+            const size_t cr = core_row_of(row_st[st] < 0 ? 0 : row_st[st], ag);
+            own_st[st] = a.owner[cr];
+            me_st[st] = (int8_t)(ag + 1);
+        }
+#pragma unroll
+        for (int st = 0; st < MS; st++)
+            if (i_begin + 64 * st < i_end)
+                scan_step(row_st[st], row_st[st] >= 0, row_st[st] >= 0 && own_st[st] != me_st[st]);
+    } else {
+        // (one 64-row step ahead in registers)
+        if (i_begin < i_end) load_step(i_begin);
+        for (int i0 = i_begin; i0 < i_end; i0 += 64) {
+            const int row = n_row;
+            const bool in = n_in;
+            const bool common = cs.lane_row_common(lane) && in;
+            if (i0 + 64 < i_end) load_step(i0 + 64);
+            scan_step(row, in, common);
+        }
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -604,34 +626,69 @@ __global__ void __launch_bounds__(256) k_act_common(ActArgs a) {
     }
 }
 
-template <int S1, int NT>
-static hipError_t launch_act_common_t(ActArgs& a, hipStream_t st) {
-    auto kern = a.owner ? (a.uniforms ? k_act_common<S1, NT, true, true> : k_act_common<S1, NT, false, true>)
-                        : (a.uniforms ? k_act_common<S1, NT, true, false> : k_act_common<S1, NT, false, false>);
+// launch-shape knobs for measurements (tools/); the defaults are the measured best for cfg3
+static long long env_int(const char* name, long long dflt) {
+    const char* v = getenv(name);
+    return v && *v ? atoll(v) : dflt;
+}
+
+template <int S1, int NT, bool EXT_U, bool OWN>
+__global__ void __launch_bounds__(256) k_act_common(ActArgs a) {
+    act_common_rows<S1, NT, EXT_U, OWN>(a, blockIdx.x);
+}
+
+// getActionForAllAgents of a free-price round (SchedulingEnvironment.py:150-172) in one launch: the
+// first off_blocks blocks run the offer units (core + price chooser, k_act), the rest the acceptor
+// units on compact rows (k_act_common). The two workloads' waves share the CUs, so one's waits
+// hide under the other's work instead of each launch waiting out its own chain.
+template <int S1a, int NTa, int NT2a, int S1b, int NTb>
+__global__ void __launch_bounds__(256) k_act_pair(ActArgs off, ActArgs acc, int off_blocks) {
+    if ((int)blockIdx.x < off_blocks)
+        act_tiles<S1a, NTa, NT2a, false>(off, blockIdx.x);
+    else
+        act_common_rows<S1b, NTb, false, true>(acc, (int)blockIdx.x - off_blocks);
+}
+
+// launch shapes (set the wave split in a, return the blocks)
+static unsigned act_common_blocks(ActArgs& a, long long target) {
     const int G = a.n1.n_groups;
-    // ~3072 waves over all groups (measured best for cfg3), whole 64-row scan steps each, at most
-    // one LDS list of rows
-    long long ipw = ((long long)a.n_items * G + 3071) / 3072;
+    // ~target waves over all groups, whole 64-row scan steps each, at most one LDS list of rows
+    long long ipw = ((long long)a.n_items * G + target - 1) / target;
     ipw = (ipw + 63) / 64 * 64;
     ipw = ipw < 64 ? 64 : (ipw > kCommonSeg ? kCommonSeg : ipw);
     a.items_per_wave = (int)ipw;
     a.waves_per_group = (a.n_items + a.items_per_wave - 1) / a.items_per_wave;
     const long long waves = (long long)a.waves_per_group * G;
-    hipLaunchKernelGGL(kern, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, st, a);
+    return (unsigned)((waves + 3) / 4);
+}
+
+template <int S1, int NT>
+static hipError_t launch_act_common_t(ActArgs& a, hipStream_t st) {
+    auto kern = a.owner ? (a.uniforms ? k_act_common<S1, NT, true, true> : k_act_common<S1, NT, false, true>)
+                        : (a.uniforms ? k_act_common<S1, NT, true, false> : k_act_common<S1, NT, false, false>);
+    static const long long target = env_int("MS_ACT_COMMON_WAVES", 1536);  // measured best for cfg3 alone
+    const unsigned blocks = act_common_blocks(a, target);
+    hipLaunchKernelGGL(kern, dim3(blocks), dim3(256), 0, st, a);
     return hipGetLastError();
+}
+
+static unsigned act_blocks(ActArgs& a, long long target) {
+    const int G = a.n1.n_groups;
+    const int tiles = (a.n_items + 15) / 16;
+    // ~target waves over all groups; each wave walks a contiguous tile range with a register prefetch
+    int tpw = (int)(((long long)tiles * G + target - 1) / target);
+    a.tiles_per_wave = tpw < 1 ? 1 : tpw;
+    a.waves_per_group = (tiles + a.tiles_per_wave - 1) / a.tiles_per_wave;
+    const long long waves = (long long)a.waves_per_group * G;
+    return (unsigned)((waves + 3) / 4);
 }
 
 template <int S1, int NT, int NT2>
 static hipError_t launch_act_t(ActArgs& a, hipStream_t st) {
     auto kern = a.uniforms ? k_act<S1, NT, NT2, true> : k_act<S1, NT, NT2, false>;
-    const int G = a.n1.n_groups;
-    const int tiles = (a.n_items + 15) / 16;
-    // ~8192 waves over all groups; each wave walks a contiguous tile range with a register prefetch
-    int tpw = (int)(((long long)tiles * G + 8191) / 8192);
-    a.tiles_per_wave = tpw < 1 ? 1 : tpw;
-    a.waves_per_group = (tiles + a.tiles_per_wave - 1) / a.tiles_per_wave;
-    const long long waves = (long long)a.waves_per_group * G;
-    hipLaunchKernelGGL(kern, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, st, a);
+    static const long long target = env_int("MS_ACT_WAVES", 8192);  // measured best for cfg3 alone
+    const unsigned blocks = act_blocks(a, target);
+    hipLaunchKernelGGL(kern, dim3(blocks), dim3(256), 0, st, a);
     return hipGetLastError();
 }
 
@@ -693,11 +750,9 @@ hipError_t launch_policy_act(const ms_mlp_params* p, const int8_t* obs, int stri
     return dispatch_act(a, st);
 }
 
-hipError_t launch_policy_act_compact(const ms_mlp_params* p, const int8_t* core_rows, const int8_t* core_owner,
-                                     int stride, int64_t E, int U, int S, int n_cores, const int8_t* common,
-                                     uint64_t seed, uint64_t offset, const uint64_t* offset_dev, const float* uniforms,
-                                     int8_t* action, float* logprob, hipStream_t st) {
-    if (!common || stride < 16 || n_cores < 1 || U % n_cores != 0) return hipErrorInvalidValue;
+static ActArgs compact_args(const ms_mlp_params* p, const int8_t* core_rows, const int8_t* core_owner, int stride,
+                            int64_t E, int U, int S, int n_cores, const int8_t* common, uint64_t seed, uint64_t offset,
+                            const uint64_t* offset_dev, const float* uniforms, int8_t* action, float* logprob) {
     ActArgs a{};
     a.common = common;
     a.owner = core_owner;
@@ -716,14 +771,24 @@ hipError_t launch_policy_act_compact(const ms_mlp_params* p, const int8_t* core_
     a.uniforms = uniforms;
     a.action = action;
     a.logprob = logprob;
+    return a;
+}
+
+hipError_t launch_policy_act_compact(const ms_mlp_params* p, const int8_t* core_rows, const int8_t* core_owner,
+                                     int stride, int64_t E, int U, int S, int n_cores, const int8_t* common,
+                                     uint64_t seed, uint64_t offset, const uint64_t* offset_dev, const float* uniforms,
+                                     int8_t* action, float* logprob, hipStream_t st) {
+    if (!common || stride < 16 || n_cores < 1 || U % n_cores != 0) return hipErrorInvalidValue;
+    ActArgs a = compact_args(p, core_rows, core_owner, stride, E, U, S, n_cores, common, seed, offset, offset_dev,
+                             uniforms, action, logprob);
     return dispatch_act(a, st);
 }
 
-hipError_t launch_offer_act_free(const ms_mlp_params* core, const ms_mlp_params* price, const int8_t* obs, int stride,
-                                 int64_t E, int U, int S, int n_cores, uint64_t seed, uint64_t offset,
-                                 const uint64_t* offset_dev, const float* uniforms, int8_t* core_action,
-                                 float* core_logprob, int8_t* price_state, int8_t* price_action, float* price_logprob,
-                                 int8_t* env_price, hipStream_t st) {
+static ActArgs offer_free_args(const ms_mlp_params* core, const ms_mlp_params* price, const int8_t* obs, int stride,
+                               int64_t E, int U, int S, int n_cores, uint64_t seed, uint64_t offset,
+                               const uint64_t* offset_dev, const float* uniforms, int8_t* core_action,
+                               float* core_logprob, int8_t* price_state, int8_t* price_action, float* price_logprob,
+                               int8_t* env_price) {
     ActArgs a{};
     a.n1 = *core;
     a.n2 = *price;
@@ -744,7 +809,48 @@ hipError_t launch_offer_act_free(const ms_mlp_params* core, const ms_mlp_params*
     a.price_action = price_action;
     a.price_logprob = price_logprob;
     a.env_price = env_price;
+    return a;
+}
+
+hipError_t launch_offer_act_free(const ms_mlp_params* core, const ms_mlp_params* price, const int8_t* obs, int stride,
+                                 int64_t E, int U, int S, int n_cores, uint64_t seed, uint64_t offset,
+                                 const uint64_t* offset_dev, const float* uniforms, int8_t* core_action,
+                                 float* core_logprob, int8_t* price_state, int8_t* price_action, float* price_logprob,
+                                 int8_t* env_price, hipStream_t st) {
+    ActArgs a = offer_free_args(core, price, obs, stride, E, U, S, n_cores, seed, offset, offset_dev, uniforms,
+                                core_action, core_logprob, price_state, price_action, price_logprob, env_price);
     return dispatch_act(a, st);
+}
+
+// both halves of a free-price round's acting in one launch when their shapes have a paired kernel
+// (cfg3: offer rows of <= 32 bytes, <= 16 actions; acceptor rows of <= 64 bytes, <= 32 actions),
+// else the two launches in order
+hipError_t launch_act_round(const ms_mlp_params* core, const ms_mlp_params* price, const int8_t* off_obs,
+                            int off_stride, int off_U, int off_S, const ms_mlp_params* acc,
+                            const int8_t* core_rows, const int8_t* core_owner, int acc_stride, int acc_U, int acc_S,
+                            int n_cores, const int8_t* common, int64_t E, uint64_t seed, uint64_t off_offset,
+                            uint64_t acc_offset, const uint64_t* offset_dev, int8_t* core_action, float* core_logprob,
+                            int8_t* price_state, int8_t* price_action, float* price_logprob, int8_t* env_price,
+                            int8_t* acc_action, float* acc_logprob, hipStream_t st) {
+    if (!common || acc_stride < 16 || n_cores < 1 || acc_U % n_cores != 0) return hipErrorInvalidValue;
+    if (price->in_dim != 4) return hipErrorInvalidValue;
+    ActArgs o = offer_free_args(core, price, off_obs, off_stride, E, off_U, off_S, n_cores, seed, off_offset,
+                                offset_dev, nullptr, core_action, core_logprob, price_state, price_action,
+                                price_logprob, env_price);
+    ActArgs c = compact_args(acc, core_rows, core_owner, acc_stride, E, acc_U, acc_S, n_cores, common, seed,
+                             acc_offset, offset_dev, nullptr, acc_action, acc_logprob);
+    const bool paired = (off_stride + 31) / 32 == 1 && core->n_actions <= 16 && price->n_actions <= 16 &&
+                        (acc_stride + 31) / 32 == 2 && acc->n_actions <= 32 && !env_int("MS_ACT_UNPAIRED", 0);
+    if (!paired) {
+        hipError_t e = dispatch_act(o, st);
+        return e != hipSuccess ? e : dispatch_act(c, st);
+    }
+    // fewer, longer waves than either launch alone: the other half's waves fill the gaps
+    // (tools/sweep_act.sh: 2048 / 768 -> 2048 offer and 2048 acceptor waves at cfg3)
+    static const long long t_off = env_int("MS_ACT_PAIR_WAVES", 2048), t_acc = env_int("MS_ACT_PAIR_COMMON_WAVES", 768);
+    const unsigned ob = act_blocks(o, t_off), cb = act_common_blocks(c, t_acc);
+    hipLaunchKernelGGL((k_act_pair<1, 1, 1, 2, 2>), dim3(ob + cb), dim3(256), 0, st, o, c, (int)ob);
+    return hipGetLastError();
 }
 
 // ---------------------------------------------------------------------------

@@ -45,16 +45,8 @@ __device__ __forceinline__ float xsum16(float v) {  // sum over the 16 lanes sha
     v += __shfl_xor(v, 8);
     return v;
 }
-__device__ __forceinline__ float xsum4g(float v) {  // sum over lanes j, j+16, j+32, j+48
-    v += __shfl_xor(v, 16);
-    v += __shfl_xor(v, 32);
-    return v;
-}
-__device__ __forceinline__ float xmax4g(float v) {
-    v = fmaxf(v, __shfl_xor(v, 16));
-    v = fmaxf(v, __shfl_xor(v, 32));
-    return v;
-}
+__device__ __forceinline__ float xsum4g(float v) { return rows_sum(v); }  // sum over lanes j, j+16, j+32, j+48
+__device__ __forceinline__ float xmax4g(float v) { return rows_max(v); }
 
 // tanh(x) = sign(x) (1 - t) / (1 + t), t = exp(-2|x|): absolute error ~1e-7 everywhere
 // tanh(x) = 1 - 2 / (1 + exp(2x)): exp overflows to inf for large x (-> 1) and underflows to 0 for

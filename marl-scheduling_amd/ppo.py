@@ -187,6 +187,26 @@ class GroupedActorCritic(nn.Module):
         return action, logprob
 
 
+@torch.no_grad()
+def act_round_free(core: GroupedActorCritic, price: GroupedActorCritic, off_obs, acc: GroupedActorCritic, core_rows,
+                   core_owner, common_row, n_cores: int, seed: int, off_offset: int, acc_offset: int, out: dict,
+                   acc_action, acc_logprob, offset_dev=None, stream=None):
+    """``offer_act_free`` + ``act_compact`` of one free-price round in one launch (ms_act_round_free):
+    getActionForAllAgents (SchedulingEnvironment.py:150-172); outputs identical to the two calls."""
+    E, U_off, off_stride = off_obs.shape
+    _, C, acc_stride = core_rows.shape
+    U_acc = acc_action.shape[1]
+    assert off_obs.is_contiguous() and core_rows.is_contiguous() and core_owner.is_contiguous()
+    pc, pp, pa = core.mlp_params(), price.mlp_params(), acc.mlp_params()
+    check(lib.ms_act_round_free(ct.byref(pc), ct.byref(pp), ptr(off_obs), off_stride, U_off, U_off // core.G,
+                                ct.byref(pa), ptr(core_rows), ptr(core_owner), acc_stride, U_acc, U_acc // acc.G,
+                                n_cores, ptr(common_row), E, ct.c_uint64(seed), ct.c_uint64(off_offset),
+                                ct.c_uint64(acc_offset), ptr(offset_dev), ptr(out["core_action"]),
+                                ptr(out["core_logprob"]), ptr(out["price_state"]), ptr(out["price_action"]),
+                                ptr(out["price_logprob"]), ptr(out["env_price"]), ptr(acc_action), ptr(acc_logprob),
+                                stream_ptr(stream)))
+
+
 def regen_acceptor_rows(core_rows, core_owner, common_row, n_agents: int):
     """The [..., N*C, stride] acceptor rows of compact observations (core_rows [..., C, stride],
     core_owner [..., C]): row (a, c) = core_rows[c] if core_owner[c] == a + 1 else common_row

@@ -27,7 +27,8 @@ import torch
 
 from . import abi
 from .env import BatchedEnv
-from .ppo import PPOGroup, discounted_returns, offer_act_free, reference_init_order, reference_nets, unit_returns
+from .ppo import (PPOGroup, act_round_free, discounted_returns, offer_act_free, reference_init_order, reference_nets,
+                  unit_returns)
 
 
 @dataclass
@@ -286,12 +287,20 @@ class Trainer:
             out = dict(core_action=sl(self.off.actions[t]), core_logprob=sl(self.off.logprobs[t]),
                        price_state=sl(self.price_obs[t]), price_action=sl(self.price.actions[t]),
                        price_logprob=sl(self.price.logprobs[t]), env_price=sl(self.env_price))
-            offer_act_free(self.off.group.policy_old, self.price.group.policy_old, sl(self.off_obs[t]), C, seed,
-                           base + 1, out, offset_dev=self.rng_ctr, stream=st)
+            if self.compact:  # the acceptors too, in the same launch
+                act_round_free(self.off.group.policy_old, self.price.group.policy_old, sl(self.off_obs[t]),
+                               self.acc.group.policy_old, sl(self.acc_rows[t]), sl(self.acc_owner[t]), self.acc_common,
+                               C, seed, base + 1, base + 3, out, sl(self.acc.actions[t]), sl(self.acc.logprobs[t]),
+                               offset_dev=self.rng_ctr, stream=st)
+            else:
+                offer_act_free(self.off.group.policy_old, self.price.group.policy_old, sl(self.off_obs[t]), C, seed,
+                               base + 1, out, offset_dev=self.rng_ctr, stream=st)
         else:
             self.off.group.policy_old.act(sl(self.off_obs[t]), N * L, seed, base + 1, action=sl(self.off.actions[t]),
                                           logprob=sl(self.off.logprobs[t]), offset_dev=self.rng_ctr, stream=st)
-        if self.compact:
+        if self.compact and self.free:
+            pass  # acted above with the offers
+        elif self.compact:
             self.acc.group.policy_old.act_compact(sl(self.acc_rows[t]), sl(self.acc_owner[t]), N * C, seed, base + 3,
                                                   self.acc_common, action=sl(self.acc.actions[t]),
                                                   logprob=sl(self.acc.logprobs[t]), offset_dev=self.rng_ctr, stream=st)

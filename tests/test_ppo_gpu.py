@@ -378,6 +378,47 @@ def test_fused_grad_compact_rows_bit_identical(ms, G, T, E, N, C, O, K):
         assert torch.equal(res[0][1][k], res[1][1][k]), k
 
 
+@pytest.mark.parametrize("N,C,L,O,E", [(8, 8, 3, 24, 2048), (4, 4, 3, 12, 301), (16, 16, 3, 48, 97)])
+def test_act_round_free_matches_separate_calls(ms, N, C, L, O, E):
+    """ms_act_round_free (offer units + compact acceptor units in one launch; the paired kernel for
+    cfg3's shapes, two launches otherwise) == ms_offer_act_free + ms_policy_act_compact, bit for bit."""
+    ppo = _ppo(ms)
+    torch.manual_seed(11)
+    D_off, A_off, D_acc, A_acc = 2 * C + 2, C + 1, 3 + 2 * O, O + 1
+    s_off, s_acc = (D_off + 3) & ~3, (D_acc + 3) & ~3
+    core = ppo.GroupedActorCritic(N, D_off, A_off).cuda()
+    price = ppo.GroupedActorCritic(N, 4, 13).cuda()
+    acc = ppo.GroupedActorCritic(N, D_acc, A_acc).cuda()
+    gen = torch.Generator().manual_seed(12)
+    off_obs = torch.zeros((E, N * L, s_off), dtype=torch.int8)
+    off_obs[..., :D_off] = torch.randint(-1, 13, (E, N * L, D_off), generator=gen, dtype=torch.int8)
+    rows = torch.zeros((E, C, s_acc), dtype=torch.int8)
+    rows[..., :D_acc] = torch.randint(-5, 13, (E, C, D_acc), generator=gen, dtype=torch.int8)
+    owner = torch.randint(0, N + 1, (E, C), generator=gen, dtype=torch.int8)
+    off_obs, rows, owner = off_obs.cuda(), rows.cuda(), owner.cuda()
+    crow = _common_row(D_acc, s_acc, O).cuda()
+    ctr = torch.tensor([40], dtype=torch.int64, device="cuda")
+
+    def outs():
+        d = "cuda"
+        return dict(core_action=torch.empty((E, N * L), dtype=torch.int8, device=d),
+                    core_logprob=torch.empty((E, N * L), device=d),
+                    price_state=torch.empty((E, N * L, 4), dtype=torch.int8, device=d),
+                    price_action=torch.empty((E, N * L), dtype=torch.int8, device=d),
+                    price_logprob=torch.empty((E, N * L), device=d),
+                    env_price=torch.empty((E, N * L), dtype=torch.int8, device=d))
+    o1, o2 = outs(), outs()
+    ppo.offer_act_free(core, price, off_obs, C, 77, 5, o1, offset_dev=ctr)
+    a1, l1 = acc.act_compact(rows, owner, N * C, 77, 7, crow, offset_dev=ctr)
+    a2 = torch.empty_like(a1)
+    l2 = torch.empty_like(l1)
+    ppo.act_round_free(core, price, off_obs, acc, rows, owner, crow, C, 77, 5, 7, o2, a2, l2, offset_dev=ctr)
+    for k in o1:
+        assert torch.equal(o1[k].view(torch.int8), o2[k].view(torch.int8)), k
+    assert torch.equal(a1, a2)
+    assert torch.equal(l1.view(torch.int32), l2.view(torch.int32))
+
+
 def test_trainer_compact_matches_materialised(ms):
     """The trainer on compact acceptor rings (the env emits core rows + owners, the act and gradient
     kernels read them) == the trainer on the materialised [N*C] rows, bit for bit over two PPO
