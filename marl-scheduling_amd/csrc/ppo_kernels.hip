@@ -104,7 +104,7 @@ __device__ __forceinline__ u4v bytes_to_bf16(uint32_t d0, uint32_t d1) {
     return r;
 }
 
-constexpr int kCommonSeg = 1024;  // rows scanned per segment of the common-row path
+constexpr int kCommonSeg = 512;   // rows scanned per segment of the common-row path
 constexpr int kScanDepth = 1;     // 64-row scan steps in flight (2 spills registers at <4, 2>: slower)
 
 template <bool B>
@@ -125,14 +125,14 @@ struct GradLds {
     static constexpr int XPD = (NQ & 1) ? 4 * NQ + 6 : 4 * NQ + 2;  // staged input row pitch (dwords)
     static constexpr int TP = 20;                     // 16-row transpose pitch (floats)
     static constexpr int TP2 = 36;                    // 32-row transpose pitch (floats)
-    static constexpr int NTR = 5 + NT;                // 16-row transposed arrays per tile
+    static constexpr int NTR = NT + 1;               // 16-row transposes live at once (three phases per tile)
     // block: split W1 / C1 [2][3][16][W1B] bf16, then W2, C2, W3 and the biases (floats)
     static constexpr int w1s_floats = 2 * 3 * 16 * W1B / 2;
     static constexpr int shared_floats = w1s_floats + 2 * 256 + 256 * NT + 16 * 5 + 16 * NT + 4;
     // per wave: d1 / e1 transposes over a tile pair, the per-tile transposes, 32 staged input rows
     // (common-row path: the common row's clamped logs, V, entropy, the list of the other rows,
-    //  and per lane the summed d loss / d logp of every action, [16*NT][64])
-    static constexpr int CMF = CM ? 16 * NT + 4 + kCommonSeg + 64 + 64 * 16 * NT : 0;
+    //  and the wave's int64 fixed-point sums of d min(surr)/d ratio * ratio per action [16*NT])
+    static constexpr int CMF = CM ? 16 * NT + 4 + kCommonSeg + 64 + 2 * 16 * NT : 0;
     static constexpr int wave_floats = 2 * 16 * TP2 + NTR * 16 * TP + 32 * XPD + CMF;
     // waves per block: 4 when they fit the 160 KB of LDS, else 2 (each wave then walks two chunks)
     static constexpr int WPB = shared_floats + 4 * wave_floats <= 40960 ? 4 : 2;
@@ -467,23 +467,19 @@ __global__ void __launch_bounds__((64 * GradLds<NQ, NT, MODE>::WPB), ((NQ * NT >
         //      value of (feature f, row r) at T[f*TP + 4*(r%4) + r/4], so lane (j, g4) reads rows
         //      g4, g4+4, g4+8, g4+12 of feature j with one ds_read_b128 (k step s = row g4 + 4s).
         //      d1 / e1 go to the tile pair's 32-row transposes (row 16*half + j at T2[f*TP2 + row]).
+        //      Three phases share the transpose space (L::NTR arrays): dW2, dC2, then dW3.
         float* T_d2 = sT1;
         float* T_h1 = sT1 + 1 * 16 * TP;
-        float* T_h2 = sT1 + 2 * 16 * TP;
-        float* T_e2 = sT1 + 3 * 16 * TP;
-        float* T_k1 = sT1 + 4 * 16 * TP;
-        float* T_gz = sT1 + 5 * 16 * TP;
+        float* T_e2 = sT1;
+        float* T_k1 = sT1 + 1 * 16 * TP;
+        float* T_h2 = sT1;
+        float* T_gz = sT1 + 1 * 16 * TP;
         const int pr = 4 * (j & 3) + (j >> 2);  // this lane's row position
 #pragma unroll
         for (int q = 0; q < 4; q++) {
             const int fo = (4 * g4 + q) * TP + pr;
             T_d2[fo] = dl2[q];
             T_h1[fo] = f.h1[q];
-            T_h2[fo] = f.h2[q];
-            T_e2[fo] = dc2[q];
-            T_k1[fo] = f.hc1[q];
-#pragma unroll
-            for (int t = 0; t < NT; t++) T_gz[t * 16 * TP + fo] = gz[t][q];
             const int f2 = (4 * g4 + q) * TP2 + 16 * half + j;
             T_d1[f2] = dl1[q];
             T_e1[f2] = dc1[q];
@@ -500,9 +496,28 @@ __global__ void __launch_bounds__((64 * GradLds<NQ, NT, MODE>::WPB), ((NQ * NT >
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
         const int rd = j * TP + 4 * g4;
         const f4 ad2 = *reinterpret_cast<const f4*>(T_d2 + rd);
-        const f4 ae2 = *reinterpret_cast<const f4*>(T_e2 + rd);
         const f4 bh1 = *reinterpret_cast<const f4*>(T_h1 + rd);
+        __builtin_amdgcn_wave_barrier();  // (the wave's LDS reads complete in order before its writes)
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            const int fo = (4 * g4 + q) * TP + pr;
+            T_e2[fo] = dc2[q];
+            T_k1[fo] = f.hc1[q];
+        }
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        const f4 ae2 = *reinterpret_cast<const f4*>(T_e2 + rd);
         const f4 bk1 = *reinterpret_cast<const f4*>(T_k1 + rd);
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            const int fo = (4 * g4 + q) * TP + pr;
+            T_h2[fo] = f.h2[q];
+#pragma unroll
+            for (int t = 0; t < NT; t++) T_gz[t * 16 * TP + fo] = gz[t][q];
+        }
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
         const f4 bh2 = *reinterpret_cast<const f4*>(T_h2 + rd);
         f4 agz[NT];
 #pragma unroll
@@ -511,9 +526,11 @@ __global__ void __launch_bounds__((64 * GradLds<NQ, NT, MODE>::WPB), ((NQ * NT >
         for (int s = 0; s < 4; s++) {
             gW2 = mfma4(ad2[s], bh1[s], gW2);
             gC2 = mfma4(ae2[s], bk1[s], gC2);
+        }
+#pragma unroll
+        for (int s = 0; s < 4; s++)
 #pragma unroll
             for (int t = 0; t < NT; t++) gW3[t] = mfma4(agz[t][s], bh2[s], gW3[t]);
-        }
         if (pair_done) {
             // dW1 / dC1 over the pair's 32 rows on the bf16 MFMA: A = d1 (e1) of rows 8*g4..+7 of
             // hidden unit j as three exact bf16 terms, B = the int8 inputs of those rows; output
@@ -735,11 +752,15 @@ __global__ void __launch_bounds__((64 * GradLds<NQ, NT, MODE>::WPB), ((NQ * NT >
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         }
         const float Vc = sCm[16 * NT], ent_c = sCm[16 * NT + 1];
-        // per lane: summed d loss / d logp of each action over its common rows, in LDS (k-major:
-        // lane l's entry of action k at vsl[64 k + l], conflict-free for any actions)
-        float* vsl = reinterpret_cast<float*>(list + kCommonSeg + 64);
-#pragma unroll
-        for (int k = 0; k < 16 * NT; k++) vsl[64 * k + lane] = 0.f;
+        // the wave's sums of d min(surr)/d ratio * ratio per action over its common rows: int64
+        // fixed point (2^-28) with LDS atomics, so the order of the adds does not matter; a row
+        // whose term could overflow them is listed for the tiles instead
+        long long* vacc = reinterpret_cast<long long*>(list + kCommonSeg + 64);
+        if (lane < 16 * NT) vacc[lane] = 0;
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        const float qbound = 34359738368.f / (float)max(re - rb, 1);  // |q| * 2^28 * rows < 2^63
         float sgv = 0.f, sl_min = 0.f, sl_mse = 0.f, sl_ent = 0.f;
         int scnt = 0;
         const uint64_t below = (1ull << lane) - 1ull;
@@ -799,19 +820,25 @@ __global__ void __launch_bounds__((64 * GradLds<NQ, NT, MODE>::WPB), ((NQ * NT >
                     const int act = s_act[k];
                     const float olp = s_olp[k], G = s_G[k];
                     if (r0 + 64 * PF < seg_end) load_slot(k, r0 + 64 * PF, seg_end);
+                    float qd = 0.f, sur1 = 0.f, sur2 = 0.f;
                     if (common) {
                         // the tile path's per-row derivatives with the common row's forward values
                         const float lp = (unsigned)act < (unsigned)A ? sCm[act] : 0.f;
                         const float ratio = fast_exp(lp - olp);
                         const float adv = G - Vc;
-                        const float sur1 = ratio * adv;
+                        sur1 = ratio * adv;
                         const float rc = fminf(fmaxf(ratio, 1.f - p.eps_clip), 1.f + p.eps_clip);
-                        const float sur2 = rc * adv;
+                        sur2 = rc * adv;
                         const float inr = (ratio >= 1.f - p.eps_clip && ratio <= 1.f + p.eps_clip) ? 1.f : 0.f;
                         const float dmin =
                             sur1 < sur2 ? adv : (sur2 < sur1 ? adv * inr : 0.5f * adv + 0.5f * adv * inr);
-                        const float g_lp = -dmin * p.inv_R * ratio;
-                        if ((unsigned)act < (unsigned)A) vsl[64 * act + lane] += g_lp;
+                        qd = dmin * ratio;
+                        common = fabsf(qd) <= qbound;  // NaN or huge: the tile path
+                    }
+                    if (common) {
+                        if ((unsigned)act < (unsigned)A)
+                            atomicAdd(reinterpret_cast<unsigned long long*>(vacc + act),
+                                      (unsigned long long)__float2ll_rn(qd * 268435456.f));
                         sgv += (Vc - G) * p.inv_R;
                         scnt++;
                         sl_min += -fminf(sur1, sur2);
@@ -845,21 +872,15 @@ __global__ void __launch_bounds__((64 * GradLds<NQ, NT, MODE>::WPB), ((NQ * NT >
         // the virtual tile: column 0 carries the common rows' summed derivatives
         // wave totals per action (lane k sums action k's 64 entries in lane order), then column 0
         // of the virtual tile: lane (0, g4) takes actions 16t + 4*g4 + q
-        float tot = 0.f;
-        if (lane < 16 * NT)
-            for (int l = 0; l < 64; l++) tot += vsl[64 * lane + l];
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        if (lane < 16 * NT) vsl[lane] = tot;
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        const double fx_lp = -(double)p.inv_R / 268435456.0;
         float vsum[NT][4];
 #pragma unroll
         for (int t = 0; t < NT; t++)
 #pragma unroll
-            for (int q = 0; q < 4; q++) vsum[t][q] = j == 0 ? vsl[16 * t + 4 * g4 + q] : 0.f;
+            for (int q = 0; q < 4; q++) vsum[t][q] = j == 0 ? (float)((double)vacc[16 * t + 4 * g4 + q] * fx_lp) : 0.f;
         const float gv_tot = xsum16(xsum4g(sgv));
         const float cnt_tot = (float)(int)xsum16(xsum4g((float)scnt));
         tile_step(BoolC<true>{}, txr, 0, 0.f, 0.f, true, otile & 1, true, vsum, j == 0 ? -0.01f * p.inv_R * cnt_tot : 0.f,
