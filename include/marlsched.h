@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define MS_ABI_VERSION 7
+#define MS_ABI_VERSION 8
 
 #define MS_MAX_KINDS 16
 #define MS_MAX_AGENTS 64
@@ -328,17 +328,35 @@ int ms_offer_act_free(const ms_mlp_params* core_chooser, const ms_mlp_params* pr
                       float* core_logprob, int8_t* price_state, int8_t* price_action,
                       float* price_logprob, int8_t* env_price, void* stream);
 
+/* The price chooser's sampling table (FreePriceOfferPPO's second net, PPOmodules.py:316-330): its
+ * input is 4 bytes taking few values, so the forward of every tabulated input is computed once per
+ * weight update and each acting row samples from its entry (bit-identical to computing it).
+ *   digit [4][256] int16: key offset of byte value v at position p (index v + 128), -1 = not
+ *                         tabulated (such a row's tile computes the net instead);
+ *   rows  [n_keys][4] int8: the input of every key (key = sum of its bytes' offsets);
+ *   table [G][n_keys][32*ceil(A/16) + 4] f32: running sums, log-probs, S, last nonzero action. */
+typedef struct ms_price_table {
+    const int16_t* digit;
+    const int8_t* rows;
+    int32_t n_keys;
+    float* table;
+} ms_price_table;
+int ms_price_table_build(const ms_mlp_params* price_chooser, const ms_price_table* table, void* stream);
+
 /* getActionForAllAgents of a free-price round (SchedulingEnvironment.py:150-172) in one launch:
  * ms_offer_act_free on off_obs (Philox offset off_offset) and ms_policy_act_compact on (core_rows,
  * core_owner) (offset acc_offset), same seed and offset_dev; outputs identical to the two calls.
- * The offer and acceptor waves share the CUs, so neither launch waits out its own latency alone. */
+ * The offer and acceptor waves share the CUs, so neither launch waits out its own latency alone.
+ * price_table (optional, built for the current price-chooser weights): the price chooser samples
+ * from it. */
 int ms_act_round_free(const ms_mlp_params* core_chooser, const ms_mlp_params* price_chooser, const int8_t* off_obs,
                       int32_t off_stride, int32_t off_units, int32_t off_units_per_group, const ms_mlp_params* acceptor,
                       const int8_t* core_rows, const int8_t* core_owner, int32_t acc_stride, int32_t acc_units,
                       int32_t acc_units_per_group, int32_t n_cores, const int8_t* common_row, int64_t n_envs,
                       uint64_t seed, uint64_t off_offset, uint64_t acc_offset, const uint64_t* offset_dev,
                       int8_t* core_action, float* core_logprob, int8_t* price_state, int8_t* price_action,
-                      float* price_logprob, int8_t* env_price, int8_t* acc_action, float* acc_logprob, void* stream);
+                      float* price_logprob, int8_t* env_price, int8_t* acc_action, float* acc_logprob,
+                      const ms_price_table* price_table, void* stream);
 
 /* Discounted Monte-Carlo returns + per-sequence normalisation (PPOmodules.py:128-137):
  * rewards [T][M] (f32, as stored per round), for each sequence m:

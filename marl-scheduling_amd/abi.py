@@ -232,6 +232,15 @@ class MsPpoBatch(ct.Structure):
     ]
 
 
+class MsPriceTable(ct.Structure):
+    _fields_ = [
+        ("digit", ct.c_void_p),
+        ("rows", ct.c_void_p),
+        ("n_keys", ct.c_int32),
+        ("table", ct.c_void_p),
+    ]
+
+
 class MsAdamTensor(ct.Structure):
     _fields_ = [
         ("param", ct.c_void_p),

@@ -32,7 +32,8 @@ hipError_t launch_policy_act_compact(const ms_mlp_params*, const int8_t*, const 
 hipError_t launch_act_round(const ms_mlp_params*, const ms_mlp_params*, const int8_t*, int, int, int,
                             const ms_mlp_params*, const int8_t*, const int8_t*, int, int, int, int, const int8_t*,
                             int64_t, uint64_t, uint64_t, uint64_t, const uint64_t*, int8_t*, float*, int8_t*, int8_t*,
-                            float*, int8_t*, int8_t*, float*, hipStream_t);
+                            float*, int8_t*, int8_t*, float*, const float*, const int16_t*, int, hipStream_t);
+hipError_t launch_price_table(const ms_mlp_params*, const int8_t*, int, float*, hipStream_t);
 hipError_t launch_offer_act_free(const ms_mlp_params*, const ms_mlp_params*, const int8_t*, int, int64_t, int, int, int,
                                  uint64_t, uint64_t, const uint64_t*, const float*, int8_t*, float*, int8_t*, int8_t*,
                                  float*, int8_t*, hipStream_t);
@@ -529,7 +530,7 @@ int ms_act_round_free(const ms_mlp_params* core, const ms_mlp_params* price, con
                       int32_t n_cores, const int8_t* common_row, int64_t n_envs, uint64_t seed, uint64_t off_offset,
                       uint64_t acc_offset, const uint64_t* offset_dev, int8_t* core_action, float* core_logprob,
                       int8_t* price_state, int8_t* price_action, float* price_logprob, int8_t* env_price,
-                      int8_t* acc_action, float* acc_logprob, void* stream) {
+                      int8_t* acc_action, float* acc_logprob, const ms_price_table* price_table, void* stream) {
     if (!off_obs || !core_rows || !core_owner || !common_row || !core_action || !core_logprob || !price_state ||
         !price_action || !price_logprob || !env_price || !acc_action || !acc_logprob)
         return fail(MS_EINVAL, "NULL argument");
@@ -545,11 +546,24 @@ int ms_act_round_free(const ms_mlp_params* core, const ms_mlp_params* price, con
         return fail(MS_EINVAL, "core chooser must be (2C+2) -> C+1");
     if (n_cores < 1 || acc_units % n_cores != 0 || acc_stride < 16)
         return fail(MS_EINVAL, "acceptor units must be n_agents * n_cores with obs_stride >= 16");
+    if (price_table && (!price_table->digit || !price_table->table || price_table->n_keys < 1))
+        return fail(MS_EINVAL, "price_table needs digit, table and n_keys >= 1");
     HIP_TRY(ms::launch_act_round(core, price, off_obs, off_stride, off_units, off_units_per_group, acc, core_rows,
                                  core_owner, acc_stride, acc_units, acc_units_per_group, n_cores, common_row, n_envs,
                                  seed, off_offset, acc_offset, offset_dev, core_action, core_logprob, price_state,
                                  price_action, price_logprob, env_price, acc_action, acc_logprob,
-                                 (hipStream_t)stream));
+                                 price_table ? price_table->table : nullptr, price_table ? price_table->digit : nullptr,
+                                 price_table ? price_table->n_keys : 0, (hipStream_t)stream));
+    return MS_OK;
+}
+
+int ms_price_table_build(const ms_mlp_params* price_chooser, const ms_price_table* t, void* stream) {
+    if (!price_chooser || !t || !t->rows || !t->table || t->n_keys < 1) return fail(MS_EINVAL, "NULL argument");
+    int rc = check_mlp(price_chooser, 4, price_chooser->n_groups, 1);
+    if (rc) return rc;
+    if (price_chooser->in_dim != 4 || price_chooser->n_actions > 32)
+        return fail(MS_EINVAL, "price chooser must be 4 -> A with A <= 32");
+    HIP_TRY(ms::launch_price_table(price_chooser, t->rows, t->n_keys, t->table, (hipStream_t)stream));
     return MS_OK;
 }
 

@@ -256,6 +256,21 @@ struct Head {
         return fast_log(fminf(fmaxf(pa, eps), 1.f - eps));
     }
 
+    // The sampling entries of the tile's 16 rows, one row per column j: lane (j, g4) gets its four
+    // actions' running sums c and log-probs lp (what run() would compare and return), and S and the
+    // last nonzero action of row j (every lane of the row).
+    __device__ __forceinline__ void row_table(f4 a1, int j, int g4, float (&c)[NT][4], float (&lp)[NT][4], float& S,
+                                              int& last_nz) const {
+        float z[NT][4];
+        numerators(a1, j, g4, z, c, S);
+        last_nz = last_nonzero(z, g4);
+        const float rS = __builtin_amdgcn_rcpf(S);
+#pragma unroll
+        for (int t = 0; t < NT; t++)
+#pragma unroll
+            for (int q = 0; q < 4; q++) lp[t][q] = clamped_log(z[t][q] * rS);
+    }
+
     // The sampling table of one row (all 16 rows of the tile equal): cum[a] = running sum through
     // action a, lp[a] = the log-prob run() returns for action a, *S and *last_nz. With it, a row equal
     // to this one samples and scores exactly as run() would.
@@ -301,6 +316,17 @@ struct ActArgs {
     // compact acceptor observations (k_act_common<.., OWN>): obs = core rows [E][C][stride], owner
     // [E][C]; row (e, u = a*C + c) is core row (e, c) if owner[e][c] == a + 1, else the common row
     const int8_t* owner;
+    // price chooser sampling table (ms_price_table): ptab [G][pkeys][kPriceTW], pdigit [4][256]
+    // (key offset of byte value v at position p, index v + 128; -1: not tabulated); NULL: computed
+    const float* ptab;
+    const int16_t* pdigit;
+    int pkeys;
+};
+
+// floats per price-table entry: running sums and log-probs of 16 * NT2 actions, S, last nonzero
+template <int NT2>
+struct PriceTW {
+    static constexpr int v = 32 * NT2 + 4;
 };
 
 // One wave = a contiguous range of 16-row tiles of one group; no LDS. Layer 1 runs on the bf16 MFMA
@@ -413,11 +439,44 @@ __device__ __forceinline__ void act_tiles(const ActArgs& a, int block) {
                     if (s == ks && h == kh) dw = v;
                 }
             const int8_t pin = act == 0 ? (int8_t)-5 : (int8_t)(dw >> (8 * (k & 3)));
-            f4 acc2 = {0, 0, 0, 0};
-            acc2 = mfma4(pw1, (float)pin, acc2);
             int pact;
             float plp;
-            h2.run(acc2, a.n2.n_actions, j, g4, u2, pact, plp);
+            // the row's key in the price table: the sum of its four bytes' offsets (lane g4: byte g4)
+            const int dg = a.ptab ? (int)a.pdigit[g4 * 256 + (int)pin + 128] : -1;
+            const int key = rows_sum_i(dg), miss = rows_max_i(dg < 0 ? 1 : 0);
+            if (a.ptab && __ballot(miss != 0) == 0ull) {
+                // every row of the tile is tabulated: sample from the table (Head::run's arithmetic)
+                constexpr int TW = PriceTW<NP>::v;
+                const float* te = a.ptab + ((size_t)grp * a.pkeys + key) * TW;
+                float cum[NP][4], lpv[NP][4];
+#pragma unroll
+                for (int t = 0; t < NP; t++) {
+                    const f4 c4 = *reinterpret_cast<const f4*>(te + 16 * t + 4 * g4);
+                    const f4 l4 = *reinterpret_cast<const f4*>(te + 16 * NP + 16 * t + 4 * g4);
+#pragma unroll
+                    for (int q = 0; q < 4; q++) cum[t][q] = c4[q], lpv[t][q] = l4[q];
+                }
+                const float S2 = te[32 * NP];
+                const int lnz = __float_as_int(te[32 * NP + 1]);
+                const float target = u2 * S2;
+                int cnt = 0;
+#pragma unroll
+                for (int t = 0; t < NP; t++)
+#pragma unroll
+                    for (int q = 0; q < 4; q++) cnt += (cum[t][q] <= target) ? 1 : 0;
+                cnt = rows_sum_i(cnt);
+                pact = cnt >= a.n2.n_actions ? lnz : cnt;
+                float mine = 0.f;
+#pragma unroll
+                for (int t = 0; t < NP; t++)
+#pragma unroll
+                    for (int q = 0; q < 4; q++) mine = (16 * t + 4 * g4 + q == pact) ? lpv[t][q] : mine;
+                plp = rows_sum(mine);
+            } else {
+                f4 acc2 = {0, 0, 0, 0};
+                acc2 = mfma4(pw1, (float)pin, acc2);
+                h2.run(acc2, a.n2.n_actions, j, g4, u2, pact, plp);
+            }
             if (valid) {
                 a.price_state[(size_t)cur * 4 + g4] = pin;
                 if (g4 == 0) {
@@ -822,6 +881,56 @@ hipError_t launch_offer_act_free(const ms_mlp_params* core, const ms_mlp_params*
     return dispatch_act(a, st);
 }
 
+// The price chooser's sampling table (ms_price_table_build): the forward of every tabulated 4-byte
+// input per group (16 keys per tile, one per column), stored as Head::run would use it.
+template <int NT2>
+__global__ void __launch_bounds__(256) k_price_table(ms_mlp_params pn, const int8_t* rows, int K, float* tab) {
+    constexpr int TW = PriceTW<NT2>::v;
+    const int tid = threadIdx.x, lane = tid & 63, j = lane & 15, g4 = lane >> 4;
+    const int gw = blockIdx.x * 4 + (tid >> 6);
+    const int tiles = (K + 15) / 16;
+    const int grp = gw / tiles, tile = gw - grp * tiles;
+    if (grp >= pn.n_groups) return;
+    Head<NT2> h;
+    h.load(pn, grp, j, g4);
+    const float pw1 = pn.w1[((size_t)grp * 16 + j) * 4 + g4];
+    const int key = 16 * tile + j;
+    const int8_t pin = rows[(size_t)min(key, K - 1) * 4 + g4];
+    f4 acc = {0, 0, 0, 0};
+    acc = mfma4(pw1, (float)pin, acc);
+    float c[NT2][4], lp[NT2][4], S;
+    int lnz;
+    h.row_table(acc, j, g4, c, lp, S, lnz);
+    if (key < K) {
+        float* te = tab + ((size_t)grp * K + key) * TW;
+#pragma unroll
+        for (int t = 0; t < NT2; t++)
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                te[16 * t + 4 * g4 + q] = c[t][q];
+                te[16 * NT2 + 16 * t + 4 * g4 + q] = lp[t][q];
+            }
+        if (g4 == 0) {
+            te[32 * NT2] = S;
+            te[32 * NT2 + 1] = __int_as_float(lnz);
+        }
+    }
+}
+
+hipError_t launch_price_table(const ms_mlp_params* pn, const int8_t* rows, int K, float* tab, hipStream_t st) {
+    if (pn->in_dim != 4 || pn->hidden != 16 || K < 1) return hipErrorInvalidValue;
+    const int nt = (pn->n_actions + 15) / 16;
+    const long long waves = (long long)pn->n_groups * ((K + 15) / 16);
+    const dim3 grid((unsigned)((waves + 3) / 4));
+    if (nt <= 1)
+        hipLaunchKernelGGL(k_price_table<1>, grid, dim3(256), 0, st, *pn, rows, K, tab);
+    else if (nt <= 2)
+        hipLaunchKernelGGL(k_price_table<2>, grid, dim3(256), 0, st, *pn, rows, K, tab);
+    else
+        return hipErrorInvalidValue;
+    return hipGetLastError();
+}
+
 // both halves of a free-price round's acting in one launch when their shapes have a paired kernel
 // (cfg3: offer rows of <= 32 bytes, <= 16 actions; acceptor rows of <= 64 bytes, <= 32 actions),
 // else the two launches in order
@@ -831,12 +940,16 @@ hipError_t launch_act_round(const ms_mlp_params* core, const ms_mlp_params* pric
                             int n_cores, const int8_t* common, int64_t E, uint64_t seed, uint64_t off_offset,
                             uint64_t acc_offset, const uint64_t* offset_dev, int8_t* core_action, float* core_logprob,
                             int8_t* price_state, int8_t* price_action, float* price_logprob, int8_t* env_price,
-                            int8_t* acc_action, float* acc_logprob, hipStream_t st) {
+                            int8_t* acc_action, float* acc_logprob, const float* ptab, const int16_t* pdigit,
+                            int pkeys, hipStream_t st) {
     if (!common || acc_stride < 16 || n_cores < 1 || acc_U % n_cores != 0) return hipErrorInvalidValue;
     if (price->in_dim != 4) return hipErrorInvalidValue;
     ActArgs o = offer_free_args(core, price, off_obs, off_stride, E, off_U, off_S, n_cores, seed, off_offset,
                                 offset_dev, nullptr, core_action, core_logprob, price_state, price_action,
                                 price_logprob, env_price);
+    o.ptab = ptab;
+    o.pdigit = pdigit;
+    o.pkeys = pkeys;
     ActArgs c = compact_args(acc, core_rows, core_owner, acc_stride, E, acc_U, acc_S, n_cores, common, seed,
                              acc_offset, offset_dev, nullptr, acc_action, acc_logprob);
     const bool paired = (off_stride + 31) / 32 == 1 && core->n_actions <= 16 && price->n_actions <= 16 &&

@@ -187,12 +187,46 @@ class GroupedActorCritic(nn.Module):
         return action, logprob
 
 
+class PriceTable:
+    """The price chooser's sampling table (ms_price_table): the inputs the env can hand it are
+    [prio, rem] of a core and of the offer slot (Agent.py:271-300) or the dummy [-5, -5, -5, -5]
+    (PPOmodules.py:327); every row with prio in {-5, -1, 0 .. max priority} and rem in
+    {-5, -1, 0 .. max length} is a key, and ``build`` tabulates the net's sampling entries for the
+    current weights (a row outside the table makes its tile compute the net, as without one)."""
+
+    def __init__(self, cfg, price: "GroupedActorCritic"):
+        kinds = int(cfg.n_kinds)
+        prios = [-5, -1] + list(range(0, max(int(p) for p in cfg.job_priority[:kinds]) + 1))
+        rems = [-5, -1] + list(range(0, max(int(x) for x in cfg.job_length[:kinds]) + 1))
+        sets = [prios, rems, prios, rems]
+        dev = price.w1.device
+        digit = torch.full((4, 256), -1, dtype=torch.int16)
+        stride = 1
+        for pos, vals in enumerate(sets):
+            for i, v in enumerate(vals):
+                digit[pos, v + 128] = i * stride
+            stride *= len(vals)
+        self.n_keys = stride
+        grids = torch.meshgrid(*[torch.tensor(v, dtype=torch.int8) for v in reversed(sets)], indexing="ij")
+        rows = torch.stack([g.reshape(-1) for g in reversed(grids)], 1)  # key = sum of digit offsets
+        self.digit = digit.to(dev)
+        self.rows = rows.contiguous().to(dev)
+        tw = 32 * ((price.A + 15) // 16) + 4
+        self.table = torch.zeros((price.G, self.n_keys, tw), dtype=torch.float32, device=dev)
+        self.struct = abi.MsPriceTable(ptr(self.digit), ptr(self.rows), self.n_keys, ptr(self.table))
+
+    def build(self, price: "GroupedActorCritic", stream=None):
+        p = price.mlp_params()
+        check(lib.ms_price_table_build(ct.byref(p), ct.byref(self.struct), stream_ptr(stream)))
+
+
 @torch.no_grad()
 def act_round_free(core: GroupedActorCritic, price: GroupedActorCritic, off_obs, acc: GroupedActorCritic, core_rows,
                    core_owner, common_row, n_cores: int, seed: int, off_offset: int, acc_offset: int, out: dict,
-                   acc_action, acc_logprob, offset_dev=None, stream=None):
+                   acc_action, acc_logprob, offset_dev=None, stream=None, price_table: PriceTable | None = None):
     """``offer_act_free`` + ``act_compact`` of one free-price round in one launch (ms_act_round_free):
-    getActionForAllAgents (SchedulingEnvironment.py:150-172); outputs identical to the two calls."""
+    getActionForAllAgents (SchedulingEnvironment.py:150-172); outputs identical to the two calls.
+    price_table: the price chooser samples from it (built for the current weights)."""
     E, U_off, off_stride = off_obs.shape
     _, C, acc_stride = core_rows.shape
     U_acc = acc_action.shape[1]
@@ -204,7 +238,7 @@ def act_round_free(core: GroupedActorCritic, price: GroupedActorCritic, off_obs,
                                 ct.c_uint64(acc_offset), ptr(offset_dev), ptr(out["core_action"]),
                                 ptr(out["core_logprob"]), ptr(out["price_state"]), ptr(out["price_action"]),
                                 ptr(out["price_logprob"]), ptr(out["env_price"]), ptr(acc_action), ptr(acc_logprob),
-                                stream_ptr(stream)))
+                                ct.byref(price_table.struct) if price_table is not None else None, stream_ptr(stream)))
 
 
 def regen_acceptor_rows(core_rows, core_owner, common_row, n_agents: int):

@@ -27,8 +27,8 @@ import torch
 
 from . import abi
 from .env import BatchedEnv
-from .ppo import (PPOGroup, act_round_free, discounted_returns, offer_act_free, reference_init_order, reference_nets,
-                  unit_returns)
+from .ppo import (PPOGroup, PriceTable, act_round_free, discounted_returns, offer_act_free, reference_init_order,
+                  reference_nets, unit_returns)
 
 
 @dataclass
@@ -201,6 +201,9 @@ class Trainer:
         self.off_obs = torch.zeros((T + 1, self.E, N * L, s.off_obs_stride), dtype=torch.int8, device=dev)
         self.price_obs = torch.zeros((T, self.E, N * L, 4), dtype=torch.int8, device=dev) if self.free else None
         self.env_price = torch.zeros((self.E, N * L), dtype=torch.int8, device=dev)
+        # the price chooser samples from a table of its few possible inputs, rebuilt from the current
+        # weights at the start of every rollout (PriceTable; bit-identical to computing the net)
+        self.price_table = PriceTable(cfg, self.price.group.policy_old) if (self.free and self.compact) else None
         # the acceptor row of a core the agent does not own (Agent.py:167-212): most acceptor rows
         # equal it, and the act / gradient kernels compute its network output once
         self.common_rows = common_rows
@@ -291,7 +294,7 @@ class Trainer:
                 act_round_free(self.off.group.policy_old, self.price.group.policy_old, sl(self.off_obs[t]),
                                self.acc.group.policy_old, sl(self.acc_rows[t]), sl(self.acc_owner[t]), self.acc_common,
                                C, seed, base + 1, base + 3, out, sl(self.acc.actions[t]), sl(self.acc.logprobs[t]),
-                               offset_dev=self.rng_ctr, stream=st)
+                               offset_dev=self.rng_ctr, stream=st, price_table=self.price_table)
             else:
                 offer_act_free(self.off.group.policy_old, self.price.group.policy_old, sl(self.off_obs[t]), C, seed,
                                base + 1, out, offset_dev=self.rng_ctr, stream=st)
@@ -341,6 +344,8 @@ class Trainer:
         cur = torch.cuda.current_stream(self.device)
         if self.span_every:
             self.spans[:: self.span_every].zero_()
+        if self.price_table is not None:
+            self.price_table.build(self.price.group.policy_old)
         for s in self.streams[1:]:  # fork: the side streams start after everything queued so far
             s.wait_stream(cur)
         for t in range(self.T):

@@ -419,6 +419,61 @@ def test_act_round_free_matches_separate_calls(ms, N, C, L, O, E):
     assert torch.equal(l1.view(torch.int32), l2.view(torch.int32))
 
 
+@pytest.mark.parametrize("name", ["cfg3", "cfg4"])
+def test_price_table_matches_computed_price_chooser(ms, name):
+    """The price chooser sampling from its table (ms_price_table_build + ms_act_round_free) ==
+    computing the net per row, bit for bit, including rows outside the table (injected bytes)."""
+    ppo = _ppo(ms)
+    abi = importlib.import_module("marl-scheduling_amd.abi")
+    cfg = abi.named_config(name)
+    s = abi.config_shape(cfg)
+    N, C, L, O = s["N"], s["C"], s["L"], s["O"]
+    E = 1500
+    torch.manual_seed(13)
+    D_off, A_off, D_acc, A_acc = 2 * C + 2, C + 1, 3 + 2 * O, O + 1
+    s_off, s_acc = (D_off + 3) & ~3, (D_acc + 3) & ~3
+    core = ppo.GroupedActorCritic(N, D_off, A_off).cuda()
+    price = ppo.GroupedActorCritic(N, 4, s["price_actions"]).cuda()
+    acc = ppo.GroupedActorCritic(N, D_acc, A_acc).cuda()
+    gen = torch.Generator().manual_seed(14)
+    off_obs = torch.zeros((E, N * L, s_off), dtype=torch.int8)
+    prio = torch.randint(-1, max(cfg.job_priority[: cfg.n_kinds]) + 1, (E, N * L, C + 1), generator=gen)
+    rem = torch.randint(-1, max(cfg.job_length[: cfg.n_kinds]) + 1, (E, N * L, C + 1), generator=gen)
+    off_obs[..., 0:D_off:2] = prio.to(torch.int8)
+    off_obs[..., 1:D_off:2] = rem.to(torch.int8)
+    odd = torch.rand((E, N * L), generator=gen) < 0.01  # a few rows with a byte outside the table
+    off_obs[odd, 1] = 40
+    off_obs[odd, 2 * C + 1] = 41
+    rows = torch.zeros((E, C, s_acc), dtype=torch.int8)
+    rows[..., :D_acc] = torch.randint(-5, 13, (E, C, D_acc), generator=gen, dtype=torch.int8)
+    owner = torch.randint(0, N + 1, (E, C), generator=gen, dtype=torch.int8)
+    off_obs, rows, owner = off_obs.cuda(), rows.cuda(), owner.cuda()
+    crow = _common_row(D_acc, s_acc, O).cuda()
+    table = ppo.PriceTable(cfg, price)
+    table.build(price)
+
+    def outs():
+        d = "cuda"
+        return dict(core_action=torch.empty((E, N * L), dtype=torch.int8, device=d),
+                    core_logprob=torch.empty((E, N * L), device=d),
+                    price_state=torch.empty((E, N * L, 4), dtype=torch.int8, device=d),
+                    price_action=torch.empty((E, N * L), dtype=torch.int8, device=d),
+                    price_logprob=torch.empty((E, N * L), device=d),
+                    env_price=torch.empty((E, N * L), dtype=torch.int8, device=d))
+    res = []
+    for tab in (None, table):
+        o = outs()
+        a = torch.empty((E, N * C), dtype=torch.int8, device="cuda")
+        lp = torch.empty((E, N * C), device="cuda")
+        ppo.act_round_free(core, price, off_obs, acc, rows, owner, crow, C, 5, 1, 3, o, a, lp, price_table=tab)
+        res.append((o, a, lp))
+    for k in res[0][0]:
+        assert torch.equal(res[0][0][k].view(torch.int8), res[1][0][k].view(torch.int8)), k
+    assert torch.equal(res[0][1], res[1][1]) and torch.equal(res[0][2], res[1][2])
+    # the table covers the dummy row and most sampled rows
+    assert (res[1][0]["price_state"] == -5).all(-1).any()
+
+
 def test_trainer_compact_matches_materialised(ms):
     """The trainer on compact acceptor rings (the env emits core rows + owners, the act and gradient
     kernels read them) == the trainer on the materialised [N*C] rows, bit for bit over two PPO
