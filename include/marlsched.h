@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define MS_ABI_VERSION 8
+#define MS_ABI_VERSION 9
 
 #define MS_MAX_KINDS 16
 #define MS_MAX_AGENTS 64
@@ -464,6 +464,10 @@ typedef struct ms_adam_tensor {
 } ms_adam_tensor;
 int ms_adam_step(const ms_adam_tensor* tensors, int32_t n_tensors, const double* lr, int32_t n_lr, int64_t step,
                  double beta1, double beta2, double eps, void* stream);
+/* ms_adam_step with the step count read from device memory (*step_dev, >= 1, advanced by the
+ * caller before each step): a captured HIP graph replays it with the current count. */
+int ms_adam_step_dev(const ms_adam_tensor* tensors, int32_t n_tensors, const double* lr, int32_t n_lr,
+                     const int64_t* step_dev, double beta1, double beta2, double eps, void* stream);
 
 /* ---- DQN units: DQNEntity (DQNmodules.py:34-94) and optimize_model (DQNmodules.py:97-154) for the
  * DQN env (DQNDividedFixedPricesEnv SchedulingEnvironment.py:351-436, DividedFixPriceDQNAgent

@@ -73,6 +73,8 @@ def _load():
         "ms_decode_aggregated": (ct.c_int, [ct.POINTER(abi.MsConfig), i64, P, i32, P, P, P, P]),
         "ms_adam_step": (ct.c_int, [ct.POINTER(abi.MsAdamTensor), i32, ct.POINTER(ct.c_double), i32, i64, ct.c_double,
                                     ct.c_double, ct.c_double, P]),
+        "ms_adam_step_dev": (ct.c_int, [ct.POINTER(abi.MsAdamTensor), i32, ct.POINTER(ct.c_double), i32, P,
+                                        ct.c_double, ct.c_double, ct.c_double, P]),
         "ms_dqn_act": (ct.c_int, [ct.POINTER(abi.MsQnetParams), P, i32, i64, i32, i32, ct.c_double, P, u64, u64, P,
                                   P, P, P]),
         "ms_regen_agent_rows": (ct.c_int, [ct.POINTER(abi.MsConfig), P, P, P, P, P, i64, P, P, P]),
@@ -85,7 +87,7 @@ def _load():
         fn = getattr(L, name)
         fn.restype = res
         fn.argtypes = args
-    if L.ms_abi_version() != 8:
+    if L.ms_abi_version() != 9:
         raise ImportError("libmarlsched.so ABI version mismatch")
     return L
 
@@ -99,7 +101,7 @@ EXPORTED = (
     "ms_env_get_rng", "ms_env_set_rng", "ms_env_export",
     "ms_env_import", "ms_policy_act", "ms_policy_act_common", "ms_policy_act_compact",
     "ms_act_round_free", "ms_price_table_build", "ms_offer_act_free", "ms_discounted_returns", "ms_unit_returns",
-    "ms_ppo_workspace_bytes", "ms_ppo_grad", "ms_adam_step",
+    "ms_ppo_workspace_bytes", "ms_ppo_grad", "ms_adam_step", "ms_adam_step_dev",
     "ms_aggregate_obs", "ms_decode_aggregated", "ms_dqn_act", "ms_dqn_workspace_bytes", "ms_dqn_grad",
     "ms_regen_agent_rows",
 )

@@ -44,7 +44,8 @@ int ppo_param_count(int D, int A);
 int ppo_partial_rows(int n_chunks, bool keyed);
 hipError_t launch_aggregate_obs(const AggArgs&, hipStream_t);
 hipError_t launch_decode_aggregated(const int32_t*, long long, int, int, int, int, int8_t*, int8_t*, int*, hipStream_t);
-hipError_t launch_adam(const AdamTensor*, int, const double*, int, int64_t, double, double, double, hipStream_t);
+hipError_t launch_adam(const AdamTensor*, int, const double*, int, int64_t, double, double, double, const int64_t*,
+                       hipStream_t);
 hipError_t launch_dqn_act(const DqnActArgs&, hipStream_t);
 hipError_t launch_regen_agent_rows(const RegenArgs&, hipStream_t);
 hipError_t launch_dqn_grad(const DqnGradArgs&, const DqnReduceArgs&, hipStream_t);
@@ -750,7 +751,22 @@ int ms_adam_step(const ms_adam_tensor* tensors, int32_t n_tensors, const double*
         if (t.lr_group < 0 || t.lr_group >= n_lr) return fail(MS_EINVAL, "tensor %d: lr_group out of range", i);
     }
     HIP_TRY(ms::launch_adam(reinterpret_cast<const ms::AdamTensor*>(tensors), n_tensors, lr, n_lr, step, beta1, beta2,
-                            eps, (hipStream_t)stream));
+                            eps, nullptr, (hipStream_t)stream));
+    return MS_OK;
+}
+
+int ms_adam_step_dev(const ms_adam_tensor* tensors, int32_t n_tensors, const double* lr, int32_t n_lr,
+                     const int64_t* step_dev, double beta1, double beta2, double eps, void* stream) {
+    if (!tensors || !lr || !step_dev) return fail(MS_EINVAL, "NULL argument");
+    if (n_tensors < 1 || n_tensors > MS_ADAM_MAX_TENSORS) return fail(MS_EINVAL, "n_tensors must be in [1, %d]", MS_ADAM_MAX_TENSORS);
+    if (n_lr < 1 || n_lr > ms::kAdamMaxGroups) return fail(MS_EINVAL, "n_lr must be in [1, %d]", ms::kAdamMaxGroups);
+    for (int i = 0; i < n_tensors; i++) {
+        const ms_adam_tensor& t = tensors[i];
+        if (!t.param || !t.grad || !t.exp_avg || !t.exp_avg_sq || t.numel < 0) return fail(MS_EINVAL, "bad tensor %d", i);
+        if (t.lr_group < 0 || t.lr_group >= n_lr) return fail(MS_EINVAL, "tensor %d: lr_group out of range", i);
+    }
+    HIP_TRY(ms::launch_adam(reinterpret_cast<const ms::AdamTensor*>(tensors), n_tensors, lr, n_lr, 0, beta1, beta2, eps,
+                            step_dev, (hipStream_t)stream));
     return MS_OK;
 }
 

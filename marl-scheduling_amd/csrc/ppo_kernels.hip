@@ -1302,18 +1302,28 @@ struct AdamArgs {
     AdamTensor t[kAdamMaxTensors];
     float w1, beta2, one_m_beta2, eps;
     float neg_step[kAdamMaxGroups], bc2_sqrt;
+    // device step counter (HIP-graph replays): the bias corrections from *step_dev, computed as
+    // launch_adam computes them on the host
+    const int64_t* step_dev;
+    double lr[kAdamMaxGroups], beta1d, beta2d;
 };
 
 __global__ void __launch_bounds__(256) k_adam(AdamArgs a) {
     const AdamTensor& t = a.t[blockIdx.y];
-    const float ns = a.neg_step[t.lr_group];
+    float ns = a.neg_step[t.lr_group], bc2_sqrt = a.bc2_sqrt;
+    if (a.step_dev) {
+        const double step = (double)*a.step_dev;
+        const double bc1 = 1.0 - pow(a.beta1d, step), bc2 = 1.0 - pow(a.beta2d, step);
+        ns = (float)((a.lr[t.lr_group] / bc1) * -1.0);
+        bc2_sqrt = (float)sqrt(bc2);
+    }
     for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < t.numel; i += (int64_t)gridDim.x * 256) {
         const float g = t.grad[i];
         float m = t.exp_avg[i], v = t.exp_avg_sq[i];
         m = m + a.w1 * (g - m);                  // lerp, weight < 0.5
         v = v * a.beta2;                         // mul_
         v = v + a.one_m_beta2 * (g * g);         // addcmul_
-        const float den = sqrtf(v) / a.bc2_sqrt + a.eps;
+        const float den = sqrtf(v) / bc2_sqrt + a.eps;
         t.param[i] = t.param[i] + ns * (m / den);  // addcdiv_
         t.exp_avg[i] = m;
         t.exp_avg_sq[i] = v;
@@ -1321,9 +1331,15 @@ __global__ void __launch_bounds__(256) k_adam(AdamArgs a) {
 }
 
 hipError_t launch_adam(const AdamTensor* ts, int n, const double* lr, int n_lr, int64_t step, double beta1,
-                       double beta2, double eps, hipStream_t st) {
-    if (n < 1 || n > kAdamMaxTensors || n_lr < 1 || n_lr > kAdamMaxGroups || step < 1) return hipErrorInvalidValue;
+                       double beta2, double eps, const int64_t* step_dev, hipStream_t st) {
+    if (n < 1 || n > kAdamMaxTensors || n_lr < 1 || n_lr > kAdamMaxGroups || (step < 1 && !step_dev))
+        return hipErrorInvalidValue;
+    if (step_dev) step = 1;  // the host-side corrections are unused
     AdamArgs a{};
+    a.step_dev = step_dev;
+    a.beta1d = beta1;
+    a.beta2d = beta2;
+    for (int k = 0; k < n_lr; k++) a.lr[k] = lr[k];
     int64_t mx = 1;
     for (int i = 0; i < n; i++) {
         if (ts[i].lr_group < 0 || ts[i].lr_group >= n_lr) return hipErrorInvalidValue;

@@ -304,6 +304,10 @@ class HipAdam:
         self.betas, self.eps = betas, eps
         self.step_count = 0
         self.state = {}
+        # the step count on the device as well: each step advances it with a device op and the Adam
+        # kernel reads it, so a captured HIP graph (Trainer's update) replays with the current count
+        dev = self.param_groups[0]["params"][0].device
+        self.step_dev = torch.zeros((), dtype=torch.int64, device=dev)
         for g in self.param_groups:
             for p in g["params"]:
                 assert p.is_cuda and p.dtype == torch.float32 and p.is_contiguous()
@@ -319,6 +323,11 @@ class HipAdam:
     @torch.no_grad()
     def step(self, stream=None):
         self.step_count += 1
+        if stream is None:
+            self.step_dev.add_(1)
+        else:
+            with torch.cuda.stream(stream):
+                self.step_dev.add_(1)
         ts = []
         for k, g in enumerate(self.param_groups):
             for p in g["params"]:
@@ -330,8 +339,8 @@ class HipAdam:
             return
         arr = (abi.MsAdamTensor * len(ts))(*ts)
         lrs = (ct.c_double * len(self.param_groups))(*[g["lr"] for g in self.param_groups])
-        check(lib.ms_adam_step(arr, len(ts), lrs, len(self.param_groups), self.step_count, self.betas[0],
-                               self.betas[1], self.eps, stream_ptr(stream)))
+        check(lib.ms_adam_step_dev(arr, len(ts), lrs, len(self.param_groups), ptr(self.step_dev), self.betas[0],
+                                   self.betas[1], self.eps, stream_ptr(stream)))
 
 
 class PPOGroup:

@@ -371,10 +371,10 @@ class Trainer:
         self.rounds_done += self.T
 
     # ---- update
-    def _draws(self):
+    def _draws(self, device=None):
         """Sub-unit selections, in the reference's random.randint order."""
         N, C, L, CS = self.N, self.C, self.L, self.hp.centralisation_sample
-        dev = self.device
+        dev = self.device if device is None else device
         if self.arch == "divided":
             sel = dict(acceptor=[torch.arange(N * C, device=dev)], offer=[torch.arange(N * L, device=dev)])
         elif self.arch == "local":
@@ -402,66 +402,119 @@ class Trainer:
         return sel
 
     def update(self):
-        """env.updateAgents() (SchedulingEnvironment.py:208-210 / 314-329, Agent.py:524-529,708-728)."""
+        """env.updateAgents() (SchedulingEnvironment.py:208-210 / 314-329, Agent.py:524-529,708-728).
+        With use_graph on one rank the fused update is captured into a HIP graph after its first
+        (eager) run and replayed from then on: only this iteration's sub-unit draws are copied to
+        the device first. The returned losses are then the graph's own tensors (overwritten by
+        the next update)."""
+        if self.use_graph and self.fused and self.world_size == 1:
+            return self._update_graphed()
         sel = self._draws()
-        losses = {}
-        T, E = self.T, self.E
-        def states_of(u):
-            if u is self.acc:
-                return self.acc_rows[:T] if self.compact else self.acc_obs[:T]
-            return (self.off_obs if u is self.off else self.price_obs)[:T]
         if self.fused:
-            # Each unit type's draws update its nets in sequence (draw d trains on the weights draw
-            # d-1 left), but the unit types are independent nets: step s of the update = epoch k of
-            # draw d of every unit type that has one, with ONE all-reduce of all their gradients
-            # (one flattened RCCL call per step, DESIGN §7) before each type's Adam step.
-            steps = {}
-            for u in self.units():
-                # the returns of every draw's sub-units in one launch: [T][E][sum of G], draw d at
-                # column offset d*G (returns depend on the rewards only, not on earlier draws' updates)
-                all_sel = torch.cat(sel[u.name]).to(torch.int32)
-                ret_all = unit_returns(u.rewards, all_sel, u.group.gamma)
-                common = self.acc_common if (u is self.acc and self.common_rows) else None
-                owner = self.acc_owner[:T].reshape(T * E, self.C) if (u is self.acc and self.compact) else None
-                st_u = states_of(u)
-                col, seq = 0, []
-                for u_sel in sel[u.name]:
-                    ep = u.group.fused_epoch(st_u.reshape(T * E, -1, u.stride), u.actions.view(T * E, u.U),
-                                             u.logprobs.view(T * E, u.U), ret_all.view(-1)[col:],
-                                             all_sel[col:col + u_sel.numel()], T, E, common_row=common,
-                                             returns_ld=all_sel.numel(), core_owner=owner)
-                    seq += [ep] * u.group.K
-                    col += u_sel.numel()
-                steps[u.name] = (u, seq, [])
-            for s in range(max(len(v[1]) for v in steps.values())):
-                live = [(u, seq, ls) for u, seq, ls in steps.values() if s < len(seq)]
-                for u, seq, ls in live:
-                    ls.append(seq[s]())
-                if self.world_size > 1:
-                    self._allreduce([p for u, _, _ in live for p in u.group.policy.parameters()])
-                for u, _, _ in live:
-                    u.group.hip_optimizer.step()
-            for u, _, ls in steps.values():
-                u.group.last_losses = ls
-                u.group.sync_old()
-                losses[u.name] = torch.stack(ls)
-        else:
-            for u in self.units():
-                ls = []
-                st_u = self.acceptor_rows(0, T) if (u is self.acc and self.compact) else states_of(u)
-                for u_sel in sel[u.name]:
-                    x, a, lp, ret = u.batch(st_u, u_sel)
-                    ls += u.group.update(x, a, lp, ret)
-                u.group.sync_old()
-                losses[u.name] = torch.stack(ls)
-        # next iteration starts from the last observation
+            return self._fused_update({k: torch.cat(v).to(torch.int32) for k, v in sel.items()},
+                                      {k: [x.numel() for x in v] for k, v in sel.items()})
+        return self._torch_update(sel)
+
+    def _states_of(self, u):
+        T = self.T
+        if u is self.acc:
+            return self.acc_rows[:T] if self.compact else self.acc_obs[:T]
+        return (self.off_obs if u is self.off else self.price_obs)[:T]
+
+    def _update_graphed(self):
+        host = {k: [list(map(int, d.tolist())) for d in v] for k, v in self._draws(device="cpu").items()}
+        names = [u.name for u in self.units()]
+        flat = [x for k in names for d in host[k] for x in d]
+        if getattr(self, "_sel_dev", None) is None:
+            self._sel_host = torch.empty(len(flat), dtype=torch.int32, pin_memory=True)
+            self._sel_dev = torch.empty(len(flat), dtype=torch.int32, device=self.device)
+            self._sel_event = torch.cuda.Event()
+            self._sel_counts = {k: [len(d) for d in host[k]] for k in names}
+            self.update_graph = None
+        self._sel_event.synchronize()  # the previous copy out of the pinned buffer is done
+        self._sel_host.copy_(torch.tensor(flat, dtype=torch.int32))
+        self._sel_dev.copy_(self._sel_host, non_blocking=True)
+        self._sel_event.record()
+        views, col = {}, 0
+        for k in names:
+            n = sum(self._sel_counts[k])
+            views[k] = self._sel_dev[col:col + n]
+            col += n
+        if self.update_graph is None:
+            losses = self._fused_update(views, self._sel_counts)  # this iteration's update
+            torch.cuda.synchronize(self.device)
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                self._graph_losses = self._fused_update(views, self._sel_counts)
+            self.update_graph = g
+            return losses
+        self.update_graph.replay()
+        return self._graph_losses
+
+    def _fused_update(self, all_sel, counts):
+        """The fused update: all_sel[name] = int32 device [sum of draws' G] sub-units, counts[name]
+        = each draw's number of groups."""
+        T, E = self.T, self.E
+        losses = {}
+        # Each unit type's draws update its nets in sequence (draw d trains on the weights draw d-1
+        # left), but the unit types are independent nets: step s of the update = epoch k of draw d
+        # of every unit type that has one, with ONE all-reduce of all their gradients (one
+        # flattened RCCL call per step, DESIGN §7) before each type's Adam step.
+        steps = {}
+        for u in self.units():
+            # the returns of every draw's sub-units in one launch: [T][E][sum of G], draw d at
+            # column offset d*G (returns depend on the rewards only, not on earlier draws' updates)
+            sel_u = all_sel[u.name]
+            ret_all = unit_returns(u.rewards, sel_u, u.group.gamma)
+            common = self.acc_common if (u is self.acc and self.common_rows) else None
+            owner = self.acc_owner[:T].reshape(T * E, self.C) if (u is self.acc and self.compact) else None
+            st_u = self._states_of(u)
+            col, seq = 0, []
+            for n in counts[u.name]:
+                ep = u.group.fused_epoch(st_u.reshape(T * E, -1, u.stride), u.actions.view(T * E, u.U),
+                                         u.logprobs.view(T * E, u.U), ret_all.view(-1)[col:], sel_u[col:col + n], T,
+                                         E, common_row=common, returns_ld=sel_u.numel(), core_owner=owner)
+                seq += [ep] * u.group.K
+                col += n
+            steps[u.name] = (u, seq, [])
+        for s in range(max(len(v[1]) for v in steps.values())):
+            live = [(u, seq, ls) for u, seq, ls in steps.values() if s < len(seq)]
+            for u, seq, ls in live:
+                ls.append(seq[s]())
+            if self.world_size > 1:
+                self._allreduce([p for u, _, _ in live for p in u.group.policy.parameters()])
+            for u, _, _ in live:
+                u.group.hip_optimizer.step()
+        for u, _, ls in steps.values():
+            u.group.last_losses = ls
+            u.group.sync_old()
+            losses[u.name] = torch.stack(ls)
+        self._carry_last_observation()
+        return losses
+
+    def _torch_update(self, sel):
+        """The torch-autograd update (the numerical reference of the fused one)."""
+        T = self.T
+        losses = {}
+        for u in self.units():
+            ls = []
+            st_u = self.acceptor_rows(0, T) if (u is self.acc and self.compact) else self._states_of(u)
+            for u_sel in sel[u.name]:
+                x, a, lp, ret = u.batch(st_u, u_sel)
+                ls += u.group.update(x, a, lp, ret)
+            u.group.sync_old()
+            losses[u.name] = torch.stack(ls)
+        self._carry_last_observation()
+        return losses
+
+    def _carry_last_observation(self):
+        """The next iteration starts from the last observation."""
         if self.compact:
             self.acc_rows[0].copy_(self.acc_rows[self.T])
             self.acc_owner[0].copy_(self.acc_owner[self.T])
         else:
             self.acc_obs[0].copy_(self.acc_obs[self.T])
         self.off_obs[0].copy_(self.off_obs[self.T])
-        return losses
 
     def iteration(self):
         """One PPO iteration; device time of rollout / update accumulates in self.timings (s)."""
