@@ -19,6 +19,7 @@ each optimizer step all-reduces one flattened gradient buffer (RCCL).
 """
 from __future__ import annotations
 
+import os
 import random
 import time
 from dataclasses import dataclass, field
@@ -227,6 +228,10 @@ class Trainer:
         self.metric_slots = -(-T // self.ep_len) + 1
         self.metric_bufs = [env.metrics_buffer(self.metric_slots) for env, _, _ in self.env.parts] if metrics else None
         self.episode_log = []
+        # one rank: each unit type's update on its own stream (MS_UPDATE_STREAMS=1). Measured: the
+        # update 10.06 -> 9.63 ms but the next rollout 14.50 -> 15.63 ms (every rollout launch
+        # slower after a multi-stream update graph), so it is off by default
+        self.update_streams = os.environ.get("MS_UPDATE_STREAMS", "0") == "1"
         self.span_every = 0  # > 0: every span_every-th round's env launches record their span (bench)
         self.spans = None
         self.timings = dict(rollout=0.0, update=0.0)
@@ -454,6 +459,8 @@ class Trainer:
     def _fused_update(self, all_sel, counts):
         """The fused update: all_sel[name] = int32 device [sum of draws' G] sub-units, counts[name]
         = each draw's number of groups."""
+        if self.world_size == 1 and self.update_streams:
+            return self._fused_update_streams(all_sel, counts)
         T, E = self.T, self.E
         losses = {}
         # Each unit type's draws update its nets in sequence (draw d trains on the weights draw d-1
@@ -489,6 +496,49 @@ class Trainer:
             u.group.last_losses = ls
             u.group.sync_old()
             losses[u.name] = torch.stack(ls)
+        self._carry_last_observation()
+        return losses
+
+    def _epochs(self, u, sel_u, counts_u):
+        """The gradient closures of unit type u's K epochs of every draw, in order."""
+        T, E = self.T, self.E
+        # the returns of every draw's sub-units in one launch: [T][E][sum of G], draw d at column
+        # offset d*G (returns depend on the rewards only, not on earlier draws' updates)
+        ret_all = unit_returns(u.rewards, sel_u, u.group.gamma)
+        common = self.acc_common if (u is self.acc and self.common_rows) else None
+        owner = self.acc_owner[:T].reshape(T * E, self.C) if (u is self.acc and self.compact) else None
+        st_u = self._states_of(u)
+        col, seq = 0, []
+        for n in counts_u:
+            ep = u.group.fused_epoch(st_u.reshape(T * E, -1, u.stride), u.actions.view(T * E, u.U),
+                                     u.logprobs.view(T * E, u.U), ret_all.view(-1)[col:], sel_u[col:col + n], T, E,
+                                     common_row=common, returns_ld=sel_u.numel(), core_owner=owner)
+            seq += [ep] * u.group.K
+            col += n
+        return seq
+
+    def _fused_update_streams(self, all_sel, counts):
+        """One rank: the unit types' nets are independent, so each type's whole update (its draws'
+        epochs, each a gradient then an Adam step) runs on its own stream and the types' gradient
+        kernels share the GPU (each is latency-bound at 2-3 waves per SIMD)."""
+        cur = torch.cuda.current_stream(self.device)
+        units = self.units()
+        if getattr(self, "_unit_streams", None) is None:
+            self._unit_streams = [torch.cuda.Stream(device=self.device) for _ in units]
+        losses = {}
+        for st in self._unit_streams:
+            st.wait_stream(cur)
+        for u, st in zip(units, self._unit_streams):
+            with torch.cuda.stream(st):
+                ls = []
+                for ep in self._epochs(u, all_sel[u.name], counts[u.name]):
+                    ls.append(ep())
+                    u.group.hip_optimizer.step(st)
+                u.group.last_losses = ls
+                u.group.sync_old()
+                losses[u.name] = torch.stack(ls)
+        for st in self._unit_streams:
+            cur.wait_stream(st)
         self._carry_last_observation()
         return losses
 
