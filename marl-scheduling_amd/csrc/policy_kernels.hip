@@ -1012,7 +1012,7 @@ __global__ void __launch_bounds__(256) k_unit_returns(const void* __restrict__ r
     const int64_t EG = E * G;
     const int64_t EU = E * U;
     const size_t src0 = (size_t)e * U + u;
-    double Gs = 0.0, s = 0.0;
+    double Gs = 0.0, s = 0.0, ss = 0.0;
     for (int t1 = T; t1 > 0; t1 -= kRetBatch) {
         double r[kRetBatch];
 #pragma unroll
@@ -1029,23 +1029,16 @@ __global__ void __launch_bounds__(256) k_unit_returns(const void* __restrict__ r
                 const float f = (float)Gs;
                 out[(int64_t)t * EG + m] = f;
                 s += (double)f;
+                ss += (double)f * (double)f;
             }
         }
     }
     const float mean = (float)(s / T);
-    double v = 0.0;
-    for (int t0 = 0; t0 < T; t0 += kRetBatch) {
-        float f[kRetBatch];
-#pragma unroll
-        for (int k = 0; k < kRetBatch; k++) f[k] = out[(int64_t)min(t0 + k, T - 1) * EG + m];
-#pragma unroll
-        for (int k = 0; k < kRetBatch; k++) {
-            if (t0 + k < T) {
-                const double d = (double)f[k] - (double)mean;
-                v += d * d;
-            }
-        }
-    }
+    // sum of squared deviations from the f32 mean, from the same pass's sums (no second read):
+    // sum (f - m)^2 = ss - 2 m s + T m^2 in double (the f32 inputs leave it well conditioned)
+    const double md = (double)mean;
+    double v = ss - 2.0 * md * s + (double)T * md * md;
+    v = v > 0.0 ? v : 0.0;
     const float sd = T > 1 ? (float)sqrt(v / (T - 1)) : NAN;
     const float den = sd + 1e-7f;
     for (int t0 = 0; t0 < T; t0 += kRetBatch) {

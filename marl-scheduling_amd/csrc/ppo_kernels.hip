@@ -177,6 +177,11 @@ __global__ void __launch_bounds__((64 * GradLds<NQ, NT, MODE>::WPB), ((NQ * NT >
     uint32_t* sX = reinterpret_cast<uint32_t*>(sT1 + L::NTR * 16 * TP);  // [32][XPD] dwords
     float* sCm = reinterpret_cast<float*>(sX + 32 * XPD);  // common-row path (L::CMF floats)
 
+    // behind the keyed passes (key_n set), the tile path only runs the groups they could not take;
+    // k_ppo_reduce skips this block's partial row for the others
+    if constexpr (MODE == kPlain)
+        if (p.key_n && p.key_n[grp] >= 0 && p.key_flag[grp] == 0) return;
+
     // ---- stage this group's weights (once per block); W1 / C1 as three exact bf16 terms
     {
         const float* W1 = p.w1 + (size_t)grp * 16 * D;
@@ -688,9 +693,6 @@ __global__ void __launch_bounds__((64 * GradLds<NQ, NT, MODE>::WPB), ((NQ * NT >
             }
         }
     } else if constexpr (MODE == kPlain) {
-        // behind the keyed passes (key_n set): only the groups they could not take
-        const int tile_end_g = (p.key_n && p.key_n[grp] >= 0 && p.key_flag[grp] == 0) ? tile0 : tile_end;
-        const int tile_end = tile_end_g;
         // rows past the end load row 0's values: their loss weight is 0, so every derivative of
         // theirs is exactly 0 (all inputs finite)
         auto row_of_tile = [&](int tile) { return tile * 16 + j < R ? tile * 16 + j : 0; };
@@ -962,15 +964,17 @@ __global__ void __launch_bounds__((64 * GradLds<NQ, NT, MODE>::WPB), ((NQ * NT >
 // Sum the blocks' partial vectors (fixed order: 4 interleaved row sets, then a fixed tree) and
 // scatter into the .grad tensors. Block = 64 parameters x 4 row sets.
 __global__ void __launch_bounds__(256) k_ppo_reduce(const float* __restrict__ partials, int G, int n_rows, int P,
-                                                    int D, int A, GradOut go) {
+                                                    int D, int A, GradOut go, const int32_t* key_n,
+                                                    const int32_t* key_flag, int key_rows) {
     __shared__ float part[4][64];
     const int grp = blockIdx.y;
+    const int n_used = (key_n && key_n[grp] >= 0 && key_flag[grp] == 0) ? key_rows : n_rows;  // keyed: no tile rows
     const int pi = threadIdx.x & 63, rs = threadIdx.x >> 6;
     const int i = blockIdx.x * 64 + pi;
     float s = 0.f;
     if (i < P) {
         const float* src = partials + (size_t)grp * n_rows * P + i;
-        for (int c = rs; c < n_rows; c += 4) s += src[(size_t)c * P];
+        for (int c = rs; c < n_used; c += 4) s += src[(size_t)c * P];
     }
     part[rs][pi] = s;
     __syncthreads();
@@ -1285,7 +1289,8 @@ reduce:
     {
         const int P = poff(a.D, a.A).total;
         hipLaunchKernelGGL(k_ppo_reduce, dim3((P + 63) / 64, a.G), dim3(256), 0, st, a.partials, a.G,
-                           ppo_partial_rows(a.n_chunks, keyed), P, a.D, a.A, go);
+                           ppo_partial_rows(a.n_chunks, keyed), P, a.D, a.A, go, keyed ? a.key_n : nullptr,
+                           keyed ? a.key_flag : nullptr, kKeyBlocks);
     }
     return hipGetLastError();
 }
