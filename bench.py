@@ -30,19 +30,24 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
 
 
 def env_round_bytes(shape, k_new_jobs: int, free: bool, compact: bool = False) -> int:
-    """Algorithmic HBM bytes of one env replica's round in k_env_step:
-    state record read+write, actions read, observations written (compact: the C core rows and
-    owners instead of the N*C acceptor rows), rewards written, and the MT19937 words the spawn
-    draws consume (tie-break words and liability entries are data dependent and not counted: this
-    is a lower bound)."""
+    """Algorithmic bytes of one env replica's round: SURVEY.md §8(d)'s judge figure,
+    B = B_state + B_act + B_obs + B_rew (+ B_liab),
+      B_state = 2 (4C + 8NL + 4)          compact state read + write
+      B_act   = NC + NL (+ NL free)        actions read
+      B_obs   = NC D_acc + NL D_off + C D_acc at 1 B per element (the observations the round hands
+                the agents and the auctioneer, whatever form the kernel writes them in: with
+                ``compact`` the acceptor rows go out as C owner rows + owners and are regenerated
+                where they are read, so the kernel writes fewer bytes than it delivers)
+      B_rew   = 4 (NL (1 or 2) + NC + N + C)
+    B_liab (16 B per accepted offer) is data dependent and left out: a lower bound. k_new_jobs and
+    compact do not change the figure (kept for the callers)."""
     N, C, L = shape.n_agents, shape.n_cores, shape.collection_length
-    rec = shape.env_record_bytes
-    acts = N * C + N * L * (2 if free else 1)
-    acc_obs = C * (shape.acc_obs_stride + 1) if compact else N * C * shape.acc_obs_stride
-    obs = acc_obs + N * L * shape.off_obs_stride
-    rew = 4 * (N * C + N * L * (2 if free else 1) + N + C)
-    rng = 4 * 2 * k_new_jobs * N
-    return 2 * rec + acts + obs + rew + rng
+    d_acc, d_off = shape.acc_obs_dim, shape.off_obs_dim
+    b_state = 2 * (4 * C + 8 * N * L + 4)
+    b_act = N * C + N * L * (2 if free else 1)
+    b_obs = N * C * d_acc + N * L * d_off + C * d_acc
+    b_rew = 4 * (N * L * (2 if free else 1) + N * C + N + C)
+    return b_state + b_act + b_obs + b_rew
 
 
 def cpu_baseline(seconds_budget: float = 20.0):
@@ -138,7 +143,7 @@ ROLLOUT_STREAMS = 1   # replica parts on separate HIP streams in the rollout (Tr
 SAMPLE_EVERY = 8      # rounds between timed env launches
 
 
-def committed_traffic(alg_bytes_per_launch):
+def committed_traffic(alg_bytes_per_launch, variant=""):
     """HBM bytes per k_env_step launch from the committed PMC passes of this workload
     (profiles/*/traffic.json, written by profiles/run_profile.sh: FETCH_SIZE doubled per the
     gfx950 correction + WRITE_SIZE, per launch), newest round first; None if absent."""
@@ -150,8 +155,9 @@ def committed_traffic(alg_bytes_per_launch):
                 d = json.load(f)
         except (OSError, ValueError):
             continue
-        # the passes of this workload's kernel: same algorithmic bytes per launch
-        if d.get("kernel") == "k_env_step" and d.get("bytes") and d.get("algorithmic_bytes") == alg_bytes_per_launch:
+        # the passes of this workload's kernel variant (same algorithmic bytes per launch)
+        if (d.get("kernel") == "k_env_step" and d.get("bytes") and d.get("algorithmic_bytes") == alg_bytes_per_launch
+                and d.get("variant", "") == variant):
             return {"bytes": d["bytes"], "source": os.path.relpath(p, REPO),
                     "vs_algorithmic": d["bytes"] / alg_bytes_per_launch}
     return None
@@ -313,7 +319,7 @@ def main():
     part_envs = args.envs // args.rollout_streams
     b_round = env_round_bytes(shape, tr.cfg.new_jobs_per_round, tr.free, tr.compact)
     achieved = b_round * part_envs / avg_step_s / 1e9
-    traffic = committed_traffic(b_round * part_envs)
+    traffic = committed_traffic(b_round * part_envs, "compact" if tr.compact else "")
     result = {
         "metric": METRIC,
         "value": value,
@@ -345,6 +351,9 @@ def main():
             "traffic": traffic["bytes"] if traffic else None,
             "traffic_source": traffic["source"] if traffic else None,
             "bytes_per_env_round": b_round,
+            "bytes_definition": "SURVEY.md 8(d) judge figure: state r+w, actions, observations delivered (1 B per "
+                                "element), rewards; liability entries left out (lower bound)",
+            "acceptor_observations": "compact (owner row per core + owners)" if tr.compact else "materialised",
             "envs_per_launch": part_envs,
             "avg_launch_us": avg_step_s * 1e6,
             "launches_timed": len(launch_us),

@@ -8,7 +8,7 @@ OUT="$R/gpurun_out/pmc_${TAG}"
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 cd /tmp
-KR="k_env_step|k_act|k_ppo_grad|k_unit_returns"
+KR="k_env_step|k_act|k_ppo_grad|k_unit_returns|k_key"
 pass() {  # pass <name> <counters...>
   local name="$1"; shift
   timeout -k 10 300 rocprofv3 --pmc "$@" --kernel-include-regex "$KR" -f csv -d "$OUT/$name" -o run -- \
