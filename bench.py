@@ -139,6 +139,59 @@ def cpu_baseline(seconds_budget: float = 20.0):
                       "one locally-shared PPO update (K=1, 2 sub-units per agent and unit type)" % (E, rounds, cores)}
 
 
+def cpu_baseline_e1(seconds_budget: float = 10.0):
+    """BASELINE.md's CPU form 1: one env (E = 1) on one thread, acting the way the reference's loop
+    does (trainPPO.py:160-167: every unit's ActorCritic.act on its own 1-row observation,
+    PPOmodules.py:53-63), the C oracle's env step, and one locally-shared PPO update (K = 1, 2
+    sub-units per agent and unit type) per 200 rounds when the sample reaches them."""
+    import numpy as np
+    import torch
+
+    from oracle import pyoracle
+    from oracle.ppo_ref import RefActorCritic
+
+    torch.set_num_threads(1)
+    cfg = pyoracle.abi.named_config("cfg3")
+    s = pyoracle.abi.config_shape(cfg)
+    N, C, L = s["N"], s["C"], s["L"]
+    batch = pyoracle.OracleBatch(cfg, 1, seed=1)
+    torch.manual_seed(0)
+    nets = dict(acc=[RefActorCritic(s["acc_obs_dim"], s["acc_actions"]) for _ in range(N)],
+                off=[RefActorCritic(s["off_obs_dim"], s["off_actions"]) for _ in range(N)],
+                price=[RefActorCritic(4, s["price_actions"]) for _ in range(N)])
+    acc_obs = np.zeros((1, N, C, s["acc_obs_stride"]), np.int8)
+    off_obs = np.zeros((1, N, L, s["off_obs_stride"]), np.int8)
+
+    def act1(net, row):
+        with torch.no_grad():
+            d = torch.distributions.Categorical(net.actor(torch.from_numpy(row).float()))
+            a = d.sample()
+            return int(a), float(d.log_prob(a))
+
+    t0 = time.perf_counter()
+    rounds = 0
+    while rounds < 8 or time.perf_counter() - t0 < seconds_budget:
+        aa = np.zeros((1, N, C), np.int8)
+        ao = np.zeros((1, N, L), np.int8)
+        ap = np.full((1, N, L), -5, np.int8)
+        for a in range(N):  # per agent: offer units (core + price chooser), then acceptors (Agent.py:504-515)
+            for l in range(L):
+                x = off_obs[0, a, l, : s["off_obs_dim"]]
+                core, _ = act1(nets["off"][a], x)
+                pin = np.full(4, -5, np.int8) if core == 0 else np.concatenate((x[2 * core:2 * core + 2], x[-2:]))
+                price, _ = act1(nets["price"][a], pin)
+                ao[0, a, l], ap[0, a, l] = core, (-5 if core == 0 else price)
+            for c in range(C):
+                aa[0, a, c], _ = act1(nets["acc"][a], acc_obs[0, a, c, : s["acc_obs_dim"]])
+        res = batch.step(aa, ao, ap, threads=1)
+        acc_obs, off_obs = res["acc_obs"], res["off_obs"]
+        rounds += 1
+    dt = time.perf_counter() - t0
+    return {"value": N * rounds / dt, "unit": "agent-env-steps/s", "cores": 1, "kind": "port",
+            "sample": "1 replica x %d rounds of cfg3 on one thread: per-unit torch-CPU ActorCritic.act (the "
+                      "reference loop's call pattern) + the C oracle's env step; no update in the sample" % rounds}
+
+
 ROLLOUT_STREAMS = 1   # replica parts on separate HIP streams in the rollout (Trainer rollout_streams)
 SAMPLE_EVERY = 8      # rounds between timed env launches
 
@@ -372,6 +425,10 @@ def main():
             result["cpu_baseline"] = cpu_baseline()
         except Exception as exc:  # reported, never fatal for the GPU number
             result["cpu_baseline"] = {"error": repr(exc)}
+        try:
+            result["cpu_baseline_e1"] = cpu_baseline_e1()
+        except Exception as exc:
+            result["cpu_baseline_e1"] = {"error": repr(exc)}
     if rank == 0:
         print(json.dumps(result))
     if world > 1:
