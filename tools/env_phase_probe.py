@@ -19,7 +19,7 @@ NAMES = {1: "stage (+ successor MT twist)", 2: "MT peek + masks + liab prefetch"
 ORDER = list(range(1, 13))
 
 
-def main(E=16384, steps=20, min_lpe=None):
+def main(E=16384, steps=20, min_lpe=None, compact=True):
     d = "_probe" + ("_lpe%d" % min_lpe if min_lpe else "")
     lib = ct.CDLL(os.path.join(ROOT, "tools", d, "libmarlsched_probe.so"))
     lib.ms_env_create.argtypes = [ct.POINTER(abi.MsConfig), ct.c_int64, ct.c_uint64, ct.POINTER(ct.c_void_p)]
@@ -43,7 +43,12 @@ def main(E=16384, steps=20, min_lpe=None):
     rw = [torch.empty((E, N, L), device=d), torch.empty((E, N, L), device=d),
           torch.empty((E, N, C), dtype=torch.int32, device=d), torch.empty((E, C), dtype=torch.int32, device=d),
           torch.empty((E, N), dtype=torch.int32, device=d)]
-    obs = abi.MsObsOut(oa.data_ptr(), oo.data_ptr(), None)
+    if compact:  # the training round's form: owner row per core + the owners (k_env_step<LPE, false, true>)
+        cr = torch.empty((E, C, sh.acc_obs_stride), dtype=torch.int8, device=d)
+        co = torch.empty((E, C), dtype=torch.int8, device=d)
+        obs = abi.MsObsOut(None, oo.data_ptr(), None, cr.data_ptr(), co.data_ptr())
+    else:
+        obs = abi.MsObsOut(oa.data_ptr(), oo.data_ptr(), None)
     rew = abi.MsRewardOut(*[t.data_ptr() for t in rw])
     buf = (ct.c_ulonglong * 16)()
 
@@ -94,4 +99,5 @@ def main(E=16384, steps=20, min_lpe=None):
 
 
 if __name__ == "__main__":
-    main(min_lpe=int(sys.argv[1]) if len(sys.argv) > 1 else None)
+    main(min_lpe=int(sys.argv[1]) if len(sys.argv) > 1 and sys.argv[1] != "0" else None,
+         compact=not (len(sys.argv) > 2 and sys.argv[2] == "materialised"))
