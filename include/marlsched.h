@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define MS_ABI_VERSION 9
+#define MS_ABI_VERSION 10
 
 #define MS_MAX_KINDS 16
 #define MS_MAX_AGENTS 64
@@ -320,13 +320,16 @@ int ms_policy_act_compact(const ms_mlp_params* p, const int8_t* core_rows, const
  * chooser acts on the offer observation (D_off = 2C+2); the price chooser acts on
  * price_state = [obs[2a], obs[2a+1], obs[2C], obs[2C+1]] or [-5,-5,-5,-5] when a == 0
  * (written to price_state [E][U][4]); env_price = -5 if a == 0 else the price action
- * (the offer price world.py:452 sees). uniforms: [2][E*U] (core, price) or NULL. */
+ * (the offer price world.py:452 sees). uniforms: [2][E*U] (core, price) or NULL.
+ * price_unit_stride: 0 = price_state / price_action / price_logprob in [E][U] rows; else >= E and
+ * unit-major, row (e, u) at u * price_unit_stride + e (a rollout ring [U][T][E] with the round's
+ * offset: the update reads one unit's rows of every replica contiguously). env_price stays [E][U]. */
 int ms_offer_act_free(const ms_mlp_params* core_chooser, const ms_mlp_params* price_chooser,
                       const int8_t* obs, int32_t obs_stride, int64_t n_envs, int32_t n_units,
                       int32_t units_per_group, int32_t n_cores, uint64_t seed, uint64_t offset,
                       const uint64_t* offset_dev, const float* uniforms, int8_t* core_action,
                       float* core_logprob, int8_t* price_state, int8_t* price_action,
-                      float* price_logprob, int8_t* env_price, void* stream);
+                      float* price_logprob, int8_t* env_price, int64_t price_unit_stride, void* stream);
 
 /* The price chooser's sampling table (FreePriceOfferPPO's second net, PPOmodules.py:316-330): its
  * input is 4 bytes taking few values, so the forward of every tabulated input is computed once per
@@ -356,7 +359,7 @@ int ms_act_round_free(const ms_mlp_params* core_chooser, const ms_mlp_params* pr
                       uint64_t seed, uint64_t off_offset, uint64_t acc_offset, const uint64_t* offset_dev,
                       int8_t* core_action, float* core_logprob, int8_t* price_state, int8_t* price_action,
                       float* price_logprob, int8_t* env_price, int8_t* acc_action, float* acc_logprob,
-                      const ms_price_table* price_table, void* stream);
+                      const ms_price_table* price_table, int64_t price_unit_stride, void* stream);
 
 /* Discounted Monte-Carlo returns + per-sequence normalisation (PPOmodules.py:128-137):
  * rewards [T][M] (f32, as stored per round), for each sequence m:
@@ -402,6 +405,9 @@ typedef struct ms_ppo_batch {
      * each group's distinct rows get one forward and one backward pass, and each row adds its loss
      * derivatives to its distinct row's int64 fixed-point sums (2^-28); -1: every row on its own */
     int32_t row_keys;
+    /* 0: states [R][U][stride], actions / old_logprobs [R][U]; else >= R and unit-major: row (r, u) at
+     * u * unit_stride + r in all three (e.g. [U][T][E] rollout rings; not with core_owner) */
+    int64_t unit_stride;
 } ms_ppo_batch;
 
 typedef struct ms_ppo_grads {  /* device outputs, [G][...] like the weights */

@@ -59,10 +59,10 @@ def _load():
                                              P, P, P, P, P]),
         "ms_act_round_free": (ct.c_int, [ct.POINTER(abi.MsMlpParams), ct.POINTER(abi.MsMlpParams), P, i32, i32, i32,
                                          ct.POINTER(abi.MsMlpParams), P, P, i32, i32, i32, i32, P, i64, u64, u64, u64,
-                                         P, P, P, P, P, P, P, P, P, ct.POINTER(abi.MsPriceTable), P]),
+                                         P, P, P, P, P, P, P, P, P, ct.POINTER(abi.MsPriceTable), i64, P]),
         "ms_price_table_build": (ct.c_int, [ct.POINTER(abi.MsMlpParams), ct.POINTER(abi.MsPriceTable), P]),
         "ms_offer_act_free": (ct.c_int, [ct.POINTER(abi.MsMlpParams), ct.POINTER(abi.MsMlpParams), P, i32, i64, i32,
-                                         i32, i32, u64, u64, P, P, P, P, P, P, P, P, P]),
+                                         i32, i32, u64, u64, P, P, P, P, P, P, P, P, i64, P]),
         "ms_discounted_returns": (ct.c_int, [P, i32, i64, i64, ct.c_double, P, P]),
         "ms_unit_returns": (ct.c_int, [P, i32, i32, i64, i32, P, i32, ct.c_double, P, P]),
         "ms_ppo_workspace_bytes": (ct.c_size_t, [ct.POINTER(abi.MsMlpParams), i64]),
@@ -87,7 +87,7 @@ def _load():
         fn = getattr(L, name)
         fn.restype = res
         fn.argtypes = args
-    if L.ms_abi_version() != 9:
+    if L.ms_abi_version() != 10:
         raise ImportError("libmarlsched.so ABI version mismatch")
     return L
 

@@ -229,6 +229,7 @@ class MsPpoBatch(ct.Structure):
         ("core_owner", ct.c_void_p),
         ("n_cores", ct.c_int32),
         ("row_keys", ct.c_int32),
+        ("unit_stride", ct.c_int64),
     ]
 
 

@@ -32,11 +32,11 @@ hipError_t launch_policy_act_compact(const ms_mlp_params*, const int8_t*, const 
 hipError_t launch_act_round(const ms_mlp_params*, const ms_mlp_params*, const int8_t*, int, int, int,
                             const ms_mlp_params*, const int8_t*, const int8_t*, int, int, int, int, const int8_t*,
                             int64_t, uint64_t, uint64_t, uint64_t, const uint64_t*, int8_t*, float*, int8_t*, int8_t*,
-                            float*, int8_t*, int8_t*, float*, const float*, const int16_t*, int, hipStream_t);
+                            float*, int8_t*, int8_t*, float*, const float*, const int16_t*, int, int64_t, hipStream_t);
 hipError_t launch_price_table(const ms_mlp_params*, const int8_t*, int, float*, hipStream_t);
 hipError_t launch_offer_act_free(const ms_mlp_params*, const ms_mlp_params*, const int8_t*, int, int64_t, int, int, int,
                                  uint64_t, uint64_t, const uint64_t*, const float*, int8_t*, float*, int8_t*, int8_t*,
-                                 float*, int8_t*, hipStream_t);
+                                 float*, int8_t*, int64_t, hipStream_t);
 hipError_t launch_returns(const float*, int, int64_t, int64_t, double, float*, hipStream_t);
 hipError_t launch_unit_returns(const void*, int, int, int64_t, int, const int32_t*, int, double, float*, hipStream_t);
 hipError_t launch_ppo_grad(const PpoArgs&, const GradOut&, hipStream_t);
@@ -531,7 +531,8 @@ int ms_act_round_free(const ms_mlp_params* core, const ms_mlp_params* price, con
                       int32_t n_cores, const int8_t* common_row, int64_t n_envs, uint64_t seed, uint64_t off_offset,
                       uint64_t acc_offset, const uint64_t* offset_dev, int8_t* core_action, float* core_logprob,
                       int8_t* price_state, int8_t* price_action, float* price_logprob, int8_t* env_price,
-                      int8_t* acc_action, float* acc_logprob, const ms_price_table* price_table, void* stream) {
+                      int8_t* acc_action, float* acc_logprob, const ms_price_table* price_table,
+                      int64_t price_unit_stride, void* stream) {
     if (!off_obs || !core_rows || !core_owner || !common_row || !core_action || !core_logprob || !price_state ||
         !price_action || !price_logprob || !env_price || !acc_action || !acc_logprob)
         return fail(MS_EINVAL, "NULL argument");
@@ -549,12 +550,14 @@ int ms_act_round_free(const ms_mlp_params* core, const ms_mlp_params* price, con
         return fail(MS_EINVAL, "acceptor units must be n_agents * n_cores with obs_stride >= 16");
     if (price_table && (!price_table->digit || !price_table->table || price_table->n_keys < 1))
         return fail(MS_EINVAL, "price_table needs digit, table and n_keys >= 1");
+    if (price_unit_stride != 0 && price_unit_stride < n_envs)
+        return fail(MS_EINVAL, "price_unit_stride must be 0 or >= n_envs");
     HIP_TRY(ms::launch_act_round(core, price, off_obs, off_stride, off_units, off_units_per_group, acc, core_rows,
                                  core_owner, acc_stride, acc_units, acc_units_per_group, n_cores, common_row, n_envs,
                                  seed, off_offset, acc_offset, offset_dev, core_action, core_logprob, price_state,
                                  price_action, price_logprob, env_price, acc_action, acc_logprob,
                                  price_table ? price_table->table : nullptr, price_table ? price_table->digit : nullptr,
-                                 price_table ? price_table->n_keys : 0, (hipStream_t)stream));
+                                 price_table ? price_table->n_keys : 0, price_unit_stride, (hipStream_t)stream));
     return MS_OK;
 }
 
@@ -572,7 +575,7 @@ int ms_offer_act_free(const ms_mlp_params* core, const ms_mlp_params* price, con
                       int64_t n_envs, int32_t n_units, int32_t units_per_group, int32_t n_cores, uint64_t seed,
                       uint64_t offset, const uint64_t* offset_dev, const float* uniforms, int8_t* core_action,
                       float* core_logprob, int8_t* price_state, int8_t* price_action, float* price_logprob,
-                      int8_t* env_price, void* stream) {
+                      int8_t* env_price, int64_t price_unit_stride, void* stream) {
     if (!obs || !core_action || !core_logprob || !price_state || !price_action || !price_logprob || !env_price)
         return fail(MS_EINVAL, "NULL argument");
     int rc = check_mlp(core, obs_stride, n_units, units_per_group);
@@ -583,9 +586,11 @@ int ms_offer_act_free(const ms_mlp_params* core, const ms_mlp_params* price, con
     if (core->in_dim != 2 * n_cores + 2 || core->n_actions != n_cores + 1)
         return fail(MS_EINVAL, "core chooser must be (2C+2) -> (C+1)");
     if (n_envs < 1) return fail(MS_EINVAL, "n_envs must be >= 1");
+    if (price_unit_stride != 0 && price_unit_stride < n_envs)
+        return fail(MS_EINVAL, "price_unit_stride must be 0 or >= n_envs");
     HIP_TRY(ms::launch_offer_act_free(core, price, obs, obs_stride, n_envs, n_units, units_per_group, n_cores, seed,
                                       offset, offset_dev, uniforms, core_action, core_logprob, price_state,
-                                      price_action, price_logprob, env_price, (hipStream_t)stream));
+                                      price_action, price_logprob, env_price, price_unit_stride, (hipStream_t)stream));
     return MS_OK;
 }
 
@@ -637,6 +642,8 @@ int ms_ppo_grad(const ms_mlp_params* a, const ms_mlp_params* c, const ms_ppo_bat
     if (b->core_owner && (!b->common_row || b->n_cores < 1 || b->U % b->n_cores != 0 || b->stride < 16))
         return fail(MS_EINVAL, "compact rows need common_row, stride >= 16 and U = n_agents * n_cores");
     const int64_t R = (int64_t)b->T * b->E;
+    if (b->unit_stride != 0 && (b->unit_stride < R || b->core_owner))
+        return fail(MS_EINVAL, "unit_stride must be 0 or >= T*E (and not with compact rows)");
     if (ws_bytes < ms_ppo_workspace_bytes(a, R)) return fail(MS_EINVAL, "workspace too small");
     ms::PpoArgs p{};
     p.w1 = a->w1; p.b1 = a->b1; p.w2 = a->w2; p.b2 = a->b2; p.w3 = a->w3; p.b3 = a->b3;
@@ -644,6 +651,7 @@ int ms_ppo_grad(const ms_mlp_params* a, const ms_mlp_params* c, const ms_ppo_bat
     p.states = b->states;
     p.actions = b->actions;
     p.old_lp = b->old_logprobs;
+    p.us = b->unit_stride;
     p.ret = b->returns;
     p.unit_of_group = b->unit_of_group;
     p.common = b->common_row;

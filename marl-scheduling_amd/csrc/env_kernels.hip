@@ -1570,6 +1570,14 @@ extern "C" int ms_probe_phase_cycles(unsigned long long* out, int clear) {
     }
     return 0;
 }
+// the per-phase cycles of every block (summed over the launches since the last clear): out[16 * n_blocks]
+extern "C" int ms_probe_phase_blocks(unsigned long long* out, int n_blocks) {
+    static unsigned long long host[ms::kProbeSlots][16];
+    if (n_blocks > ms::kProbeSlots) return -1;
+    if (hipMemcpyFromSymbol(host, HIP_SYMBOL(ms::g_phase_cycles), sizeof(host)) != hipSuccess) return -1;
+    memcpy(out, host, sizeof(unsigned long long) * 16 * n_blocks);
+    return 0;
+}
 // entry / exit s_memrealtime (100 MHz) of every block of the last launch: out[2 * n_blocks]
 extern "C" int ms_probe_wave_spans(unsigned long long* out, int n_blocks) {
     static unsigned long long host[ms::kProbeSlots][2];

@@ -307,9 +307,10 @@ struct ActArgs {
     const float* uniforms;  // [2][E*U] or NULL
     int8_t* action;
     float* logprob;
-    int8_t* price_state;   // [E*U][4]
+    int8_t* price_state;   // [E*U][4] (pus = 0) or unit-major: row (e, u) at u * pus + e
     int8_t* price_action;
     float* price_logprob;
+    int64_t pus;           // unit stride (rows) of the price chooser's outputs; 0: [E][U]
     int8_t* env_price;
     const int8_t* common;  // [stride] or NULL (k_act_common)
     int items_per_wave;    // k_act_common
@@ -360,6 +361,7 @@ __device__ __forceinline__ void act_tiles(const ActArgs& a, int block) {
     const int t1 = min(t0 + a.tiles_per_wave, tiles);
     // item i of this group -> obs row: e = i / S by a multiply-high with one correction step
     const uint32_t s_magic = 0xffffffffu / (uint32_t)a.S;
+    const uint32_t u_magic = 0xffffffffu / (uint32_t)a.U;  // row -> replica (unit-major price outputs)
     auto row_of_lane = [&](int tile, int jj) -> int {
         const int i = tile * 16 + jj;
         if (i >= a.n_items) return -1;
@@ -478,10 +480,18 @@ __device__ __forceinline__ void act_tiles(const ActArgs& a, int block) {
                 h2.run(acc2, a.n2.n_actions, j, g4, u2, pact, plp);
             }
             if (valid) {
-                a.price_state[(size_t)cur * 4 + g4] = pin;
+                // the price chooser's rollout rows: [E][U], or unit-major (the update reads one unit's
+                // rows of every replica, so they lie contiguous)
+                size_t pc = (size_t)cur;
+                if (a.pus) {
+                    int e = (int)__umulhi((uint32_t)cur, u_magic);
+                    if ((e + 1) * a.U <= cur) e++;
+                    pc = (size_t)(cur - e * a.U) * (size_t)a.pus + (size_t)e;
+                }
+                a.price_state[pc * 4 + g4] = pin;
                 if (g4 == 0) {
-                    a.price_action[cur] = (int8_t)pact;
-                    a.price_logprob[cur] = plp;
+                    a.price_action[pc] = (int8_t)pact;
+                    a.price_logprob[pc] = plp;
                     a.env_price[cur] = (int8_t)(act == 0 ? -5 : pact);
                 }
             }
@@ -847,7 +857,7 @@ static ActArgs offer_free_args(const ms_mlp_params* core, const ms_mlp_params* p
                                int64_t E, int U, int S, int n_cores, uint64_t seed, uint64_t offset,
                                const uint64_t* offset_dev, const float* uniforms, int8_t* core_action,
                                float* core_logprob, int8_t* price_state, int8_t* price_action, float* price_logprob,
-                               int8_t* env_price) {
+                               int8_t* env_price, int64_t pus) {
     ActArgs a{};
     a.n1 = *core;
     a.n2 = *price;
@@ -868,6 +878,7 @@ static ActArgs offer_free_args(const ms_mlp_params* core, const ms_mlp_params* p
     a.price_action = price_action;
     a.price_logprob = price_logprob;
     a.env_price = env_price;
+    a.pus = pus;
     return a;
 }
 
@@ -875,9 +886,9 @@ hipError_t launch_offer_act_free(const ms_mlp_params* core, const ms_mlp_params*
                                  int64_t E, int U, int S, int n_cores, uint64_t seed, uint64_t offset,
                                  const uint64_t* offset_dev, const float* uniforms, int8_t* core_action,
                                  float* core_logprob, int8_t* price_state, int8_t* price_action, float* price_logprob,
-                                 int8_t* env_price, hipStream_t st) {
+                                 int8_t* env_price, int64_t pus, hipStream_t st) {
     ActArgs a = offer_free_args(core, price, obs, stride, E, U, S, n_cores, seed, offset, offset_dev, uniforms,
-                                core_action, core_logprob, price_state, price_action, price_logprob, env_price);
+                                core_action, core_logprob, price_state, price_action, price_logprob, env_price, pus);
     return dispatch_act(a, st);
 }
 
@@ -941,12 +952,12 @@ hipError_t launch_act_round(const ms_mlp_params* core, const ms_mlp_params* pric
                             uint64_t acc_offset, const uint64_t* offset_dev, int8_t* core_action, float* core_logprob,
                             int8_t* price_state, int8_t* price_action, float* price_logprob, int8_t* env_price,
                             int8_t* acc_action, float* acc_logprob, const float* ptab, const int16_t* pdigit,
-                            int pkeys, hipStream_t st) {
+                            int pkeys, int64_t pus, hipStream_t st) {
     if (!common || acc_stride < 16 || n_cores < 1 || acc_U % n_cores != 0) return hipErrorInvalidValue;
     if (price->in_dim != 4) return hipErrorInvalidValue;
     ActArgs o = offer_free_args(core, price, off_obs, off_stride, E, off_U, off_S, n_cores, seed, off_offset,
                                 offset_dev, nullptr, core_action, core_logprob, price_state, price_action,
-                                price_logprob, env_price);
+                                price_logprob, env_price, pus);
     o.ptab = ptab;
     o.pdigit = pdigit;
     o.pkeys = pkeys;

@@ -243,7 +243,7 @@ __global__ void __launch_bounds__((64 * GradLds<NQ, NT, MODE>::WPB), ((NQ * NT >
         if constexpr (MODE == kOwnerRow)
             return reinterpret_cast<const uint32_t*>(p.states + ((size_t)r * p.owner_C + own_c) * p.stride);
         else
-            return reinterpret_cast<const uint32_t*>(p.states + ((size_t)r * p.U + u) * p.stride);
+            return reinterpret_cast<const uint32_t*>(p.states + ru_index(p, r, u) * p.stride);
     };
     const float zero_vs[NT][4] = {};
 
@@ -601,8 +601,9 @@ __global__ void __launch_bounds__((64 * GradLds<NQ, NT, MODE>::WPB), ((NQ * NT >
                 const int cc = 8 * s + 2 * g4 + h;
                 pre[s][h] = src[cc < stride4 ? cc : stride4 - 1];  // clamped, masked at the use
             }
-        pre_act = p.actions[(size_t)r * p.U + u];
-        pre_olp = p.old_lp[(size_t)r * p.U + u];
+        const size_t ri = ru_index(p, r, u);
+        pre_act = p.actions[ri];
+        pre_olp = p.old_lp[ri];
         pre_G = p.ret[(size_t)r * p.ret_ld + grp];
     };
 
@@ -780,8 +781,9 @@ __global__ void __launch_bounds__((64 * GradLds<NQ, NT, MODE>::WPB), ((NQ * NT >
             const int r = r0 + lane;
             const int rr = r < lim ? r : rb;
             if constexpr (MODE == kOwnerRow) s_own[k] = p.owner[(size_t)rr * p.owner_C + own_c];
-            s_act[k] = p.actions[(size_t)rr * p.U + u];
-            s_olp[k] = p.old_lp[(size_t)rr * p.U + u];
+            const size_t ri = ru_index(p, rr, u);
+            s_act[k] = p.actions[ri];
+            s_olp[k] = p.old_lp[ri];
             s_G[k] = p.ret[(size_t)rr * p.ret_ld + grp];
         };
         // the listed rows t0 .. t0 + 16*n - 1 (the last tile may be partial: cnt rows in all) in
@@ -1043,9 +1045,10 @@ __global__ void __launch_bounds__(256) k_key_gather(PpoArgs p) {
             for (int k = 0; k < GB; k++) {
                 const int grp = min(g0 + k, p.G - 1);
                 const int u = p.unit_of_group[grp];
-                w[k] = *reinterpret_cast<const uint32_t*>(p.states + (r * p.U + u) * p.stride) & kmask;
-                act[k] = p.actions[(size_t)r * p.U + u];
-                olp[k] = p.old_lp[(size_t)r * p.U + u];
+                const size_t ri = ru_index(p, r, u);
+                w[k] = *reinterpret_cast<const uint32_t*>(p.states + ri * p.stride) & kmask;
+                act[k] = p.actions[ri];
+                olp[k] = p.old_lp[ri];
                 ret[k] = p.ret[(size_t)r * p.ret_ld + grp];
             }
 #pragma unroll

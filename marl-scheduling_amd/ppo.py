@@ -223,14 +223,17 @@ class PriceTable:
 @torch.no_grad()
 def act_round_free(core: GroupedActorCritic, price: GroupedActorCritic, off_obs, acc: GroupedActorCritic, core_rows,
                    core_owner, common_row, n_cores: int, seed: int, off_offset: int, acc_offset: int, out: dict,
-                   acc_action, acc_logprob, offset_dev=None, stream=None, price_table: PriceTable | None = None):
+                   acc_action, acc_logprob, offset_dev=None, stream=None, price_table: PriceTable | None = None,
+                   price_unit_stride: int = 0):
     """``offer_act_free`` + ``act_compact`` of one free-price round in one launch (ms_act_round_free):
     getActionForAllAgents (SchedulingEnvironment.py:150-172); outputs identical to the two calls.
-    price_table: the price chooser samples from it (built for the current weights)."""
+    price_table: the price chooser samples from it (built for the current weights).
+    price_unit_stride: see ``offer_act_free``."""
     E, U_off, off_stride = off_obs.shape
     _, C, acc_stride = core_rows.shape
     U_acc = acc_action.shape[1]
     assert off_obs.is_contiguous() and core_rows.is_contiguous() and core_owner.is_contiguous()
+    _check_price_out(out, E, U_off, price_unit_stride)
     pc, pp, pa = core.mlp_params(), price.mlp_params(), acc.mlp_params()
     check(lib.ms_act_round_free(ct.byref(pc), ct.byref(pp), ptr(off_obs), off_stride, U_off, U_off // core.G,
                                 ct.byref(pa), ptr(core_rows), ptr(core_owner), acc_stride, U_acc, U_acc // acc.G,
@@ -238,7 +241,20 @@ def act_round_free(core: GroupedActorCritic, price: GroupedActorCritic, off_obs,
                                 ct.c_uint64(acc_offset), ptr(offset_dev), ptr(out["core_action"]),
                                 ptr(out["core_logprob"]), ptr(out["price_state"]), ptr(out["price_action"]),
                                 ptr(out["price_logprob"]), ptr(out["env_price"]), ptr(acc_action), ptr(acc_logprob),
-                                ct.byref(price_table.struct) if price_table is not None else None, stream_ptr(stream)))
+                                ct.byref(price_table.struct) if price_table is not None else None,
+                                int(price_unit_stride), stream_ptr(stream)))
+
+
+def _check_price_out(out, E: int, U: int, pus: int):
+    """The price chooser's outputs: [E, U(, 4)] contiguous (pus = 0), or unit-major [U, E(, 4)] views
+    whose unit stride (in rows) is pus."""
+    for k in ("price_state", "price_action", "price_logprob"):
+        x = out[k]
+        if pus == 0:
+            assert x.is_contiguous() and x.shape[:2] == (E, U), k
+        else:
+            assert x.shape[:2] == (U, E) and x.stride(1) == x[0, 0].numel() and pus >= E, k
+            assert x.stride(0) == pus * x[0, 0].numel(), k
 
 
 def regen_acceptor_rows(core_rows, core_owner, common_row, n_agents: int):
@@ -254,18 +270,20 @@ def regen_acceptor_rows(core_rows, core_owner, common_row, n_agents: int):
 
 @torch.no_grad()
 def offer_act_free(core: GroupedActorCritic, price: GroupedActorCritic, obs_i8, n_cores: int, seed: int, offset: int,
-                   out: dict, uniforms=None, offset_dev=None, stream=None):
+                   out: dict, uniforms=None, offset_dev=None, stream=None, price_unit_stride: int = 0):
     """FreePriceOfferPPO.selectAction (PPOmodules.py:312-332) for obs [E, U, stride] int8 in one launch.
     out: core_action/price_action/env_price int8 [E, U], core_logprob/price_logprob f32 [E, U],
-    price_state int8 [E, U, 4]."""
+    price_state int8 [E, U, 4]. price_unit_stride > 0: price_state / price_action / price_logprob are
+    unit-major views [U, E(, 4)] of a ring whose units lie price_unit_stride rows apart."""
     E, U, stride = obs_i8.shape
     assert obs_i8.dtype == torch.int8 and obs_i8.is_contiguous() and U % core.G == 0
+    _check_price_out(out, E, U, price_unit_stride)
     pc, pp = core.mlp_params(), price.mlp_params()
     check(lib.ms_offer_act_free(ct.byref(pc), ct.byref(pp), ptr(obs_i8), stride, E, U, U // core.G, n_cores,
                                 ct.c_uint64(seed), ct.c_uint64(offset), ptr(offset_dev), ptr(uniforms),
                                 ptr(out["core_action"]), ptr(out["core_logprob"]), ptr(out["price_state"]),
                                 ptr(out["price_action"]), ptr(out["price_logprob"]), ptr(out["env_price"]),
-                                stream_ptr(stream)))
+                                int(price_unit_stride), stream_ptr(stream)))
     return out
 
 
@@ -423,7 +441,7 @@ class PPOGroup:
         return losses
 
     def update_fused(self, states_i8, actions_i8, old_logprobs, returns_teg, unit_of_group, T: int, E: int,
-                     stream=None, common_row=None, returns_ld: int = 0, core_owner=None):
+                     stream=None, common_row=None, returns_ld: int = 0, core_owner=None, unit_major: bool = False):
         """The same K epochs with the gradient from the fused HIP kernel (ms_ppo_grad).
 
         states_i8 [R, U, stride] int8 rollout rows (R = T*E, row r = t*E + e), actions_i8 [R, U],
@@ -431,9 +449,10 @@ class PPOGroup:
         (device). Adam (HIP, ms_adam_step) applies the gradient; with several ranks the gradient is
         all-reduced first. common_row (int8 [stride], device, optional): rows equal to it share one
         forward and one backward pass (same gradient up to f32 summation order). core_owner [R, C]
-        (with common_row): states_i8 are compact acceptor rows [R, C, stride] (regen_acceptor_rows)."""
+        (with common_row): states_i8 are compact acceptor rows [R, C, stride] (regen_acceptor_rows).
+        unit_major: states_i8 [U, R, stride], actions_i8 / old_logprobs [U, R] instead."""
         epoch = self.fused_epoch(states_i8, actions_i8, old_logprobs, returns_teg, unit_of_group, T, E, stream,
-                                 common_row, returns_ld, core_owner)
+                                 common_row, returns_ld, core_owner, unit_major)
         losses = []
         for _ in range(self.K):
             loss = epoch()
@@ -445,7 +464,7 @@ class PPOGroup:
         return losses
 
     def fused_epoch(self, states_i8, actions_i8, old_logprobs, returns_teg, unit_of_group, T: int, E: int,
-                    stream=None, common_row=None, returns_ld: int = 0, core_owner=None):
+                    stream=None, common_row=None, returns_ld: int = 0, core_owner=None, unit_major: bool = False):
         """The gradient half of one K-epoch step of ``update_fused``, for callers that all-reduce
         several groups' gradients in one call (Trainer.update): returns a function that writes this
         epoch's gradient into ``policy``'s .grad tensors (ms_ppo_grad) and returns the per-group loss
@@ -453,7 +472,11 @@ class PPOGroup:
         pol = self.policy
         # compact acceptor rows (core_owner [R, C]): states are the core rows [R, C, stride], and U
         # (= N*C units) comes from the actions
-        R, U, stride = states_i8.shape
+        if unit_major:  # [U, R(, stride)]: row (r, u) at u * R + r
+            U, R, stride = states_i8.shape
+            assert core_owner is None and actions_i8.shape == (U, R) and old_logprobs.shape == (U, R)
+        else:
+            R, U, stride = states_i8.shape
         n_cores = 0
         if core_owner is not None:
             n_cores, U = U, actions_i8.shape[1]
@@ -469,7 +492,7 @@ class PPOGroup:
         ws = torch.empty(((ws_bytes + 3) // 4,), dtype=torch.float32, device=states_i8.device)
         batch = abi.MsPpoBatch(ptr(states_i8), ptr(actions_i8), ptr(old_logprobs), ptr(returns_teg),
                                ptr(unit_of_group), stride, T, U, E, ptr(common_row), int(returns_ld),
-                               ptr(core_owner), n_cores, int(getattr(self, "row_keys", 0)))
+                               ptr(core_owner), n_cores, int(getattr(self, "row_keys", 0)), R if unit_major else 0)
         grads = abi.MsPpoGrads(*[ptr(getattr(pol, k).grad) for k in ACTOR_KEYS + CRITIC_KEYS], ptr(loss_buf))
         # the structs above hold raw device pointers: the closure keeps every tensor they point into
         # alive until its last launch (a caller's temporaries would otherwise be freed and reused)

@@ -54,12 +54,21 @@ class _Unit:
     """Rollout buffers + PPO group of one unit type (acceptor / offer / price chooser)."""
 
     def __init__(self, name, E, T, n_units, per_group, in_dim, stride, n_actions, group: PPOGroup, device,
-                 reward_dtype):
+                 reward_dtype, unit_major: bool = False):
         self.name, self.E, self.T, self.U, self.S = name, E, T, n_units, per_group
         self.D, self.stride = in_dim, stride
         self.group = group
-        self.actions = torch.zeros((T, E, n_units), dtype=torch.int8, device=device)
-        self.logprobs = torch.zeros((T, E, n_units), dtype=torch.float32, device=device)
+        # unit_major: actions / log-probs stored [U][T][E] (one unit's rows of every replica are
+        # contiguous for the update's gathers); .actions / .logprobs stay [T][E][U] views
+        self.unit_major = unit_major
+        if unit_major:
+            self.actions_um = torch.zeros((n_units, T, E), dtype=torch.int8, device=device)
+            self.logprobs_um = torch.zeros((n_units, T, E), dtype=torch.float32, device=device)
+            self.actions = self.actions_um.permute(1, 2, 0)
+            self.logprobs = self.logprobs_um.permute(1, 2, 0)
+        else:
+            self.actions = torch.zeros((T, E, n_units), dtype=torch.int8, device=device)
+            self.logprobs = torch.zeros((T, E, n_units), dtype=torch.float32, device=device)
         self.rewards = torch.zeros((T, E, n_units), dtype=reward_dtype, device=device)
 
     def batch(self, states_i8, u_sel):
@@ -184,8 +193,14 @@ class Trainer:
                          mk(go, s.off_obs_dim, s.off_actions, hp.offer_gamma, k_off, nets["off"]), dev, torch.float32)
         self.price = None
         if self.free:
+            # MS_PRICE_UNIT_MAJOR=1: the price chooser's rollout rows unit-major, so its update (keyed
+            # rows) gathers one unit's rows of every replica contiguously instead of 4 B of every 256 B
+            # [E][U] line. Measured at cfg3: k_key_gather 344 -> 279 us, but the act launch's scattered
+            # price writes +1.3 us per round: no net gain, so off by default
+            self.price_unit_major = os.environ.get("MS_PRICE_UNIT_MAJOR", "0") == "1"
             self.price = _Unit("price", self.E, T, N * L, (N * L) // go, 4, 4, s.price_actions,
-                               mk(go, 4, s.price_actions, hp.offer_gamma, k_off, nets["price"]), dev, torch.float32)
+                               mk(go, 4, s.price_actions, hp.offer_gamma, k_off, nets["price"]), dev, torch.float32,
+                               unit_major=self.price_unit_major)
         if world_size > 1:
             self._broadcast_params()
         # observation ring: slot t holds the state acted on at round t; slot T the next state. With
@@ -200,7 +215,13 @@ class Trainer:
         else:
             self.acc_obs = torch.zeros((T + 1, self.E, N * C, s.acc_obs_stride), dtype=torch.int8, device=dev)
         self.off_obs = torch.zeros((T + 1, self.E, N * L, s.off_obs_stride), dtype=torch.int8, device=dev)
-        self.price_obs = torch.zeros((T, self.E, N * L, 4), dtype=torch.int8, device=dev) if self.free else None
+        # price chooser inputs [T][E][U][4] (unit-major: stored [U][T][E][4], self.price_obs its view)
+        self.price_obs_um = None
+        if self.free and self.price_unit_major:
+            self.price_obs_um = torch.zeros((N * L, T, self.E, 4), dtype=torch.int8, device=dev)
+            self.price_obs = self.price_obs_um.permute(1, 2, 0, 3)
+        else:
+            self.price_obs = torch.zeros((T, self.E, N * L, 4), dtype=torch.int8, device=dev) if self.free else None
         self.env_price = torch.zeros((self.E, N * L), dtype=torch.int8, device=dev)
         # the price chooser samples from a table of its few possible inputs, rebuilt from the current
         # weights at the start of every rollout (PriceTable; bit-identical to computing the net)
@@ -295,14 +316,20 @@ class Trainer:
             out = dict(core_action=sl(self.off.actions[t]), core_logprob=sl(self.off.logprobs[t]),
                        price_state=sl(self.price_obs[t]), price_action=sl(self.price.actions[t]),
                        price_logprob=sl(self.price.logprobs[t]), env_price=sl(self.env_price))
+            pus = 0
+            if self.price_unit_major:  # [U][E'] views of the [U][T][E] rings, units T*E rows apart
+                out.update(price_state=self.price_obs_um[:, t, e0:e1], price_action=self.price.actions_um[:, t, e0:e1],
+                           price_logprob=self.price.logprobs_um[:, t, e0:e1])
+                pus = self.T * self.E
             if self.compact:  # the acceptors too, in the same launch
                 act_round_free(self.off.group.policy_old, self.price.group.policy_old, sl(self.off_obs[t]),
                                self.acc.group.policy_old, sl(self.acc_rows[t]), sl(self.acc_owner[t]), self.acc_common,
                                C, seed, base + 1, base + 3, out, sl(self.acc.actions[t]), sl(self.acc.logprobs[t]),
-                               offset_dev=self.rng_ctr, stream=st, price_table=self.price_table)
+                               offset_dev=self.rng_ctr, stream=st, price_table=self.price_table,
+                               price_unit_stride=pus)
             else:
                 offer_act_free(self.off.group.policy_old, self.price.group.policy_old, sl(self.off_obs[t]), C, seed,
-                               base + 1, out, offset_dev=self.rng_ctr, stream=st)
+                               base + 1, out, offset_dev=self.rng_ctr, stream=st, price_unit_stride=pus)
         else:
             self.off.group.policy_old.act(sl(self.off_obs[t]), N * L, seed, base + 1, action=sl(self.off.actions[t]),
                                           logprob=sl(self.off.logprobs[t]), offset_dev=self.rng_ctr, stream=st)
@@ -420,6 +447,16 @@ class Trainer:
                                       {k: [x.numel() for x in v] for k, v in sel.items()})
         return self._torch_update(sel)
 
+    def _update_rows(self, u):
+        """(states, actions, old log-probs) of unit type u for ms_ppo_grad: [T*E, U(, stride)] rows, or
+        [U, T*E(, stride)] for a unit-major unit."""
+        T, E = self.T, self.E
+        if u.unit_major:
+            st = self.price_obs_um if u is self.price else None
+            return st.reshape(u.U, T * E, u.stride), u.actions_um.reshape(u.U, T * E), u.logprobs_um.reshape(u.U, T * E)
+        return (self._states_of(u).reshape(T * E, -1, u.stride), u.actions.view(T * E, u.U),
+                u.logprobs.view(T * E, u.U))
+
     def _states_of(self, u):
         T = self.T
         if u is self.acc:
@@ -475,12 +512,11 @@ class Trainer:
             ret_all = unit_returns(u.rewards, sel_u, u.group.gamma)
             common = self.acc_common if (u is self.acc and self.common_rows) else None
             owner = self.acc_owner[:T].reshape(T * E, self.C) if (u is self.acc and self.compact) else None
-            st_u = self._states_of(u)
             col, seq = 0, []
+            rows = self._update_rows(u)
             for n in counts[u.name]:
-                ep = u.group.fused_epoch(st_u.reshape(T * E, -1, u.stride), u.actions.view(T * E, u.U),
-                                         u.logprobs.view(T * E, u.U), ret_all.view(-1)[col:], sel_u[col:col + n], T,
-                                         E, common_row=common, returns_ld=sel_u.numel(), core_owner=owner)
+                ep = u.group.fused_epoch(*rows, ret_all.view(-1)[col:], sel_u[col:col + n], T, E, common_row=common,
+                                         returns_ld=sel_u.numel(), core_owner=owner, unit_major=u.unit_major)
                 seq += [ep] * u.group.K
                 col += n
             steps[u.name] = (u, seq, [])
@@ -507,12 +543,11 @@ class Trainer:
         ret_all = unit_returns(u.rewards, sel_u, u.group.gamma)
         common = self.acc_common if (u is self.acc and self.common_rows) else None
         owner = self.acc_owner[:T].reshape(T * E, self.C) if (u is self.acc and self.compact) else None
-        st_u = self._states_of(u)
+        rows = self._update_rows(u)
         col, seq = 0, []
         for n in counts_u:
-            ep = u.group.fused_epoch(st_u.reshape(T * E, -1, u.stride), u.actions.view(T * E, u.U),
-                                     u.logprobs.view(T * E, u.U), ret_all.view(-1)[col:], sel_u[col:col + n], T, E,
-                                     common_row=common, returns_ld=sel_u.numel(), core_owner=owner)
+            ep = u.group.fused_epoch(*rows, ret_all.view(-1)[col:], sel_u[col:col + n], T, E, common_row=common,
+                                     returns_ld=sel_u.numel(), core_owner=owner, unit_major=u.unit_major)
             seq += [ep] * u.group.K
             col += n
         return seq

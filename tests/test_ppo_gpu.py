@@ -312,6 +312,18 @@ def test_fused_grad_keyed_rows_matches_autograd(ms, G, T, E, U, A, K, n_keys):
             assert err <= 1e-4 * scale + 1e-7, (k, err, scale)
     for k in ref_grads:  # integer sums: the keyed gradient does not depend on the atomics' order
         assert torch.equal(runs[0][1][k], runs[1][1][k]), k
+    # unit-major rollout rows ([U][R], the trainer's price chooser rings): the same gradients bit for bit,
+    # keyed and on the tile path
+    um = (states.permute(1, 0, 2).contiguous().cuda(), actions.T.contiguous().cuda(), old_lp.T.contiguous().cuda())
+    for keys, base in ((0, runs[0]), (-1, runs[2])):
+        torch.manual_seed(23)
+        fus = ppo.PPOGroup(G, D, A, 0.003, 0.01, 0.9, 0.2, K, device="cuda")
+        fus.row_keys = keys
+        losses = fus.update_fused(*um, *args[3:], unit_major=True)
+        for rl, fl in zip(base[0], losses):
+            assert torch.equal(rl, fl), keys
+        for k in ref_grads:
+            assert torch.equal(getattr(fus.policy, k).grad, base[1][k]), (keys, k)
 
 
 @pytest.mark.parametrize("G,per_group,N,C,O,E", [(8, 8, 8, 8, 24, 1001), (1, 16, 4, 4, 12, 333),
@@ -417,6 +429,28 @@ def test_act_round_free_matches_separate_calls(ms, N, C, L, O, E):
         assert torch.equal(o1[k].view(torch.int8), o2[k].view(torch.int8)), k
     assert torch.equal(a1, a2)
     assert torch.equal(l1.view(torch.int32), l2.view(torch.int32))
+    # unit-major price outputs (a [U][T][E] ring at round t = 1 of T = 3, as the trainer keeps them):
+    # the same values at (u, t, e); env_price stays [E][U]
+    T, t, U = 3, 1, N * L
+    ring = dict(price_state=torch.zeros((U, T, E, 4), dtype=torch.int8, device="cuda"),
+                price_action=torch.zeros((U, T, E), dtype=torch.int8, device="cuda"),
+                price_logprob=torch.zeros((U, T, E), device="cuda"))
+    for fn in ("offer_act_free", "act_round_free"):
+        o3 = outs()
+        o3.update({k: v[:, t] for k, v in ring.items()})
+        if fn == "offer_act_free":
+            ppo.offer_act_free(core, price, off_obs, C, 77, 5, o3, offset_dev=ctr, price_unit_stride=T * E)
+        else:
+            ppo.act_round_free(core, price, off_obs, acc, rows, owner, crow, C, 77, 5, 7, o3, a2, l2, offset_dev=ctr,
+                               price_unit_stride=T * E)
+        for k in ring:
+            got = ring[k][:, t].movedim(0, 1).contiguous()  # [E][U](, 4)
+            assert torch.equal(got.view(torch.int8), o1[k].view(torch.int8)), (fn, k)
+            assert not ring[k][:, t - 1].any() and not ring[k][:, t + 1].any(), (fn, k)  # other rounds untouched
+        for k in ("core_action", "core_logprob", "env_price"):
+            assert torch.equal(o3[k].view(torch.int8), o1[k].view(torch.int8)), (fn, k)
+        for v in ring.values():
+            v.zero_()
 
 
 @pytest.mark.parametrize("name", ["cfg3", "cfg4"])
@@ -669,3 +703,25 @@ def test_unit_returns_of_several_draws_feed_the_gradient(ms):
         torch.testing.assert_close(l1[0], l2[0], rtol=0, atol=0)
         for k in ppo.ACTOR_KEYS + ppo.CRITIC_KEYS:
             torch.testing.assert_close(getattr(g1.policy, k), getattr(g2.policy, k), rtol=0, atol=0)
+
+
+def test_trainer_price_unit_major_matches(ms, monkeypatch):
+    """MS_PRICE_UNIT_MAJOR=1 (price chooser rings [U][T][E], ms_act_round_free's price_unit_stride and
+    ms_ppo_batch.unit_stride): the same rollout and update, bit for bit."""
+    tr_mod = importlib.import_module("marl-scheduling_amd.trainer")
+    trs = []
+    for flag in ("0", "1"):
+        monkeypatch.setenv("MS_PRICE_UNIT_MAJOR", flag)
+        tr = tr_mod.Trainer.from_named("cfg3", n_envs=96, update_step=10, seed=6, device="cuda:0")
+        assert tr.price_unit_major == (flag == "1")
+        losses = [tr.iteration() for _ in range(2)]
+        torch.cuda.synchronize()
+        trs.append((tr, losses))
+    (a, la), (b, lb) = trs
+    assert torch.equal(a.price_obs, b.price_obs) and torch.equal(a.price.actions, b.price.actions)
+    assert torch.equal(a.price.logprobs, b.price.logprobs) and torch.equal(a.off.actions, b.off.actions)
+    for x, y in zip(la, lb):
+        for k in x:
+            assert torch.equal(x[k], y[k]), k
+    for k in ("w1", "b3"):
+        assert torch.equal(getattr(a.price.group.policy, k), getattr(b.price.group.policy, k)), k

@@ -15,8 +15,9 @@ tr.iteration()
 t = 3
 N, C, L = tr.N, tr.C, tr.L
 off_obs = tr.off_obs[t]
-out = dict(core_action=tr.off.actions[t], core_logprob=tr.off.logprobs[t], price_state=tr.price_obs[t],
-           price_action=tr.price.actions[t], price_logprob=tr.price.logprobs[t], env_price=tr.env_price)
+out = dict(core_action=tr.off.actions[t], core_logprob=tr.off.logprobs[t], price_state=tr.price_obs_um[:, t],
+           price_action=tr.price.actions_um[:, t], price_logprob=tr.price.logprobs_um[:, t], env_price=tr.env_price)
+pus = tr.T * tr.E
 
 
 def timed(fn, n=50):
@@ -37,13 +38,13 @@ acc = tr.acc.group.policy_old
 res = {
     "core chooser alone (ms_policy_act)": timed(lambda: core.act(off_obs, N * L, 1, 1, action=out["core_action"],
                                                                  logprob=out["core_logprob"])),
-    "core + price chooser (ms_offer_act_free)": timed(lambda: ppo.offer_act_free(core, price, off_obs, C, 1, 1, out)),
+    "core + price chooser (ms_offer_act_free)": timed(lambda: ppo.offer_act_free(core, price, off_obs, C, 1, 1, out, price_unit_stride=pus)),
     "acceptors compact (ms_policy_act_compact)": timed(lambda: acc.act_compact(tr.acc_rows[t], tr.acc_owner[t], N * C, 1, 3,
                                                                                 tr.acc_common, action=tr.acc.actions[t],
                                                                                 logprob=tr.acc.logprobs[t])),
     "paired (ms_act_round_free)": timed(lambda: ppo.act_round_free(core, price, off_obs, acc, tr.acc_rows[t], tr.acc_owner[t],
                                                                    tr.acc_common, C, 1, 1, 3, out, tr.acc.actions[t],
-                                                                   tr.acc.logprobs[t])),
+                                                                   tr.acc.logprobs[t], price_unit_stride=pus)),
 }
 for k, v in res.items():
     print("%-45s %8.2f us" % (k, v))

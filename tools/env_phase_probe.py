@@ -96,6 +96,28 @@ def main(E=16384, steps=20, min_lpe=None, compact=True):
     print("    entry    %s" % fmt(st))
     print("    exit     %s" % fmt(en))
     print("    lifetime %s" % fmt(life))
+    # one more launch alone: every wave's phase cycles against its lifetime (where the slow waves
+    # lose their time)
+    lib.ms_probe_phase_cycles(buf, 1)
+    run(4)
+    torch.cuda.synchronize()
+    lib.ms_probe_phase_blocks.argtypes = [ct.POINTER(ct.c_ulonglong), ct.c_int]
+    pb = (ct.c_ulonglong * (16 * n_blocks))()
+    assert lib.ms_probe_phase_blocks(pb, n_blocks) == 0
+    assert lib.ms_probe_wave_spans(spans, n_blocks) == 0
+    ph = np.array(pb[:], dtype=np.float64).reshape(n_blocks, 16)
+    sp = np.array(spans[:], dtype=np.float64).reshape(n_blocks, 2) / 100.0
+    life = sp[:, 1] - sp[:, 0]
+    order = np.argsort(life)
+    slow, mid = order[-max(1, n_blocks // 10):], order[n_blocks // 2 - n_blocks // 20: n_blocks // 2 + n_blocks // 20]
+    print("  one launch: lifetime %s us; phase cycles per wave, median-lifetime waves vs slowest 10%%:" % fmt(life))
+    for k in ORDER:
+        print("  %2d %-34s %8.0f %8.0f  (p10 %6.0f p90 %6.0f)" % (k, NAMES[k], ph[mid, k].mean(), ph[slow, k].mean(),
+                                                               np.percentile(ph[:, k], 10), np.percentile(ph[:, k], 90)))
+    xcd = np.arange(n_blocks) % 8
+    print("  mean lifetime per XCD (block %% 8): " + " ".join("%.1f" % life[xcd == x].mean() for x in range(8)))
+    q4 = np.arange(n_blocks) * 4 // n_blocks
+    print("  mean lifetime per grid quarter: " + " ".join("%.1f" % life[q4 == x].mean() for x in range(4)))
 
 
 if __name__ == "__main__":
