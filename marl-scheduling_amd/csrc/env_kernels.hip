@@ -1136,9 +1136,94 @@ __device__ __forceinline__ void env_round(const Params& P, int64_t E, uint8_t* r
     wave_sync();
     MS_MARK(4);
 
-    // ---- apply executions in reference order (World.executeAnOffer world.py:261-293); the
-    //      groups' leaders run their envs' loops side by side
-    if (gl == 0) {
+    // ---- apply executions in reference order (World.executeAnOffer world.py:261-293). Executions
+    //      of different cores touch different cores, offer slots, liability chains and reward
+    //      entries; only the placement of a dispatched job in its recipient's first empty slot
+    //      (world.py:123-133) depends on the earlier executions, through that one collection. So the
+    //      plain round runs each execution's core part on the core's lane, then replays the
+    //      removals and insertions of every collection, in rank order, on the collection owner's
+    //      lane. With episode metrics or event records (their rank-ordered sums) the groups' leaders
+    //      run the executions one after another instead.
+    if (!EXT && io.ev_acc == nullptr) {
+        // per core, in the scratch (free between the staging and the observation emission): the
+        // job its execution dispatched away (for the insertion), the offerer and the recipient
+        int32_t* x_birth = reinterpret_cast<int32_t*>(scratch);
+        int8_t* x_kind = reinterpret_cast<int8_t*>(scratch + 4 * C);
+        int8_t* x_rem = x_kind + C;
+        int8_t* x_off = x_kind + 2 * C;
+        int8_t* x_recip = x_kind + 3 * C;
+        if (gl < C && s_exec[gl] >= 0) {
+            const int c = gl;
+            const int i = s_exec[c];
+            const int offerer = i / L + 1;
+            const int recip = o_recip[i];
+            if (recip != c_owner[c]) atomicOr(&s_flags, MS_FLAG_GUARD);  // executeAnOffer's check (world.py:266)
+            const int nk = s_kind[i], nrem = s_rem[i], nbirth = s_birth[i];
+            const int price = o_price[i];
+            // dispatchNewJobAndReturnOldOne (world.py:61-76)
+            x_kind[c] = c_kind[c];
+            x_rem[c] = c_rem[c];
+            x_birth[c] = c_birth[c];
+            x_off[c] = (int8_t)offerer;
+            x_recip[c] = (int8_t)recip;
+            c_kind[c] = (int8_t)nk;
+            c_rem[c] = (int8_t)nrem;
+            c_birth[c] = nbirth;
+            c_owner[c] = (int8_t)offerer;
+            // liability entry (deepcopy, round = world.round), appendleft (world.py:285-289)
+            const int n = l_n[c];
+            if (n < P.cap) {
+                Liab le;
+                le.offerer = (int8_t)offerer;
+                le.recipient = (int8_t)recip;
+                le.price = (int8_t)price;
+                le.nec = (int8_t)nrem;
+                le.round = round;
+                if (active) my_liab[c * P.cap + n] = le;
+                s_newle[c] = le;
+                s_fresh[c] = 1;
+                l_n[c] = (uint8_t)(n + 1);
+            } else {
+                atomicOr(&s_flags, MS_FLAG_LIABILITY_OVERFLOW);
+            }
+            // offer-side rewards from world.acceptedOffers (Reward.py:164-170 / :23-49)
+            const int prio1 = R.prio(nk);
+            off_r[i] = (float)prio1;
+            if (P.free_prices) {
+                const int diff = prio1 - price;
+                price_r[i] = P.commercial ? (diff == 0 ? P.net_zero : (float)diff) : (diff >= 0 ? (float)prio1 : (float)diff);
+            }
+        }
+        wave_sync();
+        // per collection (agent a = lane): removeAndReturnEntry of its executed offers (world.py:135-141,
+        // newJob.wait = False world.py:276) and insertJob of the jobs dispatched to it, in rank order
+        if (gl < N) {
+            const int a1 = gl + 1, base = gl * L, n_exec = s_n_exec;
+            for (int r = 0; r < n_exec; r++) {
+                const int c = s_by_rank[r];
+                if (x_off[c] == a1) {
+                    const int i = s_exec[c];
+                    s_kind[i] = -1;
+                    s_rem[i] = -1;
+                    s_wait[i] = 0;
+                    s_birth[i] = -1;
+                }
+                if (x_recip[c] == a1) {
+                    int placed = 0;
+                    for (int q = 0; q < L; q++)
+                        if (s_kind[base + q] < 0) {
+                            s_kind[base + q] = x_kind[c];
+                            s_rem[base + q] = x_rem[c];
+                            s_wait[base + q] = 0;
+                            s_birth[base + q] = x_birth[c];
+                            placed = 1;
+                            break;
+                        }
+                    if (!placed) atomicOr(&s_flags, MS_FLAG_COLLECTION_FULL);
+                }
+            }
+        }
+    } else if (gl == 0) {
         const int n_exec = s_n_exec;
         double q_sum = 0.0;  // calculateAverageAcceptionQuality (SchedulingEnvironment.py:174-192)
         int n_q = 0;
