@@ -280,8 +280,8 @@ int ms_env_import(ms_env* env, const ms_state_host* in, void* stream);
  * globally shared (n_groups = 1). Weights are torch nn.Linear layouts, stacked
  * over groups: w1 [G][H][D], b1 [G][H], w2 [G][H][H], b2 [G][H], w3 [G][A][H], b3 [G][A].
  * Sampling: inverse CDF of the normalised probabilities (torch Categorical,
- * PPOmodules.py:55-61) with u = uniform (Philox4x32-10 keyed by seed, counter
- * (offset, row)) or, when uniforms != NULL, the given per-row uniform in [0,1).
+ * PPOmodules.py:55-61) with u = uniform (Philox2x32-10 keyed by seed and the offset's high
+ * word, counter (row, offset)) or, when uniforms != NULL, the given per-row uniform in [0,1).
  * Outputs: action[e*n_units+u] int8, logprob f32 (log of clamped normalised prob). */
 typedef struct ms_mlp_params {
     const float *w1, *b1, *w2, *b2, *w3, *b3;

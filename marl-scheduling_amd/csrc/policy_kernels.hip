@@ -35,21 +35,20 @@ __device__ __forceinline__ uint32_t mulhilo(uint32_t a, uint32_t b, uint32_t& hi
     return (uint32_t)p;
 }
 
-// Philox4x32-10 (Salmon et al., SC'11); returns the first two output words.
-__device__ __forceinline__ void philox2(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t k0, uint32_t k1,
-                                        uint32_t& o0, uint32_t& o1) {
+// Philox2x32-10 (Salmon et al., SC'11, the 2-word member of the family; BigCrush-clean from 7 rounds):
+// two 32-bit outputs per (counter, key). The counter is (row, offset low word); the key folds in
+// the 64-bit seed and the offset's high word. Half the multiplies of Philox4x32 for the two words
+// a row needs (the act kernels' VALU budget: a 32-bit multiply issues at a quarter of the rate).
+__device__ __forceinline__ void philox2(uint32_t row, uint64_t off, uint64_t seed, uint32_t& o0, uint32_t& o1) {
+    uint32_t c0 = row, c1 = (uint32_t)off;
+    uint32_t k = (uint32_t)seed ^ ((uint32_t)(seed >> 32) * 0x85EBCA6Bu) ^ ((uint32_t)(off >> 32) * 0xC2B2AE35u);
+#pragma unroll
     for (int r = 0; r < 10; r++) {
-        uint32_t hi0, hi1;
-        uint32_t lo0 = mulhilo(0xD2511F53u, c0, hi0);
-        uint32_t lo1 = mulhilo(0xCD9E8D57u, c2, hi1);
-        uint32_t n0 = hi1 ^ c1 ^ k0;
-        uint32_t n2 = hi0 ^ c3 ^ k1;
-        c0 = n0;
-        c1 = lo1;
-        c2 = n2;
-        c3 = lo0;
-        k0 += 0x9E3779B9u;
-        k1 += 0xBB67AE85u;
+        uint32_t hi;
+        const uint32_t lo = mulhilo(0xD256D193u, c0, hi);
+        c0 = hi ^ k ^ c1;
+        c1 = lo;
+        k += 0x9E3779B9u;
     }
     o0 = c0;
     o1 = c1;
@@ -375,8 +374,7 @@ __device__ __forceinline__ void act_tiles(const ActArgs& a, int block) {
     uint32_t rnd0 = 0, rnd1 = 0, rb0[4] = {0, 0, 0, 0}, rb1[4] = {0, 0, 0, 0};
     auto draw4 = [&](int base) {
         const int r = base + g4 < t1 ? row_of_lane(base + g4, j) : -1;
-        philox2((uint32_t)r, 0u, (uint32_t)off, (uint32_t)(off >> 32), (uint32_t)a.seed, (uint32_t)(a.seed >> 32), rnd0,
-                rnd1);
+        philox2((uint32_t)r, off, a.seed, rnd0, rnd1);
         rows_bcast(rnd0, rb0);  // tile base + k takes row k's draws
         rows_bcast(rnd1, rb1);
     };
@@ -576,7 +574,7 @@ __device__ __forceinline__ void act_common_rows(const ActArgs& a, int block) {
     auto uniform_of = [&](int row) -> float {
         if (EXT_U) return a.uniforms[row];
         uint32_t r0, r1;
-        philox2((uint32_t)row, 0u, (uint32_t)off, (uint32_t)(off >> 32), (uint32_t)a.seed, (uint32_t)(a.seed >> 32), r0, r1);
+        philox2((uint32_t)row, off, a.seed, r0, r1);
         return u24(r0);
     };
     const int i_begin = wv * a.items_per_wave;
