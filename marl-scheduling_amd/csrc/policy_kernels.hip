@@ -68,8 +68,10 @@ __device__ __forceinline__ f4 mfma_bf16(const u4v& a, const u4v& b, f4 c) {
 
 // tanh(x) = 1 - 2 / (1 + exp(2x)): exp overflows to inf for large x (-> 1) and underflows to 0 for
 // large -x (-> -1); absolute error ~1e-7 (what feeds the next layers' sums of O(1) terms).
-__device__ __forceinline__ float fast_tanh(float x) {
-    const float t = __builtin_amdgcn_exp2f(2.8853900817779268f * x);  // exp(2x)
+// tanh(a + b) with the bias pre-scaled, bs = b * 2 log2(e) (kTanhScale): the exponent is one fma
+constexpr float kTanhScale = 2.8853900817779268f;
+__device__ __forceinline__ float fast_tanh_b(float a, float bs) {
+    const float t = __builtin_amdgcn_exp2f(fmaf(a, kTanhScale, bs));  // exp(2(a + b))
     return fmaf(-2.f, __builtin_amdgcn_rcpf(1.f + t), 1.f);
 }
 __device__ __forceinline__ float fast_exp(float x) { return __builtin_amdgcn_exp2f(x * 1.4426950408889634f); }
@@ -132,14 +134,14 @@ __device__ __forceinline__ u4v bytes_to_bf16(uint32_t d0, uint32_t d1) {
 // W3[16t + j][4*g4 + s] (the permuted-k A operands) and the biases of its accumulator rows.
 template <int NT>
 struct Head {
-    float b1[4], w2[4], b2[4], w3[NT][4], b3[NT][4];
+    float b1[4], w2[4], b2[4], w3[NT][4], b3[NT][4];  // b1, b2 pre-scaled by kTanhScale (fast_tanh_b)
     __device__ void load(const ms_mlp_params& p, int grp, int j, int g4) {
         const int A = p.n_actions;
 #pragma unroll
         for (int q = 0; q < 4; q++) {
-            b1[q] = p.b1[grp * 16 + 4 * g4 + q];
+            b1[q] = p.b1[grp * 16 + 4 * g4 + q] * kTanhScale;
             w2[q] = p.w2[(size_t)grp * 256 + j * 16 + 4 * g4 + q];
-            b2[q] = p.b2[grp * 16 + 4 * g4 + q];
+            b2[q] = p.b2[grp * 16 + 4 * g4 + q] * kTanhScale;
 #pragma unroll
             for (int t = 0; t < NT; t++) {
                 const int a = 16 * t + j, ab = 16 * t + 4 * g4 + q;
@@ -157,13 +159,13 @@ struct Head {
                                                float& S) const {
         float h1[4];
 #pragma unroll
-        for (int q = 0; q < 4; q++) h1[q] = fast_tanh(a1[q] + b1[q]);
+        for (int q = 0; q < 4; q++) h1[q] = fast_tanh_b(a1[q], b1[q]);
         f4 a2 = {0, 0, 0, 0};
 #pragma unroll
         for (int s = 0; s < 4; s++) a2 = mfma4(w2[s], h1[s], a2);
         float h2[4];
 #pragma unroll
-        for (int q = 0; q < 4; q++) h2[q] = fast_tanh(a2[q] + b2[q]);
+        for (int q = 0; q < 4; q++) h2[q] = fast_tanh_b(a2[q], b2[q]);
         float m = -INFINITY;
 #pragma unroll
         for (int t = 0; t < NT; t++) {

@@ -48,11 +48,12 @@ __device__ __forceinline__ float xsum16(float v) {  // sum over the 16 lanes sha
 __device__ __forceinline__ float xsum4g(float v) { return rows_sum(v); }  // sum over lanes j, j+16, j+32, j+48
 __device__ __forceinline__ float xmax4g(float v) { return rows_max(v); }
 
-// tanh(x) = sign(x) (1 - t) / (1 + t), t = exp(-2|x|): absolute error ~1e-7 everywhere
 // tanh(x) = 1 - 2 / (1 + exp(2x)): exp overflows to inf for large x (-> 1) and underflows to 0 for
 // large -x (-> -1); absolute error ~1e-7 (what feeds the next layers' sums of O(1) terms).
-__device__ __forceinline__ float fast_tanh(float x) {
-    const float t = __builtin_amdgcn_exp2f(2.8853900817779268f * x);  // exp(2x)
+// tanh(a + b) with the bias pre-scaled, bs = b * 2 log2(e) (kTanhScale): the exponent is one fma
+constexpr float kTanhScale = 2.8853900817779268f;
+__device__ __forceinline__ float fast_tanh_b(float a, float bs) {
+    const float t = __builtin_amdgcn_exp2f(fmaf(a, kTanhScale, bs));  // exp(2(a + b))
     return fmaf(-2.f, __builtin_amdgcn_rcpf(1.f + t), 1.f);
 }
 __device__ __forceinline__ float fast_exp(float x) { return __builtin_amdgcn_exp2f(x * 1.4426950408889634f); }
@@ -206,11 +207,11 @@ __global__ void __launch_bounds__((64 * GradLds<NQ, NT, MODE>::WPB), ((NQ * NT >
         }
         for (int i = tid; i < 16 * NT; i += NTH) sb3[i] = i < A ? p.b3[(size_t)grp * A + i] : 0.f;
         if (tid < 16) {
-            sb1[tid] = p.b1[grp * 16 + tid];
-            sb2[tid] = p.b2[grp * 16 + tid];
+            sb1[tid] = p.b1[grp * 16 + tid] * kTanhScale;  // hidden biases pre-scaled (fast_tanh_b)
+            sb2[tid] = p.b2[grp * 16 + tid] * kTanhScale;
             sc3[tid] = p.cw3[grp * 16 + tid];
-            scb1[tid] = p.cb1[grp * 16 + tid];
-            scb2[tid] = p.cb2[grp * 16 + tid];
+            scb1[tid] = p.cb1[grp * 16 + tid] * kTanhScale;
+            scb2[tid] = p.cb2[grp * 16 + tid] * kTanhScale;
         }
         if (tid == 0) scb3[0] = p.cb3[grp];
     }
@@ -272,8 +273,8 @@ __global__ void __launch_bounds__((64 * GradLds<NQ, NT, MODE>::WPB), ((NQ * NT >
         }
 #pragma unroll
         for (int q = 0; q < 4; q++) {
-            f.h1[q] = fast_tanh(a1[q] + sb1[4 * g4 + q]);
-            f.hc1[q] = fast_tanh(c1[q] + scb1[4 * g4 + q]);
+            f.h1[q] = fast_tanh_b(a1[q], sb1[4 * g4 + q]);
+            f.hc1[q] = fast_tanh_b(c1[q], scb1[4 * g4 + q]);
         }
         // layer 2: B operand = layer-1 output as is; A reads W2 with k permuted (k_true = 4*g4 + s)
         f4 a2 = {0, 0, 0, 0}, c2 = {0, 0, 0, 0};
@@ -288,8 +289,8 @@ __global__ void __launch_bounds__((64 * GradLds<NQ, NT, MODE>::WPB), ((NQ * NT >
         }
 #pragma unroll
         for (int q = 0; q < 4; q++) {
-            f.h2[q] = fast_tanh(a2[q] + sb2[4 * g4 + q]);
-            f.hc2[q] = fast_tanh(c2[q] + scb2[4 * g4 + q]);
+            f.h2[q] = fast_tanh_b(a2[q], sb2[4 * g4 + q]);
+            f.hc2[q] = fast_tanh_b(c2[q], scb2[4 * g4 + q]);
         }
         // actor layer 3 -> logits z[a = 16t + 4*g4 + q][row j]
         float z[NT][4];
