@@ -651,7 +651,8 @@ int ms_ppo_grad(const ms_mlp_params* a, const ms_mlp_params* c, const ms_ppo_bat
     p.states = b->states;
     p.actions = b->actions;
     p.old_lp = b->old_logprobs;
-    p.us = b->unit_stride;
+    p.rrs = b->unit_stride ? 1 : b->U;
+    p.rus = b->unit_stride ? b->unit_stride : 1;
     p.ret = b->returns;
     p.unit_of_group = b->unit_of_group;
     p.common = b->common_row;

@@ -12,7 +12,8 @@ struct PpoArgs {
     const int8_t* states;                            // [R][U][stride]  (R = T*E rows, r = t*E + e)
     const int8_t* actions;                           // [R][U]
     const float* old_lp;                             // [R][U]
-    int64_t us;                                      // 0, or unit-major states / actions / old_lp: row (r, u) at u*us + r
+    int64_t rrs, rus;                                // row (r, u) of states / actions / old_lp at r*rrs + u*rus:
+                                                     //   (U, 1) for [R][U], (1, unit stride) unit-major
     const float* ret;                                // [T][E][ret_ld] normalised returns
     const int32_t* unit_of_group;                    // [G]
     const int8_t* common;                            // [stride] rows equal to it share one forward, or NULL
@@ -49,7 +50,7 @@ struct PpoArgs {
 
 // row (r, u) of the rollout arrays (states rows, actions, old log-probs): [R][U] or unit-major
 __device__ __forceinline__ size_t ru_index(const PpoArgs& p, long long r, int u) {
-    return p.us ? (size_t)u * (size_t)p.us + (size_t)r : (size_t)r * p.U + u;
+    return (size_t)r * (size_t)p.rrs + (size_t)u * (size_t)p.rus;  // no branch: loads batch as before
 }
 
 constexpr int kKeyDense = 1 << 20;   // 4 bytes x 5 bits
