@@ -403,7 +403,7 @@ typedef struct ms_ppo_batch {
     int32_t n_cores;
     /* 0: rows of 4 bytes (stride 4, nets of <= 4 inputs and <= 32 actions, no common_row) are keyed:
      * each group's distinct rows get one forward and one backward pass, and each row adds its loss
-     * derivatives to its distinct row's int64 fixed-point sums (2^-28); -1: every row on its own */
+     * derivatives to its distinct row's int64 fixed-point sums (2^-20); -1: every row on its own */
     int32_t row_keys;
     /* 0: states [R][U][stride], actions / old_logprobs [R][U]; else >= R and unit-major: row (r, u) at
      * u * unit_stride + r in all three (e.g. [U][T][E] rollout rings; not with core_owner) */

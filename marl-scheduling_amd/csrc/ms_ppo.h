@@ -57,7 +57,11 @@ constexpr int kKeyDense = 1 << 20;   // 4 bytes x 5 bits
 constexpr int kKeyMaxRanks = 4096;   // distinct rows per group, more: tile path
 constexpr int kKeyBlocks = 32;       // blocks per group of the rank passes (forward, backward)
 constexpr int kKeyScanBlocks = 32;   // blocks per group of the row scan
-constexpr double kKeyFx = 268435456.0;           // 2^28: fixed-point scale of the keyed sums
+// 2^20: fixed-point scale of the keyed sums. A term's rounding is 2^-21 (a 21-bit mantissa at |term| ~ 1;
+// the integer sums themselves are exact), and terms up to 2^42 / R stay in range (1.3e6 at cfg3's
+// R = 3.3M rows: a ratio far from 1 with a negative advantage after an earlier draw's update; at
+// 2^28 the bound was 5242, and one such row sent its whole group to the tile path)
+constexpr double kKeyFx = 1048576.0;
 
 constexpr int kAdamMaxTensors = 16, kAdamMaxGroups = 4;
 struct AdamTensor {  // layout of ms_adam_tensor
