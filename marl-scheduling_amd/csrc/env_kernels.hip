@@ -521,9 +521,10 @@ __device__ void build_obs_sources(Rec& R, const Params& P, const M128* mc, const
     const int8_t* ck = R.core_kind();
     const int8_t* cr = R.core_rem();
     if (acc || auct) {
-        for (int i = gl; i < (C + 1) * nw; i += LPE) {
-            const int k = i - (i / nw) * nw;
-            crow[i] = foreign_dword(k, P.d_acc);
+        // lane-fixed column: one foreign dword per lane, stored to all C + 1 rows (no division)
+        for (int k = gl; k < nw; k += LPE) {
+            const uint32_t v = foreign_dword(k, P.d_acc);
+            for (int r = 0; r <= C; r++) crow[r * nw + k] = v;
         }
     }
     if (acc) {
@@ -634,7 +635,7 @@ __device__ __forceinline__ void emit_rows(uint32_t* base, int64_t e, int64_t E, 
 #pragma unroll
     for (int i = 0; i < 4; i++) {
         const int d = 4 * j + i;
-        ri[i] = d / nw;
+        ri[i] = div_mag(d, mag, nw);
         col[i] = d - ri[i] * nw;
     }
     const int64_t env_off = e * n_dw * 4;
