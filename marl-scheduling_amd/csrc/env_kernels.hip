@@ -458,9 +458,13 @@ __device__ __forceinline__ void m_add(double* p, double v) {
 
 // Masks of the current offers: mc[c] = offers to core c, mr[r] = offers to
 // recipient r (0 = auctioneer). Ends with a phase boundary.
+// With last1 != NULL also last1[c] = 1 when an offer to core c holds a job with one round left.
 template <int LPE>
-__device__ void build_masks(Rec& R, const Params& P, M128* mc, M128* mr, int gl) {
-    for (int i = gl; i < P.C; i += LPE) mc[i] = M128{0, 0};
+__device__ void build_masks(Rec& R, const Params& P, M128* mc, M128* mr, int gl, uint8_t* last1 = nullptr) {
+    for (int i = gl; i < P.C; i += LPE) {
+        mc[i] = M128{0, 0};
+        if (last1) last1[i] = 0;
+    }
     for (int i = gl; i <= P.N; i += LPE) mr[i] = M128{0, 0};
     wave_sync();
     const int8_t* oc = R.offer_core();
@@ -470,6 +474,7 @@ __device__ void build_masks(Rec& R, const Params& P, M128* mc, M128* mr, int gl)
         if (c >= 0) {
             mask_set(&mc[c], i);
             mask_set(&mr[orc[i]], i);
+            if (last1 && R.slot_rem()[i] == 1) last1[c] = 1;
         }
     }
     wave_sync();
@@ -561,18 +566,27 @@ __device__ void build_obs_sources(Rec& R, const Params& P, const M128* mc, const
     if (acc || auct) {
         const int8_t* op = R.offer_price();
         const int8_t* sr = R.slot_rem();
+        const int8_t* oc = R.offer_core();
+        const int8_t* orc = R.offer_recip();
         for (int c = gl; c < C; c += LPE) {
             int8_t* row = reinterpret_cast<int8_t*>(crow) + c * P.acc_stride;
             const int kind = ck[c];
             row[0] = 1;
             row[1] = (int8_t)(kind >= 0 ? R.prio(kind) : -1);
             row[2] = cr[c];
-            int w = 3;
-            for (MaskIter it(mand(mc[c], mr[owner[c]])); it.more();) {
-                const int i = it.next();
-                row[w] = op[i];
-                row[w + 1] = sr[i];
-                w += 2;
+        }
+        // the (price, necT) pairs of the offers to c addressed to c's owner, in offer-ID order
+        // (Agent.py:180-200): one lane per offer, placed at its rank among those offers (no serial
+        // walk of the core's mask)
+        for (int i = gl; i < P.NL; i += LPE) {
+            const int c = oc[i];
+            if (c >= 0 && orc[i] == owner[c]) {
+                const M128 m = mand(mc[c], mr[owner[c]]);
+                const int rank = i < 64 ? __popcll(m.lo & ((1ull << i) - 1ull))
+                                        : __popcll(m.lo) + __popcll(m.hi & ((1ull << (i - 64)) - 1ull));
+                int8_t* row = reinterpret_cast<int8_t*>(crow) + c * P.acc_stride;
+                row[3 + 2 * rank] = op[i];
+                row[4 + 2 * rank] = sr[i];
             }
         }
     }
@@ -580,6 +594,14 @@ __device__ void build_obs_sources(Rec& R, const Params& P, const M128* mc, const
 }
 
 __device__ __forceinline__ int div_mag(uint32_t w, uint32_t mag, int d) { return d == 1 ? (int)w : (int)__umulhi(w, mag); }
+
+// x / d for 0 <= x < 256 and 1 <= d < 256 without the integer-division sequence: floor((x + 1/2) * rcp(d)).
+// (x + 1/2) / d lies at least 1/(2d) >= 2^-9 from an integer and the product's error is below
+// 256 * 2^-21 = 2^-13 (rcp within 2 ulp), so the floor is exact; checked exhaustively over the range
+// with the reciprocal perturbed by +-2 ulp (tests/test_env_helpers.py).
+__device__ __forceinline__ int small_div(int x, int d) {
+    return (int)(((float)x + 0.5f) * __builtin_amdgcn_rcpf((float)d));
+}
 
 // Block e of an [E][n_dw] dword array: dword w = val(w / nw, w % nw), LPE lanes, 4 dwords per
 // lane-store (write-through) when aligned.
@@ -621,15 +643,16 @@ template <int LPE, class Src>
 __device__ __forceinline__ void emit_rows(uint32_t* base, int64_t e, int64_t E, int n_rows, int nw, uint32_t mag,
                                           int gl, Src src) {
     const int n_dw = n_rows * nw;
-    const int g4 = (nw & 1) ? 4 : ((nw & 2) ? 2 : 1);  // RG
-    const int CG = g4 * nw / 4;
+    const int lg4 = (nw & 1) ? 2 : ((nw & 2) ? 1 : 0);
+    const int g4 = 1 << lg4;  // RG
+    const int CG = (nw << lg4) >> 2;
     const WtOut o(base, E * n_dw * 4);
     if (!o.ok || (n_dw & 3) != 0 || CG > LPE) {
         emit_flat<LPE>(base, e, E, n_dw, nw, mag, gl, [&](int r, int col) { return src(r, col, 0); });
         return;
     }
-    const int GPI = LPE / CG;
-    const int j = gl % CG, q0 = gl / CG;
+    const int GPI = small_div(LPE, CG);  // CG <= LPE <= 64
+    const int q0 = small_div(gl, CG), j = gl - q0 * CG;
     if (q0 >= GPI) return;
     int ri[4], col[4];
 #pragma unroll
@@ -639,7 +662,7 @@ __device__ __forceinline__ void emit_rows(uint32_t* base, int64_t e, int64_t E, 
         col[i] = d - ri[i] * nw;
     }
     const int64_t env_off = e * n_dw * 4;
-    const int n_groups = n_rows / g4;
+    const int n_groups = n_rows >> lg4;
     for (int q = q0; q < n_groups; q += GPI) {
         const int r0 = q * g4;
         o.st4(env_off + 4 * (r0 * nw + 4 * j), src(r0 + ri[0], col[0], 0), src(r0 + ri[1], col[1], 1),
@@ -1156,7 +1179,7 @@ __device__ __forceinline__ void env_round(const Params& P, int64_t E, uint8_t* r
         if (gl < C && s_exec[gl] >= 0) {
             const int c = gl;
             const int i = s_exec[c];
-            const int offerer = i / L + 1;
+            const int offerer = small_div(i, L) + 1;  // i < NL <= 128
             const int recip = o_recip[i];
             if (recip != c_owner[c]) atomicOr(&s_flags, MS_FLAG_GUARD);  // executeAnOffer's check (world.py:266)
             const int nk = s_kind[i], nrem = s_rem[i], nbirth = s_birth[i];
@@ -1231,7 +1254,7 @@ __device__ __forceinline__ void env_round(const Params& P, int64_t E, uint8_t* r
         for (int r = 0; r < n_exec; r++) {
             const int c = s_by_rank[r];
             const int i = s_exec[c];
-            const int offerer = i / L + 1, slot = i - (offerer - 1) * L;
+            const int offerer = small_div(i, L) + 1, slot = i - (offerer - 1) * L;  // i < NL <= 128
             const int recip = o_recip[i];
             if (recip != c_owner[c]) s_flags |= MS_FLAG_GUARD;  // executeAnOffer's ownership check (world.py:266)
             const int nk = s_kind[i], nrem = s_rem[i], nbirth = s_birth[i];
