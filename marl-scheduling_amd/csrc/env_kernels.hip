@@ -1097,12 +1097,12 @@ __device__ __forceinline__ void env_round(const Params& P, int64_t E, uint8_t* r
     MtStream<LPE> rs;
     rs.init(mt + e * 2 * kMtN, R.mt_sel(), R.mti(), active);
     rs.load(0, 0, Lg);
-    build_masks<LPE>(R, P, s_mc, s_mr, gl);
+    // the scratch is free until the executions: per core, "an offer to it has one round left"
+    build_masks<LPE>(R, P, s_mc, s_mr, gl, scratch);
     Liab pf[kLiabPrefetch];
     int pf_n = 0;
     if (gl < C) {
-        bool maybe = c_kind[gl] >= 0 && c_rem[gl] == 1;
-        for (MaskIter it(s_mc[gl]); it.more() && !maybe;) maybe = s_rem[it.next()] == 1;
+        const bool maybe = (c_kind[gl] >= 0 && c_rem[gl] == 1) || scratch[gl];
         if (maybe) {
             const int n = l_n[gl];
             pf_n = min(n, kLiabPrefetch);
@@ -1151,8 +1151,11 @@ __device__ __forceinline__ void env_round(const Params& P, int64_t E, uint8_t* r
     wave_sync();
     for (int c = gl; c < C; c += LPE) {
         if (s_exec[c] >= 0) {
+            // branch-free, so the unrolled loop issues its LDS reads together
+            const int kc = s_key[c];
             int r = 0;
-            for (int d = 0; d < C; d++) r += (s_exec[d] >= 0 && s_key[d] < s_key[c]);
+#pragma unroll 8
+            for (int d = 0; d < C; d++) r += (int)(s_exec[d] >= 0) & (int)(s_key[d] < kc);
             s_by_rank[r] = (int8_t)c;
             atomicAdd(&s_n_exec, 1);
         }
