@@ -588,9 +588,15 @@ __device__ __forceinline__ void act_common_rows(const ActArgs& a, int block) {
     int n_row = 0;
     bool n_in = false;
     // compact rows: the core row of (e, u) and whether agent u / C + 1 owns core u % C
+    // (quotients by a multiply-high with one correction step, as row_of_item: no per-row
+    // integer-division sequence)
+    const uint32_t u_mag = 0xffffffffu / (uint32_t)a.U, c_mag = 0xffffffffu / (uint32_t)a.n_cores;
     auto core_row_of = [&](int row, int& c_out) -> size_t {
-        const int e = row / a.U, u = row - e * a.U;
-        const int ag = u / a.n_cores;
+        int e = (int)__umulhi((uint32_t)row, u_mag);
+        if ((e + 1) * a.U <= row) e++;
+        const int u = row - e * a.U;
+        int ag = (int)__umulhi((uint32_t)u, c_mag);
+        if ((ag + 1) * a.n_cores <= u) ag++;
         c_out = ag;
         return (size_t)e * a.n_cores + (u - ag * a.n_cores);
     };
