@@ -18,3 +18,18 @@ def test_small_div_exact_with_inexact_reciprocal():
                 rk = np.nextafter(rk, step)
             q = np.floor(x * np.float32(rk)).astype(np.int64)  # float32 product, round to nearest
             assert np.array_equal(q, want // d), (d, k)
+
+
+def test_mulhi_quotient_with_one_correction():
+    """k_act_pair's row -> (replica, unit) and unit -> agent quotients (policy_kernels.hip
+    core_row_of): q = umulhi(x, floor((2^32 - 1) / d)), plus one if (q + 1) * d <= x, equals x // d
+    for every x < 2^31 (checked on a dense low range and random draws, for the divisors in use)."""
+    rng = np.random.default_rng(7)
+    xs = np.concatenate([np.arange(0, 1 << 16, dtype=np.uint64),
+                         rng.integers(0, 1 << 31, size=1 << 16, dtype=np.uint64),
+                         np.array([(1 << 31) - 1], dtype=np.uint64)])
+    for d in list(range(1, 130)) + [256, 1024, 4096, 65536]:
+        m = np.uint64(0xFFFFFFFF // d)
+        q = (xs * m) >> np.uint64(32)
+        q = q + ((q + np.uint64(1)) * np.uint64(d) <= xs).astype(np.uint64)
+        assert np.array_equal(q, xs // np.uint64(d)), d
