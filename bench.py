@@ -9,8 +9,10 @@ collectionLength 3, free prices + commercial reward, locally shared PPO
 (SURVEY.md §8(d) cfg3). value = agents x replicas x rounds over all ranks /
 max-over-ranks wall time of the timed steps (weak scaling: replicas per GPU fixed).
 
-Run: python bench.py [--gpus N --steps K --warmup W]; N > 1 under
-torch.distributed.run (one rank per GPU, RCCL all-reduce of the shared nets' gradients).
+Run: python bench.py [--gpus N --steps K --warmup W]; N > 1 under torch.distributed.run, or
+bench.py --gpus N alone, which starts the N rank processes itself (one rank per GPU, RCCL
+all-reduce of the shared nets' gradients). The line also carries the env step kernel alone
+(pre-sampled actions, seeds {0,1,2}) as "step_kernel".
 """
 from __future__ import annotations
 
@@ -232,13 +234,7 @@ def bench_other(args):
     import torch
     import torch.distributed as dist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    world, rank, local_rank = init_ranks(args)
     device = torch.device("cuda", local_rank)
     torch.cuda.set_device(device)
     importlib.import_module("marl-scheduling_amd")
@@ -266,6 +262,8 @@ def bench_other(args):
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(device)
+    if hasattr(tr, "timings"):
+        tr.timings = dict(rollout=0.0, update=0.0)
     t0 = time.perf_counter()
     for _ in range(args.steps):
         run()
@@ -288,15 +286,181 @@ def bench_other(args):
               "config": {"workload": "%s: %s; one step = %d rounds%s" % (args.config, spec["what"], T,
                                                                        " + update" if args.config != "cfg5" else ""),
                          "replicas_per_gpu": E, "rounds_per_step": T}}
+    if hasattr(tr, "timings"):
+        tm = dict(tr.timings)
+        result["breakdown_ms_per_step"] = {k: v / args.steps * 1e3 for k, v in tm.items()}
     if rank == 0:
         print(json.dumps(result))
     if world > 1:
         dist.destroy_process_group()
 
 
+def launch_ranks(n: int, argv) -> int:
+    """``--gpus N`` without a torch.distributed launcher: start N rank processes of this script,
+    one per GPU (RANK = LOCAL_RANK = r, WORLD_SIZE = N, rendezvous on 127.0.0.1), the way
+    ``torch.distributed.run --nproc-per-node N`` would. Called before anything touches the GPU
+    (the parent never initialises HIP); if one rank fails the others are stopped (their exact
+    PIDs). Returns the exit code (0 when every rank succeeded)."""
+    import socket
+    import subprocess
+
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC only on these hosts (RCCL)
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv), env=env))
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            code = p.poll()
+            if code is None:
+                continue
+            live.remove(p)
+            if code != 0 and rc == 0:
+                rc = code if code > 0 else 128 - code
+                for q in live:  # a failed rank would leave the others waiting in a collective
+                    q.terminate()
+        time.sleep(0.05)
+    return rc
+
+
+def init_ranks(args, backend: str = "nccl"):
+    """(world, rank, local_rank) from the launcher's environment; joins the process group for
+    world > 1 (RCCL over xGMI on GPUs, gloo for the CPU stub) and checks that the group has the
+    --gpus ranks it was asked for."""
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.gpus is not None and args.gpus != world:
+        raise SystemExit("--gpus %d but the launcher started %d rank(s)" % (args.gpus, world))
+    if world > 1:
+        if backend == "nccl":
+            import torch
+            os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+            torch.cuda.set_device(local_rank)
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        else:
+            dist.init_process_group(backend)
+        if dist.get_world_size() != world:
+            raise SystemExit("process group has %d ranks, WORLD_SIZE %d" % (dist.get_world_size(), world))
+    return world, rank, local_rank
+
+
+def bench_stub(args):
+    """The launcher and process-group path without a GPU (gloo): every rank joins, checks in with
+    an all-reduce of ones, and rank 0 prints what the real bench prints about the ranks."""
+    import torch
+    import torch.distributed as dist
+
+    if os.environ.get("MS_STUB_FAIL_RANK", "-") == os.environ.get("RANK"):  # tests: a rank that dies early
+        raise SystemExit(3)
+    world, rank, _ = init_ranks(args, backend="gloo")
+    E = args.envs or 16384
+    seen = torch.ones(1)
+    replicas = torch.tensor([float(E)])
+    if world > 1:
+        dist.all_reduce(seen)
+        dist.all_reduce(replicas)
+    line = {"metric": "launcher stub", "n_gpus": world, "pg_world_size": dist.get_world_size() if world > 1 else 1,
+            "ranks_reported": int(seen.item()), "replicas_per_gpu": E, "replicas_total": int(replicas.item()),
+            "rank_pids": None}
+    if world > 1:
+        pids = [None] * world
+        dist.all_gather_object(pids, os.getpid())
+        line["rank_pids"] = pids
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+STEP_SEEDS = (0, 1, 2)
+STEP_RING = 200          # rounds of pre-sampled actions, cycled
+STEP_WARMUP_ROUNDS = 200
+STEP_TIMED_ROUNDS = 2000
+
+
+def step_kernel_line(E: int, device, world: int, rank: int):
+    """the env step kernel alone, actions pre-sampled uniformly into a device ring
+    (acceptor [0, A_acc), core chooser [0, A_off), price [0, A_pc), price -5 where the core action is
+    0 as FreePriceOfferPPO sends it), outputs written as the trainer's rollout gets them (compact
+    acceptor rows + owners, offer rows, rewards). Per seed: 200 warm-up rounds, then 2000 timed
+    rounds (10 replays of a 200-round HIP graph) between HIP events on the launch stream."""
+    import torch
+    import torch.distributed as dist
+
+    ms = importlib.import_module("marl-scheduling_amd")
+    trainer_mod = importlib.import_module("marl-scheduling_amd.trainer")
+    cfg = ms.abi.named_config("cfg3")
+    s = ms.abi.config_shape(cfg)
+    N, C, L = s["N"], s["C"], s["L"]
+    per_seed = {}
+    for seed in STEP_SEEDS:
+        env = ms.BatchedEnv(cfg, E, seed=trainer_mod.env_seed(seed, rank, E), device=device)
+        g = torch.Generator(device=device).manual_seed(seed * 7919 + rank)
+        ri = lambda hi, shape: torch.randint(0, hi, shape, generator=g, device=device, dtype=torch.int8)
+        acc = ri(s["acc_actions"], (STEP_RING, E, N, C))
+        off = ri(s["off_actions"], (STEP_RING, E, N, L))
+        price = torch.where(off == 0, torch.full_like(off, -5), ri(s["price_actions"], (STEP_RING, E, N, L)))
+        obs = env.compact_obs_buffers()
+        rew = env.reward_buffers()
+        env.reset(obs)
+
+        def body():
+            for t in range(STEP_RING):
+                env.step(acc[t], off[t], price[t], obs=obs, rewards=rew)
+
+        for _ in range(STEP_WARMUP_ROUNDS // STEP_RING):
+            body()
+        torch.cuda.synchronize(device)
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            body()
+        stream = torch.cuda.current_stream(device)
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize(device)
+        ev[0].record(stream)
+        for _ in range(STEP_TIMED_ROUNDS // STEP_RING):
+            graph.replay()
+        ev[1].record(stream)
+        ev[1].synchronize()
+        sec = ev[0].elapsed_time(ev[1]) / 1e3
+        if world > 1:
+            t = torch.tensor([sec], dtype=torch.float64, device=device)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            sec = float(t.item())
+        if env.flags():
+            raise SystemExit("env error flags set in the step-kernel run: 0x%x" % env.flags())
+        b_round = env_round_bytes(env.shape, cfg.new_jobs_per_round, True, True)
+        us = sec / STEP_TIMED_ROUNDS * 1e6
+        per_seed[str(seed)] = {"value": world * E * N * STEP_TIMED_ROUNDS / sec, "us_per_round": us,
+                               "frac": b_round * E / (us * 1e-6) / 1e9 / HBM_PEAK_GBS}
+        del graph, env
+    vals = [v["value"] for v in per_seed.values()]
+    return {"metric": "agent-env-steps/s, env step kernel alone (SURVEY 8(d)(i))", "unit": "agent-env-steps/s",
+            "value": sum(vals) / len(vals), "min": min(vals), "max": max(vals), "per_seed": per_seed,
+            "seeds": list(STEP_SEEDS), "replicas_per_gpu": E, "n_gpus": world, "warmup_rounds": STEP_WARMUP_ROUNDS,
+            "timed_rounds": STEP_TIMED_ROUNDS,
+            "actions": "uniform, pre-sampled into a %d-round device ring" % STEP_RING,
+            "timing": "HIP events on the launch stream around %d replays of a %d-round HIP graph"
+                      % (STEP_TIMED_ROUNDS // STEP_RING, STEP_RING)}
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="ranks (one per GPU); without a launcher's WORLD_SIZE, N > 1 starts N rank processes")
+    ap.add_argument("--stub", action="store_true", help="launcher / process-group check on CPU (gloo), no GPU work")
+    ap.add_argument("--no-step-kernel", action="store_true", help="skip the env-step-kernel-only line")
     ap.add_argument("--steps", type=int, default=2)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--envs", type=int, default=None, help="env replicas per GPU (default: the config's per-GPU share)")
@@ -308,19 +472,17 @@ def main():
     ap.add_argument("--config", default="cfg3", choices=["cfg2", "cfg3", "cfg4", "cfg5"],
                     help="BASELINE config (cfg3 = the headline; cfg2/cfg4/cfg5 are the other BASELINE workloads)")
     args = ap.parse_args()
+    if args.gpus is not None and args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))  # nothing has touched the GPU in this process
+    if args.stub:
+        return bench_stub(args)
     if args.config != "cfg3":
         return bench_other(args)
 
     import torch
     import torch.distributed as dist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    world, rank, local_rank = init_ranks(args)
     device = torch.device("cuda", local_rank)
     torch.cuda.set_device(device)
     ms = importlib.import_module("marl-scheduling_amd")
@@ -393,6 +555,8 @@ def main():
             "replicas_per_gpu": args.envs,
             "rounds_per_step": args.update_step,
             "parallelism": "replicas sharded over %d rank(s), RCCL grad all-reduce" % world,
+            "world_size": dist.get_world_size() if world > 1 else 1,
+            "replicas_total": world * args.envs,
         },
         "roofline": {
             "kernel": "ms::k_env_step",
@@ -420,6 +584,10 @@ def main():
                             + (", %d streams" % args.rollout_streams if args.rollout_streams > 1 else ""),
         },
     }
+    if not args.no_step_kernel:
+        del tr  # the trainer's rings are not needed by the step-kernel run
+        torch.cuda.empty_cache()
+        result["step_kernel"] = step_kernel_line(args.envs, device, world, rank)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:
             result["cpu_baseline"] = cpu_baseline()

@@ -696,7 +696,7 @@ int ms_ppo_grad(const ms_mlp_params* a, const ms_mlp_params* c, const ms_ppo_bat
         p.key_nbs = ms::kKeyScanBlocks;
         // ranks per scan pass: the LDS sums (int64 per action + V - G, a uint32 count) in 147 KB
         p.key_cap = (147 * 1024) / ((16 * ((a->n_actions + 15) / 16) + 1) * 8 + 4);
-        // |term| * 2^28 * R < 2^62: a slot's int64 sum cannot overflow
+        // |term| * kKeyFx * R < 2^62: a slot's int64 sum cannot overflow
         p.key_bound = (float)std::min(1e30, std::ldexp(1.0, 62) / ms::kKeyFx / (double)R);
     }
     ms::GradOut go{g->w1, g->b1, g->w2, g->b2, g->w3, g->b3, g->cw1, g->cb1, g->cw2, g->cb2, g->cw3, g->cb3, g->loss};

@@ -170,8 +170,9 @@ class DQNGroup:
         for k in KEYS:
             getattr(self.target, k).copy_(getattr(self.policy, k))
 
-    def grad(self, mem: ReplayMemories, samples, units_per_group: int = 1, stream=None):
-        """The minibatch gradient of every group (ms_dqn_grad) into policy's .grad, clamped."""
+    def grad(self, mem: ReplayMemories, samples, units_per_group: int = 1, stream=None, clip: float | None = None):
+        """The minibatch gradient of every group (ms_dqn_grad) into policy's .grad, clamped to
+        +-clip (default hp.grad_clip; inf = unclamped, for a multi-rank step that clamps the mean)."""
         E, U, B = samples.shape
         assert samples.dtype == torch.int32 and samples.is_contiguous() and U == mem.U and E == mem.E
         pp, tp = self.policy.params(), self.target.params()
@@ -183,7 +184,7 @@ class DQNGroup:
                            mem.stride, U, units_per_group, mem.cap, B, E, ct.c_float(self.gamma))
         pol = self.policy
         g = abi.MsQnetGrads(ptr(pol.w1.grad), ptr(pol.b1.grad), ptr(pol.w2.grad), ptr(pol.b2.grad), ptr(self.loss))
-        check(lib.ms_dqn_grad(ct.byref(pp), ct.byref(tp), ct.byref(b), ct.c_float(self.hp.grad_clip), ptr(self._ws),
+        check(lib.ms_dqn_grad(ct.byref(pp), ct.byref(tp), ct.byref(b), ct.c_float(self.hp.grad_clip if clip is None else clip), ptr(self._ws),
                               self._ws.numel() * 4, ct.byref(g), stream_ptr(stream)))
         return self.loss
 
@@ -271,10 +272,16 @@ class DQNTrainer:
         """updateAcceptorMemoriesAndOptimize then updateOfferMemoriesAndOptimize (SchedulingEnvironment.py:366-425)
         for all units at once; with several ranks one all-reduce carries both unit types' gradients."""
         grads = {}
+        # several ranks: clamp the rank-averaged gradient (DQNmodules.py:151-152 clamps the gradient
+        # of the whole minibatch), not each rank's share, so results do not depend on the rank count
+        multi = self._allreduce is not None
         for name, grp, mem in (("acc", self.acc, self.mem_acc), ("off", self.off, self.mem_off)):
-            grads[name] = grp.grad(mem, self._samples(mem)).clone()
-        if self._allreduce is not None:
-            self._allreduce(list(self.acc.policy.parameters()) + list(self.off.policy.parameters()))
+            grads[name] = grp.grad(mem, self._samples(mem), clip=float("inf") if multi else None).clone()
+        if multi:
+            params = list(self.acc.policy.parameters()) + list(self.off.policy.parameters())
+            self._allreduce(params)
+            for p in params:
+                p.grad.clamp_(-self.hp.grad_clip, self.hp.grad_clip)
         for grp in (self.acc, self.off):
             grp.opt.step()
         self.last_losses = grads

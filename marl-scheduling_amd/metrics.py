@@ -107,3 +107,18 @@ def args_dict(episodes: list, cfg: abi.MsConfig, params: dict | None = None, rep
     d["meanJob"] = statistics.mean([Fraction(cfg.job_priority[i], cfg.job_length[i]) for i in range(K)])
     d["params"] = dict(params or {})
     return d
+
+
+def save_args_dict(d: dict, file_name: str = "data{}.pkl", directory: str = ".") -> str:
+    """Pickle an argsDict the way trainPPO.py:245-251 does: the first ``file_name.format(i)``
+    (i = 0, 1, ...) that does not exist yet, so the reference's Plot.py reads it. Returns the path."""
+    import os
+    import pickle
+
+    i = 0
+    while os.path.isfile(os.path.join(directory, file_name.format(i))):
+        i += 1
+    path = os.path.join(directory, file_name.format(i))
+    with open(path, "wb") as f:
+        pickle.dump(d, f)
+    return path

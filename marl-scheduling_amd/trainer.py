@@ -484,14 +484,22 @@ class Trainer:
             col += n
         if self.update_graph is None:
             losses = self._fused_update(views, self._sel_counts)  # this iteration's update
+            eager_last = {u.name: u.group.last_losses for u in self.units()}
             torch.cuda.synchronize(self.device)
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g):
                 self._graph_losses = self._fused_update(views, self._sel_counts)
+            self._graph_last = {u.name: list(u.group.last_losses) for u in self.units()}
+            for u in self.units():  # the eager run's own losses until the first replay
+                u.group.last_losses = eager_last[u.name]
             self.update_graph = g
             return losses
         self.update_graph.replay()
-        return self._graph_losses
+        # the graph's loss tensors are overwritten by every replay: hand out copies (G floats per
+        # unit type), so losses a caller keeps from earlier iterations stay what they were
+        for u in self.units():
+            u.group.last_losses = [x.clone() for x in self._graph_last[u.name]]
+        return {k: v.clone() for k, v in self._graph_losses.items()}
 
     def _fused_update(self, all_sel, counts):
         """The fused update: all_sel[name] = int32 device [sum of draws' G] sub-units, counts[name]
@@ -639,6 +647,11 @@ class Trainer:
         p.setdefault("UPDATE_STEP", self.T)
         p.setdefault("n_envs", self.E * self.world_size)
         return mx.args_dict(self.episode_log, self.cfg, p, replica=replica)
+
+    def save_args_dict(self, directory: str = ".", file_name: str = "data{}.pkl", replica="mean", params=None):
+        """args_dict() pickled as the first free data{i}.pkl in directory (trainPPO.py:245-251)."""
+        from . import metrics as mx
+        return mx.save_args_dict(self.args_dict(replica, params), file_name, directory)
 
     @property
     def timings(self):

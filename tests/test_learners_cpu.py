@@ -130,3 +130,13 @@ def test_episode_values_from_accumulators():
     args = mx.args_dict([v], cfg, params=dict(episodeLength=10))
     assert args["acceptorRew"][0] == pytest.approx(0.5) and args["prices"][0] == [None, 7.0]
     assert float(args["meanJob"]) == pytest.approx((0.5 + 10 / 3) / 2)
+
+
+def test_save_args_dict_picks_first_free_index(tmp_path):
+    """trainPPO.py:245-251: data{i}.pkl with the first i whose file does not exist."""
+    import pickle
+    mx = _mod("metrics")
+    paths = [mx.save_args_dict({"acceptorRew": [i]}, directory=str(tmp_path)) for i in range(3)]
+    assert [p.rsplit("/", 1)[1] for p in paths] == ["data0.pkl", "data1.pkl", "data2.pkl"]
+    with open(paths[2], "rb") as f:  # written by this test
+        assert pickle.load(f) == {"acceptorRew": [2]}

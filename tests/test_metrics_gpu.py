@@ -2,6 +2,7 @@
 into trainPPO.py's per-episode values (marl-scheduling_amd/metrics.py) against the driver's own
 code restated on the object-faithful world (oracle/metrics_ref.py), same seeds and actions."""
 import importlib
+import os
 
 import numpy as np
 import pytest
@@ -95,3 +96,22 @@ def test_trainer_collects_args_dict(ms):
     d = t.args_dict()
     assert len(d["acceptorRew"]) == 4 and len(d["prices"][0]) == 6
     assert all(isinstance(v, float) for v in d["acceptionAmount"])
+
+
+def test_trainer_pickles_args_dict_like_trainppo(ms, tmp_path):
+    """save_args_dict writes the first free data{i}.pkl (trainPPO.py:245-251) with the argsDict keys
+    Plot.py reads."""
+    import pickle
+    tr_mod = importlib.import_module("marl-scheduling_amd.trainer")
+    t = tr_mod.Trainer.from_named("cfg3", n_envs=32, update_step=20, seed=2, device="cuda:0", metrics=True,
+                                  episode_length=10)
+    t.iteration()
+    (tmp_path / "data0.pkl").write_bytes(b"taken")
+    p = t.save_args_dict(str(tmp_path))
+    assert os.path.basename(p) == "data1.pkl"
+    with open(p, "rb") as f:  # our own file, written just above
+        d = pickle.load(f)
+    assert set(d) >= {"plotPath", "acceptorRew", "coreChooserRew", "priceChooserRew", "prices", "auctioneerRew",
+                      "dwellTimes", "meanJob", "agentRew", "acceptionQuality", "acceptionAmount",
+                      "terminationRevenues", "tradeRevenues", "params"}
+    assert len(d["acceptorRew"]) == 2 and d["params"]["episodeLength"] == 10

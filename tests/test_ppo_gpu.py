@@ -607,12 +607,20 @@ def test_trainer_graph_replay_matches_eager(ms):
     tr_mod = importlib.import_module("marl-scheduling_amd.trainer")
     trs = [tr_mod.Trainer.from_named("cfg3", n_envs=48, update_step=16, seed=9, device="cuda:0", use_graph=g)
            for g in (True, False)]
-    for _ in range(3):
-        outs = [t.iteration() for t in trs]
-    for k in outs[0]:
-        assert torch.equal(outs[0][k], outs[1][k]), k
+    kept = ([], [])  # every iteration's losses as a caller keeps them (no aliasing)
+    last = ([], [])
+    for _ in range(4):
+        for i, t in enumerate(trs):
+            kept[i].append(t.iteration())
+            last[i].append({u.name: u.group.last_losses for u in t.units()})
+    for it in range(4):  # earlier graphed iterations' losses were not overwritten by later replays
+        for k in kept[0][it]:
+            assert torch.equal(kept[0][it][k], kept[1][it][k]), (it, k)
+            for a, b in zip(last[0][it][k], last[1][it][k]):
+                assert torch.equal(a, b), (it, k)
+    assert not torch.equal(kept[0][1]["acceptor"], kept[0][3]["acceptor"])
     assert torch.equal(trs[0].acceptor_rows(), trs[1].acceptor_rows())
-    assert trs[0].env.round == trs[1].env.round == 48
+    assert trs[0].env.round == trs[1].env.round == 64
 
 
 def test_trainer_two_stream_rollout(ms):
