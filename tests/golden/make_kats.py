@@ -328,9 +328,215 @@ def kat_settlement_double_product():
         ])
 
 
+def kat_net_zero_offer_reward():
+    """Reward.py:22-35 (commercial free prices): the priceChooser reward of an accepted offer whose
+    price equals the job's priority is env.netZeroOfferReward (0.5, SchedulingEnvironment.py's
+    default) instead of prio1 - price = 0; the coreChooser reward is prio1. The auctioneer (explicit
+    action: position 0 of core 1) takes agent 1's offer (price 6 = prio 6); the job goes onto core 1
+    (world.py:261-293) and ticks 6 -> 5 (world.py:336-367). Agent 1 (owns core 1, no free slot
+    left after... its slot was freed, 1 + 1 > 1) does not spawn; agent 2 (0 + 1 <= 1) draws one
+    random() for its job (one kind: any u)."""
+    N, C, L = 2, 2, 1
+    st = empty_state(N, C, L, 5)
+    st["slot_kind"] = [[0], [-1]]
+    st["slot_rem"] = [[6], [-1]]
+    st["slot_birth"] = [[4], [-1]]
+    st["slot_wait"] = [[1], [0]]
+    st["offer_core"] = [[0], [-1]]
+    st["offer_recip"] = [[0], [0]]
+    st["offer_price"] = [[6], [0]]
+    words, idx = mt_state(2024)
+    r = rng_at(words, idx)
+    r.random()
+    return dict(
+        name="net_zero_offer_reward", cites=["Reward.py:22-35", "world.py:261-293", "world.py:369-376"],
+        config=dict(n_agents=N, n_cores=C, collection_length=L, priorities=[6], lengths=[6], probabilities=[1.0],
+                    free_prices=True, commercial=True),
+        state=st, mt_words=words, mt_index=idx,
+        steps=[
+            dict(acc=[[2, 2], [2, 2]], off=[[2], [2]], price=[[0], [0]], auct=[0, 2],
+                 expect=dict(state=dict(round=6, core_owner=[1, 0], core_kind=[0, -1], core_rem=[5, -1],
+                                        core_birth=[4, -1], slot_kind=[[-1], [0]], slot_rem=[[-1], [6]],
+                                        slot_birth=[[-1], [5]], slot_wait=[[0], [0]], offer_core=[[-1], [-1]],
+                                        liab=[[[1, 0, 6, 6, 5]], []]),
+                             rewards=dict(offer=[[6], [0]], price=[[0.5], [0]], acceptor=[[0, 0], [0, 0]],
+                                          auctioneer=[0, 0], agent=[0, 0]),
+                             mt_index=r.getstate()[1][624])),
+        ])
+
+
+def kat_noncommercial_price_reward():
+    """Reward.py:36-49 (non-commercial free prices): priceChooser reward = prio1 if prio1 - price >= 0,
+    else prio1 - price (negative). Agent 1 offered its prio-6 job to core 1 at price 8 (-> 6 - 8 =
+    -2), agent 2 its prio-8 job to core 2 at price 3 (-> 8). The auctioneer takes both (explicit
+    actions, position 0 of each core); both agents then own a core and have no free slot: no spawn,
+    no draw."""
+    N, C, L = 2, 2, 1
+    st = empty_state(N, C, L, 7)
+    st["slot_kind"] = [[0], [1]]
+    st["slot_rem"] = [[6], [6]]
+    st["slot_birth"] = [[6], [5]]
+    st["slot_wait"] = [[1], [1]]
+    st["offer_core"] = [[0], [1]]
+    st["offer_recip"] = [[0], [0]]
+    st["offer_price"] = [[8], [3]]
+    words, idx = mt_state(77)
+    return dict(
+        name="noncommercial_price_reward", cites=["Reward.py:36-49", "world.py:261-293"],
+        config=dict(n_agents=N, n_cores=C, collection_length=L, priorities=[6, 8], lengths=[6, 6],
+                    probabilities=[0.5, 0.5], free_prices=True, commercial=False),
+        state=st, mt_words=words, mt_index=idx,
+        steps=[
+            dict(acc=[[2, 2], [2, 2]], off=[[2], [2]], price=[[0], [0]], auct=[0, 0],
+                 expect=dict(state=dict(round=8, core_owner=[1, 2], core_kind=[0, 1], core_rem=[5, 5],
+                                        core_birth=[6, 5], slot_kind=[[-1], [-1]], offer_core=[[-1], [-1]],
+                                        liab=[[[1, 0, 8, 6, 7]], [[2, 0, 3, 6, 7]]]),
+                             rewards=dict(offer=[[6], [8]], price=[[-2], [8]], acceptor=[[0, 0], [0, 0]],
+                                          auctioneer=[0, 0], agent=[0, 0]),
+                             mt_index=idx)),
+        ])
+
+
+def kat_two_jobs_first_empty():
+    """world.py:369-376 + Agent.py:50-70 with newJobsPerRoundPerAgent = 2: agent 1 (no core, slots
+    [A, -, B, -]: 0 + 2 <= 2 free) draws two random() in a row; the kind of each is the first i with
+    u < accProbabilities[i] ([0.5, 1.0]) and it goes into the first empty slot (world.py:123-133):
+    slot 1, then slot 3. Agent 2 (slots [C, D, E, -]: 0 + 2 > 1 free) spawns nothing. No offers:
+    action 1 maps to coreID 2, which does not exist (world.py:412-413)."""
+    N, C, L = 2, 1, 4
+    st = empty_state(N, C, L, 30)
+    st["slot_kind"] = [[0, -1, 1, -1], [1, 0, 1, -1]]
+    st["slot_rem"] = [[4, -1, 2, -1], [2, 4, 1, -1]]
+    st["slot_birth"] = [[28, -1, 29, -1], [27, 26, 29, -1]]
+    words, idx = mt_state(31337)
+    r = rng_at(words, idx)
+    u1, u2 = r.random(), r.random()
+    k1, k2 = (0 if u1 < 0.5 else 1), (0 if u2 < 0.5 else 1)
+    lens = [4, 2]
+    return dict(
+        name="two_jobs_first_empty", cites=["world.py:369-376", "Agent.py:50-70", "world.py:123-133"],
+        config=dict(n_agents=N, n_cores=C, collection_length=L, priorities=[4, 8], lengths=lens, fix_prices=[2, 4],
+                    probabilities=[0.5, 0.5], new_jobs=2),
+        state=st, mt_words=words, mt_index=idx, note="u1 = %r -> kind %d, u2 = %r -> kind %d" % (u1, k1, u2, k2),
+        steps=[
+            dict(acc=[[8], [8]], off=[[1] * 4, [1] * 4], price=None, auct=[8],
+                 expect=dict(state=dict(round=31, slot_kind=[[0, k1, 1, k2], [1, 0, 1, -1]],
+                                        slot_rem=[[4, lens[k1], 2, lens[k2]], [2, 4, 1, -1]],
+                                        slot_birth=[[28, 30, 29, 30], [27, 26, 29, -1]],
+                                        slot_wait=[[0] * 4, [0] * 4], offer_core=[[-1] * 4, [-1] * 4]),
+                             mt_index=r.getstate()[1][624])),
+        ])
+
+
+def kat_hardcoded_agent_ties():
+    """HardcodedModules.py:16-45 (acceptor) and :81-109 (offerer) acting inside the round (the
+    HardcodedFixPriceEnvironment loop, SchedulingEnvironment.py:439-456), their random.sample draws
+    in getActions order (per agent: offer slots, then acceptor cores), then the auctioneer's (none:
+    it owns no core), then spawn. Both cores hold (prio 4, rem 4): every offerer sees core ratios
+    [1, 1], a tie -> cands[_randbelow(2)] per slot (empty slots draw too). Agent 1's acceptor of
+    core 1 (own ratio 1) sees agent 2's two offers (4, 2), (4, 2): ratios [2, 2, -1, -1], a tie ->
+    _randbelow(2) picks which one it takes. Agent 2's acceptor of core 2 (own ratio 1) sees agent
+    1's offer (4, 1): ratio 4 > 1, one candidate (_randbelow(1)). Executions in agent order: agent 2's
+    picked job (prio 8, rem 2) onto core 1 (owner 2), the old core-1 job to agent 1's first empty
+    slot (slot 1); agent 1's (prio 8, rem 1) onto core 2 (owner 1), the old core-2 job to agent 2's
+    first empty slot (the picked one's). Tick: core 1 -> rem 1; core 2 ends (TS 51): acc[1][2] = 8,
+    agent[1] += 8; chain (1 -> 2, price 4, necT 1, round 50): T = 1, traded = 4 -> acc[1][2] = 4,
+    agent[1] = 4, acc[2][2] = agent[2] = 4. Offers then follow the slot draws (core index ->
+    recipient = that core's owner after the tick: core 1 -> 2, core 2 -> auctioneer); agent 1 (no
+    core, 1 free slot) spawns one job into slot 0."""
+    N, C, L = 2, 2, 2
+    st = empty_state(N, C, L, 50)
+    st.update(core_owner=[1, 2], core_kind=[0, 0], core_rem=[4, 4], core_birth=[45, 46])
+    st["slot_kind"] = [[1, -1], [1, 1]]
+    st["slot_rem"] = [[1, -1], [2, 2]]
+    st["slot_birth"] = [[49, -1], [47, 48]]
+    st["slot_wait"] = [[1, 0], [1, 1]]
+    st["offer_core"] = [[1, -1], [0, 0]]
+    st["offer_recip"] = [[2, 0], [1, 1]]
+    st["offer_price"] = [[4, 0], [4, 4]]
+    words, idx = mt_state(9001)
+    r = rng_at(words, idx)
+    a1s = [r._randbelow(2), r._randbelow(2)]   # agent 1's offerers (slots 0, 1)
+    p = r._randbelow(2)                         # agent 1's acceptor of core 1: which of agent 2's offers
+    a2s = [r._randbelow(2), r._randbelow(2)]   # agent 2's offerers
+    assert r._randbelow(1) == 0                 # agent 2's acceptor of core 2: one candidate
+    u = r.random()                              # agent 1's spawn
+    kind = 0 if u < 0.5 else 1
+    owner_after = [2, 0]                        # core owners after the tick
+    # agent 1: slot 0 = spawned job; slot 1 = old core-1 job (kind 0, rem 4, birth 45), offered per a1s[1]
+    # agent 2: slot p = old core-2 job (kind 0, rem 4, birth 46), offered per a2s[p]; slot 1-p = the
+    # unaccepted offer's job (wait -> else branch: no offer, wait False)
+    a2_kind, a2_rem, a2_birth = [0, 0], [0, 0], [0, 0]
+    a2_kind[p], a2_rem[p], a2_birth[p] = 0, 4, 46
+    a2_kind[1 - p], a2_rem[1 - p], a2_birth[1 - p] = 1, 2, [47, 48][1 - p]
+    a2_off, a2_rcp, a2_pr, a2_wait = [-1, -1], [0, 0], [0, 0], [0, 0]
+    a2_off[p], a2_rcp[p], a2_pr[p], a2_wait[p] = a2s[p], owner_after[a2s[p]], 2, 1
+    return dict(
+        name="hardcoded_agent_ties", cites=["HardcodedModules.py:5-45", "HardcodedModules.py:81-109",
+                                            "SchedulingEnvironment.py:439-456", "world.py:261-293",
+                                            "world.py:336-367", "Reward.py:146-212", "world.py:406-443"],
+        device_only="the C oracle takes actions from the caller; the in-kernel hard-coded agents are "
+                    "checked here and in tests/test_hardcoded_gpu.py against oracle/pyref.py",
+        config=dict(n_agents=N, n_cores=C, collection_length=L, priorities=[4, 8], lengths=[4, 2], fix_prices=[2, 4],
+                    probabilities=[0.5, 0.5]),
+        state=st, mt_words=words, mt_index=idx,
+        note="offerer draws agent 1 %s, agent 2 %s; acceptor tie -> offer position %d; spawn u = %r -> kind %d"
+             % (a1s, a2s, p, u, kind),
+        steps=[
+            dict(acc=None, off=None, price=None, auct=None,
+                 expect=dict(state=dict(round=51, core_owner=[2, 0], core_kind=[1, -1], core_rem=[1, -1],
+                                        core_birth=[[47, 48][p], -1],
+                                        slot_kind=[[kind, 0], a2_kind], slot_rem=[[[4, 2][kind], 4], a2_rem],
+                                        slot_birth=[[50, 45], a2_birth], slot_wait=[[0, 1], a2_wait],
+                                        offer_core=[[-1, a1s[1]], a2_off],
+                                        offer_recip=[[0, owner_after[a1s[1]]], a2_rcp],
+                                        offer_price=[[0, 2], a2_pr],
+                                        liab=[[[2, 1, 4, 2, 50]], []]),
+                             rewards=dict(offer=[[8, 0], [8 if p == 0 else 0, 8 if p == 1 else 0]],
+                                          acceptor=[[0, 4], [0, 4]], auctioneer=[0, 0], agent=[4, 4]),
+                             mt_index=r.getstate()[1][624])),
+        ])
+
+
+def kat_liability_overflow():
+    """The liability chain (world.py:238, 287: an unbounded deque in the reference) is held in
+    liability_cap entries per core here. A third accepted offer on a core whose chain already holds
+    liability_cap = 2 entries is dropped and sets MS_FLAG_LIABILITY_OVERFLOW (0x01, DESIGN.md §2);
+    the flag is fatal: the next ms_env_step returns MS_EOVERFLOW (75) without launching. The
+    execution itself follows world.py:261-293 (agent 2's job onto core 1, the old job to agent 1's
+    first empty slot) and the offer reward Reward.py:164-170."""
+    N, C, L = 2, 1, 1
+    st = empty_state(N, C, L, 13)
+    st.update(core_owner=[1], core_kind=[0], core_rem=[5], core_birth=[10])
+    st["slot_kind"] = [[-1], [0]]
+    st["slot_rem"] = [[-1], [6]]
+    st["slot_birth"] = [[-1], [12]]
+    st["slot_wait"] = [[0], [1]]
+    st["offer_core"] = [[-1], [0]]
+    st["offer_recip"] = [[0], [1]]
+    st["offer_price"] = [[0], [2]]
+    st["liab"] = [[[1, 2, 2, 6, 12], [2, 0, 2, 6, 11]]]
+    words, idx = mt_state(5)
+    return dict(
+        name="liability_overflow", cites=["world.py:238", "world.py:261-293", "Reward.py:164-170"],
+        config=dict(n_agents=N, n_cores=C, collection_length=L, liability_cap=2, **README_JOBS),
+        state=st, mt_words=words, mt_index=idx,
+        steps=[
+            dict(acc=[[0], [2]], off=[[1], [1]], price=None, auct=[2],
+                 expect=dict(state=dict(round=14, core_owner=[2], core_kind=[0], core_rem=[5], core_birth=[12],
+                                        slot_kind=[[0], [-1]], slot_rem=[[5], [-1]], slot_birth=[[10], [-1]],
+                                        liab=[[[1, 2, 2, 6, 12], [2, 0, 2, 6, 11]]]),
+                             rewards=dict(offer=[[0], [3]], acceptor=[[0], [0]], auctioneer=[0], agent=[0, 0]),
+                             flags_set=0x01, mt_index=idx)),
+            dict(acc=[[1], [1]], off=[[1], [1]], price=None, auct=[1], expect=dict(error=75)),
+        ])
+
+
 def main():
     kats = [kat_wait_alternation(), kat_free_price_action0(), kat_auctioneer_ties(), kat_spawn_edge(),
-            kat_self_offer_first_empty(), kat_mixed_chain(), kat_settlement_double_product()]
+            kat_self_offer_first_empty(), kat_mixed_chain(), kat_settlement_double_product(),
+            kat_net_zero_offer_reward(), kat_noncommercial_price_reward(), kat_two_jobs_first_empty(),
+            kat_hardcoded_agent_ties(), kat_liability_overflow()]
     with open(os.path.join(HERE, "kats.json"), "w") as f:
         json.dump(kats, f)
     print("wrote %d scenarios" % len(kats))
