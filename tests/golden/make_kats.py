@@ -434,7 +434,7 @@ def kat_hardcoded_agent_ties():
     in getActions order (per agent: offer slots, then acceptor cores), then the auctioneer's (none:
     it owns no core), then spawn. Both cores hold (prio 4, rem 4): every offerer sees core ratios
     [1, 1], a tie -> cands[_randbelow(2)] per slot (empty slots draw too). Agent 1's acceptor of
-    core 1 (own ratio 1) sees agent 2's two offers (4, 2), (4, 2): ratios [2, 2, -1, -1], a tie ->
+    core 1 (own ratio 1) sees agent 2's two offers (4, 2), (4, 2): ratios [2, 2, -1, ...], a tie ->
     _randbelow(2) picks which one it takes. Agent 2's acceptor of core 2 (own ratio 1) sees agent
     1's offer (4, 1): ratio 4 > 1, one candidate (_randbelow(1)). Executions in agent order: agent 2's
     picked job (prio 8, rem 2) onto core 1 (owner 2), the old core-1 job to agent 1's first empty
@@ -443,33 +443,33 @@ def kat_hardcoded_agent_ties():
     agent[1] += 8; chain (1 -> 2, price 4, necT 1, round 50): T = 1, traded = 4 -> acc[1][2] = 4,
     agent[1] = 4, acc[2][2] = agent[2] = 4. Offers then follow the slot draws (core index ->
     recipient = that core's owner after the tick: core 1 -> 2, core 2 -> auctioneer); agent 1 (no
-    core, 1 free slot) spawns one job into slot 0."""
-    N, C, L = 2, 2, 2
+    core, 2 free slots) spawns one job into slot 0; agent 2 (1 core, 1 free slot) does not."""
+    N, C, L = 2, 2, 3
     st = empty_state(N, C, L, 50)
     st.update(core_owner=[1, 2], core_kind=[0, 0], core_rem=[4, 4], core_birth=[45, 46])
-    st["slot_kind"] = [[1, -1], [1, 1]]
-    st["slot_rem"] = [[1, -1], [2, 2]]
-    st["slot_birth"] = [[49, -1], [47, 48]]
-    st["slot_wait"] = [[1, 0], [1, 1]]
-    st["offer_core"] = [[1, -1], [0, 0]]
-    st["offer_recip"] = [[2, 0], [1, 1]]
-    st["offer_price"] = [[4, 0], [4, 4]]
+    st["slot_kind"] = [[1, -1, -1], [1, 1, -1]]
+    st["slot_rem"] = [[1, -1, -1], [2, 2, -1]]
+    st["slot_birth"] = [[49, -1, -1], [47, 48, -1]]
+    st["slot_wait"] = [[1, 0, 0], [1, 1, 0]]
+    st["offer_core"] = [[1, -1, -1], [0, 0, -1]]
+    st["offer_recip"] = [[2, 0, 0], [1, 1, 0]]
+    st["offer_price"] = [[4, 0, 0], [4, 4, 0]]
     words, idx = mt_state(9001)
     r = rng_at(words, idx)
-    a1s = [r._randbelow(2), r._randbelow(2)]   # agent 1's offerers (slots 0, 1)
+    a1s = [r._randbelow(2) for _ in range(L)]   # agent 1's offerers (slots 0, 1, 2)
     p = r._randbelow(2)                         # agent 1's acceptor of core 1: which of agent 2's offers
-    a2s = [r._randbelow(2), r._randbelow(2)]   # agent 2's offerers
+    a2s = [r._randbelow(2) for _ in range(L)]   # agent 2's offerers
     assert r._randbelow(1) == 0                 # agent 2's acceptor of core 2: one candidate
     u = r.random()                              # agent 1's spawn
     kind = 0 if u < 0.5 else 1
     owner_after = [2, 0]                        # core owners after the tick
     # agent 1: slot 0 = spawned job; slot 1 = old core-1 job (kind 0, rem 4, birth 45), offered per a1s[1]
     # agent 2: slot p = old core-2 job (kind 0, rem 4, birth 46), offered per a2s[p]; slot 1-p = the
-    # unaccepted offer's job (wait -> else branch: no offer, wait False)
-    a2_kind, a2_rem, a2_birth = [0, 0], [0, 0], [0, 0]
+    # unaccepted offer's job (wait -> else branch: no offer, wait False); slot 2 empty
+    a2_kind, a2_rem, a2_birth = [0, 0, -1], [0, 0, -1], [0, 0, -1]
     a2_kind[p], a2_rem[p], a2_birth[p] = 0, 4, 46
     a2_kind[1 - p], a2_rem[1 - p], a2_birth[1 - p] = 1, 2, [47, 48][1 - p]
-    a2_off, a2_rcp, a2_pr, a2_wait = [-1, -1], [0, 0], [0, 0], [0, 0]
+    a2_off, a2_rcp, a2_pr, a2_wait = [-1, -1, -1], [0, 0, 0], [0, 0, 0], [0, 0, 0]
     a2_off[p], a2_rcp[p], a2_pr[p], a2_wait[p] = a2s[p], owner_after[a2s[p]], 2, 1
     return dict(
         name="hardcoded_agent_ties", cites=["HardcodedModules.py:5-45", "HardcodedModules.py:81-109",
@@ -486,13 +486,13 @@ def kat_hardcoded_agent_ties():
             dict(acc=None, off=None, price=None, auct=None,
                  expect=dict(state=dict(round=51, core_owner=[2, 0], core_kind=[1, -1], core_rem=[1, -1],
                                         core_birth=[[47, 48][p], -1],
-                                        slot_kind=[[kind, 0], a2_kind], slot_rem=[[[4, 2][kind], 4], a2_rem],
-                                        slot_birth=[[50, 45], a2_birth], slot_wait=[[0, 1], a2_wait],
-                                        offer_core=[[-1, a1s[1]], a2_off],
-                                        offer_recip=[[0, owner_after[a1s[1]]], a2_rcp],
-                                        offer_price=[[0, 2], a2_pr],
+                                        slot_kind=[[kind, 0, -1], a2_kind], slot_rem=[[[4, 2][kind], 4, -1], a2_rem],
+                                        slot_birth=[[50, 45, -1], a2_birth], slot_wait=[[0, 1, 0], a2_wait],
+                                        offer_core=[[-1, a1s[1], -1], a2_off],
+                                        offer_recip=[[0, owner_after[a1s[1]], 0], a2_rcp],
+                                        offer_price=[[0, 2, 0], a2_pr],
                                         liab=[[[2, 1, 4, 2, 50]], []]),
-                             rewards=dict(offer=[[8, 0], [8 if p == 0 else 0, 8 if p == 1 else 0]],
+                             rewards=dict(offer=[[8, 0, 0], [8 if p == 0 else 0, 8 if p == 1 else 0, 0]],
                                           acceptor=[[0, 4], [0, 4]], auctioneer=[0, 0], agent=[4, 4]),
                              mt_index=r.getstate()[1][624])),
         ])

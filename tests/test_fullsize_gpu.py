@@ -104,8 +104,13 @@ def test_cfg3_fullsize_iteration_losses_match_refppo(ms):
     refs = {u.name: {a: _ref_from_group(u.group, a, u.D, u.group.policy.A, tr.hp) for a in agents}
             for u in tr.units()}
     draws = _local_draws(tr.rng.getstate(), tr.N, tr.C, tr.L, tr.hp.centralisation_sample)
+    # the update ends by carrying ring slot T into slot 0 (the next iteration's first observation):
+    # keep slot 0 as the update saw it for the reference rows
+    slot0 = [x[0].clone() for x in (tr.acc_rows, tr.acc_owner, tr.off_obs)]
     losses = tr.update()
     torch.cuda.synchronize()
+    for x, s0 in zip((tr.acc_rows, tr.acc_owner, tr.off_obs), slot0):
+        x[0].copy_(s0)
     for u in tr.units():
         got = losses[u.name].cpu().numpy()            # [steps = draws x K, G]
         K = u.group.K
