@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define MS_ABI_VERSION 10
+#define MS_ABI_VERSION 11
 
 #define MS_MAX_KINDS 16
 #define MS_MAX_AGENTS 64
@@ -522,6 +522,48 @@ typedef struct ms_qnet_grads { /* device outputs [G][...] like the weights */
 size_t ms_dqn_workspace_bytes(const ms_qnet_params* q, int64_t rows_per_group);
 int ms_dqn_grad(const ms_qnet_params* policy, const ms_qnet_params* target, const ms_dqn_batch* batch, float grad_clip,
                 void* workspace, size_t workspace_bytes, const ms_qnet_grads* grads, void* stream);
+
+/* ---- Branching DQN acting (BranchingDQNModules.py:75-123), BASELINE cfg5 ----
+ * One BranchingQNetwork (Linear(obs,128)-ReLU-Linear(128,128)-ReLU, value head, ac_dim advantage
+ * heads of n actions) with its heads stacked: head b = rows b*n .. b*n+n-1 of wa / ba. */
+typedef struct ms_bdqn_params {
+    const float *w1, *b1;   /* [128][obs], [128] */
+    const float *w2, *b2;   /* [128][128], [128] */
+    const float *wv, *bv;   /* [1][128], [1] */
+    const float *wa, *ba;   /* [ac_dim*n][128], [ac_dim*n] */
+    int32_t obs, ac_dim, n; /* n <= 128, ac_dim <= 127 */
+} ms_bdqn_params;
+
+/* Bytes of the prepared layer 1 (three exact bf16 terms of W1 over `segs` input segments of `seg`
+ * values, each padded to a multiple of 32). */
+size_t ms_bdqn_workspace_bytes(int32_t seg, int32_t segs);
+
+/* Prepares W1 for ms_bdqn_layer1_compact / ms_bdqn_act (once per weight change; seg * segs must be
+ * obs). With base != NULL also writes base[128] = b1 + sum_c W1_c F, F the foreign acceptor row of
+ * seg = D_acc values [0, -1, -1, (-2, -2) * O] (Agent.py:167-212). */
+int ms_bdqn_prepare(const ms_bdqn_params* q, int32_t seg, int32_t segs, void* workspace, size_t workspace_bytes,
+                    float* base, void* stream);
+
+/* Scratch bytes of ms_bdqn_layer1_compact (n_envs * n_cores * 128 floats). */
+size_t ms_bdqn_layer1_scratch_bytes(int64_t n_envs, int32_t n_cores);
+
+/* Layer-1 pre-activations of every agent's aggregated acceptor row (Agent.py:82-124: its C acceptor
+ * rows in core order, row c = core_rows[e][c] if core_owner[e][c] == a + 1 else F) from the compact
+ * observations: h1 [n_envs * n_agents][128], row e * n_agents + a. workspace / base from
+ * ms_bdqn_prepare(seg = acc_dim, segs = n_cores); scratch of ms_bdqn_layer1_scratch_bytes.
+ * Deterministic. */
+int ms_bdqn_layer1_compact(const ms_bdqn_params* q, const void* workspace, const float* base, const int8_t* core_rows,
+                           const int8_t* core_owner, int64_t n_envs, int32_t n_agents, int32_t n_cores,
+                           int32_t acc_dim, int32_t acc_stride, void* scratch, size_t scratch_bytes, float* h1,
+                           void* stream);
+
+/* get_action (BranchingDQNModules.py:117-123), epsilon-greedy per row (:181-186): a row with
+ * explore[r] != 0 takes rand_action[r][*]; the others take, per branch, the first maximum of
+ * q = (value + adv) - mean(adv) (:98). Layer 1 from h1 [n_rows][128] (pre-activations), or with
+ * h1 == NULL from int8 rows x [n_rows][x_stride] and workspace = ms_bdqn_prepare(seg = obs,
+ * segs = 1). explore may be NULL (all greedy). action: [n_rows][ac_dim] int8. */
+int ms_bdqn_act(const ms_bdqn_params* q, const float* h1, const int8_t* x, int32_t x_stride, const void* workspace,
+                int64_t n_rows, const uint8_t* explore, const int8_t* rand_action, int8_t* action, void* stream);
 
 const char* ms_last_error(void);
 int ms_abi_version(void);

@@ -82,12 +82,18 @@ def _load():
         "ms_dqn_grad": (ct.c_int, [ct.POINTER(abi.MsQnetParams), ct.POINTER(abi.MsQnetParams),
                                    ct.POINTER(abi.MsDqnBatch), ct.c_float, P, ct.c_size_t,
                                    ct.POINTER(abi.MsQnetGrads), P]),
+        "ms_bdqn_workspace_bytes": (ct.c_size_t, [i32, i32]),
+        "ms_bdqn_prepare": (ct.c_int, [ct.POINTER(abi.MsBdqnParams), i32, i32, P, ct.c_size_t, P, P]),
+        "ms_bdqn_layer1_scratch_bytes": (ct.c_size_t, [i64, i32]),
+        "ms_bdqn_layer1_compact": (ct.c_int, [ct.POINTER(abi.MsBdqnParams), P, P, P, P, i64, i32, i32, i32, i32, P,
+                                              ct.c_size_t, P, P]),
+        "ms_bdqn_act": (ct.c_int, [ct.POINTER(abi.MsBdqnParams), P, P, i32, P, i64, P, P, P, P]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)
         fn.restype = res
         fn.argtypes = args
-    if L.ms_abi_version() != 10:
+    if L.ms_abi_version() != 11:
         raise ImportError("libmarlsched.so ABI version mismatch")
     return L
 
@@ -103,7 +109,8 @@ EXPORTED = (
     "ms_act_round_free", "ms_price_table_build", "ms_offer_act_free", "ms_discounted_returns", "ms_unit_returns",
     "ms_ppo_workspace_bytes", "ms_ppo_grad", "ms_adam_step", "ms_adam_step_dev",
     "ms_aggregate_obs", "ms_decode_aggregated", "ms_dqn_act", "ms_dqn_workspace_bytes", "ms_dqn_grad",
-    "ms_regen_agent_rows",
+    "ms_regen_agent_rows", "ms_bdqn_workspace_bytes", "ms_bdqn_prepare", "ms_bdqn_layer1_scratch_bytes", "ms_bdqn_layer1_compact",
+    "ms_bdqn_act",
 )
 
 

@@ -201,6 +201,13 @@ class MsQnetParams(ct.Structure):
                 ("in_dim", ct.c_int32), ("hidden", ct.c_int32), ("n_actions", ct.c_int32), ("n_groups", ct.c_int32)]
 
 
+class MsBdqnParams(ct.Structure):
+    """ms_bdqn_params: one BranchingQNetwork, advantage heads stacked."""
+    _fields_ = [("w1", ct.c_void_p), ("b1", ct.c_void_p), ("w2", ct.c_void_p), ("b2", ct.c_void_p),
+                ("wv", ct.c_void_p), ("bv", ct.c_void_p), ("wa", ct.c_void_p), ("ba", ct.c_void_p),
+                ("obs", ct.c_int32), ("ac_dim", ct.c_int32), ("n", ct.c_int32)]
+
+
 class MsDqnBatch(ct.Structure):
     _fields_ = [("states", ct.c_void_p), ("next_states", ct.c_void_p), ("actions", ct.c_void_p),
                 ("rewards", ct.c_void_p), ("samples", ct.c_void_p), ("stride", ct.c_int32), ("n_units", ct.c_int32),

@@ -26,12 +26,17 @@ regenerated from them: for the minibatch by ``ms_regen_agent_rows``; for acting,
 agents of all replicas need layer 1, by its algebra. An agent's row is the owner row R_c where it
 owns core c and the constant foreign row F elsewhere, so
     W1 x_a + b1 = (b1 + sum_c W1_c F) + sum_{c owned by a} W1_c (R_c - F),
-one [E, D] x [D, 128] GEMM per core (torch.bmm over cores) scattered to the owners: C GEMVs per
-replica instead of N dense [C*D]-wide ones (32x fewer flops at cfg5). The trunk and heads are
-plain library GEMMs (hipBLASLt through torch, fp32 like the reference).
+one [D, 128] product per (replica, core) added to its owner's row: C of them per replica instead
+of N dense [C*D]-wide ones (32x fewer flops at cfg5), on the bf16 MFMA with exact products
+(ms_bdqn_layer1_compact, bdqn_kernels.hip). Acting is one fused HIP kernel per role
+(ms_bdqn_act): trunk, value head, every advantage head, the per-branch q = value + adv - mean and
+its first argmax, and the epsilon-greedy pick, on exact-f32 MFMA products; only the int8 actions
+leave it (the library-GEMM version materialised 3.25 GB of advantages per frame and read them back
+for the argmax). The update (batch 128 per role) runs in torch autograd with the HIP Adam.
 """
 from __future__ import annotations
 
+import ctypes as ct
 import math
 from dataclasses import dataclass
 
@@ -40,6 +45,7 @@ import torch.nn as nn
 import torch.nn.functional as F_
 
 from . import abi
+from ._lib import check, lib, ptr, stream_ptr
 from .ppo import HipAdam
 
 KEYS = ("w1", "b1", "w2", "b2", "wv", "bv", "wa", "ba")
@@ -68,37 +74,68 @@ class BranchingQ(nn.Module):
         advs = F_.linear(out, self.wa, self.ba).view(-1, self.ac_dim, self.n)
         return value.unsqueeze(2) + advs - advs.mean(2, keepdim=True)
 
-    def greedy(self, h1_pre):
-        """get_action's argmax (BranchingDQNModules.py:117-123) without materialising q: value and the
-        advantage mean are constant along a branch, so argmax q = argmax advantage (torch.argmax's
-        first-maximum rule may differ from q's only on exact float ties)."""
-        out = torch.relu(F_.linear(torch.relu(h1_pre), self.w2, self.b2))
-        return torch.argmax(F_.linear(out, self.wa, self.ba).view(-1, self.ac_dim, self.n), dim=2)
-
     def forward(self, x):
         """x [B, obs] float -> q [B, ac_dim, n]."""
         return self.head(F_.linear(x, self.w1, self.b1))
 
-    def layer1_compact(self, core_rows, core_owner, n_agents: int, d_acc: int):
-        """Layer-1 pre-activations of every agent's acceptor row from the compact observations (module doc):
-        core_rows [E, C, stride] int8, core_owner [E, C] int8 -> [E * N, 128] (row e * N + a)."""
-        E, C, _ = core_rows.shape
-        O = (d_acc - 3) // 2
-        foreign = torch.tensor([0.0, -1.0, -1.0] + [-2.0] * (2 * O), device=core_rows.device)
-        w1c = self.w1.view(128, C, d_acc)                                     # W1_c = w1c[:, c, :]
-        base = self.b1 + torch.einsum("jcd,d->j", w1c, foreign)               # b1 + sum_c W1_c F
-        dc = core_rows[:, :, :d_acc].float() - foreign                        # R_c - F  [E, C, D]
-        part = torch.bmm(dc.transpose(0, 1), w1c.permute(1, 2, 0))             # [C, E, 128]
-        h1 = base.expand(E * n_agents, 128).contiguous()
-        own = core_owner.long()                                               # [E, C], 0 = auctioneer
-        mask = own > 0
-        rows = (torch.arange(E, device=own.device).unsqueeze(1) * n_agents + own - 1)[mask]
-        h1 = h1.index_add(0, rows, part.transpose(0, 1)[mask])
-        return h1
+    def hip_params(self) -> abi.MsBdqnParams:
+        """ms_bdqn_params of this net (raw device pointers: the parameters change in place)."""
+        return abi.MsBdqnParams(ptr(self.w1), ptr(self.b1), ptr(self.w2), ptr(self.b2), ptr(self.wv), ptr(self.bv),
+                                ptr(self.wa), ptr(self.ba), self.obs, self.ac_dim, self.n)
 
-    def forward_compact(self, core_rows, core_owner, n_agents: int, d_acc: int):
-        """q [E * N, C, n] of every agent from the compact observations (layer1_compact + head)."""
-        return self.head(self.layer1_compact(core_rows, core_owner, n_agents, d_acc))
+
+class HipActor:
+    """get_action of one role on the HIP kernels (bdqn_kernels.hip): the prepared layer 1 (three exact
+    bf16 terms of W1; with ``compact`` also b1 + sum_c W1_c F) and the fused act kernel."""
+
+    def __init__(self, q: BranchingQ, seg: int, segs: int, device, compact: bool = False):
+        self.q, self.seg, self.segs, self.compact = q, int(seg), int(segs), compact
+        self.nbytes = int(lib.ms_bdqn_workspace_bytes(self.seg, self.segs))
+        self.ws = torch.empty(((self.nbytes + 3) // 4,), dtype=torch.int32, device=device)
+        self.base = torch.empty((128,), dtype=torch.float32, device=device) if compact else None
+
+    def prepare(self, stream=None):
+        """After every weight change (the update steps Adam in place)."""
+        p = self.q.hip_params()
+        check(lib.ms_bdqn_prepare(ct.byref(p), self.seg, self.segs, ptr(self.ws), self.nbytes, ptr(self.base),
+                                  stream_ptr(stream)))
+
+    def layer1_compact(self, core_rows, core_owner, n_agents: int, out=None, stream=None):
+        """h1 [E * N, 128] of every agent's aggregated acceptor row (ms_bdqn_layer1_compact)."""
+        E, C, stride = core_rows.shape
+        assert self.compact and C == self.segs and core_rows.dtype == torch.int8 and core_owner.dtype == torch.int8
+        assert core_rows.is_contiguous() and core_owner.is_contiguous() and core_owner.shape == (E, C)
+        if out is None:
+            out = torch.empty((E * n_agents, 128), dtype=torch.float32, device=core_rows.device)
+        sb = int(lib.ms_bdqn_layer1_scratch_bytes(E, C))
+        if getattr(self, "_scratch", None) is None or self._scratch.numel() * 4 < sb:
+            self._scratch = torch.empty(((sb + 3) // 4,), dtype=torch.float32, device=core_rows.device)
+        p = self.q.hip_params()
+        check(lib.ms_bdqn_layer1_compact(ct.byref(p), ptr(self.ws), ptr(self.base), ptr(core_rows), ptr(core_owner), E,
+                                         n_agents, C, self.seg, stride, ptr(self._scratch), self._scratch.numel() * 4,
+                                         ptr(out), stream_ptr(stream)))
+        return out
+
+    def act(self, h1=None, x=None, explore=None, rand_action=None, out=None, stream=None):
+        """ms_bdqn_act: int8 [rows, ac_dim] actions from h1 [rows, 128] f32 or int8 rows x [rows, stride]."""
+        src = h1 if h1 is not None else x
+        rows = src.shape[0]
+        assert src.is_contiguous()
+        if h1 is not None:
+            assert h1.dtype == torch.float32 and h1.shape[1] == 128
+        else:
+            assert x.dtype == torch.int8 and x.shape[1] >= self.q.obs and self.segs == 1
+        if explore is not None:
+            assert explore.dtype == torch.uint8 and explore.numel() == rows
+            assert rand_action.dtype == torch.int8 and rand_action.shape == (rows, self.q.ac_dim)
+            assert rand_action.is_contiguous()
+        if out is None:
+            out = torch.empty((rows, self.q.ac_dim), dtype=torch.int8, device=src.device)
+        p = self.q.hip_params()
+        check(lib.ms_bdqn_act(ct.byref(p), ptr(h1), ptr(x), 0 if x is None else x.shape[1],
+                              ptr(self.ws) if x is not None else None, rows, ptr(explore), ptr(rand_action), ptr(out),
+                              stream_ptr(stream)))
+        return out
 
 
 @dataclass
@@ -115,15 +152,23 @@ class BDQNConfig:
     batch_size: int = 128
     learning_starts: int = 4
     grad_clip: float = 1.0
+    graph_updates: bool = True   # BranchingRole updates replayed from a captured HIP graph
 
     def epsilon_by_frame(self, i):
         return self.epsilon_final + (self.epsilon_start - self.epsilon_final) * math.exp(-1.0 * i / self.epsilon_decay)
 
 
 class BranchingRole:
-    """BranchingDQN (BranchingDQNModules.py:104-164) of one role: online / target nets, Adam, counter."""
+    """BranchingDQN (BranchingDQNModules.py:104-164) of one role: online / target nets, Adam, counter.
 
-    def __init__(self, obs: int, ac_dim: int, n: int, cfg: BDQNConfig, device):
+    With ``graph`` the update's ~80 small launches (three forwards, the loss, the backward, the
+    clamp and the HIP Adam) are captured once into a HIP graph and replayed on static input
+    buffers: the batch is 128 rows, so the eager update is launch-bound, not compute-bound. The
+    first update runs eagerly (on a side stream, torch's capture recipe) and is this step's real
+    update; the target sync stays on the host every target_net_update_freq updates (an in-place
+    copy into the tensors the graph reads)."""
+
+    def __init__(self, obs: int, ac_dim: int, n: int, cfg: BDQNConfig, device, graph: bool = False):
         self.q = BranchingQ(obs, ac_dim, n).to(device)
         self.target = BranchingQ(obs, ac_dim, n).to(device)  # its own init draw, then overwritten (:110-112)
         self.target.load_state_dict(self.q.state_dict())
@@ -131,26 +176,52 @@ class BranchingRole:
         self.cfg = cfg
         self.opt = HipAdam([dict(params=list(self.q.parameters()), lr=cfg.lr)])
         self.update_counter = 0
+        self.graph = graph
+        self._g = None
 
-    def update(self, states, actions, rewards, next_states, masks):
-        """update_policy (BranchingDQNModules.py:125-164) on a drawn batch: states / next_states [B, obs]
-        float, actions [B, ac_dim] long, rewards / masks [B]. Returns the loss."""
+    def _body(self, states, actions, rewards, next_states, masks):
         current = self.q(states).gather(2, actions.unsqueeze(2)).squeeze(-1)
         with torch.no_grad():
             argmax = torch.argmax(self.q(next_states), dim=2)
             max_next = self.target(next_states).gather(2, argmax.unsqueeze(2)).squeeze(-1).mean(1, keepdim=True)
         expected = rewards.view(-1, 1) + max_next * self.cfg.gamma * masks.view(-1, 1)
         loss = ((expected - current) ** 2).mean()  # F.mse_loss(expected, current) broadcast over branches
-        self.opt.zero_grad()
+        for p in self.q.parameters():  # optimizer.zero_grad(), in place (the graph keeps the .grad tensors)
+            if p.grad is not None:
+                p.grad.zero_()
         loss.backward()
         for p in self.q.parameters():
             p.grad.data.clamp_(-self.cfg.grad_clip, self.cfg.grad_clip)
         self.opt.step()
+        return loss.detach()
+
+    def update(self, states, actions, rewards, next_states, masks):
+        """update_policy (BranchingDQNModules.py:125-164) on a drawn batch: states / next_states [B, obs]
+        float, actions [B, ac_dim] long, rewards / masks [B]. Returns the loss."""
+        if not self.graph:
+            loss = self._body(states, actions, rewards, next_states, masks)
+        elif self._g is None:
+            self._in = [x.detach().clone() for x in (states, actions, rewards, next_states, masks)]
+            side = torch.cuda.Stream(device=states.device)
+            side.wait_stream(torch.cuda.current_stream(states.device))
+            with torch.cuda.stream(side):
+                loss = self._body(*self._in).clone()  # this step's update (and the warm-up of the capture)
+            torch.cuda.current_stream(states.device).wait_stream(side)
+            torch.cuda.synchronize(states.device)
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                self._loss = self._body(*self._in)
+            self._g = g
+        else:
+            for dst, src in zip(self._in, (states, actions, rewards, next_states, masks)):
+                dst.copy_(src)
+            self._g.replay()
+            loss = self._loss.clone()
         self.update_counter += 1
         if self.update_counter % self.cfg.target_net_update_freq == 0:
             self.update_counter = 0
             self.target.load_state_dict(self.q.state_dict())
-        return loss.detach()
+        return loss
 
 
 class BDQNTrainer:
@@ -177,10 +248,16 @@ class BDQNTrainer:
         self.ld_acc = dims["acceptor"][1]
         torch.manual_seed(seed)
         dev = self.device
-        self.roles = dict(acc=BranchingRole(C * s.acc_obs_dim, C, O + 1, self.b, dev),
-                          off=BranchingRole(self.d_off, L, C + 1, self.b, dev))
+        gr = self.b.graph_updates
+        self.roles = dict(acc=BranchingRole(C * s.acc_obs_dim, C, O + 1, self.b, dev, graph=gr),
+                          off=BranchingRole(self.d_off, L, C + 1, self.b, dev, graph=gr))
         if self.free:
-            self.roles["price"] = BranchingRole(self.d_off, L, s.price_actions, self.b, dev)
+            self.roles["price"] = BranchingRole(self.d_off, L, s.price_actions, self.b, dev, graph=gr)
+        # acting on the HIP kernels: the acceptor's layer 1 from the compact rows, the offer / price
+        # roles' on the aggregated offer rows inside the act kernel
+        self.actors = {k: (HipActor(r.q, self.d_acc, C, dev, compact=True) if k == "acc"
+                           else HipActor(r.q, self.d_off, 1, dev)) for k, r in self.roles.items()}
+        self._h1 = torch.empty((self.E * N, 128), dtype=torch.float32, device=dev)
         # compact replay ring: states of frames 0..F (slot F + 1 holds the next state of the newest frame)
         Fm = self.b.memory_frames
         self.n_slots = Fm + 1
@@ -214,8 +291,9 @@ class BDQNTrainer:
     def _store_slot_pairs(self, slot):
         self.slot_pairs[slot].copy_(self.off_rows[..., 2 * self.C:2 * self.C + 2])
 
-    def _offer_rows(self, slot):
-        """The aggregated offer rows of every (replica, agent) of ring slot `slot` (ms_regen_agent_rows)."""
+    def _offer_rows_i8(self, slot):
+        """The aggregated offer rows [E * N, ld_off] int8 of every (replica, agent) of ring slot `slot`
+        (ms_regen_agent_rows)."""
         E, N = self.E, self.N
         frame = (torch.arange(E, device=self.device, dtype=torch.int64) + slot * E).repeat_interleave(N)
         _, off = self.env.regen_agent_rows(self.core_rows.view(-1, self.C, self.stride),
@@ -223,26 +301,26 @@ class BDQNTrainer:
                                            frame, self._agent_idx,
                                            offer=torch.empty((E * N, self.ld_off), dtype=torch.int8,
                                                              device=self.device))
-        return off[:, : self.d_off].float()
+        return off
 
     @torch.no_grad()
     def _actions(self, slot, eps):
-        """get_action (BranchingDQNModules.py:117-123) of every agent, epsilon-greedy per agent (:181-186)."""
+        """get_action (BranchingDQNModules.py:117-123) of every agent, epsilon-greedy per agent (:181-186):
+        one fused HIP act kernel per role (ms_bdqn_act)."""
         E, N = self.E, self.N
-        qa = self.roles["acc"].q
-        h1 = dict(acc=qa.layer1_compact(self.core_rows[slot], self.core_owner[slot], N, self.d_acc))
-        x_off = self._offer_rows(slot)
-        for k in ("off", "price"):
-            if k in self.roles:
-                q = self.roles[k].q
-                h1[k] = F_.linear(x_off, q.w1, q.b1)
-        explore = torch.rand((E * N,), generator=self.gen, device=self.device) <= eps
+        for a in self.actors.values():
+            a.prepare()  # the weights changed in the last update
+        ea = self.actors["acc"]
+        h1 = ea.layer1_compact(self.core_rows[slot], self.core_owner[slot], N, out=self._h1)
+        x_off = self._offer_rows_i8(slot)
+        explore = (torch.rand((E * N,), generator=self.gen, device=self.device) <= eps).to(torch.uint8)
         out = {}
-        for k, h in h1.items():
-            q = self.roles[k].q
-            greedy = q.greedy(h)
-            rnd = torch.randint(0, q.n, greedy.shape, generator=self.gen, device=self.device)
-            out[k] = torch.where(explore.unsqueeze(1), rnd, greedy).to(torch.int8).view(E, N, -1)
+        for k, actor in self.actors.items():
+            q = actor.q
+            rnd = torch.randint(0, q.n, (E * N, q.ac_dim), generator=self.gen, device=self.device).to(torch.int8)
+            a = actor.act(h1=h1, explore=explore, rand_action=rnd) if k == "acc" else \
+                actor.act(x=x_off, explore=explore, rand_action=rnd)
+            out[k] = a.view(E, N, -1)
         return out
 
     def step(self):

@@ -15,6 +15,7 @@
 
 #include "ms_layout.h"
 #include "ms_dqn.h"
+#include "ms_bdqn.h"
 #include "ms_ppo.h"
 
 namespace ms {
@@ -49,6 +50,10 @@ hipError_t launch_adam(const AdamTensor*, int, const double*, int, int64_t, doub
 hipError_t launch_dqn_act(const DqnActArgs&, hipStream_t);
 hipError_t launch_regen_agent_rows(const RegenArgs&, hipStream_t);
 hipError_t launch_dqn_grad(const DqnGradArgs&, const DqnReduceArgs&, hipStream_t);
+hipError_t launch_bdqn_w1split(const float*, int, int, int, uint16_t*, hipStream_t);
+hipError_t launch_bdqn_l1_base(const float*, const float*, int, int, float*, hipStream_t);
+hipError_t launch_bdqn_l1_compact(const BdqnL1Compact&, hipStream_t);
+hipError_t launch_bdqn_act(const BdqnAct&, hipStream_t);
 }  // namespace ms
 
 // work split of k_ppo_grad: ~8192 wave chunks over all groups (4 per block), >= 8 tiles of 16 rows each
@@ -938,5 +943,94 @@ int ms_regen_agent_rows(const ms_config* cfg, const int8_t* core_rows, const int
     g.acc_ld = ms::align4(P.C * P.d_acc);
     g.off_ld = ms::align4(2 * P.C + 2 * P.L);
     HIP_TRY(ms::launch_regen_agent_rows(g, (hipStream_t)stream));
+    return MS_OK;
+}
+
+// ---- Branching DQN acting (bdqn_kernels.hip)
+static int bdqn_pad(int seg) { return (seg + 31) & ~31; }
+
+size_t ms_bdqn_workspace_bytes(int32_t seg, int32_t segs) {
+    if (seg < 1 || segs < 1) return 0;
+    return (size_t)3 * ms::kBH * segs * bdqn_pad(seg) * sizeof(uint16_t);
+}
+
+static int bdqn_check(const ms_bdqn_params* q, const char* who) {
+    if (!q || !q->w1 || !q->b1 || !q->w2 || !q->b2 || !q->wv || !q->bv || !q->wa || !q->ba)
+        return fail(MS_EINVAL, "%s: NULL parameter", who);
+    if (q->obs < 1 || q->ac_dim < 1 || q->ac_dim > 127 || q->n < 1 || q->n > 128)
+        return fail(MS_EINVAL, "%s: bad net shape (obs %d, ac_dim %d, n %d)", who, q->obs, q->ac_dim, q->n);
+    return MS_OK;
+}
+
+static ms::BdqnNet bdqn_net(const ms_bdqn_params* q) {
+    return ms::BdqnNet{q->w1, q->b1, q->w2, q->b2, q->wv, q->bv, q->wa, q->ba, q->obs, q->ac_dim, q->n};
+}
+
+int ms_bdqn_prepare(const ms_bdqn_params* q, int32_t seg, int32_t segs, void* workspace, size_t workspace_bytes,
+                    float* base, void* stream) {
+    if (int rc = bdqn_check(q, "ms_bdqn_prepare")) return rc;
+    if (seg < 1 || segs < 1 || (int64_t)seg * segs != q->obs)
+        return fail(MS_EINVAL, "ms_bdqn_prepare: seg * segs must equal obs");
+    if (!workspace || workspace_bytes < ms_bdqn_workspace_bytes(seg, segs))
+        return fail(MS_EINVAL, "ms_bdqn_prepare: workspace too small");
+    HIP_TRY(ms::launch_bdqn_w1split(q->w1, seg, segs, bdqn_pad(seg), (uint16_t*)workspace, (hipStream_t)stream));
+    if (base) HIP_TRY(ms::launch_bdqn_l1_base(q->w1, q->b1, seg, segs, base, (hipStream_t)stream));
+    return MS_OK;
+}
+
+size_t ms_bdqn_layer1_scratch_bytes(int64_t n_envs, int32_t n_cores) {
+    if (n_envs < 1 || n_cores < 1) return 0;
+    return sizeof(float) * (size_t)n_envs * n_cores * ms::kBH;
+}
+
+int ms_bdqn_layer1_compact(const ms_bdqn_params* q, const void* workspace, const float* base, const int8_t* core_rows,
+                           const int8_t* core_owner, int64_t n_envs, int32_t n_agents, int32_t n_cores,
+                           int32_t acc_dim, int32_t acc_stride, void* scratch, size_t scratch_bytes, float* h1,
+                           void* stream) {
+    if (int rc = bdqn_check(q, "ms_bdqn_layer1_compact")) return rc;
+    if (!workspace || !base || !core_rows || !core_owner || !h1 || !scratch)
+        return fail(MS_EINVAL, "ms_bdqn_layer1_compact: NULL argument");
+    if (n_envs < 1 || n_agents < 1 || n_agents > 127 || n_cores < 1 || acc_dim < 4 || acc_dim > 256 ||
+        acc_stride < acc_dim || (acc_stride & 3) || (int64_t)acc_dim * n_cores != q->obs)
+        return fail(MS_EINVAL, "ms_bdqn_layer1_compact: bad shape (obs must be n_cores * acc_dim)");
+    if (scratch_bytes < ms_bdqn_layer1_scratch_bytes(n_envs, n_cores))
+        return fail(MS_EINVAL, "ms_bdqn_layer1_compact: scratch too small");
+    ms::BdqnL1Compact p{};
+    p.w1s = (const uint16_t*)workspace;
+    p.base = base;
+    p.core_rows = core_rows;
+    p.core_owner = core_owner;
+    p.E = n_envs;
+    p.N = n_agents;
+    p.C = n_cores;
+    p.D = acc_dim;
+    p.Dp = bdqn_pad(acc_dim);
+    p.stride = acc_stride;
+    p.P = (float*)scratch;
+    p.h1 = h1;
+    HIP_TRY(ms::launch_bdqn_l1_compact(p, (hipStream_t)stream));
+    return MS_OK;
+}
+
+int ms_bdqn_act(const ms_bdqn_params* q, const float* h1, const int8_t* x, int32_t x_stride, const void* workspace,
+                int64_t n_rows, const uint8_t* explore, const int8_t* rand_action, int8_t* action, void* stream) {
+    if (int rc = bdqn_check(q, "ms_bdqn_act")) return rc;
+    if (n_rows < 1 || !action) return fail(MS_EINVAL, "ms_bdqn_act: no rows / no action buffer");
+    if (explore && !rand_action) return fail(MS_EINVAL, "ms_bdqn_act: explore needs rand_action");
+    if (!h1 && (!x || !workspace || x_stride < q->obs || (x_stride & 3) || q->obs > 256))
+        return fail(MS_EINVAL, "ms_bdqn_act: without h1, int8 rows (x_stride >= obs, multiple of 4, obs <= 256) "
+                               "and the prepared workspace are needed");
+    ms::BdqnAct p{};
+    p.q = bdqn_net(q);
+    p.h1 = h1;
+    p.x = x;
+    p.w1s = (const uint16_t*)workspace;
+    p.x_stride = x_stride;
+    p.Kp = bdqn_pad(q->obs);
+    p.rows = n_rows;
+    p.explore = explore;
+    p.rnd = rand_action;
+    p.action = action;
+    HIP_TRY(ms::launch_bdqn_act(p, (hipStream_t)stream));
     return MS_OK;
 }

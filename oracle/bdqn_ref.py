@@ -66,3 +66,22 @@ def update_policy_reference(q, target, adam, states, actions, rewards, next_stat
         p.grad.data.clamp_(-1.0, 1.0)
     adam.step()
     return loss.detach()
+
+
+def layer1_compact_reference(w1, b1, core_rows, core_owner, n_agents: int, d_acc: int):
+    """The structured layer 1 of the aggregated acceptor rows in torch fp32 (the algebra
+    ms_bdqn_layer1_compact implements): an agent's row is R_c on the cores it owns and the foreign
+    row F elsewhere (Agent.py:167-212), so W1 x_a + b1 = (b1 + sum_c W1_c F) + sum_{c owned by a}
+    W1_c (R_c - F). core_rows [E, C, stride] int8, core_owner [E, C] -> [E * N, 128]."""
+    E, C, _ = core_rows.shape
+    O = (d_acc - 3) // 2
+    foreign = torch.tensor([0.0, -1.0, -1.0] + [-2.0] * (2 * O), device=core_rows.device)
+    w1c = w1.view(w1.shape[0], C, d_acc)
+    base = b1 + torch.einsum("jcd,d->j", w1c, foreign)
+    dc = core_rows[:, :, :d_acc].float() - foreign
+    part = torch.bmm(dc.transpose(0, 1), w1c.permute(1, 2, 0))             # [C, E, 128]
+    h1 = base.expand(E * n_agents, w1.shape[0]).contiguous()
+    own = core_owner.long()
+    mask = own > 0
+    rows = (torch.arange(E, device=own.device).unsqueeze(1) * n_agents + own - 1)[mask]
+    return h1.index_add(0, rows, part.transpose(0, 1)[mask])

@@ -12,7 +12,7 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 def _declared():
     with open(os.path.join(REPO, "include", "marlsched.h")) as f:
         src = f.read()
-    return sorted(set(re.findall(r"\b(ms_[a-z_]+)\s*\(", src)) - {"ms_env"})
+    return sorted(set(re.findall(r"\b(ms_[a-z0-9_]+)\s*\(", src)) - {"ms_env"})
 
 
 def test_exports_every_declared_symbol(ms):

@@ -8,7 +8,7 @@ import numpy as np
 import pytest
 import torch
 
-from oracle.bdqn_ref import RefBranchingQNetwork, update_policy_reference
+from oracle.bdqn_ref import RefBranchingQNetwork, layer1_compact_reference, update_policy_reference
 from tests.drivers import offer_counts_from_obs, random_actions
 
 pytestmark = pytest.mark.gpu
@@ -76,41 +76,115 @@ def test_compact_observations_regenerate_the_rows(ms, kw):
         assert torch.equal(ro[b], aggs[t]["offer"][e, a].cpu()), b
 
 
-def test_structured_layer1_matches_dense(ms):
-    bdqn = _bdqn()
+def _cfg5_compact(ms, E, steps=30, seed=5):
     abi = ms.abi
     cfg = abi.named_config("cfg5")
     s = abi.config_shape(cfg)
     N, C = s["N"], s["C"]
-    E = 64
-    env = ms.BatchedEnv(cfg, E, seed=5)
+    env = ms.BatchedEnv(cfg, E, seed=seed)
     comp = env.compact_obs_buffers()
     env.reset(comp)
     rng = np.random.default_rng(2)
-    for _ in range(30):
+    for _ in range(steps):
         acc = torch.tensor(rng.integers(0, s["O"] + 1, (E, N, C)), dtype=torch.int8, device=env.device)
         off = torch.tensor(rng.integers(0, C + 1, (E, N, s["L"])), dtype=torch.int8, device=env.device)
         pr = torch.tensor(rng.integers(0, s["price_actions"], (E, N, s["L"])), dtype=torch.int8, device=env.device) \
             if cfg.free_prices else None
         env.step(acc, off, pr, obs=comp)
+    return env, comp, s
+
+
+def _dense_rows(env, comp, s):
+    N, C = s["N"], s["C"]
+    E = comp["core_owner"].shape[0]
+    frame = torch.arange(E, device=env.device).repeat_interleave(N)
+    agent = torch.arange(N, dtype=torch.int32, device=env.device).repeat(E)
+    pairs = comp["offer"][..., 2 * C:2 * C + 2].contiguous()
+    return env.regen_agent_rows(comp["core_rows"], comp["core_owner"], pairs, frame, agent)
+
+
+def test_structured_layer1_matches_dense(ms):
+    """ms_bdqn_layer1_compact (exact bf16 products, f32 sums, owners' rows added in core order) against
+    the dense Linear(C * D_acc, 128) of the regenerated aggregated acceptor rows (fp32 torch), and the
+    torch algebra of oracle/bdqn_ref.layer1_compact_reference; bit-identical on a repeat."""
+    bdqn = _bdqn()
+    E = 64
+    env, comp, s = _cfg5_compact(ms, E)
+    N, C, D = s["N"], s["C"], s["acc_obs_dim"]
     torch.manual_seed(0)
-    net = bdqn.BranchingQ(C * s["acc_obs_dim"], C, s["O"] + 1).cuda()
+    net = bdqn.BranchingQ(C * D, C, s["O"] + 1).cuda()
+    actor = bdqn.HipActor(net, D, C, "cuda", compact=True)
+    actor.prepare()
+    h_k = actor.layer1_compact(comp["core_rows"], comp["core_owner"], N)
+    h_k2 = actor.layer1_compact(comp["core_rows"], comp["core_owner"], N)
+    assert torch.equal(h_k, h_k2)
     with torch.no_grad():
-        q_c = net.forward_compact(comp["core_rows"], comp["core_owner"], N, s["acc_obs_dim"])
-        frame = torch.arange(E, device=env.device).repeat_interleave(N)
-        agent = torch.arange(N, dtype=torch.int32, device=env.device).repeat(E)
-        pairs = comp["offer"][..., 2 * C:2 * C + 2].contiguous()
-        ra, _ = env.regen_agent_rows(comp["core_rows"], comp["core_owner"], pairs, frame, agent)
-        x = ra[:, : C * s["acc_obs_dim"]].float()
-        q_d = net(x)
-        ref = RefBranchingQNetwork(C * s["acc_obs_dim"], C, s["O"] + 1)
-        ref.load_stacked({k: getattr(net, k).detach().cpu() for k in bdqn.KEYS})
-        q_r = ref(x.cpu())
-    scale = q_r.abs().max().item()
-    assert (q_d.cpu() - q_r).abs().max().item() <= 1e-4 * scale
-    assert (q_c.cpu() - q_r).abs().max().item() <= 1e-4 * scale
-    owned = (comp["core_owner"] > 0).sum().item()
-    assert owned > 0  # the structured path saw agent-owned cores
+        ra, _ = _dense_rows(env, comp, s)
+        x = ra[:, : C * D].float()
+        h_d = torch.nn.functional.linear(x.cpu().double(), net.w1.detach().cpu().double(),
+                                         net.b1.detach().cpu().double())
+        h_r = layer1_compact_reference(net.w1, net.b1, comp["core_rows"], comp["core_owner"], N, D)
+    scale = h_d.abs().max().item()
+    assert (h_k.cpu().double() - h_d).abs().max().item() <= 1e-5 * scale
+    assert (h_r.cpu().double() - h_d).abs().max().item() <= 1e-5 * scale
+    assert (comp["core_owner"] > 0).sum().item() > 0  # the structured path saw agent-owned cores
+
+
+def _check_greedy(q, got, gap=1e-5):
+    """got [B, ac] int8 vs the first argmax of q [B, ac, n] (fp32): equal wherever the best q is ahead
+    of the second by more than gap of the q scale (elsewhere the two are within f32 rounding)."""
+    top2 = q.topk(2, dim=2).values
+    scale = q.abs().max().item()
+    clear = (top2[..., 0] - top2[..., 1]) > gap * scale
+    want = q.argmax(2)
+    assert clear.float().mean().item() > 0.95
+    assert torch.equal(got.long()[clear], want[clear])
+    return (got.long() == want).float().mean().item()
+
+
+@pytest.mark.parametrize("role", ["acc", "off", "price"])
+def test_act_kernel_is_the_argmax_of_q(ms, role):
+    """ms_bdqn_act (trunk + value + advantage heads + per-branch q and first argmax, epsilon-greedy)
+    against q = value + adv - mean(adv) of the reference BranchingQNetwork (oracle/bdqn_ref.py,
+    BranchingDQNModules.py:75-101, fp32 on the CPU); explored rows take the given random actions."""
+    bdqn = _bdqn()
+    E = 96
+    env, comp, s = _cfg5_compact(ms, E, steps=25, seed=7)
+    N, C, L, D = s["N"], s["C"], s["L"], s["acc_obs_dim"]
+    dims = env.aggregated_dims()
+    ra, ro = _dense_rows(env, comp, s)
+    if role == "acc":
+        obs, ac, n = C * D, C, s["O"] + 1
+    else:
+        obs, ac, n = dims["offer"][0], L, (C + 1 if role == "off" else s["price_actions"])
+    torch.manual_seed(11)
+    net = bdqn.BranchingQ(obs, ac, n).cuda()
+    actor = bdqn.HipActor(net, D if role == "acc" else obs, C if role == "acc" else 1, "cuda", compact=role == "acc")
+    actor.prepare()
+    rows = E * N
+    g = torch.Generator(device="cuda").manual_seed(3)
+    explore = (torch.rand((rows,), generator=g, device="cuda") < 0.3).to(torch.uint8)
+    rnd = torch.randint(0, n, (rows, ac), generator=g, device="cuda").to(torch.int8)
+    if role == "acc":
+        h1 = actor.layer1_compact(comp["core_rows"], comp["core_owner"], N)
+        got = actor.act(h1=h1, explore=explore, rand_action=rnd)
+        greedy = actor.act(h1=h1)
+        x = ra[:, :obs].float()
+    else:
+        got = actor.act(x=ro, explore=explore, rand_action=rnd)
+        greedy = actor.act(x=ro)
+        x = ro[:, :obs].float()
+    assert torch.equal(got, actor.act(h1=h1, explore=explore, rand_action=rnd) if role == "acc"
+                       else actor.act(x=ro, explore=explore, rand_action=rnd))  # deterministic
+    ref = RefBranchingQNetwork(obs, ac, n)
+    ref.load_stacked({k: getattr(net, k).detach().cpu() for k in bdqn.KEYS})
+    with torch.no_grad():
+        q = ref(x.cpu())
+    agree = _check_greedy(q, greedy.cpu())
+    assert agree > 0.995
+    ex = explore.cpu().bool()
+    assert torch.equal(got.cpu()[ex], rnd.cpu()[ex])
+    assert torch.equal(got.cpu()[~ex], greedy.cpu()[~ex])
 
 
 def test_update_matches_reference(ms):
@@ -142,6 +216,31 @@ def test_update_matches_reference(ms):
     assert torch.equal(role.target.w1, role.q.w1.detach()) is False  # synced at update 2, updated once since
 
 
+def test_graphed_update_equals_eager(ms):
+    """BranchingRole(graph=True): the first update eager (on a side stream), then replays of the captured
+    graph on the static inputs; with the target sync on the host. Same losses and weights as eager."""
+    bdqn = _bdqn()
+    obs, ac, n, B = 70, 3, 33, 128
+    cfg = bdqn.BDQNConfig(target_net_update_freq=2)
+    roles = []
+    for graph in (False, True):
+        torch.manual_seed(3)
+        roles.append(bdqn.BranchingRole(obs, ac, n, cfg, "cuda", graph=graph))
+    g = torch.Generator().manual_seed(4)
+    for step in range(5):
+        s = torch.randint(-5, 13, (B, obs), generator=g).float().cuda()
+        s1 = torch.randint(-5, 13, (B, obs), generator=g).float().cuda()
+        a = torch.randint(0, n, (B, ac), generator=g).cuda()
+        r = torch.randint(-30, 30, (B,), generator=g).float().cuda()
+        m = (torch.rand((B,), generator=g) > 0.1).float().cuda()
+        l0, l1 = [ro.update(s, a, r, s1, m) for ro in roles]
+        torch.testing.assert_close(l1, l0, rtol=1e-6, atol=1e-7)
+    for k in bdqn.KEYS:
+        torch.testing.assert_close(getattr(roles[1].q, k), getattr(roles[0].q, k), rtol=1e-5, atol=1e-7)
+        torch.testing.assert_close(getattr(roles[1].target, k), getattr(roles[0].target, k), rtol=1e-5, atol=1e-7)
+    assert roles[1]._g is not None
+
+
 def test_bdqn_trainer_cfg5(ms):
     bdqn = _bdqn()
     cfg = ms.abi.named_config("cfg5")
@@ -152,16 +251,3 @@ def test_bdqn_trainer_cfg5(ms):
     assert tr.flags() == 0 and tr.env.round == 9 and tr.stored == 6
     assert set(tr.last_losses) >= {"acc", "off"}
     assert all(torch.isfinite(v) for v in tr.last_losses.values())
-
-
-def test_greedy_is_the_argmax_of_q(ms):
-    bdqn = _bdqn()
-    torch.manual_seed(9)
-    net = bdqn.BranchingQ(70, 3, 33).cuda()
-    x = torch.randint(-5, 13, (4096, 70), device="cuda").float()
-    with torch.no_grad():
-        q = net(x)
-        g = net.greedy(torch.nn.functional.linear(x, net.w1, net.b1))
-    top2 = q.topk(2, dim=2).values
-    clear = (top2[..., 0] - top2[..., 1]) > 1e-4
-    assert torch.equal(g[clear], q.argmax(2)[clear])
