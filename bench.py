@@ -253,6 +253,7 @@ def bench_other(args):
         trainer_mod = importlib.import_module("marl-scheduling_amd.trainer")
         tr = trainer_mod.Trainer.from_named(args.config, n_envs=E, update_step=T, seed=0, device=device, rank=rank,
                                             world_size=world)
+        tr.record_launch_spans(SAMPLE_EVERY)
         tr.use_graph = not args.no_graph
         run = tr.iteration
         N = tr.N
@@ -286,13 +287,59 @@ def bench_other(args):
               "config": {"workload": "%s: %s; one step = %d rounds%s" % (args.config, spec["what"], T,
                                                                        " + update" if args.config != "cfg5" else ""),
                          "replicas_per_gpu": E, "rounds_per_step": T}}
-    if hasattr(tr, "timings"):
-        tm = dict(tr.timings)
-        result["breakdown_ms_per_step"] = {k: v / args.steps * 1e3 for k, v in tm.items()}
+    tm = dict(tr.timings)
+    result["breakdown_ms_per_step"] = {k: v / args.steps * 1e3 for k, v in tm.items()}
+    if args.config == "cfg5":
+        result["roofline"] = bdqn_act_roofline(tr, device)
+    else:
+        launch_us = tr.launch_spans_us()
+        b_round = env_round_bytes(tr.env.shape, tr.cfg.new_jobs_per_round, tr.free, tr.compact)
+        result["roofline"] = env_roofline(b_round, E, launch_us, tr.compact)
     if rank == 0:
         print(json.dumps(result))
     if world > 1:
         dist.destroy_process_group()
+
+
+F32_MFMA_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: dense f32 matrix (v_mfma_f32_16x16x4_f32) peak
+
+
+def bdqn_act_roofline(tr, device, reps: int = 10):
+    """The acceptor role's fused act kernel (ms_bdqn_act, k_bdqn_act<7>): algorithmic flops per launch
+    = 2 x rows x (128*128 + 128 + 128 * ac_dim * n) (trunk, value head, advantage heads) over its
+    average duration between HIP events on its stream, against the dense f32 MFMA peak."""
+    import torch
+
+    actor = tr.actors["acc"]
+    q = actor.q
+    rows = tr.E * tr.N
+    st = torch.cuda.current_stream(device)
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    actor.act(h1=tr._h1)
+    ev[0].record(st)
+    for _ in range(reps):
+        actor.act(h1=tr._h1)
+    ev[1].record(st)
+    ev[1].synchronize()
+    sec = ev[0].elapsed_time(ev[1]) / 1e3 / reps
+    flops = 2.0 * rows * (128 * 128 + 128 + 128 * q.ac_dim * q.n)
+    achieved = flops / sec / 1e12
+    return {"kernel": "ms::k_bdqn_act<7, false>", "bound": "mfma", "achieved": achieved,
+            "peak": F32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": achieved / F32_MFMA_PEAK_TFLOPS, "traffic": None,
+            "flops_per_launch": flops, "avg_launch_us": sec * 1e6, "rows_per_launch": rows,
+            "launch_timing": "HIP events around %d launches on the trainer's last h1, after the timed region" % reps}
+
+
+def env_roofline(b_round: int, envs: int, launch_us, compact: bool, variant_traffic: bool = True):
+    """k_env_step's roofline entry: SURVEY 8(d) algorithmic bytes per env-round x replicas per launch
+    over the in-region launch span (tr.record_launch_spans)."""
+    avg_s = sum(launch_us) / len(launch_us) / 1e6
+    achieved = b_round * envs / avg_s / 1e9
+    traffic = committed_traffic(b_round * envs, "compact" if compact else "") if variant_traffic else None
+    return {"kernel": "ms::k_env_step", "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBS, "traffic": traffic["bytes"] if traffic else None,
+            "traffic_source": traffic["source"] if traffic else None, "bytes_per_env_round": b_round,
+            "envs_per_launch": envs, "avg_launch_us": avg_s * 1e6, "launches_timed": len(launch_us)}
 
 
 def launch_ranks(n: int, argv) -> int:

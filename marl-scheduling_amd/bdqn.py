@@ -281,6 +281,7 @@ class BDQNTrainer:
         self._observe_into(self.head, reset=True)
         self._store_slot_pairs(self.head)
         self.last_losses = {}
+        self.timings = None
 
     def _observe_into(self, slot, reset=False):
         obs = dict(core_rows=self.core_rows[slot], core_owner=self.core_owner[slot], offer=self.off_rows)
@@ -323,6 +324,23 @@ class BDQNTrainer:
             out[k] = a.view(E, N, -1)
         return out
 
+    @property
+    def timings(self):
+        """Device time (s) of the frames' acting, env step + storing, and learning, accumulated from
+        HIP events (read lazily)."""
+        for ev in self._pending_events:
+            ev[-1].synchronize()
+            self._timings["act"] += ev[0].elapsed_time(ev[1]) / 1e3
+            self._timings["env"] += ev[1].elapsed_time(ev[2]) / 1e3
+            self._timings["learn"] += ev[2].elapsed_time(ev[3]) / 1e3
+        self._pending_events = []
+        return self._timings
+
+    @timings.setter
+    def timings(self, value):
+        self._pending_events = []
+        self._timings = dict(act=0.0, env=0.0, learn=0.0)
+
     def step(self):
         """One frame: act, env.step, store the transition, learn (BranchingDQNModules.py:179-208)."""
         E, N, C, L = self.E, self.N, self.C, self.L
@@ -330,7 +348,10 @@ class BDQNTrainer:
         cur = self.head
         nxt = (cur + 1) % self.n_slots
         eps = b.epsilon_by_frame(self.frame)
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+        ev[0].record()
         acts = self._actions(cur, eps)
+        ev[1].record()
         for k, a in acts.items():
             self.act[k][cur].copy_(a)
         obs = self._observe_into(nxt)
@@ -347,8 +368,11 @@ class BDQNTrainer:
         self.head = nxt
         self.stored = min(self.stored + 1, self.b.memory_frames)
         self.frame += 1
+        ev[2].record()
         if self.frame > b.learning_starts:
             self._learn()
+        ev[3].record()
+        self._pending_events.append(ev)
         return done
 
     def _sample(self):
