@@ -15,9 +15,10 @@ tr.iteration()
 t = 3
 N, C, L = tr.N, tr.C, tr.L
 off_obs = tr.off_obs[t]
-out = dict(core_action=tr.off.actions[t], core_logprob=tr.off.logprobs[t], price_state=tr.price_obs_um[:, t],
-           price_action=tr.price.actions_um[:, t], price_logprob=tr.price.logprobs_um[:, t], env_price=tr.env_price)
-pus = tr.T * tr.E
+out = dict(core_action=tr.off.actions[t], core_logprob=tr.off.logprobs[t], price_state=tr.price_obs[t],
+           price_action=tr.price.actions[t], price_logprob=tr.price.logprobs[t], env_price=tr.env_price)
+pus = 0
+pt = tr.price_table
 
 
 def timed(fn, n=50):
@@ -44,7 +45,7 @@ res = {
                                                                                 logprob=tr.acc.logprobs[t])),
     "paired (ms_act_round_free)": timed(lambda: ppo.act_round_free(core, price, off_obs, acc, tr.acc_rows[t], tr.acc_owner[t],
                                                                    tr.acc_common, C, 1, 1, 3, out, tr.acc.actions[t],
-                                                                   tr.acc.logprobs[t], price_unit_stride=pus)),
+                                                                   tr.acc.logprobs[t], price_unit_stride=pus, price_table=pt)),
 }
 for k, v in res.items():
     print("%-45s %8.2f us" % (k, v))
