@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define MS_ABI_VERSION 11
+#define MS_ABI_VERSION 12
 
 #define MS_MAX_KINDS 16
 #define MS_MAX_AGENTS 64
@@ -439,6 +439,35 @@ int ms_aggregate_obs(const ms_config* cfg, int64_t n_envs, const int8_t* acc_obs
  * action space exceeds int32. */
 int ms_decode_aggregated(const ms_config* cfg, int64_t n_envs, const int32_t* actions, int32_t fully,
                          int8_t* acceptor, int8_t* offer_core, int32_t* n_bad, void* stream);
+
+/* The aggregated agents' nets (AggregatedAcceptorPPO / AggregatedOfferPPO, PPOmodules.py:177-210,
+ * 32 hidden units; FullyAggregatedPPO :213-232, 64): ActorCritic of hidden width 32 or 64, in_dim
+ * 1..255, n_actions 1..2^24, one net per group (agent). Replace ActorCritic.act's torch forward +
+ * Categorical.sample (PPOmodules.py:53-63, called by PPO.selectAction :114-125) and the autograd
+ * of PPO.update (:127-174).
+ *
+ * ms_wide_act: rows (e, g) of obs [n_rows][G][obs_stride] int8 (obs_stride >= in_dim, multiple of
+ * 4) through group g's actor; the action is the inverse-CDF sample at uniforms[e][g] (the number of
+ * running sums of exp(z - max) that stay <= u * S) and logprob its log(clamp(p, eps, 1 - eps)).
+ * action / logprob [n_rows][G]. */
+int ms_wide_act(const ms_mlp_params* actor, const int8_t* obs, int32_t obs_stride, int64_t n_rows,
+                const float* uniforms, int32_t* action, float* logprob, void* stream);
+
+typedef struct ms_wide_batch {
+    const int8_t* states;      /* row r of group g at states + (r * G + g) * stride (the [T][E][N] rings, r = t*E + e) */
+    const int32_t* actions;    /* [R][G] */
+    const float* old_logprob;  /* [R][G] */
+    const float* returns;      /* [G][R] normalised */
+    int32_t stride;            /* >= in_dim, multiple of 4 */
+    int64_t rows;              /* R */
+} ms_wide_batch;
+
+/* One K-epoch gradient of PPO.update for the wide nets: grads = d/dθ of each group's
+ * mean_r[-min(surr)] + 0.5 mean_r[(V-G)^2] - 0.01 mean_r[entropy] (same outputs as ms_ppo_grad;
+ * the tensors are overwritten). Deterministic (fixed-order sums). */
+size_t ms_wide_workspace_bytes(const ms_mlp_params* actor, int64_t rows);
+int ms_wide_grad(const ms_mlp_params* actor, const ms_mlp_params* critic, const ms_wide_batch* batch, float eps_clip,
+                 void* workspace, size_t workspace_bytes, const ms_ppo_grads* grads, void* stream);
 
 /* Agent rows regenerated from compact observations (ms_obs_out.core_rows / core_owner, kept per
  * record in a replay memory of M records): for b < n_rows, record frame[b] seen by agent agent[b]

@@ -88,12 +88,17 @@ def _load():
         "ms_bdqn_layer1_compact": (ct.c_int, [ct.POINTER(abi.MsBdqnParams), P, P, P, P, i64, i32, i32, i32, i32, P,
                                               ct.c_size_t, P, P]),
         "ms_bdqn_act": (ct.c_int, [ct.POINTER(abi.MsBdqnParams), P, P, i32, P, i64, P, P, P, P]),
+        "ms_wide_act": (ct.c_int, [ct.POINTER(abi.MsMlpParams), P, i32, i64, P, P, P, P]),
+        "ms_wide_workspace_bytes": (ct.c_size_t, [ct.POINTER(abi.MsMlpParams), i64]),
+        "ms_wide_grad": (ct.c_int, [ct.POINTER(abi.MsMlpParams), ct.POINTER(abi.MsMlpParams),
+                                    ct.POINTER(abi.MsWideBatch), ct.c_float, P, ct.c_size_t,
+                                    ct.POINTER(abi.MsPpoGrads), P]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)
         fn.restype = res
         fn.argtypes = args
-    if L.ms_abi_version() != 11:
+    if L.ms_abi_version() != 12:
         raise ImportError("libmarlsched.so ABI version mismatch")
     return L
 
@@ -110,7 +115,7 @@ EXPORTED = (
     "ms_ppo_workspace_bytes", "ms_ppo_grad", "ms_adam_step", "ms_adam_step_dev",
     "ms_aggregate_obs", "ms_decode_aggregated", "ms_dqn_act", "ms_dqn_workspace_bytes", "ms_dqn_grad",
     "ms_regen_agent_rows", "ms_bdqn_workspace_bytes", "ms_bdqn_prepare", "ms_bdqn_layer1_scratch_bytes", "ms_bdqn_layer1_compact",
-    "ms_bdqn_act",
+    "ms_bdqn_act", "ms_wide_act", "ms_wide_workspace_bytes", "ms_wide_grad",
 )
 
 

@@ -263,6 +263,12 @@ class MsAdamTensor(ct.Structure):
 ADAM_MAX_TENSORS = 16
 
 
+class MsWideBatch(ct.Structure):
+    """ms_wide_batch: rollout rows of the aggregated nets (ms_wide_grad)."""
+    _fields_ = [("states", ct.c_void_p), ("actions", ct.c_void_p), ("old_logprob", ct.c_void_p),
+                ("returns", ct.c_void_p), ("stride", ct.c_int32), ("rows", ct.c_int64)]
+
+
 class MsPpoGrads(ct.Structure):
     _fields_ = [(name, ct.c_void_p) for name in (
         "w1", "b1", "w2", "b2", "w3", "b3", "cw1", "cb1", "cw2", "cb2", "cw3", "cb3", "loss")]

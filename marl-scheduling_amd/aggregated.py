@@ -7,12 +7,12 @@ An aggregated agent has one acceptor net over all its cores and one offer net ov
 PPOmodules.py:213-232: 64 hidden units, (O+1)^C (C+1)^L actions). The world is the divided one,
 so each round is
 
-  aggregated obs (ms_aggregate_obs, HIP) -> act (PyTorch-ROCm: the 16-wide HIP policy kernels do
-  not cover these widths) -> decode the action numbers (ms_decode_aggregated, HIP) -> env step
+  aggregated obs (ms_aggregate_obs, HIP) -> act (ms_wide_act, HIP: the 32 / 64-hidden nets with
+  (O+1)^C-sized softmaxes) -> decode the action numbers (ms_decode_aggregated, HIP) -> env step
   (ms_env_step, HIP, with the aggregated rewards of Reward.py:92-143 from the same settlement)
 
 and UPDATE_STEP rounds are followed by PPO.update of every agent's nets (PPOmodules.py:127-174;
-HIP returns kernel + torch autograd + torch Adam). Rewards saved per agent follow
+HIP returns kernel + the ms_wide_grad gradient + HIP Adam). Rewards saved per agent follow
 SchedulingEnvironment.py:223-247: the acceptor net trains on agentReward, the offer net on the
 aggregated offer reward, the fully aggregated net on their sum. The aggregated envs are
 fixed-price only in the reference; so are these.
@@ -42,19 +42,20 @@ class _AggUnit:
         self.rewards = torch.zeros((T, E, N), dtype=torch.float32, device=device)
 
     def act(self, t):
-        x = self.obs[t][..., : self.D].float().permute(1, 0, 2)  # [N, E, D]: agent n's net on its E rows
-        a, lp = self.group.sample(x)
-        self.actions[t].copy_(a.T)
-        self.logprobs[t].copy_(lp.T)
+        """Every agent's net on its E rows of round t (ms_wide_act), into the rings."""
+        self.group.wide_act(self.obs[t], action=self.actions[t], logprob=self.logprobs[t])
+
+    def batch(self):
+        """The update's rows r = t*E + e: states [T*E, N, stride], actions / log-probs [T*E, N] (views of
+        the rings) and the normalised returns [N, T*E]."""
+        T, E, N = self.T, self.E, self.N
+        ret = discounted_returns(self.rewards.reshape(T, E * N), self.group.gamma)  # [E*N, T]
+        ret = ret.view(E, N, T).permute(1, 2, 0).reshape(N, T * E).contiguous()
+        return (self.obs[:T].view(T * E, N, self.stride), self.actions.view(T * E, N),
+                self.logprobs.view(T * E, N), ret)
 
     def update(self):
-        T, E, N = self.T, self.E, self.N
-        x = self.obs[:T][..., : self.D].permute(2, 0, 1, 3).reshape(N, T * E, self.D).float()  # rows r = t*E + e
-        a = self.actions.permute(2, 0, 1).reshape(N, T * E).long()
-        lp = self.logprobs.permute(2, 0, 1).reshape(N, T * E)
-        ret = discounted_returns(self.rewards.reshape(T, E * N), self.group.gamma)  # [E*N, T]
-        ret = ret.view(E, N, T).permute(1, 2, 0).reshape(N, T * E)
-        losses = self.group.update(x, a, lp, ret)
+        losses = self.group.update_wide(*self.batch())
         self.group.sync_old()
         return torch.stack(losses)
 

@@ -13,11 +13,11 @@ FLAGS=(-O3 -std=c++17 -fPIC --offload-arch="${ARCH}" -Wall -Wno-unused-function
 OBJDIR="${MS_OBJDIR:-${HERE}/build}"
 [[ "${MS_CLEAN:-0}" == 1 ]] && rm -rf "${OBJDIR}"
 mkdir -p "${OBJDIR}"
-HEADERS=("${HERE}/csrc/ms_layout.h" "${HERE}/csrc/ms_ppo.h" "${HERE}/csrc/ms_dqn.h" "${HERE}/csrc/ms_bdqn.h" "${HERE}/csrc/ms_common.h" "${HERE}/../include/marlsched.h")
+HEADERS=("${HERE}/csrc/ms_layout.h" "${HERE}/csrc/ms_ppo.h" "${HERE}/csrc/ms_dqn.h" "${HERE}/csrc/ms_bdqn.h" "${HERE}/csrc/ms_wide.h" "${HERE}/csrc/ms_common.h" "${HERE}/../include/marlsched.h")
 CCVER="$("${HIPCC}" --version 2>/dev/null | head -3 | tr '\n' ' ')"
 objs=()
 pids=()
-for src in env_kernels.hip policy_kernels.hip ppo_kernels.hip agg_kernels.hip dqn_kernels.hip bdqn_kernels.hip capi.cpp; do
+for src in env_kernels.hip policy_kernels.hip ppo_kernels.hip agg_kernels.hip dqn_kernels.hip bdqn_kernels.hip wide_kernels.hip capi.cpp; do
   obj="${OBJDIR}/${src%.*}.o"
   # the env round reproduces Python's float64 arithmetic: no contraction there; the policy
   # and PPO kernels follow torch's f32 (which fuses freely) within tolerance: fma allowed
@@ -25,7 +25,7 @@ for src in env_kernels.hip policy_kernels.hip ppo_kernels.hip agg_kernels.hip dq
   [[ "${src}" == policy_kernels.hip ]] && contract=(-ffp-contract=fast)
   # the gradient kernel's variants (common rows by bytes or by owners) must agree bit for bit: fma only
   # where an expression asks for it, never across statements (fast contraction depends on the code around)
-  [[ "${src}" == ppo_kernels.hip || "${src}" == bdqn_kernels.hip ]] && contract=(-ffp-contract=on)
+  [[ "${src}" == ppo_kernels.hip || "${src}" == bdqn_kernels.hip || "${src}" == wide_kernels.hip ]] && contract=(-ffp-contract=on)
   key="$( { cat "${HERE}/csrc/${src}" "${HEADERS[@]}"; echo "${CCVER} ${FLAGS[*]} ${contract[*]}"; } | sha256sum | cut -d' ' -f1)"
   if [[ ! -f "${obj}" || "$(cat "${obj}.key" 2>/dev/null)" != "${key}" ]]; then
     rm -f "${obj}.key"

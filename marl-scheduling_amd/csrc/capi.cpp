@@ -16,6 +16,7 @@
 #include "ms_layout.h"
 #include "ms_dqn.h"
 #include "ms_bdqn.h"
+#include "ms_wide.h"
 #include "ms_ppo.h"
 
 namespace ms {
@@ -54,6 +55,8 @@ hipError_t launch_bdqn_w1split(const float*, int, int, int, uint16_t*, hipStream
 hipError_t launch_bdqn_l1_base(const float*, const float*, int, int, float*, hipStream_t);
 hipError_t launch_bdqn_l1_compact(const BdqnL1Compact&, hipStream_t);
 hipError_t launch_bdqn_act(const BdqnAct&, hipStream_t);
+hipError_t launch_wide_act(const WideAct&, hipStream_t);
+hipError_t launch_wide_grad(const WideRows&, const WideGrads&, const WideReduce&, hipStream_t);
 }  // namespace ms
 
 // work split of k_ppo_grad: ~8192 wave chunks over all groups (4 per block), >= 8 tiles of 16 rows each
@@ -1032,5 +1035,151 @@ int ms_bdqn_act(const ms_bdqn_params* q, const float* h1, const int8_t* x, int32
     p.rnd = rand_action;
     p.action = action;
     HIP_TRY(ms::launch_bdqn_act(p, (hipStream_t)stream));
+    return MS_OK;
+}
+
+// ---- wide nets: the aggregated agents' ActorCritics (wide_kernels.hip)
+static int wide_check(const ms_mlp_params* a, const char* who) {
+    if (!a || !a->w1 || !a->b1 || !a->w2 || !a->b2 || !a->w3 || !a->b3) return fail(MS_EINVAL, "%s: NULL parameter", who);
+    if (a->hidden != 32 && a->hidden != 64) return fail(MS_EINVAL, "%s: hidden width %d not built (32, 64)", who, a->hidden);
+    if (a->in_dim < 1 || a->in_dim > 255 || a->n_actions < 1 || a->n_actions > (1 << 24) || a->n_groups < 1)
+        return fail(MS_EINVAL, "%s: in_dim must be in [1, 255], n_actions in [1, 2^24], n_groups >= 1", who);
+    return MS_OK;
+}
+
+static ms::WideNet wide_net(const ms_mlp_params* a) { return ms::WideNet{a->w1, a->b1, a->w2, a->b2, a->w3, a->b3}; }
+
+int ms_wide_act(const ms_mlp_params* a, const int8_t* obs, int32_t obs_stride, int64_t n_rows, const float* uniforms,
+                int32_t* action, float* logprob, void* stream) {
+    if (int rc = wide_check(a, "ms_wide_act")) return rc;
+    if (!obs || !uniforms || !action || !logprob) return fail(MS_EINVAL, "ms_wide_act: NULL argument");
+    if (n_rows < 1 || obs_stride < a->in_dim || (obs_stride & 3))
+        return fail(MS_EINVAL, "ms_wide_act: n_rows >= 1 and obs_stride >= in_dim, multiple of 4");
+    if ((n_rows + 15) / 16 > 0x7fffffffLL || a->n_groups > 65535) return fail(MS_EINVAL, "ms_wide_act: grid too large");
+    ms::WideAct p{};
+    p.actor = wide_net(a);
+    p.D = a->in_dim;
+    p.H = a->hidden;
+    p.A = a->n_actions;
+    p.G = a->n_groups;
+    p.obs = obs;
+    p.stride = obs_stride;
+    p.E = n_rows;
+    p.uniforms = uniforms;
+    p.action = action;
+    p.logprob = logprob;
+    HIP_TRY(ms::launch_wide_act(p, (hipStream_t)stream));
+    return MS_OK;
+}
+
+// work split and workspace layout of ms_wide_grad: NB row-tile blocks per group (k_wide_rows), RS
+// row splits of the weight-gradient reductions (partials [RS][G][total], at most 1 GiB)
+struct WidePlan {
+    int NB, RS;
+    long long rps;
+    ms::WideOffsets off;
+    size_t zbuf, rec, part, loss;  // byte offsets
+    size_t bytes;
+};
+static WidePlan wide_plan(const ms_mlp_params* a, int64_t rows) {
+    const long long R = rows;
+    WidePlan w{};
+    const long long H = a->hidden, D = a->in_dim, A = a->n_actions, G = a->n_groups;
+    const long long cnt[ms::kWideSegs] = {H * D, H, H * H, H, A * H, A, H * D, H, H * H, H, H, 1};
+    w.off.o[0] = 0;
+    for (int i = 0; i < ms::kWideSegs; i++) w.off.o[i + 1] = w.off.o[i] + cnt[i];
+    const long long total = w.off.o[ms::kWideSegs];
+    const long long tiles = (R + 15) / 16;
+    const long long nb_cap = std::max(1LL, 2048 / G);
+    w.NB = (int)std::min(tiles, nb_cap);
+    long long rs = std::min(64LL, std::max(1LL, (R + 255) / 256));
+    const long long rs_mem = std::max(1LL, (1LL << 28) / (G * total));
+    rs = std::min(rs, rs_mem);
+    w.rps = ((R + rs - 1) / rs + 15) / 16 * 16;
+    w.RS = (int)((R + w.rps - 1) / w.rps);
+    const long long RW = 8 * H + ms::kWideStats;
+    size_t o = 0;
+    w.zbuf = o;
+    o += align256(sizeof(float) * (size_t)(G * w.NB * 16 * A));
+    w.rec = o;
+    o += align256(sizeof(float) * (size_t)(G * R * RW));
+    w.part = o;
+    o += align256(sizeof(float) * (size_t)(w.RS * G * total));
+    w.loss = o;
+    o += align256(sizeof(float) * (size_t)(G * w.NB * 3));
+    w.bytes = o;
+    return w;
+}
+
+size_t ms_wide_workspace_bytes(const ms_mlp_params* a, int64_t rows) {
+    if (!a || rows < 1 || a->n_groups < 1 || a->n_actions < 1 || a->in_dim < 1 ||
+        (a->hidden != 32 && a->hidden != 64))
+        return 0;
+    return wide_plan(a, rows).bytes;
+}
+
+int ms_wide_grad(const ms_mlp_params* a, const ms_mlp_params* c, const ms_wide_batch* b, float eps_clip, void* ws,
+                 size_t ws_bytes, const ms_ppo_grads* g, void* stream) {
+    if (int rc = wide_check(a, "ms_wide_grad")) return rc;
+    if (!c || !b || !g || !ws) return fail(MS_EINVAL, "ms_wide_grad: NULL argument");
+    if (!c->w1 || !c->b1 || !c->w2 || !c->b2 || !c->w3 || !c->b3 || c->hidden != a->hidden || c->n_actions != 1 ||
+        c->in_dim != a->in_dim || c->n_groups != a->n_groups)
+        return fail(MS_EINVAL, "ms_wide_grad: critic must be [D -> H -> H -> 1] with the actor's groups");
+    if (!b->states || !b->actions || !b->old_logprob || !b->returns || b->rows < 1 || b->stride < a->in_dim ||
+        (b->stride & 3))
+        return fail(MS_EINVAL, "ms_wide_grad: bad batch (rows >= 1, stride >= in_dim, multiple of 4)");
+    if (a->n_groups > 65535) return fail(MS_EINVAL, "ms_wide_grad: too many groups");
+    float* dst[ms::kWideSegs] = {g->w1, g->b1, g->w2, g->b2, g->w3, g->b3, g->cw1, g->cb1, g->cw2, g->cb2, g->cw3, g->cb3};
+    for (float* d : dst)
+        if (!d) return fail(MS_EINVAL, "ms_wide_grad: NULL gradient tensor");
+    if (!g->loss) return fail(MS_EINVAL, "ms_wide_grad: NULL loss buffer");
+    const WidePlan w = wide_plan(a, b->rows);
+    if (ws_bytes < w.bytes) return fail(MS_EINVAL, "ms_wide_grad: workspace too small (%zu < %zu)", ws_bytes, w.bytes);
+    char* base = (char*)ws;
+    ms::WideRows r{};
+    r.actor = wide_net(a);
+    r.critic = wide_net(c);
+    r.D = a->in_dim;
+    r.H = a->hidden;
+    r.A = a->n_actions;
+    r.G = a->n_groups;
+    r.states = b->states;
+    r.stride = b->stride;
+    r.R = b->rows;
+    r.actions = b->actions;
+    r.old_logprob = b->old_logprob;
+    r.returns = b->returns;
+    r.eps_clip = eps_clip;
+    r.inv_R = (float)(1.0 / (double)b->rows);
+    r.NB = w.NB;
+    r.zbuf = (float*)(base + w.zbuf);
+    r.rec = (float*)(base + w.rec);
+    r.loss_part = (float*)(base + w.loss);
+    ms::WideGrads gp{};
+    gp.actor = r.actor;
+    gp.critic = r.critic;
+    gp.D = r.D;
+    gp.H = r.H;
+    gp.A = r.A;
+    gp.G = r.G;
+    gp.states = b->states;
+    gp.stride = b->stride;
+    gp.R = b->rows;
+    gp.RS = w.RS;
+    gp.rows_per_split = w.rps;
+    gp.rec = r.rec;
+    gp.part = (float*)(base + w.part);
+    gp.off = w.off;
+    ms::WideReduce rp{};
+    rp.part = gp.part;
+    rp.RS = w.RS;
+    rp.G = r.G;
+    rp.NB = w.NB;
+    rp.off = w.off;
+    for (int i = 0; i < ms::kWideSegs; i++) rp.dst[i] = dst[i];
+    rp.loss_part = r.loss_part;
+    rp.loss = g->loss;
+    rp.inv_R = r.inv_R;
+    HIP_TRY(ms::launch_wide_grad(r, gp, rp, (hipStream_t)stream));
     return MS_OK;
 }

@@ -324,9 +324,19 @@ class LocallySharedParamsDividedFreePriceEnv(PPODividedFreePriceEnv):
     _arch = "local"
 
 
+def _int8_rows(x):
+    """[N, D] float observation rows (integer valued, as the env writes them) -> [1, N, align4(D)] int8."""
+    N, D = x.shape
+    xi = torch.zeros((1, N, (D + 3) // 4 * 4), dtype=torch.int8, device=x.device)
+    xi[0, :, :D] = x.to(torch.int8)
+    if not torch.equal(xi[0, :, :D].float(), x):
+        raise ValueError("aggregated observations must be int8-valued integers")
+    return xi
+
+
 class _AggUnits:
     """ExperienceBuffer (PPOmodules.py:9-22) of one aggregated net per agent: per round the agents'
-    states [N, D] f32, actions [N] and log-probs [N] on the device, rewards [N] on the host."""
+    int8 rows [N, stride], actions [N] int32 and log-probs [N] on the device, rewards [N] on the host."""
 
     def __init__(self, group):
         self.group = group
@@ -340,17 +350,17 @@ class _AggUnits:
         self.states, self.actions, self.logprobs, self.rewards = [], [], [], []
 
     def update(self):
-        """PPO.update (PPOmodules.py:127-174) of every agent's net: HIP returns + torch autograd / Adam."""
+        """PPO.update (PPOmodules.py:127-174) of every agent's net: HIP returns + ms_wide_grad + HIP Adam."""
         if not self.actions:
             return []
         if len(self.rewards) != len(self.actions):
             raise RuntimeError("%d rewards saved for %d actions" % (len(self.rewards), len(self.actions)))
-        x = torch.stack(self.states, 1)            # [N, T, D]
-        a = torch.stack(self.actions, 1)           # [N, T]
-        lp = torch.stack(self.logprobs, 1)
+        x = torch.stack(self.states, 0)            # [T, N, stride] int8
+        a = torch.stack(self.actions, 0)           # [T, N] int32
+        lp = torch.stack(self.logprobs, 0)
         r = torch.tensor(np.stack(self.rewards), dtype=torch.float32, device=x.device)  # [T, N]
-        ret = ppo.discounted_returns(r, self.group.gamma)  # [N, T]
-        losses = self.group.update(x, a, lp, ret)
+        ret = ppo.discounted_returns(r, self.group.gamma).contiguous()  # [N, T]
+        losses = self.group.update_wide(x, a, lp, ret)
         self.group.sync_old()
         self.clear()
         return losses
@@ -361,7 +371,7 @@ class _AggregatedPPOEnv(SchedulingEnv):
 
     Observations per agent are the aggregated rows of AggregatedAgent (Agent.py:82-134): the acceptor
     row as a 1-D float32 tensor (torch.cat onto torch.tensor([]) promotes it), the offer row as
-    int64. Actions are drawn as one number per net (PyTorch-ROCm: 32 / 64 hidden units) and decoded
+    int64. Actions are drawn as one number per net (ms_wide_act: 32 / 64 hidden units) and decoded
     on the device (ms_decode_aggregated, numberToNDimensionalAction Agent.py:644-666); rewards are
     getAggregatedFixedPricesReward's (Reward.py:92-143) from the env step."""
 
@@ -449,11 +459,12 @@ class _AggregatedPPOEnv(SchedulingEnv):
             xs = dict(acc=acc_x, off=off_x)
         for i, (k, x) in enumerate(xs.items()):
             u = self._units[k]
-            a, lp = u.group.sample(x.unsqueeze(1))  # [N, 1]
-            u.states.append(x)
-            u.actions.append(a[:, 0])
-            u.logprobs.append(lp[:, 0])
-            self._numbers[i, 0].copy_(a[:, 0])
+            xi = _int8_rows(x)  # [1, N, stride]: the nets' kernels read int8 rows
+            a, lp = u.group.wide_act(xi)  # [1, N]
+            u.states.append(xi[0])
+            u.actions.append(a[0])
+            u.logprobs.append(lp[0])
+            self._numbers[i, 0].copy_(a[0])
         self._bad.zero_()  # per call: one illegal number raises for that call only
         acc, off = eng.env.decode_aggregated(self._numbers, self._fully, n_bad=self._bad)
         acc_h, off_h = acc[0].cpu().tolist(), off[0].cpu().tolist()

@@ -399,14 +399,74 @@ class PPOGroup:
         return self._hip_opt
 
     @torch.no_grad()
-    def sample(self, x, generator=None):
-        """PPO.selectAction + ActorCritic.act (PPOmodules.py:53-63, 114-125) in PyTorch-ROCm for nets the
-        16-wide HIP kernels do not cover (the aggregated agents' 32 / 64 hidden units and (O+1)^C
-        actions): x [G, R, D] float on the device -> (actions [G, R] long, log-probs [G, R] f32) from
-        policy_old, torch's Categorical (probs renormalised, multinomial sampling)."""
-        dist = Categorical(self.policy_old.actor_probs(x))
-        a = dist.sample()
-        return a, dist.log_prob(a)
+    def wide_act(self, obs_i8, uniforms=None, action=None, logprob=None, generator=None, stream=None):
+        """PPO.selectAction + ActorCritic.act (PPOmodules.py:53-63, 114-125) of the aggregated agents'
+        nets (32 / 64 hidden units, (O+1)^C-sized action spaces; ms_wide_act): row (e, g) of obs
+        [E, G, stride] int8 through group g's policy_old, the action drawn by inverse CDF at
+        uniforms [E, G] (default: torch.rand on the device). Returns (action int32 [E, G],
+        log-prob f32 [E, G]), written into ``action`` / ``logprob`` when given."""
+        E, G, stride = obs_i8.shape
+        pol = self.policy_old
+        assert G == pol.G and obs_i8.dtype == torch.int8 and obs_i8.is_contiguous() and stride >= pol.D
+        dev = obs_i8.device
+        if uniforms is None:
+            uniforms = torch.rand((E, G), device=dev, generator=generator)
+        assert uniforms.shape == (E, G) and uniforms.dtype == torch.float32 and uniforms.is_contiguous()
+        if action is None:
+            action = torch.empty((E, G), dtype=torch.int32, device=dev)
+        if logprob is None:
+            logprob = torch.empty((E, G), dtype=torch.float32, device=dev)
+        assert action.dtype == torch.int32 and action.is_contiguous() and action.shape == (E, G)
+        assert logprob.dtype == torch.float32 and logprob.is_contiguous() and logprob.shape == (E, G)
+        check(lib.ms_wide_act(ct.byref(pol.mlp_params()), ptr(obs_i8), stride, E, ptr(uniforms), ptr(action),
+                              ptr(logprob), stream_ptr(stream)))
+        return action, logprob
+
+    def wide_epoch(self, states_i8, actions_i32, old_logprobs, returns_gr, stream=None):
+        """The gradient half of one K-epoch step of ``update_wide`` (ms_wide_grad): returns a function
+        that writes the epoch's gradient into ``policy``'s .grad tensors and returns the per-group loss."""
+        R, G, stride = states_i8.shape
+        pol = self.policy
+        assert G == pol.G and states_i8.dtype == torch.int8 and states_i8.is_contiguous()
+        assert actions_i32.shape == (R, G) and actions_i32.dtype == torch.int32 and actions_i32.is_contiguous()
+        assert old_logprobs.shape == (R, G) and old_logprobs.is_contiguous()
+        assert returns_gr.shape == (G, R) and returns_gr.is_contiguous()
+        for prm in pol.parameters():
+            if prm.grad is None:
+                prm.grad = torch.zeros_like(prm)
+        dev = states_i8.device
+        loss_buf = torch.empty((G, 3), dtype=torch.float32, device=dev)
+        a = pol.mlp_params()
+        c = pol.critic_mlp_params()
+        ws_bytes = lib.ms_wide_workspace_bytes(ct.byref(a), R)
+        ws = torch.empty(((ws_bytes + 3) // 4,), dtype=torch.float32, device=dev)
+        batch = abi.MsWideBatch(ptr(states_i8), ptr(actions_i32), ptr(old_logprobs), ptr(returns_gr), stride, R)
+        grads = abi.MsPpoGrads(*[ptr(getattr(pol, k).grad) for k in ACTOR_KEYS + CRITIC_KEYS], ptr(loss_buf))
+        keep = (states_i8, actions_i32, old_logprobs, returns_gr, ws, loss_buf)  # the structs' pointees
+
+        def run():
+            assert keep
+            check(lib.ms_wide_grad(ct.byref(a), ct.byref(c), ct.byref(batch), ct.c_float(self.eps_clip), ptr(ws),
+                                   ws_bytes, ct.byref(grads), stream_ptr(stream)))
+            return loss_buf[:, 0] + 0.5 * loss_buf[:, 1] - 0.01 * loss_buf[:, 2]
+
+        return run
+
+    def update_wide(self, states_i8, actions_i32, old_logprobs, returns_gr, stream=None):
+        """K epochs of PPO.update (PPOmodules.py:127-174) for the aggregated agents' nets: the gradient
+        of each group's mean loss from ms_wide_grad (HIP), all-reduced across ranks when set, then
+        the HIP Adam. states_i8 [R, G, stride] int8 rows, actions [R, G] int32, old_logprobs [R, G]
+        f32, returns [G, R] f32 normalised (discounted_returns). Returns the K per-group losses."""
+        epoch = self.wide_epoch(states_i8, actions_i32, old_logprobs, returns_gr, stream)
+        losses = []
+        for _ in range(self.K):
+            loss = epoch()
+            if self.allreduce is not None:
+                self.allreduce(self.policy.parameters())
+            self.hip_optimizer.step(stream)
+            losses.append(loss)
+        self.last_losses = losses
+        return losses
 
     @torch.no_grad()
     def sync_old(self):

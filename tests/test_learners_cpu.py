@@ -79,6 +79,7 @@ def test_branching_update_matches_reference_on_cpu():
             self.cfg = a[3]
             self.opt = torch.optim.Adam(self.q.parameters(), lr=a[3].lr)
             self.update_counter = 0
+            self.graph = False  # eager update (the HIP-graph capture needs a GPU)
 
     torch.manual_seed(2)
     obs, ac, n, B = 12, 3, 7, 32
