@@ -435,11 +435,12 @@ class Trainer:
 
     def update(self):
         """env.updateAgents() (SchedulingEnvironment.py:208-210 / 314-329, Agent.py:524-529,708-728).
-        With use_graph on one rank the fused update is captured into a HIP graph after its first
-        (eager) run and replayed from then on: only this iteration's sub-unit draws are copied to
-        the device first. The returned losses are then the graph's own tensors (overwritten by
-        the next update)."""
-        if self.use_graph and self.fused and self.world_size == 1:
+        With use_graph the fused update is captured into HIP graphs after its first (eager) run and
+        replayed from then on: only this iteration's sub-unit draws are copied to the device
+        first. One rank: one graph. Several ranks: one graph per stretch between two gradient
+        all-reduces, the RCCL calls eager in between (_capture_update). The returned losses are
+        copies of the graph's own tensors."""
+        if self.use_graph and self.fused:
             return self._update_graphed()
         sel = self._draws()
         if self.fused:
@@ -486,26 +487,57 @@ class Trainer:
             losses = self._fused_update(views, self._sel_counts)  # this iteration's update
             eager_last = {u.name: u.group.last_losses for u in self.units()}
             torch.cuda.synchronize(self.device)
-            g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g):
-                self._graph_losses = self._fused_update(views, self._sel_counts)
+            self._graph_losses = self._capture_update(views)
             self._graph_last = {u.name: list(u.group.last_losses) for u in self.units()}
             for u in self.units():  # the eager run's own losses until the first replay
                 u.group.last_losses = eager_last[u.name]
-            self.update_graph = g
             return losses
-        self.update_graph.replay()
+        self._replay_update()
         # the graph's loss tensors are overwritten by every replay: hand out copies (G floats per
         # unit type), so losses a caller keeps from earlier iterations stay what they were
         for u in self.units():
             u.group.last_losses = [x.clone() for x in self._graph_last[u.name]]
         return {k: v.clone() for k, v in self._graph_losses.items()}
 
+    def _capture_update(self, views):
+        """Capture the fused update: segment i = the kernels between all-reduce i-1 and i (one
+        segment on one rank), all in one memory pool. Returns the graph's loss tensors."""
+        out, graphs, params = {}, [], []
+        phases = self._fused_phases(views, self._sel_counts, out)
+        pool = None
+        while True:
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, pool=pool):
+                p = next(phases, None)
+            if pool is None:
+                pool = g.pool()
+            graphs.append(g)
+            if p is None:
+                break
+            params.append(p)
+        self.update_graph = graphs
+        self._graph_params = params
+        return out["losses"]
+
+    def _replay_update(self):
+        for i, g in enumerate(self.update_graph):
+            g.replay()
+            if i < len(self._graph_params):
+                self._allreduce(self._graph_params[i])
+
     def _fused_update(self, all_sel, counts):
         """The fused update: all_sel[name] = int32 device [sum of draws' G] sub-units, counts[name]
         = each draw's number of groups."""
         if self.world_size == 1 and self.update_streams:
             return self._fused_update_streams(all_sel, counts)
+        out = {}
+        for params in self._fused_phases(all_sel, counts, out):
+            self._allreduce(params)
+        return out["losses"]
+
+    def _fused_phases(self, all_sel, counts, out):
+        """_fused_update as a generator: yields the parameters whose gradients the ranks all-reduce
+        (several ranks only) and leaves the losses in out["losses"]."""
         T, E = self.T, self.E
         losses = {}
         # Each unit type's draws update its nets in sequence (draw d trains on the weights draw d-1
@@ -533,7 +565,7 @@ class Trainer:
             for u, seq, ls in live:
                 ls.append(seq[s]())
             if self.world_size > 1:
-                self._allreduce([p for u, _, _ in live for p in u.group.policy.parameters()])
+                yield [p for u, _, _ in live for p in u.group.policy.parameters()]
             for u, _, _ in live:
                 u.group.hip_optimizer.step()
         for u, _, ls in steps.values():
@@ -541,7 +573,7 @@ class Trainer:
             u.group.sync_old()
             losses[u.name] = torch.stack(ls)
         self._carry_last_observation()
-        return losses
+        out["losses"] = losses
 
     def _epochs(self, u, sel_u, counts_u):
         """The gradient closures of unit type u's K epochs of every draw, in order."""

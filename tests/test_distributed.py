@@ -74,22 +74,22 @@ def test_rank_env_seeds_are_disjoint():
             assert spans[i][1] <= spans[j][0] or spans[j][1] <= spans[i][0]
 
 
-def _trainer_rank(rank, world, port, out_dir):
+def _trainer_rank(rank, world, port, out_dir, use_graph=False, iters=2):
     import torch.distributed as dist
 
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     tr = importlib.import_module("marl-scheduling_amd.trainer")
     t = tr.Trainer.from_named("cfg3", n_envs=32, update_step=12, seed=3, rank=rank, world_size=world,
-                              use_graph=False)
-    t.iteration()
-    t.iteration()
+                              use_graph=use_graph)
+    for _ in range(iters):
+        t.iteration()
     out = {}
     for u in t.units():
         for k, v in u.group.policy.named_parameters():
             out[u.name + "." + k] = v.detach().cpu().clone()
     out["flags"] = torch.tensor(t.flags())
-    torch.save(out, os.path.join(out_dir, "trainer%d.pt" % rank))
+    torch.save(out, os.path.join(out_dir, "trainer%s%d.pt" % ("_graph" if use_graph else "", rank)))
     dist.destroy_process_group()
 
 
@@ -102,3 +102,18 @@ def test_two_rank_trainer_stays_in_lockstep(tmp_path):
     assert int(w0.pop("flags")) == 0 and int(w1.pop("flags")) == 0
     for k in w0:
         assert torch.equal(w0[k], w1[k]), k
+
+
+@pytest.mark.gpu
+def test_two_rank_graphed_update_equals_eager(tmp_path):
+    """Several ranks: the update replays one HIP graph per stretch between all-reduces, the
+    collectives eager in between (Trainer._capture_update). Three iterations (eager + capture,
+    then two replays) end on the same weights as the eager update, bit for bit, on both ranks."""
+    mp.spawn(_trainer_rank, args=(2, _free_port(), str(tmp_path), True, 3), nprocs=2, join=True)
+    mp.spawn(_trainer_rank, args=(2, _free_port(), str(tmp_path), False, 3), nprocs=2, join=True)
+    for r in range(2):
+        g = torch.load(tmp_path / ("trainer_graph%d.pt" % r), weights_only=True)
+        e = torch.load(tmp_path / ("trainer%d.pt" % r), weights_only=True)
+        assert int(g.pop("flags")) == 0 and int(e.pop("flags")) == 0
+        for k in e:
+            assert torch.equal(g[k], e[k]), (r, k)
