@@ -295,6 +295,7 @@ def bench_other(args):
         launch_us = tr.launch_spans_us()
         b_round = env_round_bytes(tr.env.shape, tr.cfg.new_jobs_per_round, tr.free, tr.compact)
         result["roofline"] = env_roofline(b_round, E, launch_us, tr.compact)
+        result["act_roofline"] = act_roofline(tr, device)
     if rank == 0:
         print(json.dumps(result))
     if world > 1:
@@ -328,6 +329,63 @@ def bdqn_act_roofline(tr, device, reps: int = 10):
             "peak": F32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": achieved / F32_MFMA_PEAK_TFLOPS, "traffic": None,
             "flops_per_launch": flops, "avg_launch_us": sec * 1e6, "rows_per_launch": rows,
             "launch_timing": "HIP events around %d launches on the trainer's last h1, after the timed region" % reps}
+
+
+def act_roofline(tr, device, reps: int = 20):
+    """One round's acting launch(es) of the PPO trainer (replica part 0: k_act_pair at cfg3) timed
+    with HIP events around graph replays of `reps` repeats of round 0, after the timed region.
+    Algorithmic flops = 2 (D*16 + 16*16 + 16*A) per row that runs through the MFMA tiles: every
+    offer (core chooser) row and, with compact acceptor rows, one owner row per core (the foreign
+    rows are sampled from the group's common row; the price chooser from its table), against the
+    dense f32 MFMA peak. The kernel is VALU-issue bound (softmax, sampling, input packing), so the
+    fraction says how much of the matrix peak acting reaches, not what bounds it."""
+    import torch
+
+    e0, e1 = tr.env.parts[0][1], tr.env.parts[0][2]
+    E, N, C, L = e1 - e0, tr.N, tr.C, tr.L
+    # round 0's act, `reps` times in one HIP graph (as the rollout replays it: eager launches from
+    # Python would time the host), on a stream of its own
+    st = torch.cuda.Stream(device)
+    saved = tr.streams[0]
+    tr.streams[0] = st
+    try:
+        with torch.cuda.stream(st):
+            tr._act_part(0, 0)  # warm
+        st.synchronize()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=st):
+            for _ in range(reps):
+                tr._act_part(0, 0)
+    finally:
+        tr.streams[0] = saved
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    with torch.cuda.stream(st):
+        g.replay()
+        ev[0].record(st)
+        for _ in range(5):
+            g.replay()
+        ev[1].record(st)
+    ev[1].synchronize()
+    sec = ev[0].elapsed_time(ev[1]) / 1e3 / (5 * reps)
+    fl = lambda g: 2.0 * (g.D * g.H + g.H * g.H + g.H * g.A)
+    off = tr.off.group.policy_old
+    acc = tr.acc.group.policy_old
+    off_rows = E * N * L
+    acc_rows = E * C if tr.compact else E * N * C
+    flops = fl(off) * off_rows + fl(acc) * acc_rows
+    ref_flops = fl(off) * off_rows + fl(acc) * E * N * C
+    if tr.free:
+        ref_flops += fl(tr.price.group.policy_old) * off_rows
+    achieved = flops / sec / 1e12
+    kern = ("ms::k_act_pair (offer + price table + compact acceptors, one launch)" if tr.compact and tr.free
+            else "ms::k_act (offers) + ms::k_act / k_act_common (acceptors)")
+    return {"kernel": kern, "bound": "mfma",
+            "achieved": achieved, "peak": F32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
+            "frac": achieved / F32_MFMA_PEAK_TFLOPS, "traffic": None, "flops_per_launch": flops,
+            "mfma_rows": {"offer": off_rows, "acceptor": acc_rows},
+            "reference_flops_per_launch": ref_flops, "avg_launch_us": sec * 1e6,
+            "launch_timing": "HIP events around 5 replays of a HIP graph of %d repeats of round 0's act, "
+                             "after the timed region" % reps}
 
 
 def env_roofline(b_round: int, envs: int, launch_us, compact: bool, variant_traffic: bool = True):
@@ -631,6 +689,7 @@ def main():
                             + (", %d streams" % args.rollout_streams if args.rollout_streams > 1 else ""),
         },
     }
+    result["act_roofline"] = act_roofline(tr, device)
     if not args.no_step_kernel:
         del tr  # the trainer's rings are not needed by the step-kernel run
         torch.cuda.empty_cache()

@@ -301,6 +301,11 @@ class Trainer:
             self._round_part(t, k)
 
     def _round_part(self, t: int, k: int):
+        self._act_part(t, k)
+        self._step_part(t, k)
+
+    def _act_part(self, t: int, k: int):
+        """getActionForAllAgents of round t for replica part k (on stream k)."""
         env, e0, e1 = self.env.parts[k]
         st = self.streams[k]
         E, N, C, L = e1 - e0, self.N, self.C, self.L
@@ -343,6 +348,13 @@ class Trainer:
             self.acc.group.policy_old.act(sl(self.acc_obs[t]), N * C, seed, base + 3, action=sl(self.acc.actions[t]),
                                           logprob=sl(self.acc.logprobs[t]), offset_dev=self.rng_ctr,
                                           common_row=self.acc_common if self.common_rows else None, stream=st)
+
+    def _step_part(self, t: int, k: int):
+        """env.step + saveRewards of round t for replica part k (on stream k)."""
+        env, e0, e1 = self.env.parts[k]
+        st = self.streams[k]
+        E, N, C, L = e1 - e0, self.N, self.C, self.L
+        sl = lambda x: x[e0:e1]
         obs = dict(self._acc_out(t + 1, e0, e1), offer=sl(self.off_obs[t + 1]))
         rew = dict(offer=sl(self.off.rewards[t]).view(E, N, L), acceptor=sl(self.acc.rewards[t]).view(E, N, C),
                    agent=sl(self.agent_reward), auctioneer=sl(self.auct_reward),
