@@ -35,6 +35,20 @@ __device__ __forceinline__ float rows_sum(float v) {
     swap32(__float_as_uint(s), a, b);
     return __uint_as_float(a) + __uint_as_float(b);
 }
+// rows_sum of two values at once (three swaps instead of four, bit-identical to rows_sum of each):
+// swap16(x, y) leaves rows (x0, y0, x2, y2) and (x1, y1, x3, y3), whose sum holds x's pair sums in
+// rows 0 / 2 and y's in rows 1 / 3; swap32 + add gives the totals (x, y, x, y), and one more swap16
+// spreads each over all four rows
+__device__ __forceinline__ void rows_sum2(float& x, float& y) {
+    const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(y), false, false);
+    const float s = __uint_as_float(r[0]) + __uint_as_float(r[1]);
+    uint32_t a, b;
+    swap32(__float_as_uint(s), a, b);
+    const float t = __uint_as_float(a) + __uint_as_float(b);
+    swap16(__float_as_uint(t), a, b);
+    x = __uint_as_float(a);
+    y = __uint_as_float(b);
+}
 __device__ __forceinline__ float rows_max(float v) {
     uint32_t a, b;
     swap16(__float_as_uint(v), a, b);

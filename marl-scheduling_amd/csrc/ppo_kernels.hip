@@ -147,7 +147,9 @@ __global__ void __launch_bounds__((64 * GradLds<NQ, NT, MODE>::WPB), ((NQ * NT >
     using L = GradLds<NQ, NT, MODE>;
     constexpr int TP = L::TP, TP2 = L::TP2, XPD = L::XPD, S1 = L::S1, W1B = L::W1B;
     constexpr int NTH = 64 * L::WPB, CPW = 4 / L::WPB;  // threads per block, chunks per wave
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    // the wave index through readfirstlane: everything derived from it (chunk, tile range, row buffers)
+    // is wave-uniform to the compiler and lives in scalar registers
+    const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int g4 = lane >> 4;  // MFMA k-group / C-row group
     const int j = lane & 15;   // batch row within the tile (C column)
     // groups interleaved over the block index: the G groups' blocks of the same rows run at the
@@ -303,11 +305,11 @@ __global__ void __launch_bounds__((64 * GradLds<NQ, NT, MODE>::WPB), ((NQ * NT >
 #pragma unroll
             for (int q = 0; q < 4; q++) z[t][q] = zz[q] + sb3[16 * t + 4 * g4 + q];
         }
-        // critic output V (one row of the last layer, summed across the 4 lane groups)
+        // critic output V (one row of the last layer, summed across the 4 lane groups together with
+        // the softmax denominator below)
         float vp = 0.f;
 #pragma unroll
         for (int q = 0; q < 4; q++) vp = fmaf(sc3[4 * g4 + q], f.hc2[q], vp);
-        f.V = xsum4g(vp) + scb3[0];
         float mx = -INFINITY;
 #pragma unroll
         for (int t = 0; t < NT; t++)
@@ -324,7 +326,9 @@ __global__ void __launch_bounds__((64 * GradLds<NQ, NT, MODE>::WPB), ((NQ * NT >
                 f.pe[t][q] = (16 * t + 4 * g4 + q < A) ? fast_exp_sub(z[t][q], mx_l2e) : 0.f;
                 s0 += f.pe[t][q];
             }
-        const float inv0 = __builtin_amdgcn_rcpf(xsum4g(s0));
+        rows_sum2(s0, vp);
+        f.V = vp + scb3[0];
+        const float inv0 = __builtin_amdgcn_rcpf(s0);
         float s1 = 0.f;
 #pragma unroll
         for (int t = 0; t < NT; t++)
@@ -343,8 +347,9 @@ __global__ void __launch_bounds__((64 * GradLds<NQ, NT, MODE>::WPB), ((NQ * NT >
                 f.cl[t][q] = fast_log(fminf(fmaxf(f.pn[t][q], eps), 1.f - eps));
                 if (16 * t + 4 * g4 + q < A) ent -= f.cl[t][q] * f.pn[t][q];
             }
-        f.ent = xsum4g(ent);
+        f.ent = ent;  // this lane's part: the row's entropy is xsum4g(f.ent) (ent_of)
     };
+    auto ent_of = [&](const Fwd& f) { return xsum4g(f.ent); };
 
     // ---- one 16-row tile: forward, per-row loss derivatives, backward, weight gradients.
     //      xr = the rows' raw dwords (B-fragment layout), act/olp/G/valid = row j's scalars.
@@ -381,7 +386,8 @@ __global__ void __launch_bounds__((64 * GradLds<NQ, NT, MODE>::WPB), ((NQ * NT >
 #pragma unroll
                 for (int q = 0; q < 4; q++)
                     if (16 * t + 4 * g4 + q < A && 16 * t + 4 * g4 + q == act) lp += f.cl[t][q];
-            lp = xsum4g(lp);
+            float ent = f.ent;
+            rows_sum2(lp, ent);  // the action's log-prob and the row's entropy
             // ---- per-row loss derivatives (loss.mean() over R rows)
             const float ratio = fast_exp(lp - olp);
             const float adv = G - V;
@@ -398,26 +404,49 @@ __global__ void __launch_bounds__((64 * GradLds<NQ, NT, MODE>::WPB), ((NQ * NT >
             if (valid && g4 == 0) {
                 l_min += -fminf(sur1, sur2);
                 l_mse += (V - G) * (V - G);
-                l_ent += f.ent;
+                l_ent += ent;
             }
         }
         // d loss / d pn  -> d / d p (renormalisation) -> d / d z (softmax)
         float gz[NT][4], x1 = 0.f;
+        if constexpr (VIRT) {
 #pragma unroll
-        for (int t = 0; t < NT; t++)
+            for (int t = 0; t < NT; t++)
 #pragma unroll
-            for (int q = 0; q < 4; q++) {
-                const int a = 16 * t + 4 * g4 + q;
-                float v = 0.f;
-                if (a < A) {
-                    const float dl = VIRT ? vsum[t][q] : (a == act ? g_lp : 0.f);
-                    const float dc = dl - g_h * f.pn[t][q];
-                    const float in = (f.pn[t][q] >= eps && f.pn[t][q] <= 1.f - eps) ? 1.f : 0.f;
-                    v = dc * in * __builtin_amdgcn_rcpf(fminf(fmaxf(f.pn[t][q], eps), 1.f - eps)) - g_h * f.cl[t][q];
+                for (int q = 0; q < 4; q++) {
+                    const int a = 16 * t + 4 * g4 + q;
+                    float v = 0.f;
+                    if (a < A) {
+                        const float dc = vsum[t][q] - g_h * f.pn[t][q];
+                        const float in = (f.pn[t][q] >= eps && f.pn[t][q] <= 1.f - eps) ? 1.f : 0.f;
+                        v = dc * in * __builtin_amdgcn_rcpf(fminf(fmaxf(f.pn[t][q], eps), 1.f - eps)) -
+                            g_h * f.cl[t][q];
+                    }
+                    gz[t][q] = v;
+                    x1 += v * f.pe[t][q];
                 }
-                gz[t][q] = v;
-                x1 += v * f.pe[t][q];
-            }
+        } else {
+            // one row's loss touches the log-prob of its own action only: d/d pn_a of
+            // g_lp * log(clamp(pn_act)) - g_h * H is (g_lp / pn_act at a = act) - g_h (in range),
+            // - g_h * cl_a throughout; the one reciprocal per lane is of its copy of pn_act
+            float pa = 1.f;
+#pragma unroll
+            for (int t = 0; t < NT; t++)
+#pragma unroll
+                for (int q = 0; q < 4; q++) pa = (16 * t + 4 * g4 + q == act) ? f.pn[t][q] : pa;
+            const float dact = g_lp * __builtin_amdgcn_rcpf(pa);
+#pragma unroll
+            for (int t = 0; t < NT; t++)
+#pragma unroll
+                for (int q = 0; q < 4; q++) {
+                    const int a = 16 * t + 4 * g4 + q;
+                    const bool in = f.pn[t][q] >= eps && f.pn[t][q] <= 1.f - eps;
+                    const float d_in = (a == act ? dact : 0.f) - g_h;
+                    const float v = a < A ? fmaf(-g_h, f.cl[t][q], in ? d_in : 0.f) : 0.f;
+                    gz[t][q] = v;
+                    x1 += v * f.pe[t][q];
+                }
+        }
         x1 = xsum4g(x1);
         const float inv1 = f.inv1;
         float x2 = 0.f;
@@ -589,23 +618,58 @@ __global__ void __launch_bounds__((64 * GradLds<NQ, NT, MODE>::WPB), ((NQ * NT >
     };
 
     // lane (j, g4) loads dwords 8s + 2*g4 + {0, 1} of row r (its bf16 B fragment of k-step s) and
-    // row r's scalars (register prefetch: issued before the current tile is processed)
+    // row r's scalars (register prefetch: issued before the current tile is processed).
+    // The rollout arrays are read as raw buffers whose base is a wave-uniform first row r0 (the
+    // descriptors are built on the scalar unit): a lane's load is a 32-bit offset (r - r0) * row
+    // bytes, with no 64-bit address arithmetic per row, and rows at or past R read 0.
     uint32_t pre[S1][2];
     int pre_act = 0;
     float pre_olp = 0.f, pre_G = 0.f;
-    auto prefetch_row = [&](int r) {  // r in [0, R)
-        const uint32_t* src = row_src(r);
+    const int st_rb = (MODE == kOwnerRow ? p.owner_C : (int)p.rrs) * p.stride;  // bytes between rows
+    const int ac_rb = (int)p.rrs, lp_rb = 4 * (int)p.rrs, rt_rb = 4 * p.ret_ld;
+    const int8_t* st_base =
+        MODE == kOwnerRow ? p.states + (size_t)own_c * p.stride : p.states + (size_t)u * (size_t)p.rus * p.stride;
+    const int8_t* ac_base = p.actions + (size_t)u * (size_t)p.rus;
+    const float* lp_base = p.old_lp + (size_t)u * (size_t)p.rus;
+    const float* rt_base = p.ret + grp;
+    struct RowBufs {
+        __amdgpu_buffer_rsrc_t st, ac, lp, rt;
+    };
+    // rows per descriptor before its byte count passes 2^31 - 1 (32-bit scalar compares in the loop)
+    const int lim_st = 0x7fffffff / st_rb, lim_lp = 0x7fffffff / max(lp_rb, rt_rb);
+    auto row_bufs = [&](int r0) {  // r0 wave-uniform
+        const int nrow = max(R - r0, 0);
+        auto mk = [&](const void* base, int step, int lim) {
+            const int n = nrow > lim ? 0x7fffffff : nrow * step;
+            return __builtin_amdgcn_make_buffer_rsrc(
+                const_cast<void*>(reinterpret_cast<const void*>(reinterpret_cast<const int8_t*>(base) +
+                                                                (long long)r0 * step)),
+                0, n, 0x00020000);
+        };
+        RowBufs b;
+        b.st = mk(st_base, st_rb, lim_st);
+        b.ac = mk(ac_base, ac_rb, lim_lp);
+        b.lp = mk(lp_base, lp_rb, lim_lp);
+        b.rt = mk(rt_base, rt_rb, lim_lp);
+        return b;
+    };
+    int ccol[S1][2];  // this lane's dword columns of a row (clamped: the bytes past the row meet zero weights)
+#pragma unroll
+    for (int s = 0; s < S1; s++)
+#pragma unroll
+        for (int h = 0; h < 2; h++) {
+            const int cc = 8 * s + 2 * g4 + h;
+            ccol[s][h] = 4 * (cc < stride4 ? cc : stride4 - 1);
+        }
+    auto prefetch_rel = [&](const RowBufs& b, uint32_t rel) {  // row r0 + rel of b
 #pragma unroll
         for (int s = 0; s < S1; s++)
 #pragma unroll
-            for (int h = 0; h < 2; h++) {
-                const int cc = 8 * s + 2 * g4 + h;
-                pre[s][h] = src[cc < stride4 ? cc : stride4 - 1];  // clamped, masked at the use
-            }
-        const size_t ri = ru_index(p, r, u);
-        pre_act = p.actions[ri];
-        pre_olp = p.old_lp[ri];
-        pre_G = p.ret[(size_t)r * p.ret_ld + grp];
+            for (int h = 0; h < 2; h++)
+                pre[s][h] = __builtin_amdgcn_raw_buffer_load_b32(b.st, (int)(__umul24(rel, st_rb) + ccol[s][h]), 0, 0);
+        pre_act = (int8_t)__builtin_amdgcn_raw_buffer_load_b8(b.ac, (int)__umul24(rel, ac_rb), 0, 0);
+        pre_olp = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(b.lp, (int)__umul24(rel, lp_rb), 0, 0));
+        pre_G = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(b.rt, (int)__umul24(rel, rt_rb), 0, 0));
     };
 
     if constexpr (MODE == kKeyFwd || MODE == kKeyBack) {
@@ -635,6 +699,7 @@ __global__ void __launch_bounds__((64 * GradLds<NQ, NT, MODE>::WPB), ((NQ * NT >
             if constexpr (MODE == kKeyFwd) {
                 Fwd f;
                 forward(xr, f);
+                const float ent_row = ent_of(f);  // (a cross-lane sum: outside the branches)
                 if (occ) {
                     float* dst = p.key_fwd + (gr + rank) * KF;
 #pragma unroll
@@ -643,7 +708,7 @@ __global__ void __launch_bounds__((64 * GradLds<NQ, NT, MODE>::WPB), ((NQ * NT >
                         for (int q = 0; q < 4; q++) dst[16 * t + 4 * g4 + q] = f.cl[t][q];
                     if (g4 == 0) {
                         dst[16 * NT] = f.V;
-                        dst[16 * NT + 1] = f.ent;
+                        dst[16 * NT + 1] = ent_row;
                     }
                 }
             } else {
@@ -695,10 +760,9 @@ __global__ void __launch_bounds__((64 * GradLds<NQ, NT, MODE>::WPB), ((NQ * NT >
             }
         }
     } else if constexpr (MODE == kPlain) {
-        // rows past the end load row 0's values: their loss weight is 0, so every derivative of
+        // rows past the end read zeros (row_bufs): their loss weight is 0, so every derivative of
         // theirs is exactly 0 (all inputs finite)
-        auto row_of_tile = [&](int tile) { return tile * 16 + j < R ? tile * 16 + j : 0; };
-        if (tile0 < tile_end) prefetch_row(row_of_tile(tile0));
+        if (tile0 < tile_end) prefetch_rel(row_bufs(16 * tile0), (uint32_t)j);
         for (int tile = tile0; tile < tile_end; tile++) {
             const int half = (tile - tile0) & 1;  // position in the tile pair of the dW1 step
             uint32_t xr[S1][2];
@@ -707,7 +771,7 @@ __global__ void __launch_bounds__((64 * GradLds<NQ, NT, MODE>::WPB), ((NQ * NT >
             const bool valid = tile * 16 + j < R;
             const int act = pre_act;
             const float olp = pre_olp, G = pre_G;
-            if (tile + 1 < tile_end) prefetch_row(row_of_tile(tile + 1));
+            if (tile + 1 < tile_end) prefetch_rel(row_bufs(16 * (tile + 1)), (uint32_t)j);
             tile_step(BoolC<false>{}, xr, act, olp, G, valid, half, half == 1 || tile + 1 == tile_end, zero_vs, 0.f,
                       0.f);
         }
@@ -741,6 +805,7 @@ __global__ void __launch_bounds__((64 * GradLds<NQ, NT, MODE>::WPB), ((NQ * NT >
                 }
             Fwd f;
             forward(xw, f);
+            const float ent_row = ent_of(f);
             if (j == 0) {
 #pragma unroll
                 for (int t = 0; t < NT; t++)
@@ -748,7 +813,7 @@ __global__ void __launch_bounds__((64 * GradLds<NQ, NT, MODE>::WPB), ((NQ * NT >
                     for (int q = 0; q < 4; q++) sCm[16 * t + 4 * g4 + q] = f.cl[t][q];
                 if (g4 == 0) {
                     sCm[16 * NT] = f.V;
-                    sCm[16 * NT + 1] = f.ent;
+                    sCm[16 * NT + 1] = ent_row;
                 }
             }
             __builtin_amdgcn_wave_barrier();
@@ -776,21 +841,27 @@ __global__ void __launch_bounds__((64 * GradLds<NQ, NT, MODE>::WPB), ((NQ * NT >
         int s_act[PF];
         int8_t s_own[PF];
         float s_olp[PF], s_G[PF];
+        // the wave's rows as raw buffers from row rb (32-bit per-lane offsets)
+        const RowBufs wb = row_bufs(rb);
+        const __amdgpu_buffer_rsrc_t ob =
+            __builtin_amdgcn_make_buffer_rsrc(const_cast<int8_t*>(MODE == kOwnerRow ? p.owner + (size_t)rb * p.owner_C + own_c
+                                                                                     : p.actions),
+                                              0, MODE == kOwnerRow ? (int)((re - rb) * p.owner_C) : 0, 0x00020000);
         auto load_slot = [&](int k, int r0, int lim) {
             if constexpr (MODE == kCommonRow)
                 cs.load_into(sc[k], [&](int q) { return row_src(r0 + q < lim ? r0 + q : rb); }, lane);
             const int r = r0 + lane;
-            const int rr = r < lim ? r : rb;
-            if constexpr (MODE == kOwnerRow) s_own[k] = p.owner[(size_t)rr * p.owner_C + own_c];
-            const size_t ri = ru_index(p, rr, u);
-            s_act[k] = p.actions[ri];
-            s_olp[k] = p.old_lp[ri];
-            s_G[k] = p.ret[(size_t)rr * p.ret_ld + grp];
+            const uint32_t rel = (uint32_t)((r < lim ? r : rb) - rb);
+            if constexpr (MODE == kOwnerRow)
+                s_own[k] = (int8_t)__builtin_amdgcn_raw_buffer_load_b8(ob, (int)__umul24(rel, p.owner_C), 0, 0);
+            s_act[k] = (int8_t)__builtin_amdgcn_raw_buffer_load_b8(wb.ac, (int)__umul24(rel, ac_rb), 0, 0);
+            s_olp[k] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(wb.lp, (int)__umul24(rel, lp_rb), 0, 0));
+            s_G[k] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(wb.rt, (int)__umul24(rel, rt_rb), 0, 0));
         };
         // the listed rows t0 .. t0 + 16*n - 1 (the last tile may be partial: cnt rows in all) in
         // 16-row tiles, the next tile's rows prefetched
         auto owner_tiles = [&](int cnt) {
-            auto pf = [&](int t0) { prefetch_row(list[t0 + (t0 + j < cnt ? j : 0)]); };
+            auto pf = [&](int t0) { prefetch_rel(wb, (uint32_t)(list[t0 + (t0 + j < cnt ? j : 0)] - rb)); };
             pf(0);
             for (int t0 = 0; t0 < cnt; t0 += 16) {
                 uint32_t xr[S1][2];
