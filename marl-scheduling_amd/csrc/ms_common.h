@@ -49,6 +49,26 @@ __device__ __forceinline__ void rows_sum2(float& x, float& y) {
     x = __uint_as_float(a);
     y = __uint_as_float(b);
 }
+__device__ __forceinline__ void rows_max2(float& x, float& y) {
+    const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(y), false, false);
+    const float s = fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+    uint32_t a, b;
+    swap32(__float_as_uint(s), a, b);
+    const float t = fmaxf(__uint_as_float(a), __uint_as_float(b));
+    swap16(__float_as_uint(t), a, b);
+    x = __uint_as_float(a);
+    y = __uint_as_float(b);
+}
+__device__ __forceinline__ void rows_sum2_i(int& x, int& y) {
+    const auto r = __builtin_amdgcn_permlane16_swap((uint32_t)x, (uint32_t)y, false, false);
+    const int s = (int)r[0] + (int)r[1];
+    uint32_t a, b;
+    swap32((uint32_t)s, a, b);
+    const int t = (int)a + (int)b;
+    swap16((uint32_t)t, a, b);
+    x = (int)a;
+    y = (int)b;
+}
 __device__ __forceinline__ float rows_max(float v) {
     uint32_t a, b;
     swap16(__float_as_uint(v), a, b);

@@ -193,7 +193,9 @@ struct Head {
         float lane_tot = 0.f;
 #pragma unroll
         for (int t = 0; t < NT; t++) lane_tot += bs[t];
-        S = xsum4g(lane_tot);
+        // (one 16-action tile: S is the running sums' total, (gs0 + gs1) + (gs2 + gs3), which is
+        //  xsum4g(lane_tot) bit for bit)
+        if (NT > 1) S = xsum4g(lane_tot);
         float cum = 0.f;
 #pragma unroll
         for (int t = 0; t < NT; t++) {
@@ -209,36 +211,133 @@ struct Head {
             }
             cum += (gs0 + gs1) + (gs2 + gs3);
         }
+        if (NT == 1) S = cum;
     }
 
-    // The inverse-CDF sample and log-prob of row j given its uniform u: every lane of row j returns
-    // them. The Categorical renormalisation of the softmax output changes probabilities by < 1e-7
-    // relative, so the sample compares u * S with the running sums (the action is the number of
-    // actions whose running sum stays <= u * S; zero-width intervals are skipped by construction)
-    // and the log-prob is log(clamp(z_a / S)) (torch: log(clamp(p_a / sum(p)))).
-    __device__ __forceinline__ void run(f4 a1, int A, int j, int g4, float u, int& action, float& logprob) const {
-        float z[NT][4], c[NT][4], S;
-        numerators(a1, j, g4, z, c, S);
-        const float target = u * S;
-        int cnt = 0;
+    // run() of two tiles side by side: their MFMA chains and transcendentals interleave, and their
+    // cross-lane reductions pair up (rows_max2, rows_sum2, rows_sum2_i). The running sums are compared
+    // with u * S as they are formed instead of being kept. Bit-identical to two run() calls.
+    __device__ __forceinline__ void run2(const f4 (&a1)[2], int A, int g4, const float (&u)[2], int (&action)[2],
+                                         float (&logprob)[2]) const {
+        float h1[2][4];
 #pragma unroll
-        for (int t = 0; t < NT; t++)
+        for (int i = 0; i < 2; i++)
 #pragma unroll
-            for (int q = 0; q < 4; q++) cnt += (c[t][q] <= target) ? 1 : 0;
-        cnt = rows_sum_i(cnt);
-        int a_sel = cnt;
-        if (__builtin_expect(__ballot(a_sel >= A) != 0, 0)) {
-            // u * S at or beyond the rounded total: the last action with nonzero probability
-            const int last_nz = last_nonzero(z, g4);
-            if (a_sel >= A) a_sel = last_nz;
+            for (int q = 0; q < 4; q++) h1[i][q] = fast_tanh_b(a1[i][q], b1[q]);
+        f4 a2[2] = {{0, 0, 0, 0}, {0, 0, 0, 0}};
+#pragma unroll
+        for (int s = 0; s < 4; s++)
+#pragma unroll
+            for (int i = 0; i < 2; i++) a2[i] = mfma4(w2[s], h1[i][s], a2[i]);
+        float h2[2][4];
+#pragma unroll
+        for (int i = 0; i < 2; i++)
+#pragma unroll
+            for (int q = 0; q < 4; q++) h2[i][q] = fast_tanh_b(a2[i][q], b2[q]);
+        float z[2][NT][4];
+        float m[2] = {-INFINITY, -INFINITY};
+#pragma unroll
+        for (int t = 0; t < NT; t++) {
+            f4 zz[2] = {{0, 0, 0, 0}, {0, 0, 0, 0}};
+#pragma unroll
+            for (int s = 0; s < 4; s++)
+#pragma unroll
+                for (int i = 0; i < 2; i++) zz[i] = mfma4(w3[t][s], h2[i][s], zz[i]);
+#pragma unroll
+            for (int i = 0; i < 2; i++)
+#pragma unroll
+                for (int q = 0; q < 4; q++) {
+                    z[i][t][q] = zz[i][q] + b3[t][q];
+                    m[i] = fmaxf(m[i], z[i][t][q]);
+                }
         }
-        float mine = 0.f;
+        rows_max2(m[0], m[1]);
+        float bs[2][NT], S[2];
 #pragma unroll
-        for (int t = 0; t < NT; t++)
+        for (int i = 0; i < 2; i++) {
+            const float m_l2e = m[i] * 1.4426950408889634f;
+            S[i] = 0.f;
 #pragma unroll
-            for (int q = 0; q < 4; q++) mine = (16 * t + 4 * g4 + q == a_sel) ? z[t][q] : mine;
-        action = a_sel;
-        logprob = clamped_log(xsum4g(mine) * __builtin_amdgcn_rcpf(S));
+            for (int t = 0; t < NT; t++) {
+                bs[i][t] = 0.f;
+#pragma unroll
+                for (int q = 0; q < 4; q++) {
+                    z[i][t][q] = fast_exp_sub(z[i][t][q], m_l2e);
+                    bs[i][t] += z[i][t][q];
+                }
+            }
+#pragma unroll
+            for (int t = 0; t < NT; t++) S[i] += bs[i][t];
+        }
+        int cnt[2];
+        if (NT > 1) {
+            rows_sum2(S[0], S[1]);  // = xsum4g(lane_tot) of numerators()
+#pragma unroll
+            for (int i = 0; i < 2; i++) {
+                const float target = u[i] * S[i];
+                float cum = 0.f;
+                cnt[i] = 0;
+#pragma unroll
+                for (int t = 0; t < NT; t++) {
+                    uint32_t gsr[4];
+                    rows_bcast(__float_as_uint(bs[i][t]), gsr);
+                    const float gs0 = __uint_as_float(gsr[0]), gs1 = __uint_as_float(gsr[1]),
+                                gs2 = __uint_as_float(gsr[2]), gs3 = __uint_as_float(gsr[3]);
+                    float cc = cum + (g4 > 0 ? gs0 : 0.f) + (g4 > 1 ? gs1 : 0.f) + (g4 > 2 ? gs2 : 0.f);
+#pragma unroll
+                    for (int q = 0; q < 4; q++) {
+                        cc += z[i][t][q];
+                        cnt[i] += (cc <= target) ? 1 : 0;
+                    }
+                    cum += (gs0 + gs1) + (gs2 + gs3);
+                }
+            }
+        } else {
+            // one 16-action tile: S is the running sums' total (gs0 + gs1) + (gs2 + gs3), known only
+            // after the broadcast, so the running sums are kept for the compare
+            float c[2][4];
+#pragma unroll
+            for (int i = 0; i < 2; i++) {
+                uint32_t gsr[4];
+                rows_bcast(__float_as_uint(bs[i][0]), gsr);
+                const float gs0 = __uint_as_float(gsr[0]), gs1 = __uint_as_float(gsr[1]), gs2 = __uint_as_float(gsr[2]),
+                            gs3 = __uint_as_float(gsr[3]);
+                const float cum = 0.f;  // numerators()' expression, term for term
+                float cc = cum + (g4 > 0 ? gs0 : 0.f) + (g4 > 1 ? gs1 : 0.f) + (g4 > 2 ? gs2 : 0.f);
+#pragma unroll
+                for (int q = 0; q < 4; q++) {
+                    cc += z[i][0][q];
+                    c[i][q] = cc;
+                }
+                S[i] = cum + ((gs0 + gs1) + (gs2 + gs3));
+                const float target = u[i] * S[i];
+                cnt[i] = 0;
+#pragma unroll
+                for (int q = 0; q < 4; q++) cnt[i] += (c[i][q] <= target) ? 1 : 0;
+            }
+        }
+        rows_sum2_i(cnt[0], cnt[1]);
+        if (__builtin_expect(__ballot(cnt[0] >= A || cnt[1] >= A) != 0, 0)) {
+            // u * S at or beyond the rounded total: the last action with nonzero probability
+#pragma unroll
+            for (int i = 0; i < 2; i++) {
+                const int last_nz = last_nonzero(z[i], g4);
+                if (cnt[i] >= A) cnt[i] = last_nz;
+            }
+        }
+        float mine[2] = {0.f, 0.f};
+#pragma unroll
+        for (int i = 0; i < 2; i++)
+#pragma unroll
+            for (int t = 0; t < NT; t++)
+#pragma unroll
+                for (int q = 0; q < 4; q++) mine[i] = (16 * t + 4 * g4 + q == cnt[i]) ? z[i][t][q] : mine[i];
+        rows_sum2(mine[0], mine[1]);
+#pragma unroll
+        for (int i = 0; i < 2; i++) {
+            action[i] = cnt[i];
+            logprob[i] = clamped_log(mine[i] * __builtin_amdgcn_rcpf(S[i]));
+        }
     }
 
     __device__ __forceinline__ static int last_nonzero(const float (&z)[NT][4], int g4) {
@@ -338,7 +437,7 @@ struct PriceTW {
 template <int S1, int NT, int NT2, bool EXT_U>
 __device__ __forceinline__ void act_tiles(const ActArgs& a, int block) {
     const int tid = threadIdx.x, lane = tid & 63;
-    const int gw = block * 4 + (tid >> 6);  // global wave index
+    const int gw = block * 4 + __builtin_amdgcn_readfirstlane(tid >> 6);  // global wave index (wave-uniform)
     const int grp = gw / a.waves_per_group;
     const int wv = gw - grp * a.waves_per_group;
     if (grp >= a.n1.n_groups) return;
@@ -348,12 +447,6 @@ __device__ __forceinline__ void act_tiles(const ActArgs& a, int block) {
     Head<NT> h1;
     h1.load(a.n1, grp, j, g4);
     constexpr int NP = NT2 > 0 ? NT2 : 1;
-    Head<NP> h2;
-    float pw1 = 0.f;  // price chooser layer 1 (K = 4 inputs): lane (j, g4) holds W1p[j][g4]
-    if (NT2 > 0) {
-        h2.load(a.n2, grp, j, g4);
-        pw1 = a.n2.w1[((size_t)grp * 16 + j) * 4 + g4];
-    }
     const uint64_t off = a.offset + (a.offset_dev ? *a.offset_dev : 0ull);
     const int stride4 = a.stride >> 2;
     const int n_rows_total = a.E * a.U;
@@ -381,124 +474,212 @@ __device__ __forceinline__ void act_tiles(const ActArgs& a, int block) {
         rows_bcast(rnd1, rb1);
     };
     auto pick4 = [](const uint32_t (&v)[4], int k) { return k == 0 ? v[0] : (k == 1 ? v[1] : (k == 2 ? v[2] : v[3])); };
-    uint32_t pre[S1][2];
-    // unconditional loads from clamped addresses, used as loaded: the rows past the end are never
-    // written and the dwords past the row meet zero weights (so the wait lands at the use)
-    auto prefetch = [&](int r) {
-        const uint32_t* src = reinterpret_cast<const uint32_t*>(a.obs + (size_t)(r < 0 ? 0 : r) * a.stride);
-#pragma unroll
-        for (int s = 0; s < S1; s++)
-#pragma unroll
-            for (int h = 0; h < 2; h++) {
-                const int cc = 8 * s + 2 * g4 + h;
-                pre[s][h] = src[cc < stride4 ? cc : stride4 - 1];
-            }
-    };
-    int row = t0 < t1 ? row_of(t0) : -1;
-    if (t0 < t1) prefetch(row);
-    for (int tile = t0; tile < t1; tile++) {
-        uint32_t xd[S1][2];
-#pragma unroll
-        for (int s = 0; s < S1; s++) xd[s][0] = pre[s][0], xd[s][1] = pre[s][1];
-        const int cur = row;
-        if (tile + 1 < t1) {
-            row = row_of(tile + 1);
-            prefetch(row);
-        }
-        const bool valid = cur >= 0;
-        float u1, u2;
+    // Two tiles per step: their MFMA chains, transcendentals and memory round trips interleave (the
+    // kernel is latency-bound with a few waves per SIMD), and their cross-lane sums pair up. A lone
+    // last tile runs beside an empty partner (rows -1: nothing written).
+    const int A1 = a.n1.n_actions;
+    // the pair's uniforms (Philox for 4 tiles at a time, or the given ones)
+    auto uniforms2 = [&](int tile, const int (&cur)[2], float (&u1)[2], float (&u2)[2]) {
         if (EXT_U) {
-            u1 = valid ? a.uniforms[cur] : 0.f;
-            u2 = valid && NT2 > 0 ? a.uniforms[n_rows_total + cur] : 0.f;
+#pragma unroll
+            for (int i = 0; i < 2; i++) {
+                u1[i] = cur[i] >= 0 ? a.uniforms[cur[i]] : 0.f;
+                u2[i] = cur[i] >= 0 && NT2 > 0 ? a.uniforms[n_rows_total + cur[i]] : 0.f;
+            }
         } else {
-            const int k = (tile - t0) & 3;
+            const int k = (tile - t0) & 3;  // 0 or 2
             if (k == 0) draw4(tile);
-            u1 = u24(pick4(rb0, k));
-            u2 = u24(pick4(rb1, k));
+#pragma unroll
+            for (int i = 0; i < 2; i++) {
+                u1[i] = u24(pick4(rb0, k + i));
+                u2[i] = u24(pick4(rb1, k + i));
+            }
         }
-        f4 acc = {0, 0, 0, 0};
+    };
+    // the core chooser (or the only net) of both tiles
+    auto core2 = [&](const uint32_t (&xd)[2][S1][2], const float (&u1)[2], int (&act)[2], float (&lp)[2]) {
+        f4 acc[2] = {{0, 0, 0, 0}, {0, 0, 0, 0}};
 #pragma unroll
         for (int s = 0; s < S1; s++) {
-            const u4v x = bytes_to_bf16(xd[s][0], xd[s][1]);
-            acc = mfma_bf16(w1.hi[s], x, acc);
-            acc = mfma_bf16(w1.mid[s], x, acc);
-            acc = mfma_bf16(w1.lo[s], x, acc);
+            u4v x[2];
+#pragma unroll
+            for (int i = 0; i < 2; i++) x[i] = bytes_to_bf16(xd[i][s][0], xd[i][s][1]);
+#pragma unroll
+            for (int i = 0; i < 2; i++) acc[i] = mfma_bf16(w1.hi[s], x[i], acc[i]);
+#pragma unroll
+            for (int i = 0; i < 2; i++) acc[i] = mfma_bf16(w1.mid[s], x[i], acc[i]);
+#pragma unroll
+            for (int i = 0; i < 2; i++) acc[i] = mfma_bf16(w1.lo[s], x[i], acc[i]);
         }
-        int act;
-        float lp;
-        h1.run(acc, a.n1.n_actions, j, g4, u1, act, lp);
-        if (NT2 > 0) {
-            // price chooser input (PPOmodules.py:316-327): lane g4 takes row byte k of
-            // [obs[2a], obs[2a+1], obs[-2], obs[-1]] (obs[-2:] = the slot's pair at 2C), or -5 for a = 0
-            const int k = g4 < 2 ? 2 * act + g4 : 2 * a.n_cores + (g4 - 2);
+        h1.run2(acc, A1, g4, u1, act, lp);
+    };
+    // price chooser input (PPOmodules.py:316-327): lane g4 takes row byte k of
+    // [obs[2a], obs[2a+1], obs[-2], obs[-1]] (obs[-2:] = the slot's pair at 2C), or -5 for a = 0; and
+    // the byte's offset in the price table's key (-1: not tabulated; rows of an empty tile: 0)
+    auto price_in2 = [&](const uint32_t (&xd)[2][S1][2], const int (&cur)[2], const int (&act)[2], int (&pin)[2],
+                         int (&dg)[2]) {
+#pragma unroll
+        for (int i = 0; i < 2; i++) {
+            const int k = g4 < 2 ? 2 * act[i] + g4 : 2 * a.n_cores + (g4 - 2);
             const int src = j + 16 * ((k >> 3) & 3), ks = k >> 5, kh = (k >> 2) & 1;
             uint32_t dw = 0;
 #pragma unroll
             for (int s = 0; s < S1; s++)
 #pragma unroll
                 for (int h = 0; h < 2; h++) {
-                    const uint32_t v = (uint32_t)__shfl((int)xd[s][h], src);
+                    const uint32_t v = (uint32_t)__shfl((int)xd[i][s][h], src);
                     if (s == ks && h == kh) dw = v;
                 }
-            const int8_t pin = act == 0 ? (int8_t)-5 : (int8_t)(dw >> (8 * (k & 3)));
-            int pact;
-            float plp;
-            // the row's key in the price table: the sum of its four bytes' offsets (lane g4: byte g4)
-            const int dg = a.ptab ? (int)a.pdigit[g4 * 256 + (int)pin + 128] : -1;
-            const int key = rows_sum_i(dg), miss = rows_max_i(dg < 0 ? 1 : 0);
-            if (a.ptab && __ballot(miss != 0) == 0ull) {
-                // every row of the tile is tabulated: sample from the table (Head::run's arithmetic)
-                constexpr int TW = PriceTW<NP>::v;
-                const float* te = a.ptab + ((size_t)grp * a.pkeys + key) * TW;
-                float cum[NP][4], lpv[NP][4];
+            pin[i] = act[i] == 0 ? -5 : (int)(int8_t)(dw >> (8 * (k & 3)));
+            dg[i] = !a.ptab ? -1 : (cur[i] >= 0 ? (int)a.pdigit[g4 * 256 + pin[i] + 128] : 0);
+        }
+    };
+    // the price chooser's outputs of both tiles
+    auto price_out2 = [&](const int (&cur)[2], const int (&act)[2], const int (&pin)[2], const int (&pact)[2],
+                          const float (&plp)[2]) {
 #pragma unroll
-                for (int t = 0; t < NP; t++) {
-                    const f4 c4 = *reinterpret_cast<const f4*>(te + 16 * t + 4 * g4);
-                    const f4 l4 = *reinterpret_cast<const f4*>(te + 16 * NP + 16 * t + 4 * g4);
-#pragma unroll
-                    for (int q = 0; q < 4; q++) cum[t][q] = c4[q], lpv[t][q] = l4[q];
-                }
-                const float S2 = te[32 * NP];
-                const int lnz = __float_as_int(te[32 * NP + 1]);
-                const float target = u2 * S2;
-                int cnt = 0;
-#pragma unroll
-                for (int t = 0; t < NP; t++)
-#pragma unroll
-                    for (int q = 0; q < 4; q++) cnt += (cum[t][q] <= target) ? 1 : 0;
-                cnt = rows_sum_i(cnt);
-                pact = cnt >= a.n2.n_actions ? lnz : cnt;
-                float mine = 0.f;
-#pragma unroll
-                for (int t = 0; t < NP; t++)
-#pragma unroll
-                    for (int q = 0; q < 4; q++) mine = (16 * t + 4 * g4 + q == pact) ? lpv[t][q] : mine;
-                plp = rows_sum(mine);
-            } else {
-                f4 acc2 = {0, 0, 0, 0};
-                acc2 = mfma4(pw1, (float)pin, acc2);
-                h2.run(acc2, a.n2.n_actions, j, g4, u2, pact, plp);
-            }
-            if (valid) {
+        for (int i = 0; i < 2; i++) {
+            if (cur[i] >= 0) {
                 // the price chooser's rollout rows: [E][U], or unit-major (the update reads one unit's
                 // rows of every replica, so they lie contiguous)
-                size_t pc = (size_t)cur;
+                size_t pc = (size_t)cur[i];
                 if (a.pus) {
-                    int e = (int)__umulhi((uint32_t)cur, u_magic);
-                    if ((e + 1) * a.U <= cur) e++;
-                    pc = (size_t)(cur - e * a.U) * (size_t)a.pus + (size_t)e;
+                    int e = (int)__umulhi((uint32_t)cur[i], u_magic);
+                    if ((e + 1) * a.U <= cur[i]) e++;
+                    pc = (size_t)(cur[i] - e * a.U) * (size_t)a.pus + (size_t)e;
                 }
-                a.price_state[pc * 4 + g4] = pin;
+                a.price_state[pc * 4 + g4] = (int8_t)pin[i];
                 if (g4 == 0) {
-                    a.price_action[pc] = (int8_t)pact;
-                    a.price_logprob[pc] = plp;
-                    a.env_price[cur] = (int8_t)(act == 0 ? -5 : pact);
+                    a.price_action[pc] = (int8_t)pact[i];
+                    a.price_logprob[pc] = plp[i];
+                    a.env_price[cur[i]] = (int8_t)(act[i] == 0 ? -5 : pact[i]);
                 }
             }
         }
-        if (valid && g4 == 0) {
-            a.action[cur] = (int8_t)act;
-            a.logprob[cur] = lp;
+    };
+    uint32_t pre[2][S1][2];
+#pragma unroll
+    for (int i = 0; i < 2; i++)
+#pragma unroll
+        for (int s = 0; s < S1; s++) pre[i][s][0] = pre[i][s][1] = 0u;
+    // unconditional loads from clamped addresses, used as loaded: the rows past the end are never
+    // written and the dwords past the row meet zero weights (so the wait lands at the use)
+    auto load_rows = [&](int r, uint32_t (&dst)[S1][2]) {
+        const uint32_t* src = reinterpret_cast<const uint32_t*>(a.obs + (size_t)(r < 0 ? 0 : r) * a.stride);
+#pragma unroll
+        for (int s = 0; s < S1; s++)
+#pragma unroll
+            for (int h = 0; h < 2; h++) {
+                const int cc = 8 * s + 2 * g4 + h;
+                dst[s][h] = src[cc < stride4 ? cc : stride4 - 1];
+            }
+    };
+    int row[2];
+#pragma unroll
+    for (int i = 0; i < 2; i++) {
+        row[i] = t0 + i < t1 ? row_of(t0 + i) : -1;
+        if (t0 + i < t1) load_rows(row[i], pre[i]);
+    }
+    bool any_miss = false;  // a pair with a price input outside the table: priced after the loop
+    for (int tile = t0; tile < t1; tile += 2) {
+        uint32_t xd[2][S1][2];
+        int cur[2];
+#pragma unroll
+        for (int i = 0; i < 2; i++) {
+#pragma unroll
+            for (int s = 0; s < S1; s++) xd[i][s][0] = pre[i][s][0], xd[i][s][1] = pre[i][s][1];
+            cur[i] = row[i];
+        }
+#pragma unroll
+        for (int i = 0; i < 2; i++) {
+            row[i] = tile + 2 + i < t1 ? row_of(tile + 2 + i) : -1;
+            if (tile + 2 + i < t1) load_rows(row[i], pre[i]);
+        }
+        float u1[2], u2[2];
+        uniforms2(tile, cur, u1, u2);
+        int act[2];
+        float lp[2];
+        core2(xd, u1, act, lp);
+        if (NT2 > 0) {
+            int pin[2], dg[2];
+            price_in2(xd, cur, act, pin, dg);
+            if (a.ptab && __ballot(dg[0] < 0 || dg[1] < 0) == 0ull) {
+                // every row of both tiles is tabulated: sample from the table (Head::run's arithmetic)
+                rows_sum2_i(dg[0], dg[1]);
+                constexpr int TW = PriceTW<NP>::v;
+                float cum[2][NP][4], S2[2];
+                int lnz[2], cnt[2], pact[2];
+                float plp[2];
+                const float* te[2];
+#pragma unroll
+                for (int i = 0; i < 2; i++) {
+                    te[i] = a.ptab + ((size_t)grp * a.pkeys + dg[i]) * TW;
+#pragma unroll
+                    for (int t = 0; t < NP; t++) {
+                        const f4 c4 = *reinterpret_cast<const f4*>(te[i] + 16 * t + 4 * g4);
+#pragma unroll
+                        for (int q = 0; q < 4; q++) cum[i][t][q] = c4[q];
+                    }
+                    S2[i] = te[i][32 * NP];
+                    lnz[i] = __float_as_int(te[i][32 * NP + 1]);
+                }
+#pragma unroll
+                for (int i = 0; i < 2; i++) {
+                    const float target = u2[i] * S2[i];
+                    cnt[i] = 0;
+#pragma unroll
+                    for (int t = 0; t < NP; t++)
+#pragma unroll
+                        for (int q = 0; q < 4; q++) cnt[i] += (cum[i][t][q] <= target) ? 1 : 0;
+                }
+                rows_sum2_i(cnt[0], cnt[1]);
+                // the chosen action's log-prob straight from its table entry (one load per row)
+#pragma unroll
+                for (int i = 0; i < 2; i++) {
+                    pact[i] = cnt[i] >= a.n2.n_actions ? lnz[i] : cnt[i];
+                    plp[i] = te[i][16 * NP + pact[i]];
+                }
+                price_out2(cur, act, pin, pact, plp);
+            } else {
+                any_miss = true;
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < 2; i++)
+            if (cur[i] >= 0 && g4 == 0) {
+                a.action[cur[i]] = (int8_t)act[i];
+                a.logprob[cur[i]] = lp[i];
+            }
+    }
+    if (NT2 > 0 && any_miss) {
+        // the pairs the table could not serve (or every pair, without a table): the same pairs and
+        // draws again, the core chooser recomputed (bit-identical), then the price net itself; its
+        // weights take registers only here, after the main loop
+        Head<NP> h2;
+        h2.load(a.n2, grp, j, g4);
+        const float pw1 = a.n2.w1[((size_t)grp * 16 + j) * 4 + g4];  // W1p[j][g4] (K = 4 inputs)
+        for (int tile = t0; tile < t1; tile += 2) {
+            uint32_t xd[2][S1][2];
+            int cur[2];
+#pragma unroll
+            for (int i = 0; i < 2; i++) {
+                cur[i] = tile + i < t1 ? row_of(tile + i) : -1;
+                load_rows(cur[i], xd[i]);
+            }
+            float u1[2], u2[2];
+            uniforms2(tile, cur, u1, u2);
+            int act[2], pin[2], dg[2];
+            float lp[2];
+            core2(xd, u1, act, lp);
+            price_in2(xd, cur, act, pin, dg);
+            if (a.ptab && __ballot(dg[0] < 0 || dg[1] < 0) == 0ull) continue;  // priced in the main loop
+            int pact[2];
+            float plp[2];
+            f4 acc2[2];
+#pragma unroll
+            for (int i = 0; i < 2; i++) acc2[i] = mfma4(pw1, (float)pin[i], (f4){0, 0, 0, 0});
+            h2.run2(acc2, a.n2.n_actions, g4, u2, pact, plp);
+            price_out2(cur, act, pin, pact, plp);
         }
     }
 }
@@ -521,10 +702,11 @@ __global__ void __launch_bounds__(256) k_act(ActArgs a) {
 template <int S1, int NT, bool EXT_U, bool OWN>
 __device__ __forceinline__ void act_common_rows(const ActArgs& a, int block) {
     __shared__ int32_t s_list[4][kCommonSeg];
+    __shared__ float s_ulist[4][kCommonSeg];  // the listed rows' uniforms (drawn in the scan)
     __shared__ float s_cum[4][16 * NT], s_lp[4][16 * NT], s_S[4];
     __shared__ int s_lnz[4];
     __shared__ uint32_t s_tmpl[4][8 * S1];
-    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int gw = block * 4 + wid;
     const int grp = gw / a.waves_per_group;
     const int wv = gw - grp * a.waves_per_group;
@@ -538,6 +720,7 @@ __device__ __forceinline__ void act_common_rows(const ActArgs& a, int block) {
     h1.load(a.n1, grp, j, g4);
     const uint64_t off = a.offset + (a.offset_dev ? *a.offset_dev : 0ull);
     int32_t* list = s_list[wid];
+    float* ulist = s_ulist[wid];
     // the common row's dwords (zero past the row: they meet zero weights, like k_act's clamped loads)
     const uint32_t* crow = reinterpret_cast<const uint32_t*>(a.common);
     for (int d = lane; d < 8 * S1; d += 64) s_tmpl[wid][d] = d < stride4 ? crow[d] : 0u;
@@ -613,8 +796,11 @@ __device__ __forceinline__ void act_common_rows(const ActArgs& a, int block) {
     };
     // one 64-row step: common rows sample from the table, the others are listed
     auto scan_step = [&](int row, bool in, bool common) {
+        // every lane draws (the lanes of listed rows keep theirs for the tile pass: no second draw
+        // there, and no lane-group-replicated one)
+        const float u = uniform_of(row);
         if (common) {
-            const float target = uniform_of(row) * S;
+            const float target = u * S;
             int cnt = 0;
 #pragma unroll
             for (int k = 0; k < 16 * NT; k++) cnt += (cum[k] <= target) ? 1 : 0;
@@ -624,7 +810,10 @@ __device__ __forceinline__ void act_common_rows(const ActArgs& a, int block) {
         }
         const bool other = in && !common;
         const uint64_t m = __ballot(other);
-        if (other) list[n_list + __popcll(m & below)] = row;
+        if (other) {
+            list[n_list + __popcll(m & below)] = row;
+            ulist[n_list + __popcll(m & below)] = u;
+        }
         n_list += __popcll(m);
     };
     if constexpr (OWN) {
@@ -659,45 +848,66 @@ __device__ __forceinline__ void act_common_rows(const ActArgs& a, int block) {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    // ---- the listed rows in 16-row MFMA tiles (k_act's per-tile path, next tile's rows prefetched)
-    uint32_t tp[S1][2];
-    int t_row = 0;
-    auto load_tile = [&](int t0) {
-        const int k = t0 + j;
-        t_row = list[k < n_list ? k : t0];
-        size_t sr = (size_t)t_row;
+    // ---- the listed rows in 16-row MFMA tiles, two tiles per step (k_act's path; the next pair's rows
+    //      prefetched, a lone last tile beside an empty partner)
+    uint32_t tp[2][S1][2];
+#pragma unroll
+    for (int i = 0; i < 2; i++)
+#pragma unroll
+        for (int s = 0; s < S1; s++) tp[i][s][0] = tp[i][s][1] = 0u;
+    int t_row[2] = {-1, -1};
+    float t_u[2] = {0.f, 0.f};
+    auto load_tile = [&](int i, int t0) {  // tile starting at list entry t0 (< n_list)
+        const int k = t0 + j < n_list ? t0 + j : t0;
+        t_row[i] = t0 + j < n_list ? list[k] : -1;
+        t_u[i] = ulist[k];
+        size_t sr = (size_t)list[k];
         if constexpr (OWN) {
             int ag;
-            sr = core_row_of(t_row, ag);
+            sr = core_row_of(list[k], ag);
         }
         const uint32_t* src = reinterpret_cast<const uint32_t*>(a.obs + sr * a.stride);
 #pragma unroll
         for (int s = 0; s < S1; s++) {
             const int c0 = 8 * s + 2 * g4;
-            tp[s][0] = src[c0 < stride4 ? c0 : stride4 - 1];
-            tp[s][1] = src[c0 + 1 < stride4 ? c0 + 1 : stride4 - 1];
+            tp[i][s][0] = src[c0 < stride4 ? c0 : stride4 - 1];
+            tp[i][s][1] = src[c0 + 1 < stride4 ? c0 + 1 : stride4 - 1];
         }
     };
-    if (n_list > 0) load_tile(0);
-    for (int t0 = 0; t0 < n_list; t0 += 16) {
-        const bool valid = t0 + j < n_list;
-        const int row = t_row;
-        f4 acc = {0, 0, 0, 0};
+#pragma unroll
+    for (int i = 0; i < 2; i++)
+        if (16 * i < n_list) load_tile(i, 16 * i);
+    for (int t0 = 0; t0 < n_list; t0 += 32) {
+        int row[2];
+        float u[2];
+        f4 acc[2] = {{0, 0, 0, 0}, {0, 0, 0, 0}};
 #pragma unroll
         for (int s = 0; s < S1; s++) {
-            const u4v x = bytes_to_bf16(tp[s][0], tp[s][1]);
-            acc = mfma_bf16(w1.hi[s], x, acc);
-            acc = mfma_bf16(w1.mid[s], x, acc);
-            acc = mfma_bf16(w1.lo[s], x, acc);
+            u4v x[2];
+#pragma unroll
+            for (int i = 0; i < 2; i++) x[i] = bytes_to_bf16(tp[i][s][0], tp[i][s][1]);
+#pragma unroll
+            for (int i = 0; i < 2; i++) acc[i] = mfma_bf16(w1.hi[s], x[i], acc[i]);
+#pragma unroll
+            for (int i = 0; i < 2; i++) acc[i] = mfma_bf16(w1.mid[s], x[i], acc[i]);
+#pragma unroll
+            for (int i = 0; i < 2; i++) acc[i] = mfma_bf16(w1.lo[s], x[i], acc[i]);
         }
-        if (t0 + 16 < n_list) load_tile(t0 + 16);
-        int act;
-        float lp;
-        h1.run(acc, A, j, g4, uniform_of(row), act, lp);
-        if (valid && g4 == 0) {
-            a.action[row] = (int8_t)act;
-            a.logprob[row] = lp;
+#pragma unroll
+        for (int i = 0; i < 2; i++) {
+            row[i] = t0 + 16 * i < n_list ? t_row[i] : -1;
+            u[i] = t_u[i];
+            if (t0 + 32 + 16 * i < n_list) load_tile(i, t0 + 32 + 16 * i);
         }
+        int act[2];
+        float lp[2];
+        h1.run2(acc, A, g4, u, act, lp);
+#pragma unroll
+        for (int i = 0; i < 2; i++)
+            if (row[i] >= 0 && g4 == 0) {
+                a.action[row[i]] = (int8_t)act[i];
+                a.logprob[row[i]] = lp[i];
+            }
     }
 }
 
@@ -717,7 +927,7 @@ __global__ void __launch_bounds__(256) k_act_common(ActArgs a) {
 // units on compact rows (k_act_common). The two workloads' waves share the CUs, so one's waits
 // hide under the other's work instead of each launch waiting out its own chain.
 template <int S1a, int NTa, int NT2a, int S1b, int NTb>
-__global__ void __launch_bounds__(256) k_act_pair(ActArgs off, ActArgs acc, int off_blocks) {
+__global__ void __launch_bounds__(256, 4) k_act_pair(ActArgs off, ActArgs acc, int off_blocks) {
     if ((int)blockIdx.x < off_blocks)
         act_tiles<S1a, NTa, NT2a, false>(off, blockIdx.x);
     else
