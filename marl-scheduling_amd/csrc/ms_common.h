@@ -98,6 +98,31 @@ __device__ __forceinline__ void rows_bcast(uint32_t v, uint32_t (&r)[4]) {
     swap32(b, r[1], r[3]);    // rows 1 and 3
 }
 
+// ---- an array addressed as a raw buffer: a wave-uniform base in scalar registers and 32-bit per-lane
+// byte offsets (no 64-bit address arithmetic per access; a 32-bit multiply is a quarter-rate VALU
+// op, __umul24 a full-rate one). Accesses at or past `bytes` read 0 / are dropped.
+struct RawBuf {
+    __amdgpu_buffer_rsrc_t r;
+    __device__ __forceinline__ RawBuf(const void* base, long long bytes) {
+        r = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0,
+                                              (int)(bytes < 0 ? 0 : (bytes > 0x7fffffffll ? 0x7fffffffll : bytes)),
+                                              0x00020000);
+    }
+    __device__ __forceinline__ uint32_t ld32(uint32_t off) const {
+        return __builtin_amdgcn_raw_buffer_load_b32(r, (int)off, 0, 0);
+    }
+    __device__ __forceinline__ float ldf(uint32_t off) const { return __uint_as_float(ld32(off)); }
+    __device__ __forceinline__ int ld8s(uint32_t off) const {
+        return (int)(int8_t)__builtin_amdgcn_raw_buffer_load_b8(r, (int)off, 0, 0);
+    }
+    __device__ __forceinline__ void st8(uint32_t off, int v) const {
+        __builtin_amdgcn_raw_buffer_store_b8((uint8_t)v, r, (int)off, 0, 0);
+    }
+    __device__ __forceinline__ void stf(uint32_t off, float v) const {
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), r, (int)off, 0, 0);
+    }
+};
+
 typedef uint32_t u4a __attribute__((ext_vector_type(4), aligned(4)));  // 4-byte aligned 16-byte load
 
 template <int LPR>

@@ -442,11 +442,38 @@ __device__ __forceinline__ void act_tiles(const ActArgs& a, int block) {
     const int wv = gw - grp * a.waves_per_group;
     if (grp >= a.n1.n_groups) return;
     const int j = lane & 15, g4 = lane >> 4;
+    constexpr int NP = NT2 > 0 ? NT2 : 1;
+    constexpr int TW = PriceTW<NP>::v;
+    // the arrays this wave touches as raw buffers (32-bit offsets: row indices < 2^24 and arrays
+    // < 2^31 bytes, checked at the launch)
+    const long long n_rows = (long long)a.E * a.U;
+    const long long n_pc = a.pus ? (long long)a.U * a.pus : n_rows;  // price chooser rows
+    const RawBuf obs_b(a.obs, n_rows * a.stride), act_b(a.action, n_rows), lp_b(a.logprob, 4 * n_rows);
+    const RawBuf pst_b(a.price_state, 4 * n_pc), pact_b(a.price_action, n_pc), plp_b(a.price_logprob, 4 * n_pc),
+        envp_b(a.env_price, n_rows);
+    const RawBuf tab_b(a.ptab ? a.ptab + (size_t)grp * a.pkeys * TW : nullptr, 4ll * a.pkeys * TW);
+    // the price table's key digits, this wave's copy in LDS (a lookup per row: no memory round trip)
+    int16_t* pdig = nullptr;
+    if constexpr (NT2 > 0) {
+        __shared__ uint32_t s_pd[4][512];
+        const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+        if (a.ptab) {
+            const uint32_t* src = reinterpret_cast<const uint32_t*>(a.pdigit);
+            uint32_t v[8];
+#pragma unroll
+            for (int k = 0; k < 8; k++) v[k] = src[64 * k + lane];
+#pragma unroll
+            for (int k = 0; k < 8; k++) s_pd[wid][64 * k + lane] = v[k];
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        }
+        pdig = reinterpret_cast<int16_t*>(s_pd[wid]);
+    }
     W1Split<S1> w1;
     w1.load(a.n1.w1 + (size_t)grp * 16 * a.n1.in_dim, a.n1.in_dim, j, g4);
     Head<NT> h1;
     h1.load(a.n1, grp, j, g4);
-    constexpr int NP = NT2 > 0 ? NT2 : 1;
     const uint64_t off = a.offset + (a.offset_dev ? *a.offset_dev : 0ull);
     const int stride4 = a.stride >> 2;
     const int n_rows_total = a.E * a.U;
@@ -467,11 +494,21 @@ __device__ __forceinline__ void act_tiles(const ActArgs& a, int block) {
     // Philox uniforms, computed for 4 tiles at a time: lane (j, g4) draws for row j of tile
     // base + g4 (counter = the obs row index, so the values do not depend on the tiling)
     uint32_t rnd0 = 0, rnd1 = 0, rb0[4] = {0, 0, 0, 0}, rb1[4] = {0, 0, 0, 0};
+    // With a price net the row's two words are its two uniforms. A single net's row takes word
+    // (i >> 6) & 1 of the draw countered by the row of item i & ~64: the rule of k_act_common's scan
+    // (one draw per two 64-item steps there), so both kernels sample a row alike.
     auto draw4 = [&](int base) {
-        const int r = base + g4 < t1 ? row_of_lane(base + g4, j) : -1;
-        philox2((uint32_t)r, off, a.seed, rnd0, rnd1);
+        if (NT2 > 0) {
+            const int r = base + g4 < t1 ? row_of_lane(base + g4, j) : -1;
+            philox2((uint32_t)r, off, a.seed, rnd0, rnd1);
+            rows_bcast(rnd1, rb1);
+        } else {
+            const int i = (base + g4) * 16 + j;
+            const int r = base + g4 < t1 ? row_of_lane(0, i & ~64) : -1;
+            philox2((uint32_t)r, off, a.seed, rnd0, rnd1);
+            if (i & 64) rnd0 = rnd1;
+        }
         rows_bcast(rnd0, rb0);  // tile base + k takes row k's draws
-        rows_bcast(rnd1, rb1);
     };
     auto pick4 = [](const uint32_t (&v)[4], int k) { return k == 0 ? v[0] : (k == 1 ? v[1] : (k == 2 ? v[2] : v[3])); };
     // Two tiles per step: their MFMA chains, transcendentals and memory round trips interleave (the
@@ -531,7 +568,7 @@ __device__ __forceinline__ void act_tiles(const ActArgs& a, int block) {
                     if (s == ks && h == kh) dw = v;
                 }
             pin[i] = act[i] == 0 ? -5 : (int)(int8_t)(dw >> (8 * (k & 3)));
-            dg[i] = !a.ptab ? -1 : (cur[i] >= 0 ? (int)a.pdigit[g4 * 256 + pin[i] + 128] : 0);
+            dg[i] = !a.ptab ? -1 : (cur[i] >= 0 ? (int)pdig[g4 * 256 + pin[i] + 128] : 0);
         }
     };
     // the price chooser's outputs of both tiles
@@ -542,17 +579,17 @@ __device__ __forceinline__ void act_tiles(const ActArgs& a, int block) {
             if (cur[i] >= 0) {
                 // the price chooser's rollout rows: [E][U], or unit-major (the update reads one unit's
                 // rows of every replica, so they lie contiguous)
-                size_t pc = (size_t)cur[i];
+                uint32_t pc = (uint32_t)cur[i];
                 if (a.pus) {
                     int e = (int)__umulhi((uint32_t)cur[i], u_magic);
                     if ((e + 1) * a.U <= cur[i]) e++;
-                    pc = (size_t)(cur[i] - e * a.U) * (size_t)a.pus + (size_t)e;
+                    pc = (uint32_t)(cur[i] - e * a.U) * (uint32_t)a.pus + (uint32_t)e;
                 }
-                a.price_state[pc * 4 + g4] = (int8_t)pin[i];
+                pst_b.st8(4 * pc + g4, pin[i]);
                 if (g4 == 0) {
-                    a.price_action[pc] = (int8_t)pact[i];
-                    a.price_logprob[pc] = plp[i];
-                    a.env_price[cur[i]] = (int8_t)(act[i] == 0 ? -5 : pact[i]);
+                    pact_b.st8(pc, pact[i]);
+                    plp_b.stf(4 * pc, plp[i]);
+                    envp_b.st8((uint32_t)cur[i], act[i] == 0 ? -5 : pact[i]);
                 }
             }
         }
@@ -565,13 +602,13 @@ __device__ __forceinline__ void act_tiles(const ActArgs& a, int block) {
     // unconditional loads from clamped addresses, used as loaded: the rows past the end are never
     // written and the dwords past the row meet zero weights (so the wait lands at the use)
     auto load_rows = [&](int r, uint32_t (&dst)[S1][2]) {
-        const uint32_t* src = reinterpret_cast<const uint32_t*>(a.obs + (size_t)(r < 0 ? 0 : r) * a.stride);
+        const uint32_t rb = __umul24((uint32_t)(r < 0 ? 0 : r), (uint32_t)a.stride);
 #pragma unroll
         for (int s = 0; s < S1; s++)
 #pragma unroll
             for (int h = 0; h < 2; h++) {
                 const int cc = 8 * s + 2 * g4 + h;
-                dst[s][h] = src[cc < stride4 ? cc : stride4 - 1];
+                dst[s][h] = obs_b.ld32(rb + 4 * (cc < stride4 ? cc : stride4 - 1));
             }
     };
     int row[2];
@@ -606,22 +643,21 @@ __device__ __forceinline__ void act_tiles(const ActArgs& a, int block) {
             if (a.ptab && __ballot(dg[0] < 0 || dg[1] < 0) == 0ull) {
                 // every row of both tiles is tabulated: sample from the table (Head::run's arithmetic)
                 rows_sum2_i(dg[0], dg[1]);
-                constexpr int TW = PriceTW<NP>::v;
                 float cum[2][NP][4], S2[2];
                 int lnz[2], cnt[2], pact[2];
                 float plp[2];
-                const float* te[2];
+                uint32_t te[2];  // byte offset of the row's table entry
 #pragma unroll
                 for (int i = 0; i < 2; i++) {
-                    te[i] = a.ptab + ((size_t)grp * a.pkeys + dg[i]) * TW;
+                    te[i] = __umul24((uint32_t)dg[i], 4u * TW);
 #pragma unroll
                     for (int t = 0; t < NP; t++) {
-                        const f4 c4 = *reinterpret_cast<const f4*>(te[i] + 16 * t + 4 * g4);
+                        const auto c4 = __builtin_amdgcn_raw_buffer_load_b128(tab_b.r, (int)(te[i] + 4 * (16 * t + 4 * g4)), 0, 0);
 #pragma unroll
-                        for (int q = 0; q < 4; q++) cum[i][t][q] = c4[q];
+                        for (int q = 0; q < 4; q++) cum[i][t][q] = __uint_as_float(c4[q]);
                     }
-                    S2[i] = te[i][32 * NP];
-                    lnz[i] = __float_as_int(te[i][32 * NP + 1]);
+                    S2[i] = tab_b.ldf(te[i] + 4 * (32 * NP));
+                    lnz[i] = (int)tab_b.ld32(te[i] + 4 * (32 * NP + 1));
                 }
 #pragma unroll
                 for (int i = 0; i < 2; i++) {
@@ -637,7 +673,7 @@ __device__ __forceinline__ void act_tiles(const ActArgs& a, int block) {
 #pragma unroll
                 for (int i = 0; i < 2; i++) {
                     pact[i] = cnt[i] >= a.n2.n_actions ? lnz[i] : cnt[i];
-                    plp[i] = te[i][16 * NP + pact[i]];
+                    plp[i] = tab_b.ldf(te[i] + 4 * (16 * NP + pact[i]));
                 }
                 price_out2(cur, act, pin, pact, plp);
             } else {
@@ -647,8 +683,8 @@ __device__ __forceinline__ void act_tiles(const ActArgs& a, int block) {
 #pragma unroll
         for (int i = 0; i < 2; i++)
             if (cur[i] >= 0 && g4 == 0) {
-                a.action[cur[i]] = (int8_t)act[i];
-                a.logprob[cur[i]] = lp[i];
+                act_b.st8((uint32_t)cur[i], act[i]);
+                lp_b.stf(4 * (uint32_t)cur[i], lp[i]);
             }
     }
     if (NT2 > 0 && any_miss) {
@@ -741,10 +777,7 @@ __device__ __forceinline__ void act_common_rows(const ActArgs& a, int block) {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    // the table is wave-uniform: scalar registers
-    float cum[16 * NT];
-#pragma unroll
-    for (int k = 0; k < 16 * NT; k++) cum[k] = __uint_as_float(__builtin_amdgcn_readfirstlane(__float_as_uint(s_cum[wid][k])));
+    const float* cum = s_cum[wid];  // the running sums, non-decreasing (z >= 0): binary-searched in LDS
     constexpr int LPR = S1 <= 2 ? 4 : (S1 <= 4 ? 8 : 16);
     CommonScan<LPR> cs;
     if (!OWN) cs.init(crow, stride4, lane);
@@ -756,14 +789,21 @@ __device__ __forceinline__ void act_common_rows(const ActArgs& a, int block) {
         if ((e + 1) * a.S <= i) e++;
         return e * a.U + grp * a.S + (i - e * a.S);
     };
-    auto uniform_of = [&](int row) -> float {
-        if (EXT_U) return a.uniforms[row];
-        uint32_t r0, r1;
-        philox2((uint32_t)row, off, a.seed, r0, r1);
-        return u24(r0);
-    };
     const int i_begin = wv * a.items_per_wave;
     const int i_end = min(i_begin + a.items_per_wave, a.n_items);  // <= kCommonSeg rows
+    // Item i's uniform: word (i >> 6) & 1 of the Philox draw countered by the row of item i & ~64, so
+    // one draw serves the rows of two 64-item scan steps (the second step reuses the first's other
+    // word). A function of the item index alone: the same for any split of the items into waves.
+    uint32_t u_other = 0;  // the draw's second word, kept from the first step of the pair
+    auto step_uniform = [&](int i0, int row) -> float {  // i0 = the step's first item (multiple of 64)
+        if (EXT_U) return a.uniforms[row < 0 ? 0 : row];
+        if ((i0 & 64) && i0 > i_begin) return u24(u_other);
+        const int ib = (i0 & ~64) + lane;
+        uint32_t r0, r1;
+        philox2((uint32_t)row_of_item(ib), off, a.seed, r0, r1);
+        u_other = r1;
+        return u24((i0 & 64) ? r1 : r0);
+    };
     const uint64_t below = (1ull << lane) - 1ull;
     int n_list = 0;
     // ---- scan (one 64-row step ahead in registers): rows equal to the common row are sampled
@@ -795,15 +835,17 @@ __device__ __forceinline__ void act_common_rows(const ActArgs& a, int block) {
         n_row = n_in ? row_of_item(i) : 0;
     };
     // one 64-row step: common rows sample from the table, the others are listed
-    auto scan_step = [&](int row, bool in, bool common) {
+    auto scan_step = [&](int i0, int row, bool in, bool common) {
         // every lane draws (the lanes of listed rows keep theirs for the tile pass: no second draw
         // there, and no lane-group-replicated one)
-        const float u = uniform_of(row);
+        const float u = step_uniform(i0, row);
         if (common) {
             const float target = u * S;
+            // the number of running sums <= target (Head::run's count), by binary search
             int cnt = 0;
 #pragma unroll
-            for (int k = 0; k < 16 * NT; k++) cnt += (cum[k] <= target) ? 1 : 0;
+            for (int step = 16 * NT; step >= 1; step >>= 1)
+                if (cnt + step <= 16 * NT && cum[cnt + step - 1] <= target) cnt += step;
             const int act = cnt >= A ? last_nz : cnt;
             a.action[row] = (int8_t)act;
             a.logprob[row] = s_lp[wid][act];
@@ -833,7 +875,7 @@ __device__ __forceinline__ void act_common_rows(const ActArgs& a, int block) {
 #pragma unroll
         for (int st = 0; st < MS; st++)
             if (i_begin + 64 * st < i_end)
-                scan_step(row_st[st], row_st[st] >= 0, row_st[st] >= 0 && own_st[st] != me_st[st]);
+                scan_step(i_begin + 64 * st, row_st[st], row_st[st] >= 0, row_st[st] >= 0 && own_st[st] != me_st[st]);
     } else {
         // (one 64-row step ahead in registers)
         if (i_begin < i_end) load_step(i_begin);
@@ -842,7 +884,7 @@ __device__ __forceinline__ void act_common_rows(const ActArgs& a, int block) {
             const bool in = n_in;
             const bool common = cs.lane_row_common(lane) && in;
             if (i0 + 64 < i_end) load_step(i0 + 64);
-            scan_step(row, in, common);
+            scan_step(i0, row, in, common);
         }
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -939,8 +981,8 @@ static unsigned act_common_blocks(ActArgs& a, long long target) {
     const int G = a.n1.n_groups;
     // ~target waves over all groups, whole 64-row scan steps each, at most one LDS list of rows
     long long ipw = ((long long)a.n_items * G + target - 1) / target;
-    ipw = (ipw + 63) / 64 * 64;
-    ipw = ipw < 64 ? 64 : (ipw > kCommonSeg ? kCommonSeg : ipw);
+    ipw = (ipw + 127) / 128 * 128;  // whole step pairs (one Philox draw serves two steps)
+    ipw = ipw < 128 ? 128 : (ipw > kCommonSeg ? kCommonSeg : ipw);
     a.items_per_wave = (int)ipw;
     a.waves_per_group = (a.n_items + a.items_per_wave - 1) / a.items_per_wave;
     const long long waves = (long long)a.waves_per_group * G;
@@ -957,6 +999,14 @@ static hipError_t launch_act_common_t(ActArgs& a, hipStream_t st) {
     return hipGetLastError();
 }
 
+// act_tiles addresses rows with 24-bit row indices and 31-bit byte offsets (RawBuf)
+static bool act_tiles_fits(const ActArgs& a) {
+    const long long rows = (long long)a.E * a.U;
+    const long long pc = a.pus ? (long long)a.U * a.pus : rows;
+    return rows < (1ll << 24) && rows * a.stride <= 0x7fffffffll && 4 * pc <= 0x7fffffffll &&
+           (long long)a.pkeys * PriceTW<8>::v * 4 <= 0x7fffffffll;
+}
+
 static unsigned act_blocks(ActArgs& a, long long target) {
     const int G = a.n1.n_groups;
     const int tiles = (a.n_items + 15) / 16;
@@ -970,6 +1020,7 @@ static unsigned act_blocks(ActArgs& a, long long target) {
 
 template <int S1, int NT, int NT2>
 static hipError_t launch_act_t(ActArgs& a, hipStream_t st) {
+    if (!act_tiles_fits(a)) return hipErrorInvalidValue;
     auto kern = a.uniforms ? k_act<S1, NT, NT2, true> : k_act<S1, NT, NT2, false>;
     static const long long target = env_int("MS_ACT_WAVES", 8192);  // measured best for cfg3 alone
     const unsigned blocks = act_blocks(a, target);
@@ -1181,6 +1232,7 @@ hipError_t launch_act_round(const ms_mlp_params* core, const ms_mlp_params* pric
                              acc_offset, offset_dev, nullptr, acc_action, acc_logprob);
     const bool paired = (off_stride + 31) / 32 == 1 && core->n_actions <= 16 && price->n_actions <= 16 &&
                         (acc_stride + 31) / 32 == 2 && acc->n_actions <= 32 && !env_int("MS_ACT_UNPAIRED", 0);
+    if (paired && !act_tiles_fits(o)) return hipErrorInvalidValue;
     if (!paired) {
         hipError_t e = dispatch_act(o, st);
         return e != hipSuccess ? e : dispatch_act(c, st);
