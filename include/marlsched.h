@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define MS_ABI_VERSION 12
+#define MS_ABI_VERSION 13
 
 #define MS_MAX_KINDS 16
 #define MS_MAX_AGENTS 64
@@ -289,7 +289,23 @@ typedef struct ms_mlp_params {
     int32_t hidden;    /* H (<= 64) */
     int32_t n_actions; /* A (<= 128) */
     int32_t n_groups;  /* G */
+    /* Optional (ABI 13): the act kernels' per-lane weight fragments and the common row's sampling
+     * table, made by ms_act_prepare from these weights (NULL: each acting wave derives them). A
+     * fragment block whose header does not match the call's shape is ignored. Rebuild it whenever
+     * the weights change (like ms_price_table_build). Other entry points ignore the field. */
+    const void* act_frag;
 } ms_mlp_params;
+
+/* Bytes of the act fragment block of net p acting on rows of obs_stride bytes. */
+size_t ms_act_frag_bytes(const ms_mlp_params* p, int32_t obs_stride);
+
+/* Writes the act fragment block (frag, ms_act_frag_bytes) for net p's current weights: each acting
+ * lane's layer-1 weight terms (hi + mid + lo, exact), its layer-2/3 weights and pre-scaled biases,
+ * and, with common_row != NULL, the common row's sampling table (ms_policy_act_common /
+ * _compact / ms_act_round_free). Acting with the block is bit-identical to acting without it; a
+ * rollout makes it once instead of every acting wave of every round deriving it
+ * (PPOmodules.py:53-63 runs policy_old, fixed between two updates). */
+int ms_act_prepare(const ms_mlp_params* p, const int8_t* common_row, int32_t obs_stride, void* frag, void* stream);
 
 /* The Philox counter offset is offset + *offset_dev (offset_dev may be NULL); a
  * device-resident offset lets a captured HIP graph draw fresh numbers per replay. */

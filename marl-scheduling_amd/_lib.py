@@ -61,6 +61,8 @@ def _load():
                                          ct.POINTER(abi.MsMlpParams), P, P, i32, i32, i32, i32, P, i64, u64, u64, u64,
                                          P, P, P, P, P, P, P, P, P, ct.POINTER(abi.MsPriceTable), i64, P]),
         "ms_price_table_build": (ct.c_int, [ct.POINTER(abi.MsMlpParams), ct.POINTER(abi.MsPriceTable), P]),
+        "ms_act_frag_bytes": (ct.c_size_t, [ct.POINTER(abi.MsMlpParams), i32]),
+        "ms_act_prepare": (ct.c_int, [ct.POINTER(abi.MsMlpParams), P, i32, P, P]),
         "ms_offer_act_free": (ct.c_int, [ct.POINTER(abi.MsMlpParams), ct.POINTER(abi.MsMlpParams), P, i32, i64, i32,
                                          i32, i32, u64, u64, P, P, P, P, P, P, P, P, i64, P]),
         "ms_discounted_returns": (ct.c_int, [P, i32, i64, i64, ct.c_double, P, P]),
@@ -98,7 +100,7 @@ def _load():
         fn = getattr(L, name)
         fn.restype = res
         fn.argtypes = args
-    if L.ms_abi_version() != 12:
+    if L.ms_abi_version() != 13:
         raise ImportError("libmarlsched.so ABI version mismatch")
     return L
 
@@ -111,7 +113,7 @@ EXPORTED = (
     "ms_env_reset", "ms_env_step", "ms_env_round", "ms_env_flags", "ms_env_randbelow", "ms_env_auctioneer",
     "ms_env_get_rng", "ms_env_set_rng", "ms_env_export",
     "ms_env_import", "ms_policy_act", "ms_policy_act_common", "ms_policy_act_compact",
-    "ms_act_round_free", "ms_price_table_build", "ms_offer_act_free", "ms_discounted_returns", "ms_unit_returns",
+    "ms_act_round_free", "ms_price_table_build", "ms_act_frag_bytes", "ms_act_prepare", "ms_offer_act_free", "ms_discounted_returns", "ms_unit_returns",
     "ms_ppo_workspace_bytes", "ms_ppo_grad", "ms_adam_step", "ms_adam_step_dev",
     "ms_aggregate_obs", "ms_decode_aggregated", "ms_dqn_act", "ms_dqn_workspace_bytes", "ms_dqn_grad",
     "ms_regen_agent_rows", "ms_bdqn_workspace_bytes", "ms_bdqn_prepare", "ms_bdqn_layer1_scratch_bytes", "ms_bdqn_layer1_compact",

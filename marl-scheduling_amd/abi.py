@@ -193,6 +193,7 @@ class MsMlpParams(ct.Structure):
         ("hidden", ct.c_int32),
         ("n_actions", ct.c_int32),
         ("n_groups", ct.c_int32),
+        ("act_frag", ct.c_void_p),  # ms_act_prepare's block, or NULL
     ]
 
 

@@ -36,6 +36,8 @@ hipError_t launch_act_round(const ms_mlp_params*, const ms_mlp_params*, const in
                             int64_t, uint64_t, uint64_t, uint64_t, const uint64_t*, int8_t*, float*, int8_t*, int8_t*,
                             float*, int8_t*, int8_t*, float*, const float*, const int16_t*, int, int64_t, hipStream_t);
 hipError_t launch_price_table(const ms_mlp_params*, const int8_t*, int, float*, hipStream_t);
+size_t act_frag_bytes(const ms_mlp_params*, int);
+hipError_t launch_act_prepare(const ms_mlp_params*, const int8_t*, int, void*, hipStream_t);
 hipError_t launch_offer_act_free(const ms_mlp_params*, const ms_mlp_params*, const int8_t*, int, int64_t, int, int, int,
                                  uint64_t, uint64_t, const uint64_t*, const float*, int8_t*, float*, int8_t*, int8_t*,
                                  float*, int8_t*, int64_t, hipStream_t);
@@ -576,6 +578,20 @@ int ms_price_table_build(const ms_mlp_params* price_chooser, const ms_price_tabl
     if (price_chooser->in_dim != 4 || price_chooser->n_actions > 32)
         return fail(MS_EINVAL, "price chooser must be 4 -> A with A <= 32");
     HIP_TRY(ms::launch_price_table(price_chooser, t->rows, t->n_keys, t->table, (hipStream_t)stream));
+    return MS_OK;
+}
+
+size_t ms_act_frag_bytes(const ms_mlp_params* p, int32_t obs_stride) {
+    if (!p || obs_stride < 1 || p->n_groups < 1) return 0;
+    return ms::act_frag_bytes(p, obs_stride);
+}
+
+int ms_act_prepare(const ms_mlp_params* p, const int8_t* common_row, int32_t obs_stride, void* frag, void* stream) {
+    if (!p || !frag) return fail(MS_EINVAL, "NULL argument");
+    if (obs_stride < 4 || (obs_stride & 3)) return fail(MS_EINVAL, "obs_stride must be a positive multiple of 4");
+    int rc = check_mlp(p, obs_stride, p->n_groups, 1);
+    if (rc) return rc;
+    HIP_TRY(ms::launch_act_prepare(p, common_row, obs_stride, frag, (hipStream_t)stream));
     return MS_OK;
 }
 

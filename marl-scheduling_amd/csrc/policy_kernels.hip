@@ -93,6 +93,23 @@ __device__ __forceinline__ float trunc_bf16(float x) { return __uint_as_float(__
 template <int S1>
 struct W1Split {
     u4v hi[S1], mid[S1], lo[S1];
+    // the 12*S1 dwords of a lane's fragment (ms_act_prepare) in the act fragment block
+    __device__ __forceinline__ void store_frag(uint32_t* f) const {
+#pragma unroll
+        for (int s = 0; s < S1; s++) {
+            *reinterpret_cast<u4v*>(f + 12 * s) = hi[s];
+            *reinterpret_cast<u4v*>(f + 12 * s + 4) = mid[s];
+            *reinterpret_cast<u4v*>(f + 12 * s + 8) = lo[s];
+        }
+    }
+    __device__ __forceinline__ void load_frag(const uint32_t* f) {
+#pragma unroll
+        for (int s = 0; s < S1; s++) {
+            hi[s] = *reinterpret_cast<const u4v*>(f + 12 * s);
+            mid[s] = *reinterpret_cast<const u4v*>(f + 12 * s + 4);
+            lo[s] = *reinterpret_cast<const u4v*>(f + 12 * s + 8);
+        }
+    }
     __device__ void load(const float* w1 /* [16][D] of this group */, int D, int i, int g) {
 #pragma unroll
         for (int s = 0; s < S1; s++) {
@@ -135,6 +152,35 @@ __device__ __forceinline__ u4v bytes_to_bf16(uint32_t d0, uint32_t d1) {
 template <int NT>
 struct Head {
     float b1[4], w2[4], b2[4], w3[NT][4], b3[NT][4];  // b1, b2 pre-scaled by kTanhScale (fast_tanh_b)
+    static constexpr int FW = 12 + 8 * NT;  // dwords of a lane's fragment
+    __device__ __forceinline__ void store_frag(float* f) const {
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            f[q] = b1[q];
+            f[4 + q] = w2[q];
+            f[8 + q] = b2[q];
+#pragma unroll
+            for (int t = 0; t < NT; t++) {
+                f[12 + 4 * t + q] = w3[t][q];
+                f[12 + 4 * NT + 4 * t + q] = b3[t][q];
+            }
+        }
+    }
+    __device__ __forceinline__ void load_frag(const float* f) {
+#pragma unroll
+        for (int q4 = 0; q4 < 3 + 2 * NT; q4++) {
+            const f4 v = *reinterpret_cast<const f4*>(f + 4 * q4);
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                const float x = v[q];
+                if (q4 == 0) b1[q] = x;
+                else if (q4 == 1) w2[q] = x;
+                else if (q4 == 2) b2[q] = x;
+                else if (q4 < 3 + NT) w3[q4 - 3][q] = x;
+                else b3[q4 - 3 - NT][q] = x;
+            }
+        }
+    }
     __device__ void load(const ms_mlp_params& p, int grp, int j, int g4) {
         const int A = p.n_actions;
 #pragma unroll
@@ -430,6 +476,28 @@ struct PriceTW {
     static constexpr int v = 32 * NT2 + 4;
 };
 
+// ---- act fragment block (ms_act_prepare): a header {magic, S1, NT, has common table}, then per group
+//      [64 lanes][LW] dwords (the lane's W1Split<S1> terms and Head<NT> parameters, exactly what the
+//      acting wave would derive) and the common row's sampling table [16 NT running sums][16 NT
+//      log-probs][S][last nonzero][2 pad] (Head::table)
+constexpr uint32_t kFragMagic = 0x4D534641u;
+template <int S1, int NT>
+struct FragLayout {
+    static constexpr int LW = 12 * S1 + Head<NT>::FW;  // dwords per lane (a multiple of 4)
+    static constexpr int TB = 32 * NT + 4;              // common table dwords
+    static constexpr int GB = 64 * LW + TB;             // dwords per group
+};
+// the group blocks of p's fragment block, or NULL when it is absent or made for another shape
+template <int S1, int NT>
+__device__ __forceinline__ const uint32_t* frag_groups(const ms_mlp_params& p, bool need_common) {
+    const uint32_t* f = static_cast<const uint32_t*>(p.act_frag);
+    if (!f) return nullptr;
+    const uint32_t h0 = __builtin_amdgcn_readfirstlane(f[0]), h1 = __builtin_amdgcn_readfirstlane(f[1]),
+                   h2 = __builtin_amdgcn_readfirstlane(f[2]), h3 = __builtin_amdgcn_readfirstlane(f[3]);
+    if (h0 != kFragMagic || h1 != (uint32_t)S1 || h2 != (uint32_t)NT || (need_common && !h3)) return nullptr;
+    return f + 4;
+}
+
 // One wave = a contiguous range of 16-row tiles of one group; no LDS. Layer 1 runs on the bf16 MFMA
 // with the weights split in three bf16 terms (exact f32 weights; the int8 inputs are exact in bf16):
 // lane (j, g) loads dwords 8s + 2g, 8s + 2g + 1 of tile row j, which are exactly its B fragment of
@@ -471,9 +539,16 @@ __device__ __forceinline__ void act_tiles(const ActArgs& a, int block) {
         pdig = reinterpret_cast<int16_t*>(s_pd[wid]);
     }
     W1Split<S1> w1;
-    w1.load(a.n1.w1 + (size_t)grp * 16 * a.n1.in_dim, a.n1.in_dim, j, g4);
     Head<NT> h1;
-    h1.load(a.n1, grp, j, g4);
+    if (const uint32_t* fg = frag_groups<S1, NT>(a.n1, false)) {  // made once per weight update
+        using FL = FragLayout<S1, NT>;
+        const uint32_t* lf = fg + (size_t)grp * FL::GB + lane * FL::LW;
+        w1.load_frag(lf);
+        h1.load_frag(reinterpret_cast<const float*>(lf + 12 * S1));
+    } else {
+        w1.load(a.n1.w1 + (size_t)grp * 16 * a.n1.in_dim, a.n1.in_dim, j, g4);
+        h1.load(a.n1, grp, j, g4);
+    }
     const uint64_t off = a.offset + (a.offset_dev ? *a.offset_dev : 0ull);
     const int stride4 = a.stride >> 2;
     const int n_rows_total = a.E * a.U;
@@ -735,6 +810,29 @@ __global__ void __launch_bounds__(256) k_act(ActArgs a) {
     act_tiles<S1, NT, NT2, EXT_U>(a, blockIdx.x);
 }
 
+// The common row's sampling table (Head::table) into LDS: its dwords (zero past the row: they meet
+// zero weights, like k_act's clamped loads) through layer 1 and the head. One wave.
+template <int S1, int NT>
+__device__ __forceinline__ void common_table(const W1Split<S1>& w1, const Head<NT>& h1, const int8_t* common,
+                                             int stride4, uint32_t* tmpl, float* cum, float* lp, float* S, int* lnz,
+                                             int lane) {
+    const int j = lane & 15, g4 = lane >> 4;
+    const uint32_t* crow = reinterpret_cast<const uint32_t*>(common);
+    for (int d = lane; d < 8 * S1; d += 64) tmpl[d] = d < stride4 ? crow[d] : 0u;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    f4 acc = {0, 0, 0, 0};
+#pragma unroll
+    for (int s = 0; s < S1; s++) {
+        const u4v x = bytes_to_bf16(tmpl[8 * s + 2 * g4], tmpl[8 * s + 2 * g4 + 1]);
+        acc = mfma_bf16(w1.hi[s], x, acc);
+        acc = mfma_bf16(w1.mid[s], x, acc);
+        acc = mfma_bf16(w1.lo[s], x, acc);
+    }
+    h1.table(acc, j, g4, cum, lp, S, lnz);
+}
+
 template <int S1, int NT, bool EXT_U, bool OWN>
 __device__ __forceinline__ void act_common_rows(const ActArgs& a, int block) {
     __shared__ int32_t s_list[4][kCommonSeg];
@@ -751,32 +849,38 @@ __device__ __forceinline__ void act_common_rows(const ActArgs& a, int block) {
     const int A = a.n1.n_actions;
     const int stride4 = a.stride >> 2;
     W1Split<S1> w1;
-    w1.load(a.n1.w1 + (size_t)grp * 16 * a.n1.in_dim, a.n1.in_dim, j, g4);
     Head<NT> h1;
-    h1.load(a.n1, grp, j, g4);
-    const uint64_t off = a.offset + (a.offset_dev ? *a.offset_dev : 0ull);
-    int32_t* list = s_list[wid];
-    float* ulist = s_ulist[wid];
-    // the common row's dwords (zero past the row: they meet zero weights, like k_act's clamped loads)
-    const uint32_t* crow = reinterpret_cast<const uint32_t*>(a.common);
-    for (int d = lane; d < 8 * S1; d += 64) s_tmpl[wid][d] = d < stride4 ? crow[d] : 0u;
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    {
-        f4 acc = {0, 0, 0, 0};
-#pragma unroll
-        for (int s = 0; s < S1; s++) {
-            const u4v x = bytes_to_bf16(s_tmpl[wid][8 * s + 2 * g4], s_tmpl[wid][8 * s + 2 * g4 + 1]);
-            acc = mfma_bf16(w1.hi[s], x, acc);
-            acc = mfma_bf16(w1.mid[s], x, acc);
-            acc = mfma_bf16(w1.lo[s], x, acc);
+    if (const uint32_t* fg = frag_groups<S1, NT>(a.n1, true)) {
+        // the weights and the common row's sampling table as ms_act_prepare made them
+        using FL = FragLayout<S1, NT>;
+        const uint32_t* gb = fg + (size_t)grp * FL::GB;
+        w1.load_frag(gb + lane * FL::LW);
+        h1.load_frag(reinterpret_cast<const float*>(gb + lane * FL::LW + 12 * S1));
+        const uint32_t* tb = gb + 64 * FL::LW;
+        for (int k = lane; k < 32 * NT + 2; k += 64) {
+            const uint32_t v = tb[k];
+            if (k < 16 * NT)
+                s_cum[wid][k] = __uint_as_float(v);
+            else if (k < 32 * NT)
+                s_lp[wid][k - 16 * NT] = __uint_as_float(v);
+            else if (k == 32 * NT)
+                s_S[wid] = __uint_as_float(v);
+            else
+                s_lnz[wid] = (int)v;
         }
-        h1.table(acc, j, g4, s_cum[wid], s_lp[wid], &s_S[wid], &s_lnz[wid]);
+    } else {
+        w1.load(a.n1.w1 + (size_t)grp * 16 * a.n1.in_dim, a.n1.in_dim, j, g4);
+        h1.load(a.n1, grp, j, g4);
+        common_table<S1, NT>(w1, h1, a.common, stride4, s_tmpl[wid], s_cum[wid], s_lp[wid], &s_S[wid], &s_lnz[wid],
+                             lane);
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const uint64_t off = a.offset + (a.offset_dev ? *a.offset_dev : 0ull);
+    int32_t* list = s_list[wid];
+    float* ulist = s_ulist[wid];
+    const uint32_t* crow = reinterpret_cast<const uint32_t*>(a.common);
     const float* cum = s_cum[wid];  // the running sums, non-decreasing (z >= 0): binary-searched in LDS
     constexpr int LPR = S1 <= 2 ? 4 : (S1 <= 4 ? 8 : 16);
     CommonScan<LPR> cs;
@@ -1157,6 +1261,78 @@ hipError_t launch_offer_act_free(const ms_mlp_params* core, const ms_mlp_params*
     ActArgs a = offer_free_args(core, price, obs, stride, E, U, S, n_cores, seed, offset, offset_dev, uniforms,
                                 core_action, core_logprob, price_state, price_action, price_logprob, env_price, pus);
     return dispatch_act(a, st);
+}
+
+// ms_act_prepare: one wave per group writes each lane's fragment (what the acting waves would derive:
+// W1Split::load, Head::load) and, with a common row, its sampling table (common_table: the same
+// arithmetic as the acting waves', so acting with the block is bit-identical to acting without).
+template <int S1, int NT>
+__global__ void __launch_bounds__(64) k_act_prep(ms_mlp_params p, const int8_t* common, int stride, uint32_t* frag) {
+    using FL = FragLayout<S1, NT>;
+    __shared__ uint32_t tmpl[8 * S1];
+    __shared__ float cum[16 * NT], lp[16 * NT], S;
+    __shared__ int lnz;
+    const int grp = blockIdx.x, lane = threadIdx.x, j = lane & 15, g4 = lane >> 4;
+    W1Split<S1> w1;
+    w1.load(p.w1 + (size_t)grp * 16 * p.in_dim, p.in_dim, j, g4);
+    Head<NT> h1;
+    h1.load(p, grp, j, g4);
+    uint32_t* gb = frag + 4 + (size_t)grp * FL::GB;
+    w1.store_frag(gb + lane * FL::LW);
+    h1.store_frag(reinterpret_cast<float*>(gb + lane * FL::LW + 12 * S1));
+    if (common) {
+        common_table<S1, NT>(w1, h1, common, stride >> 2, tmpl, cum, lp, &S, &lnz, lane);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        uint32_t* tb = gb + 64 * FL::LW;
+        for (int k = lane; k < FL::TB; k += 64)
+            tb[k] = k < 16 * NT ? __float_as_uint(cum[k])
+                                : (k < 32 * NT ? __float_as_uint(lp[k - 16 * NT])
+                                               : (k == 32 * NT ? __float_as_uint(S) : (k == 32 * NT + 1 ? (uint32_t)lnz : 0u)));
+    }
+    if (grp == 0 && lane < 4)
+        frag[lane] = lane == 0 ? kFragMagic : (lane == 1 ? (uint32_t)S1 : (lane == 2 ? (uint32_t)NT : (common ? 1u : 0u)));
+}
+
+static bool act_frag_shape(int stride, int A, int& s1, int& nt) {
+    s1 = (stride + 31) / 32;
+    s1 = s1 <= 1 ? 1 : (s1 <= 2 ? 2 : (s1 <= 4 ? 4 : (s1 <= 8 ? 8 : 0)));
+    nt = (A + 15) / 16;
+    nt = nt <= 1 ? 1 : (nt <= 2 ? 2 : (nt <= 4 ? 4 : (nt <= 8 ? 8 : 0)));
+    return s1 > 0 && nt > 0;
+}
+
+size_t act_frag_bytes(const ms_mlp_params* p, int stride) {
+    int s1, nt;
+    if (!act_frag_shape(stride, p->n_actions, s1, nt)) return 0;
+    const int lw = 12 * s1 + 12 + 8 * nt, gb = 64 * lw + 32 * nt + 4;
+    return 4 * (4 + (size_t)p->n_groups * gb);
+}
+
+template <int S1>
+static hipError_t launch_act_prep_s(const ms_mlp_params* p, const int8_t* common, int stride, uint32_t* frag, int nt,
+                                    hipStream_t st) {
+    const dim3 grid((unsigned)p->n_groups);
+    switch (nt) {
+        case 1: hipLaunchKernelGGL((k_act_prep<S1, 1>), grid, dim3(64), 0, st, *p, common, stride, frag); break;
+        case 2: hipLaunchKernelGGL((k_act_prep<S1, 2>), grid, dim3(64), 0, st, *p, common, stride, frag); break;
+        case 4: hipLaunchKernelGGL((k_act_prep<S1, 4>), grid, dim3(64), 0, st, *p, common, stride, frag); break;
+        default: hipLaunchKernelGGL((k_act_prep<S1, 8>), grid, dim3(64), 0, st, *p, common, stride, frag); break;
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_act_prepare(const ms_mlp_params* p, const int8_t* common, int stride, void* frag, hipStream_t st) {
+    int s1, nt;
+    if (!act_frag_shape(stride, p->n_actions, s1, nt) || p->hidden != 16) return hipErrorInvalidValue;
+    uint32_t* f = static_cast<uint32_t*>(frag);
+    switch (s1) {
+        case 1: return launch_act_prep_s<1>(p, common, stride, f, nt, st);
+        case 2: return launch_act_prep_s<2>(p, common, stride, f, nt, st);
+        case 4: return launch_act_prep_s<4>(p, common, stride, f, nt, st);
+        default: return launch_act_prep_s<8>(p, common, stride, f, nt, st);
+    }
 }
 
 // The price chooser's sampling table (ms_price_table_build): the forward of every tabulated 4-byte

@@ -28,7 +28,7 @@ import torch
 
 from . import abi
 from .env import BatchedEnv
-from .ppo import (PPOGroup, PriceTable, act_round_free, discounted_returns, offer_act_free, reference_init_order,
+from .ppo import (ActFrag, PPOGroup, PriceTable, act_round_free, discounted_returns, offer_act_free, reference_init_order,
                   reference_nets, unit_returns)
 
 
@@ -232,6 +232,12 @@ class Trainer:
         O = s.max_offers
         crow = [0, -1, -1] + [-2] * (2 * O) + [0] * (s.acc_obs_stride - s.acc_obs_dim)
         self.acc_common = torch.tensor(crow, dtype=torch.int8, device=dev)
+        # the acting nets' weight fragments (and the acceptors' common-row table), rebuilt at the start
+        # of every rollout like the price table (ActFrag; bit-identical to acting without them)
+        # (MS_ACT_FRAG=0: without them, for A/B measurements)
+        use_frag = os.environ.get("MS_ACT_FRAG", "1") != "0"
+        self.off_frag = ActFrag(self.off.group.policy_old, s.off_obs_stride) if use_frag else None
+        self.acc_frag = ActFrag(self.acc.group.policy_old, s.acc_obs_stride, self.acc_common) if use_frag else None
         self.agent_reward = torch.zeros((self.E, N), dtype=torch.int32, device=dev)
         self.auct_reward = torch.zeros((self.E, C), dtype=torch.int32, device=dev)
         self.rng = random.Random(seed)  # sub-unit draws (random.randint), identical on every rank
@@ -331,23 +337,27 @@ class Trainer:
                                self.acc.group.policy_old, sl(self.acc_rows[t]), sl(self.acc_owner[t]), self.acc_common,
                                C, seed, base + 1, base + 3, out, sl(self.acc.actions[t]), sl(self.acc.logprobs[t]),
                                offset_dev=self.rng_ctr, stream=st, price_table=self.price_table,
-                               price_unit_stride=pus)
+                               price_unit_stride=pus, core_frag=self.off_frag, acc_frag=self.acc_frag)
             else:
                 offer_act_free(self.off.group.policy_old, self.price.group.policy_old, sl(self.off_obs[t]), C, seed,
-                               base + 1, out, offset_dev=self.rng_ctr, stream=st, price_unit_stride=pus)
+                               base + 1, out, offset_dev=self.rng_ctr, stream=st, price_unit_stride=pus,
+                               core_frag=self.off_frag)
         else:
             self.off.group.policy_old.act(sl(self.off_obs[t]), N * L, seed, base + 1, action=sl(self.off.actions[t]),
-                                          logprob=sl(self.off.logprobs[t]), offset_dev=self.rng_ctr, stream=st)
+                                          logprob=sl(self.off.logprobs[t]), offset_dev=self.rng_ctr, stream=st,
+                                          frag=self.off_frag)
         if self.compact and self.free:
             pass  # acted above with the offers
         elif self.compact:
             self.acc.group.policy_old.act_compact(sl(self.acc_rows[t]), sl(self.acc_owner[t]), N * C, seed, base + 3,
                                                   self.acc_common, action=sl(self.acc.actions[t]),
-                                                  logprob=sl(self.acc.logprobs[t]), offset_dev=self.rng_ctr, stream=st)
+                                                  logprob=sl(self.acc.logprobs[t]), offset_dev=self.rng_ctr, stream=st,
+                                                  frag=self.acc_frag)
         else:
             self.acc.group.policy_old.act(sl(self.acc_obs[t]), N * C, seed, base + 3, action=sl(self.acc.actions[t]),
                                           logprob=sl(self.acc.logprobs[t]), offset_dev=self.rng_ctr,
-                                          common_row=self.acc_common if self.common_rows else None, stream=st)
+                                          common_row=self.acc_common if self.common_rows else None, stream=st,
+                                          frag=self.acc_frag)
 
     def _step_part(self, t: int, k: int):
         """env.step + saveRewards of round t for replica part k (on stream k)."""
@@ -390,6 +400,9 @@ class Trainer:
             self.spans[:: self.span_every].zero_()
         if self.price_table is not None:
             self.price_table.build(self.price.group.policy_old)
+        if self.off_frag is not None:
+            self.off_frag.build(self.off.group.policy_old)
+            self.acc_frag.build(self.acc.group.policy_old)
         for s in self.streams[1:]:  # fork: the side streams start after everything queued so far
             s.wait_stream(cur)
         for t in range(self.T):

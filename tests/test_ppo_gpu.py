@@ -76,6 +76,14 @@ def test_act_common_rows_bit_identical(ms, G, per_group, O, A, frac, ext_u):
     a1, l1 = net.act(dobs, U, seed=3, offset=11, uniforms=u, common_row=crow.cuda())
     assert torch.equal(a0, a1)
     assert torch.equal(l0.view(torch.int32), l1.view(torch.int32))
+    # the same with ms_act_prepare's fragments (the common-row table made once, not per wave)
+    frag = ppo.ActFrag(net, stride, crow.cuda())
+    frag.build(net)
+    a2, l2 = net.act(dobs, U, seed=3, offset=11, uniforms=u, common_row=crow.cuda(), frag=frag)
+    a3, l3 = net.act(dobs, U, seed=3, offset=11, uniforms=u, frag=frag)
+    for a, l in ((a2, l2), (a3, l3)):
+        assert torch.equal(a0, a)
+        assert torch.equal(l0.view(torch.int32), l.view(torch.int32))
 
 
 def test_act_kernel_sampling_distribution(ms):
@@ -429,6 +437,24 @@ def test_act_round_free_matches_separate_calls(ms, N, C, L, O, E):
         assert torch.equal(o1[k].view(torch.int8), o2[k].view(torch.int8)), k
     assert torch.equal(a1, a2)
     assert torch.equal(l1.view(torch.int32), l2.view(torch.int32))
+    # with ms_act_prepare's weight fragments (and the acceptors' common-row table): bit-identical; a
+    # block made for another row shape is ignored (its header does not match the call)
+    fc, fa = ppo.ActFrag(core, s_off), ppo.ActFrag(acc, s_acc, crow)
+    fc.build(core)
+    fa.build(acc)
+    wrong = ppo.ActFrag(acc, s_acc + 32, crow)  # another layer-1 k-step count
+    wrong.build(acc)
+    for core_frag, acc_frag in ((fc, fa), (None, fa), (fc, None), (None, wrong)):
+        o4 = outs()
+        a4, l4 = torch.empty_like(a1), torch.empty_like(l1)
+        ppo.act_round_free(core, price, off_obs, acc, rows, owner, crow, C, 77, 5, 7, o4, a4, l4, offset_dev=ctr,
+                           core_frag=core_frag, acc_frag=acc_frag)
+        for k in o1:
+            assert torch.equal(o1[k].view(torch.int8), o4[k].view(torch.int8)), (k, core_frag, acc_frag)
+        assert torch.equal(a1, a4)
+        assert torch.equal(l1.view(torch.int32), l4.view(torch.int32))
+    a5, l5 = acc.act_compact(rows, owner, N * C, 77, 7, crow, offset_dev=ctr, frag=fa)
+    assert torch.equal(a1, a5) and torch.equal(l1.view(torch.int32), l5.view(torch.int32))
     # unit-major price outputs (a [U][T][E] ring at round t = 1 of T = 3, as the trainer keeps them):
     # the same values at (u, t, e); env_price stays [E][U]
     T, t, U = 3, 1, N * L
