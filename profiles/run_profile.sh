@@ -10,11 +10,11 @@ mkdir -p "$OUT"
 export TMPDIR=/tmp
 cd /tmp
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -f csv -d "$OUT/trace" -o run -- \
-  python3 "$R/bench.py" --steps 1 --warmup 1 --no-cpu-baseline > "$OUT/bench.json" 2> "$OUT/trace.err"
+  python3 "$R/bench.py" --steps 1 --warmup 1 --no-cpu-baseline --no-step-kernel > "$OUT/bench.json" 2> "$OUT/trace.err"
 timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex k_env_step -f csv -d "$OUT/pmc_fetch" -o run -- \
-  python3 "$R/bench.py" --steps 1 --warmup 0 --update-step 20 --no-cpu-baseline > "$OUT/pmc_fetch.json" 2> "$OUT/pmc_fetch.err"
+  python3 "$R/bench.py" --steps 1 --warmup 0 --update-step 20 --no-cpu-baseline --no-step-kernel > "$OUT/pmc_fetch.json" 2> "$OUT/pmc_fetch.err"
 timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex k_env_step -f csv -d "$OUT/pmc_write" -o run -- \
-  python3 "$R/bench.py" --steps 1 --warmup 0 --update-step 20 --no-cpu-baseline > "$OUT/pmc_write.json" 2> "$OUT/pmc_write.err"
+  python3 "$R/bench.py" --steps 1 --warmup 0 --update-step 20 --no-cpu-baseline --no-step-kernel > "$OUT/pmc_write.json" 2> "$OUT/pmc_write.err"
 ALG=$(python3 -c "import json; r = json.load(open('$OUT/pmc_fetch.json'))['roofline']; print(r['bytes_per_env_round'] * r['envs_per_launch'])")
 VAR=$(python3 -c "import json; r = json.load(open('$OUT/pmc_fetch.json'))['roofline']; print('compact' if r.get('acceptor_observations', '').startswith('compact') else '')")
 python3 "$R/profiles/traffic_from_pmc.py" "$OUT/pmc_fetch/run_counter_collection.csv" "$OUT/pmc_write/run_counter_collection.csv" "$ALG" "$OUT/traffic.json" "$VAR"
