@@ -353,7 +353,7 @@ def act_roofline(tr, device, reps: int = 20):
             tr._act_part(0, 0)  # warm
         st.synchronize()
         g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g, stream=st):
+        with importlib.import_module("marl-scheduling_amd._lib").hip_capture(g, stream=st):
             for _ in range(reps):
                 tr._act_part(0, 0)
     finally:
@@ -526,7 +526,7 @@ def step_kernel_line(E: int, device, world: int, rank: int):
             body()
         torch.cuda.synchronize(device)
         graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(graph):
+        with importlib.import_module("marl-scheduling_amd._lib").hip_capture(graph):
             body()
         stream = torch.cuda.current_stream(device)
         ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]

@@ -7,7 +7,9 @@ libamdhip64.so.7).
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes as ct
+import gc
 import os
 
 import torch  # noqa: F401  (load torch's HIP runtime before the library)
@@ -131,6 +133,22 @@ def ptr(t) -> ct.c_void_p | None:
     if t is None:
         return None
     return ct.c_void_p(t.data_ptr())
+
+
+@contextlib.contextmanager
+def hip_capture(graph, **kw):
+    """torch.cuda.graph(graph, **kw) with Python's cyclic garbage collector held off: a finalizer that a
+    collection runs inside the capture (BatchedEnv.close -> ms_env_destroy -> hipFree of an env left in a
+    reference cycle) is an operation a global-mode capture does not permit, and it invalidates the graph."""
+    gc.collect()
+    was = gc.isenabled()
+    gc.disable()
+    try:
+        with torch.cuda.graph(graph, **kw):
+            yield
+    finally:
+        if was:
+            gc.enable()
 
 
 def stream_ptr(stream=None):

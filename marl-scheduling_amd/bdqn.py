@@ -45,7 +45,7 @@ import torch.nn as nn
 import torch.nn.functional as F_
 
 from . import abi
-from ._lib import check, lib, ptr, stream_ptr
+from ._lib import check, hip_capture, lib, ptr, stream_ptr
 from .ppo import HipAdam
 
 KEYS = ("w1", "b1", "w2", "b2", "wv", "bv", "wa", "ba")
@@ -209,7 +209,7 @@ class BranchingRole:
             torch.cuda.current_stream(states.device).wait_stream(side)
             torch.cuda.synchronize(states.device)
             g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g):
+            with hip_capture(g):
                 self._loss = self._body(*self._in)
             self._g = g
         else:

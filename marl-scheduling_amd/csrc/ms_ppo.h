@@ -25,6 +25,7 @@ struct PpoArgs {
     int chunk_tiles, n_chunks, P;
     float eps_clip, inv_R;
     int part_rows, part_off;  // partial vectors per group, this launch's first one
+    int blocks_per_group;     // blocks per group of this launch (set by the launcher)
     // keyed rows (rows of <= 4 bytes whose values lie in [-8, 24), ppo_kernels.hip): a row's dense
     // index packs its bytes 5 bits each; the distinct rows of a group, ranked by dense index, get
     // one forward and one backward pass, and every row adds its loss derivatives to its rank's

@@ -106,7 +106,19 @@ __device__ __forceinline__ u4v bytes_to_bf16(uint32_t d0, uint32_t d1) {
 }
 
 constexpr int kCommonSeg = 512;   // rows scanned per segment of the common-row path
+#ifndef MS_XCD_MAP
+#define MS_XCD_MAP 1
+#endif
+#ifndef MS_OWN_SEG
+#define MS_OWN_SEG 512
+#endif
+template <int MODE>
+constexpr int seg_rows() { return MODE == 2 ? MS_OWN_SEG : kCommonSeg; }  // (2 = kOwnerRow)
 constexpr int kScanDepth = 1;     // 64-row scan steps in flight (2 spills registers at <4, 2>: slower)
+#ifndef MS_OWN_DEPTH
+#define MS_OWN_DEPTH 1
+#endif
+constexpr int kScanDepthOwn = MS_OWN_DEPTH;  // the same for compact rows (no row chunks in the scan registers)
 
 template <bool B>
 struct BoolC {
@@ -117,6 +129,13 @@ struct BoolC {
 // from the core owners of compact acceptor observations); keyed rows (the backward and the forward
 // of a group's distinct rows, k_key_scan sums the rows' loss derivatives in between)
 enum GradMode { kPlain = 0, kCommonRow = 1, kOwnerRow = 2, kKeyBack = 3, kKeyFwd = 4 };
+
+#ifdef MS_GRAD_PROBE
+// Probe build only (tools/grad_probe.py): per wave of the last common/owner-row launch, s_memrealtime
+// at entry, after the scan, at exit, and the rows the scan listed for the tiles.
+constexpr int kGradProbeWaves = 1 << 15;
+__device__ unsigned long long g_grad_probe[kGradProbeWaves][4];
+#endif
 
 template <int NQ, int NT, int MODE>
 struct GradLds {
@@ -133,7 +152,7 @@ struct GradLds {
     // per wave: d1 / e1 transposes over a tile pair, the per-tile transposes, 32 staged input rows
     // (common-row path: the common row's clamped logs, V, entropy, the list of the other rows,
     //  and the wave's int64 fixed-point sums of d min(surr)/d ratio * ratio per action [16*NT])
-    static constexpr int CMF = CM ? 16 * NT + 4 + kCommonSeg + 64 + 2 * 16 * NT : 0;
+    static constexpr int CMF = CM ? 16 * NT + 4 + seg_rows<MODE>() + 64 + 2 * 16 * NT : 0;
     static constexpr int wave_floats = 2 * 16 * TP2 + NTR * 16 * TP + 32 * XPD + CMF;
     // waves per block: 4 when they fit the 160 KB of LDS, else 2 (each wave then walks two chunks)
     static constexpr int WPB = shared_floats + 4 * wave_floats <= 40960 ? 4 : 2;
@@ -152,11 +171,19 @@ __global__ void __launch_bounds__((64 * GradLds<NQ, NT, MODE>::WPB), ((NQ * NT >
     const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int g4 = lane >> 4;  // MFMA k-group / C-row group
     const int j = lane & 15;   // batch row within the tile (C column)
-    // groups interleaved over the block index: the G groups' blocks of the same rows run at the
-    // same time, so the rollout lines they share (rows [r][0..U) of states, actions, log-probs)
-    // come from HBM once and hit in the Infinity Cache for the other groups
+    // XCD-aware block map: blocks b and b + 8 run on one XCD (round-robin placement, speed only), so
+    // the G groups' blocks of one row range take block indices 8 apart: they run on the same XCD at
+    // about the same time, and the rollout lines they share (rows [r][0..U) of states, actions,
+    // log-probs, returns) come into that XCD's L2 once instead of once per group's XCD
+#if MS_XCD_MAP
+    const int xq = blockIdx.x >> 3;
+    const int grp = xq % p.G;
+    const int blk = (xq / p.G) * 8 + (blockIdx.x & 7);
+    if (blk >= p.blocks_per_group) return;  // padding of the grid to whole 8-block sets (whole block)
+#else
     const int grp = blockIdx.x % p.G;
     const int blk = blockIdx.x / p.G;
+#endif
     const int chunk = blk * 4 + wave * CPW;
     const int D = p.D, A = p.A;
     const int u = p.unit_of_group[grp];
@@ -184,6 +211,10 @@ __global__ void __launch_bounds__((64 * GradLds<NQ, NT, MODE>::WPB), ((NQ * NT >
     // k_ppo_reduce skips this block's partial row for the others
     if constexpr (MODE == kPlain)
         if (p.key_n && p.key_n[grp] >= 0 && p.key_flag[grp] == 0) return;
+#ifdef MS_GRAD_PROBE
+    const unsigned long long probe_t0 = __builtin_amdgcn_s_memrealtime();
+    unsigned long long probe_listed = 0, probe_t1 = 0;
+#endif
 
     // ---- stage this group's weights (once per block); W1 / C1 as three exact bf16 terms
     {
@@ -682,7 +713,7 @@ __global__ void __launch_bounds__((64 * GradLds<NQ, NT, MODE>::WPB), ((NQ * NT >
         const bool keyed = p.key_n[grp] >= 0 && p.key_flag[grp] == 0;
         const int n = keyed ? p.key_n[grp] : 0;
         const int tiles = (n + 15) / 16;
-        const int wpg = (int)(gridDim.x / p.G) * L::WPB;
+        const int wpg = p.blocks_per_group * L::WPB;
         const int tpw = (tiles + wpg - 1) / wpg;
         const int st0 = (blk * L::WPB + wave) * tpw, st1 = min(st0 + tpw, tiles);
         const size_t gr = (size_t)grp * kKeyMaxRanks;
@@ -824,7 +855,8 @@ __global__ void __launch_bounds__((64 * GradLds<NQ, NT, MODE>::WPB), ((NQ * NT >
         // the wave's sums of d min(surr)/d ratio * ratio per action over its common rows: int64
         // fixed point (2^-28) with LDS atomics, so the order of the adds does not matter; a row
         // whose term could overflow them is listed for the tiles instead
-        long long* vacc = reinterpret_cast<long long*>(list + kCommonSeg + 64);
+        constexpr int SEG = seg_rows<MODE>();
+        long long* vacc = reinterpret_cast<long long*>(list + SEG + 64);
         if (lane < 16 * NT) vacc[lane] = 0;
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -836,7 +868,7 @@ __global__ void __launch_bounds__((64 * GradLds<NQ, NT, MODE>::WPB), ((NQ * NT >
         int n_list = 0, otile = 0;
         // scan registers, kScanDepth 64-row steps in flight: the rows' chunks (cooperative 16-byte
         // loads) and row r0 + lane's scalars
-        constexpr int PF = kScanDepth;
+        constexpr int PF = MODE == kOwnerRow ? kScanDepthOwn : kScanDepth;
         u4a sc[MODE == kCommonRow ? PF : 1][MODE == kCommonRow ? LPR : 1];
         int s_act[PF];
         int8_t s_own[PF];
@@ -876,8 +908,8 @@ __global__ void __launch_bounds__((64 * GradLds<NQ, NT, MODE>::WPB), ((NQ * NT >
                 otile++;
             }
         };
-        for (int seg = rb; seg < re; seg += kCommonSeg) {
-            const int seg_end = min(seg + kCommonSeg, re);
+        for (int seg = rb; seg < re; seg += SEG) {
+            const int seg_end = min(seg + SEG, re);
 #pragma unroll
             for (int k = 0; k < PF; k++)
                 if (seg + 64 * k < seg_end) load_slot(k, seg + 64 * k, seg_end);
@@ -923,6 +955,9 @@ __global__ void __launch_bounds__((64 * GradLds<NQ, NT, MODE>::WPB), ((NQ * NT >
                     }
                     const bool other = in && !common;
                     const uint64_t m = __ballot(other);
+#ifdef MS_GRAD_PROBE
+                    probe_listed += __popcll(m);
+#endif
                     if (other) list[n_list + __popcll(m & below)] = r;
                     n_list += __popcll(m);
                 }
@@ -945,6 +980,9 @@ __global__ void __launch_bounds__((64 * GradLds<NQ, NT, MODE>::WPB), ((NQ * NT >
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         }
         if (n_list > 0) owner_tiles(n_list);
+#ifdef MS_GRAD_PROBE
+        probe_t1 = __builtin_amdgcn_s_memrealtime();
+#endif
         // the virtual tile: column 0 carries the common rows' summed derivatives
         // wave totals per action (lane k sums action k's 64 entries in lane order), then column 0
         // of the virtual tile: lane (0, g4) takes actions 16t + 4*g4 + q
@@ -1033,6 +1071,17 @@ __global__ void __launch_bounds__((64 * GradLds<NQ, NT, MODE>::WPB), ((NQ * NT >
     }
     float* outp = p.partials + ((size_t)grp * p.part_rows + p.part_off + blk) * p.P;
     for (int i = tid; i < p.P; i += NTH) outp[i] = acc[i];
+#ifdef MS_GRAD_PROBE
+    if constexpr (L::CM) {
+        const int wi = blockIdx.x * L::WPB + wave;
+        if (lane == 0 && wi < kGradProbeWaves) {
+            g_grad_probe[wi][0] = probe_t0;
+            g_grad_probe[wi][1] = probe_t1;
+            g_grad_probe[wi][2] = __builtin_amdgcn_s_memrealtime();
+            g_grad_probe[wi][3] = probe_listed | ((unsigned long long)grp << 32);
+        }
+    }
+#endif
 }
 
 // Sum the blocks' partial vectors (fixed order: 4 interleaved row sets, then a fixed tree) and
@@ -1078,8 +1127,14 @@ static hipError_t launch_grad_cm(const PpoArgs& a, unsigned blocks_per_group, hi
     using L = GradLds<NQ, NT, MODE>;
     const size_t lds = sizeof(float) * L::lds_floats;
     if (lds > 160 * 1024 || (size_t)a.P > (size_t)L::lds_floats) return hipErrorInvalidValue;  // partial in LDS
-    hipLaunchKernelGGL((k_ppo_grad<NQ, NT, MODE>), dim3((unsigned)a.G * blocks_per_group), dim3(64 * L::WPB), lds, st,
-                       a);
+    PpoArgs b = a;
+    b.blocks_per_group = (int)blocks_per_group;
+#if MS_XCD_MAP
+    const unsigned grid = (unsigned)a.G * ((blocks_per_group + 7) / 8 * 8);
+#else
+    const unsigned grid = (unsigned)a.G * blocks_per_group;
+#endif
+    hipLaunchKernelGGL((k_ppo_grad<NQ, NT, MODE>), dim3(grid), dim3(64 * L::WPB), lds, st, b);
     return hipGetLastError();
 }
 
@@ -1371,6 +1426,13 @@ reduce:
 }
 
 int ppo_param_count(int D, int A) { return poff(D, A).total; }
+}  // namespace ms
+#ifdef MS_GRAD_PROBE
+extern "C" int ms_grad_probe_read(void* host, size_t bytes) {
+    return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(ms::g_grad_probe), bytes, 0, hipMemcpyDeviceToHost);
+}
+#endif
+namespace ms {
 
 // ---------------------------------------------------------------------------
 // Adam (torch.optim.Adam's foreach step, torch/optim/adam.py _multi_tensor_adam) over up to 16

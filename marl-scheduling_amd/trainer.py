@@ -27,6 +27,7 @@ from dataclasses import dataclass, field
 import torch
 
 from . import abi
+from ._lib import hip_capture
 from .env import BatchedEnv
 from .ppo import (ActFrag, PPOGroup, PriceTable, act_round_free, discounted_returns, offer_act_free, reference_init_order,
                   reference_nets, unit_returns)
@@ -420,7 +421,7 @@ class Trainer:
             self._rollout_body()
             torch.cuda.synchronize(self.device)
             g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g):
+            with hip_capture(g):
                 self._rollout_body()
             self.graph = g
         else:
@@ -532,7 +533,7 @@ class Trainer:
         pool = None
         while True:
             g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g, pool=pool):
+            with hip_capture(g, pool=pool):
                 p = next(phases, None)
             if pool is None:
                 pool = g.pool()
