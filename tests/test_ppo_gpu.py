@@ -123,11 +123,12 @@ def test_returns_kernel_matches_reference(ms):
         np.testing.assert_allclose(got[m].numpy(), want.numpy(), rtol=1e-5, atol=2e-6)
 
 
+@pytest.mark.parametrize("T", [60, 200])  # 200: the kernel holding each sequence in registers
 @pytest.mark.parametrize("dtype", [torch.int32, torch.float32])
-def test_unit_returns_gathers_and_matches_reference(ms, dtype):
+def test_unit_returns_gathers_and_matches_reference(ms, dtype, T):
     ppo = _ppo(ms)
     gen = torch.Generator().manual_seed(8)
-    T, E, U, G = 60, 33, 24, 8
+    E, U, G = 33, 24, 8
     r = torch.randint(-20, 30, (T, E, U), generator=gen)
     r = r.to(dtype) if dtype == torch.int32 else (0.5 * r).float()
     sel = torch.randint(0, U, (G,), generator=gen).to(torch.int32)
