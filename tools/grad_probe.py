@@ -15,7 +15,7 @@ importlib.import_module("marl-scheduling_amd")
 trainer_mod = importlib.import_module("marl-scheduling_amd.trainer")
 lib_mod = importlib.import_module("marl-scheduling_amd._lib")
 
-tr = trainer_mod.Trainer.from_named("cfg3", n_envs=int(os.environ.get("E", "16384")), update_step=200, seed=0,
+tr = trainer_mod.Trainer.from_named(os.environ.get("CFG", "cfg3"), n_envs=int(os.environ.get("E", "16384")), update_step=200, seed=0,
                                     device=torch.device("cuda:0"))
 for _ in range(2):
     tr.iteration()
@@ -36,10 +36,10 @@ end = (b[:, 2].astype(np.int64) - base) / 100.0
 listed = (b[:, 3] & 0xffffffff).astype(np.int64)
 grp = (b[:, 3] >> 32).astype(np.int64)
 pct = [0, 10, 50, 90, 99, 100]
-print("waves", used.sum(), "launch span %.1f us" % end.max())
+print("waves", used.sum(), "launch span %.1f us" % end.max(), "scan-only waves (none listed): lifetime mean %.1f us" % life[listed == 0].mean() if (listed == 0).any() else "")
 for name, v in (("start", start), ("scan+tiles", scan), ("lifetime", life), ("end", end), ("listed", listed)):
     print("%-11s" % name, " ".join("%9.1f" % np.percentile(v, q) for q in pct))
-for g in range(grp.max() + 1):
+for g in range(min(grp.max() + 1, 16)):
     m = grp == g
     print("group %d: waves %d listed mean %.0f max %d lifetime mean %.1f max %.1f us" % (
         g, m.sum(), listed[m].mean(), listed[m].max(), life[m].mean(), life[m].max()))
