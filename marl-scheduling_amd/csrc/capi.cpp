@@ -61,10 +61,14 @@ hipError_t launch_wide_act(const WideAct&, hipStream_t);
 hipError_t launch_wide_grad(const WideRows&, const WideGrads&, const WideReduce&, hipStream_t);
 }  // namespace ms
 
-// work split of k_ppo_grad: ~8192 wave chunks over all groups (4 per block), >= 8 tiles of 16 rows each
+// work split of k_ppo_grad: ~kGradWaves wave chunks over all groups (4 per block), >= 8 tiles of 16 rows each
+#ifndef MS_GRAD_WAVES
+#define MS_GRAD_WAVES 8192
+#endif
 static void ppo_split(int64_t rows, int G, int* chunk_tiles, int* n_chunks) {
+    constexpr int64_t kGradWaves = MS_GRAD_WAVES;
     int64_t tiles = (rows + 15) / 16;
-    int64_t ct = (tiles * G + 8191) / 8192;
+    int64_t ct = (tiles * G + kGradWaves - 1) / kGradWaves;
     if (ct < 8) ct = 8;
     ct = (ct + 1) & ~1LL;  // whole tile pairs (the dW1 step runs on 32 rows)
     *chunk_tiles = (int)ct;
