@@ -29,7 +29,7 @@ for src in env_kernels.hip policy_kernels.hip returns_kernels.hip ppo_kernels.hi
   # the acting kernels are latency-bound chains: the ILP-first machine scheduler shortens them (rollout
   # 12.14 -> 11.87 ms at cfg3, profiles/r3f2/ab_sched_strategy.txt); the env round gains nothing and the
   # gradient and returns kernels lose with it (update 8.64 -> 9.22 ms), so they keep the default
-  [[ "${src}" == policy_kernels.hip ]] && contract+=(-mllvm -amdgpu-sched-strategy=max-ilp)
+  [[ "${src}" == policy_kernels.hip && "${MS_NO_ILP:-0}" != 1 ]] && contract+=(-mllvm -amdgpu-sched-strategy=max-ilp)
   key="$( { cat "${HERE}/csrc/${src}" "${HEADERS[@]}"; echo "${CCVER} ${FLAGS[*]} ${contract[*]}"; } | sha256sum | cut -d' ' -f1)"
   if [[ ! -f "${obj}" || "$(cat "${obj}.key" 2>/dev/null)" != "${key}" ]]; then
     rm -f "${obj}.key"
