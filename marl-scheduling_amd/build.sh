@@ -17,20 +17,23 @@ HEADERS=("${HERE}/csrc/ms_layout.h" "${HERE}/csrc/ms_ppo.h" "${HERE}/csrc/ms_dqn
 CCVER="$("${HIPCC}" --version 2>/dev/null | head -3 | tr '\n' ' ')"
 objs=()
 pids=()
-for src in env_kernels.hip policy_kernels.hip returns_kernels.hip ppo_kernels.hip agg_kernels.hip dqn_kernels.hip bdqn_kernels.hip wide_kernels.hip capi.cpp; do
+for src in env_kernels.hip policy_kernels.hip act_pair_kernels.hip returns_kernels.hip ppo_kernels.hip agg_kernels.hip dqn_kernels.hip bdqn_kernels.hip wide_kernels.hip capi.cpp; do
   obj="${OBJDIR}/${src%.*}.o"
   # the env round reproduces Python's float64 arithmetic: no contraction there; the policy
   # and PPO kernels follow torch's f32 (which fuses freely) within tolerance: fma allowed
   contract=(-ffp-contract=off)
-  [[ "${src}" == policy_kernels.hip || "${src}" == returns_kernels.hip ]] && contract=(-ffp-contract=fast)
+  [[ "${src}" == policy_kernels.hip || "${src}" == act_pair_kernels.hip || "${src}" == returns_kernels.hip ]] && contract=(-ffp-contract=fast)
   # the gradient kernel's variants (common rows by bytes or by owners) must agree bit for bit: fma only
   # where an expression asks for it, never across statements (fast contraction depends on the code around)
   [[ "${src}" == ppo_kernels.hip || "${src}" == bdqn_kernels.hip || "${src}" == wide_kernels.hip ]] && contract=(-ffp-contract=on)
-  # the acting kernels are latency-bound chains: the ILP-first machine scheduler shortens them (rollout
-  # 12.14 -> 11.87 ms at cfg3, profiles/r3f2/ab_sched_strategy.txt); the env round gains nothing and the
-  # gradient and returns kernels lose with it (update 8.64 -> 9.22 ms), so they keep the default
-  [[ "${src}" == policy_kernels.hip && "${MS_NO_ILP:-0}" != 1 ]] && contract+=(-mllvm -amdgpu-sched-strategy=max-ilp)
-  key="$( { cat "${HERE}/csrc/${src}" "${HEADERS[@]}"; echo "${CCVER} ${FLAGS[*]} ${contract[*]}"; } | sha256sum | cut -d' ' -f1)"
+  # cfg3's paired acting kernel is a latency-bound chain: the ILP-first machine scheduler shortens it
+  # (rollout 12.14 -> 11.88 ms, profiles/r3f2/ab_sched_ilp_act.txt); the env round gains nothing, and the
+  # gradient, returns and cfg4 acting kernels lose with it, so they keep the default (act_pair_kernels.hip)
+  [[ "${src}" == policy_kernels.hip ]] && contract+=(-DMS_SPLIT_PAIR)
+  [[ "${src}" == act_pair_kernels.hip && "${MS_NO_ILP:-0}" != 1 ]] && contract+=(-mllvm -amdgpu-sched-strategy=max-ilp)
+  inc=()
+  [[ "${src}" == act_pair_kernels.hip ]] && inc=("${HERE}/csrc/policy_kernels.hip")  # it includes that file
+  key="$( { cat "${HERE}/csrc/${src}" "${inc[@]}" "${HEADERS[@]}"; echo "${CCVER} ${FLAGS[*]} ${contract[*]}"; } | sha256sum | cut -d' ' -f1)"
   if [[ ! -f "${obj}" || "$(cat "${obj}.key" 2>/dev/null)" != "${key}" ]]; then
     rm -f "${obj}.key"
     lang=()

@@ -1168,6 +1168,7 @@ static hipError_t dispatch_act(ActArgs& a, hipStream_t st) {
     return hipErrorInvalidValue;
 }
 
+#ifndef MS_ACT_PAIR_TU  // (the paired act kernel's translation unit defines only launch_act_round)
 hipError_t launch_policy_act(const ms_mlp_params* p, const int8_t* obs, int stride, int64_t E, int U, int S,
                              const int8_t* common, uint64_t seed, uint64_t offset, const uint64_t* offset_dev,
                              const float* uniforms, int8_t* action, float* logprob, hipStream_t st) {
@@ -1189,6 +1190,7 @@ hipError_t launch_policy_act(const ms_mlp_params* p, const int8_t* obs, int stri
     a.logprob = logprob;
     return dispatch_act(a, st);
 }
+#endif
 
 static ActArgs compact_args(const ms_mlp_params* p, const int8_t* core_rows, const int8_t* core_owner, int stride,
                             int64_t E, int U, int S, int n_cores, const int8_t* common, uint64_t seed, uint64_t offset,
@@ -1214,6 +1216,7 @@ static ActArgs compact_args(const ms_mlp_params* p, const int8_t* core_rows, con
     return a;
 }
 
+#ifndef MS_ACT_PAIR_TU  // (the paired act kernel's translation unit defines only launch_act_round)
 hipError_t launch_policy_act_compact(const ms_mlp_params* p, const int8_t* core_rows, const int8_t* core_owner,
                                      int stride, int64_t E, int U, int S, int n_cores, const int8_t* common,
                                      uint64_t seed, uint64_t offset, const uint64_t* offset_dev, const float* uniforms,
@@ -1223,6 +1226,7 @@ hipError_t launch_policy_act_compact(const ms_mlp_params* p, const int8_t* core_
                              uniforms, action, logprob);
     return dispatch_act(a, st);
 }
+#endif
 
 static ActArgs offer_free_args(const ms_mlp_params* core, const ms_mlp_params* price, const int8_t* obs, int stride,
                                int64_t E, int U, int S, int n_cores, uint64_t seed, uint64_t offset,
@@ -1253,6 +1257,7 @@ static ActArgs offer_free_args(const ms_mlp_params* core, const ms_mlp_params* p
     return a;
 }
 
+#ifndef MS_ACT_PAIR_TU  // (the paired act kernel's translation unit defines only launch_act_round)
 hipError_t launch_offer_act_free(const ms_mlp_params* core, const ms_mlp_params* price, const int8_t* obs, int stride,
                                  int64_t E, int U, int S, int n_cores, uint64_t seed, uint64_t offset,
                                  const uint64_t* offset_dev, const float* uniforms, int8_t* core_action,
@@ -1262,6 +1267,7 @@ hipError_t launch_offer_act_free(const ms_mlp_params* core, const ms_mlp_params*
                                 core_action, core_logprob, price_state, price_action, price_logprob, env_price, pus);
     return dispatch_act(a, st);
 }
+#endif
 
 // ms_act_prepare: one wave per group writes each lane's fragment (what the acting waves would derive:
 // W1Split::load, Head::load) and, with a common row, its sampling table (common_table: the same
@@ -1303,12 +1309,14 @@ static bool act_frag_shape(int stride, int A, int& s1, int& nt) {
     return s1 > 0 && nt > 0;
 }
 
+#ifndef MS_ACT_PAIR_TU  // (the paired act kernel's translation unit defines only launch_act_round)
 size_t act_frag_bytes(const ms_mlp_params* p, int stride) {
     int s1, nt;
     if (!act_frag_shape(stride, p->n_actions, s1, nt)) return 0;
     const int lw = 12 * s1 + 12 + 8 * nt, gb = 64 * lw + 32 * nt + 4;
     return 4 * (4 + (size_t)p->n_groups * gb);
 }
+#endif
 
 template <int S1>
 static hipError_t launch_act_prep_s(const ms_mlp_params* p, const int8_t* common, int stride, uint32_t* frag, int nt,
@@ -1323,6 +1331,7 @@ static hipError_t launch_act_prep_s(const ms_mlp_params* p, const int8_t* common
     return hipGetLastError();
 }
 
+#ifndef MS_ACT_PAIR_TU  // (the paired act kernel's translation unit defines only launch_act_round)
 hipError_t launch_act_prepare(const ms_mlp_params* p, const int8_t* common, int stride, void* frag, hipStream_t st) {
     int s1, nt;
     if (!act_frag_shape(stride, p->n_actions, s1, nt) || p->hidden != 16) return hipErrorInvalidValue;
@@ -1334,6 +1343,7 @@ hipError_t launch_act_prepare(const ms_mlp_params* p, const int8_t* common, int 
         default: return launch_act_prep_s<8>(p, common, stride, f, nt, st);
     }
 }
+#endif
 
 // The price chooser's sampling table (ms_price_table_build): the forward of every tabulated 4-byte
 // input per group (16 keys per tile, one per column), stored as Head::run would use it.
@@ -1371,6 +1381,7 @@ __global__ void __launch_bounds__(256) k_price_table(ms_mlp_params pn, const int
     }
 }
 
+#ifndef MS_ACT_PAIR_TU  // (the paired act kernel's translation unit defines only launch_act_round)
 hipError_t launch_price_table(const ms_mlp_params* pn, const int8_t* rows, int K, float* tab, hipStream_t st) {
     if (pn->in_dim != 4 || pn->hidden != 16 || K < 1) return hipErrorInvalidValue;
     const int nt = (pn->n_actions + 15) / 16;
@@ -1384,10 +1395,12 @@ hipError_t launch_price_table(const ms_mlp_params* pn, const int8_t* rows, int K
         return hipErrorInvalidValue;
     return hipGetLastError();
 }
+#endif
 
 // both halves of a free-price round's acting in one launch when their shapes have a paired kernel
 // (cfg3: offer rows of <= 32 bytes, <= 16 actions; acceptor rows of <= 64 bytes, <= 32 actions),
 // else the two launches in order
+#if !defined(MS_SPLIT_PAIR) || defined(MS_ACT_PAIR_TU)  // act_pair_kernels.hip (build.sh)
 hipError_t launch_act_round(const ms_mlp_params* core, const ms_mlp_params* price, const int8_t* off_obs,
                             int off_stride, int off_U, int off_S, const ms_mlp_params* acc,
                             const int8_t* core_rows, const int8_t* core_owner, int acc_stride, int acc_U, int acc_S,
@@ -1420,5 +1433,6 @@ hipError_t launch_act_round(const ms_mlp_params* core, const ms_mlp_params* pric
     hipLaunchKernelGGL((k_act_pair<1, 1, 1, 2, 2>), dim3(ob + cb), dim3(256), 0, st, o, c, (int)ob);
     return hipGetLastError();
 }
+#endif
 
 }  // namespace ms
