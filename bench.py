@@ -201,10 +201,12 @@ SAMPLE_EVERY = 8      # rounds between timed env launches
 def committed_traffic(alg_bytes_per_launch, variant=""):
     """HBM bytes per k_env_step launch from the committed PMC passes of this workload
     (profiles/*/traffic.json, written by profiles/run_profile.sh: FETCH_SIZE doubled per the
-    gfx950 correction + WRITE_SIZE, per launch), newest round first; None if absent."""
+    gfx950 correction + WRITE_SIZE, per launch): the most recent measurement by its ``measured_at``
+    stamp (UTC, written by traffic_from_pmc.py; not by directory name, whose order is not the
+    order of the rounds); None if absent."""
     import glob
-    paths = sorted(glob.glob(os.path.join(REPO, "profiles", "*", "traffic.json")), reverse=True)  # newest round first
-    for p in paths:
+    best = None
+    for p in glob.glob(os.path.join(REPO, "profiles", "*", "traffic.json")):
         try:
             with open(p) as f:
                 d = json.load(f)
@@ -213,9 +215,11 @@ def committed_traffic(alg_bytes_per_launch, variant=""):
         # the passes of this workload's kernel variant (same algorithmic bytes per launch)
         if (d.get("kernel") == "k_env_step" and d.get("bytes") and d.get("algorithmic_bytes") == alg_bytes_per_launch
                 and d.get("variant", "") == variant):
-            return {"bytes": d["bytes"], "source": os.path.relpath(p, REPO),
-                    "vs_algorithmic": d["bytes"] / alg_bytes_per_launch}
-    return None
+            key = (d.get("measured_at", ""), p)
+            if best is None or key > best[0]:
+                best = (key, {"bytes": d["bytes"], "source": os.path.relpath(p, REPO),
+                              "measured_at": d.get("measured_at"), "vs_algorithmic": d["bytes"] / alg_bytes_per_launch})
+    return best[1] if best else None
 
 
 OTHER = {  # BASELINE configs[1], [3], [4]: per-GPU replicas of the 1-GPU / 8-GPU sharded workloads
@@ -396,7 +400,8 @@ def env_roofline(b_round: int, envs: int, launch_us, compact: bool, variant_traf
     traffic = committed_traffic(b_round * envs, "compact" if compact else "") if variant_traffic else None
     return {"kernel": "ms::k_env_step", "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS, "traffic": traffic["bytes"] if traffic else None,
-            "traffic_source": traffic["source"] if traffic else None, "bytes_per_env_round": b_round,
+            "traffic_source": traffic["source"] if traffic else None, "variant": "compact" if compact else "",
+            "bytes_per_env_round": b_round,
             "envs_per_launch": envs, "avg_launch_us": avg_s * 1e6, "launches_timed": len(launch_us)}
 
 

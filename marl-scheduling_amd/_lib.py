@@ -135,20 +135,57 @@ def ptr(t) -> ct.c_void_p | None:
     return ct.c_void_p(t.data_ptr())
 
 
+_capture_depth = 0          # hip_capture bodies currently open in this process
+_pending_destroy: list = []  # (fn, handle) released while a capture was open, run after it closes
+
+
+def capturing() -> bool:
+    """True inside a hip_capture body or any stream capture on the current stream."""
+    if _capture_depth > 0:
+        return True
+    try:
+        return bool(torch.cuda.is_available() and torch.cuda.is_current_stream_capturing())
+    except RuntimeError:
+        return False
+
+
+def release(fn, handle) -> None:
+    """fn(handle) now, or after the open capture ends: a hipFree inside a global-mode stream capture is an
+    operation the capture does not permit and invalidates the graph being recorded (the last reference to
+    a BatchedEnv can drop inside a captured body, and its finalizer frees the env's device state)."""
+    if capturing():
+        _pending_destroy.append((fn, handle))
+    else:
+        fn(handle)
+
+
+def drain_released() -> None:
+    """Run the releases deferred by captures that have closed."""
+    if _capture_depth > 0:
+        return
+    while _pending_destroy:
+        fn, handle = _pending_destroy.pop()
+        fn(handle)
+
+
 @contextlib.contextmanager
 def hip_capture(graph, **kw):
-    """torch.cuda.graph(graph, **kw) with Python's cyclic garbage collector held off: a finalizer that a
-    collection runs inside the capture (BatchedEnv.close -> ms_env_destroy -> hipFree of an env left in a
-    reference cycle) is an operation a global-mode capture does not permit, and it invalidates the graph."""
+    """torch.cuda.graph(graph, **kw) with device frees held off until the capture ends: Python's cyclic
+    garbage collector is disabled (a collection would run finalizers inside the capture) and a finalizer
+    that still runs there (a refcount drop to zero) queues its free through release()."""
+    global _capture_depth
     gc.collect()
     was = gc.isenabled()
     gc.disable()
+    _capture_depth += 1
     try:
         with torch.cuda.graph(graph, **kw):
             yield
     finally:
+        _capture_depth -= 1
         if was:
             gc.enable()
+        drain_released()
 
 
 def stream_ptr(stream=None):

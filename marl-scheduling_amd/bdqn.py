@@ -328,13 +328,22 @@ class BDQNTrainer:
     def timings(self):
         """Device time (s) of the frames' acting, env step + storing, and learning, accumulated from
         HIP events (read lazily)."""
-        for ev in self._pending_events:
+        self._fold_events(block=True)
+        return self._timings
+
+    def _fold_events(self, block: bool, keep: int = 0):
+        """Add the pending frames' event spans to the timings, oldest first: all of them (block), or
+        those already complete plus any beyond the newest ``keep`` (each step folds with keep = 32,
+        so a long run holds a bounded number of HIP events)."""
+        while self._pending_events:
+            ev = self._pending_events[0]
+            if not block and len(self._pending_events) <= keep and not ev[-1].query():
+                break
             ev[-1].synchronize()
             self._timings["act"] += ev[0].elapsed_time(ev[1]) / 1e3
             self._timings["env"] += ev[1].elapsed_time(ev[2]) / 1e3
             self._timings["learn"] += ev[2].elapsed_time(ev[3]) / 1e3
-        self._pending_events = []
-        return self._timings
+            self._pending_events.pop(0)
 
     @timings.setter
     def timings(self, value):
@@ -373,6 +382,7 @@ class BDQNTrainer:
             self._learn()
         ev[3].record()
         self._pending_events.append(ev)
+        self._fold_events(block=False, keep=32)
         return done
 
     def _sample(self):

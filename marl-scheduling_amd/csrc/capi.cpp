@@ -1131,11 +1131,20 @@ static WidePlan wide_plan(const ms_mlp_params* a, int64_t rows) {
     return w;
 }
 
+// The gradient workspace grows with the action count (per-block logit tiles zbuf [G][NB][16][A]);
+// nets whose workspace would pass this bound are refused instead of asking for terabytes.
+constexpr size_t kWideWorkspaceCap = size_t(64) << 30;
+
 size_t ms_wide_workspace_bytes(const ms_mlp_params* a, int64_t rows) {
     if (!a || rows < 1 || a->n_groups < 1 || a->n_actions < 1 || a->in_dim < 1 ||
         (a->hidden != 32 && a->hidden != 64))
         return 0;
-    return wide_plan(a, rows).bytes;
+    const size_t b = wide_plan(a, rows).bytes;
+    if (b > kWideWorkspaceCap) {
+        fail(MS_EINVAL, "ms_wide_workspace_bytes: %zu bytes for %d actions exceeds the 64 GiB bound", b, a->n_actions);
+        return 0;
+    }
+    return b;
 }
 
 int ms_wide_grad(const ms_mlp_params* a, const ms_mlp_params* c, const ms_wide_batch* b, float eps_clip, void* ws,
@@ -1154,6 +1163,9 @@ int ms_wide_grad(const ms_mlp_params* a, const ms_mlp_params* c, const ms_wide_b
         if (!d) return fail(MS_EINVAL, "ms_wide_grad: NULL gradient tensor");
     if (!g->loss) return fail(MS_EINVAL, "ms_wide_grad: NULL loss buffer");
     const WidePlan w = wide_plan(a, b->rows);
+    if (w.bytes > kWideWorkspaceCap)
+        return fail(MS_EINVAL, "ms_wide_grad: workspace of %zu bytes for %d actions exceeds the 64 GiB bound", w.bytes,
+                    a->n_actions);
     if (ws_bytes < w.bytes) return fail(MS_EINVAL, "ms_wide_grad: workspace too small (%zu < %zu)", ws_bytes, w.bytes);
     char* base = (char*)ws;
     ms::WideRows r{};

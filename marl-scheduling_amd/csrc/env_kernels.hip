@@ -142,7 +142,7 @@ __device__ void mt_refill_groups(uint32_t* mt, int64_t e0, uint64_t need, uint32
 }
 
 template <int LPE>
-__device__ void mt_refill_next(uint32_t* mt, const uint8_t* recs, const Params& P, int64_t slot, bool active,
+__device__ void mt_refill_next(uint32_t* mt, const uint8_t* recs, const Geom& P, int64_t slot, bool active,
                                uint8_t* lds, int lane) {
     const int gl = lane & (LPE - 1);
     const int64_t e0 = slot * (kWave / LPE);
@@ -277,7 +277,7 @@ struct MtStream {
 
 struct Rec {
     uint8_t* b;
-    const Params* P;
+    const Geom* P;  // record offsets
     const int32_t* kt;  // kind tables in LDS: prio[16], len[16], fix[16] (per-lane lookups must not
                         // index the kernel-argument struct: that is a memory load per access)
     __device__ int prio(int k) const { return kt[k]; }
@@ -460,7 +460,7 @@ __device__ __forceinline__ void m_add(double* p, double v) {
 // recipient r (0 = auctioneer). Ends with a phase boundary.
 // With last1 != NULL also last1[c] = 1 when an offer to core c holds a job with one round left.
 template <int LPE>
-__device__ void build_masks(Rec& R, const Params& P, M128* mc, M128* mr, int gl, uint8_t* last1 = nullptr) {
+__device__ void build_masks(Rec& R, const Geom& P, M128* mc, M128* mr, int gl, uint8_t* last1 = nullptr) {
     for (int i = gl; i < P.C; i += LPE) {
         mc[i] = M128{0, 0};
         if (last1) last1[i] = 0;
@@ -518,7 +518,7 @@ __device__ __forceinline__ uint32_t foreign_dword(int k, int d_acc) {
 //   otmpl [off_stride]: offer-row template (the (prio, rem) pairs of all cores, zero tail);
 //   slot_pair [NL]: (prio, rem) of every slot.
 template <int LPE>
-__device__ void build_obs_sources(Rec& R, const Params& P, const M128* mc, const M128* mr, uint8_t* scratch, bool acc,
+__device__ void build_obs_sources(Rec& R, const Geom& P, const M128* mc, const M128* mr, uint8_t* scratch, bool acc,
                                   bool auct, bool off, int gl) {
     const int C = P.C, nw = P.acc_stride / 4;
     uint32_t* crow = reinterpret_cast<uint32_t*>(scratch);
@@ -672,7 +672,7 @@ __device__ __forceinline__ void emit_rows(uint32_t* base, int64_t e, int64_t E, 
 
 // All observations of env e (dst == NULL skips a kind; a padding group passes write = false).
 template <int LPE>
-__device__ void emit_obs(Rec& R, const Params& P, const M128* mc, const M128* mr, uint8_t* scratch, int8_t* acc,
+__device__ void emit_obs(Rec& R, const Geom& P, const M128* mc, const M128* mr, uint8_t* scratch, int8_t* acc,
                          int8_t* off, int8_t* auct, int8_t* crows, int8_t* cown, int64_t e, int64_t E, bool write,
                          int gl) {
     build_obs_sources<LPE>(R, P, mc, mr, scratch, acc != nullptr, auct != nullptr || crows != nullptr, off != nullptr,
@@ -716,7 +716,7 @@ __device__ void emit_obs(Rec& R, const Params& P, const M128* mc, const M128* mr
 // one _randbelow(count) per tied core in core order on the env stream. Writes s_auct[c] (O = reject).
 // Needs LPE >= C (group lane c owns core c).
 template <int LPE>
-__device__ void hardcoded_auctioneer(Rec& R, const Params& P, const M128* s_mc, const M128* s_mr, MtStream<LPE>& rs,
+__device__ void hardcoded_auctioneer(Rec& R, const Geom& P, const M128* s_mc, const M128* s_mr, MtStream<LPE>& rs,
                                      int16_t* s_auct, const Lanes<LPE>& L) {
     const int C = P.C, O = P.O, gl = L.gl;
     const int8_t* c_owner = R.core_owner();
@@ -774,7 +774,7 @@ __device__ void hardcoded_auctioneer(Rec& R, const Params& P, const M128* s_mc, 
 // env stream before the auctioneer draws. The offer rows of all slots hold the same core pairs, so
 // one candidate mask serves every offerer. Writes the staged action arrays (LDS). Needs LPE >= C.
 template <int LPE>
-__device__ void hardcoded_agents(Rec& R, const Params& P, const M128* s_mc, const M128* s_mr, MtStream<LPE>& rs,
+__device__ void hardcoded_agents(Rec& R, const Geom& P, const M128* s_mc, const M128* s_mr, MtStream<LPE>& rs,
                                  int8_t* a_acc, int8_t* a_off, const Lanes<LPE>& L) {
     const int C = P.C, N = P.N, NL = P.NL, O = P.O, gl = L.gl;
     const int8_t* c_owner = R.core_owner();
@@ -955,6 +955,18 @@ __global__ void __launch_bounds__(64) k_env_reset(Params P, const uint8_t* recs,
                     true, lane);
 }
 
+// Shape tags of env_round: DynShape reads the geometry from the kernel arguments; FixShape<N, C,
+// L, J> compiles it in (the BASELINE shapes, launch_env_step picks them when the config matches).
+struct DynShape {
+    static constexpr bool kStatic = false;
+    static constexpr int kN = 0, kC = 0, kL = 0, kJ = 0;
+};
+template <int N_, int C_, int L_, int J_>
+struct FixShape {
+    static constexpr bool kStatic = true;
+    static constexpr int kN = N_, kC = C_, kL = L_, kJ = J_;
+};
+
 constexpr int kLiabPrefetch = 4;  // newest chain entries loaded ahead per core that may terminate
 
 // One round of SchedulingEnv.step (SchedulingEnvironment.py:32-83): group g of block b steps env
@@ -964,55 +976,64 @@ constexpr int kLiabPrefetch = 4;  // newest chain entries loaded ahead per core 
 // none of their registers (the compact emission beside the full rows costs ~90 spilled SGPRs). CMP:
 // the plain round that emits the compact acceptor observations instead of the [N][C] rows (the
 // training loop's form: its act and gradient kernels read core rows + owners).
-template <int LPE, bool EXT, bool CMP>
+template <int LPE, bool EXT, bool CMP, class SH>
 __device__ __forceinline__ void env_round(const Params& P, int64_t E, uint8_t* recs, uint32_t* mt, Liab* liab,
                                           const StepIO& io, int64_t slot) {
     extern __shared__ __align__(16) uint8_t smem_all[];
+    // the shape: a compile-time constant for the BASELINE shapes (offsets fold into immediates,
+    // loops over agents / cores / slots get constant trip counts), else the kernel arguments
+    Geom g;
+    if constexpr (SH::kStatic) {
+        constexpr Geom kg = make_geom(SH::kN, SH::kC, SH::kL, SH::kJ);
+        g = kg;
+    } else {
+        g = P;
+    }
     const int lane = threadIdx.x;
     const Lanes<LPE> Lg(lane);
     const int gl = Lg.gl;
     const int64_t e_raw = slot * (kWave / LPE) + (lane / LPE);
     const bool active = e_raw < E;  // padding groups of the last wave replay env E-1 without writing
     const int64_t e = active ? e_raw : E - 1;
-    uint8_t* smem = smem_all + (lane / LPE) * P.s_total;
-    M128* s_mc = reinterpret_cast<M128*>(smem + P.s_mc);          // offers per core
-    M128* s_mr = reinterpret_cast<M128*>(smem + P.s_mr);          // offers per recipient (0 = auctioneer)
-    Liab* s_newle = reinterpret_cast<Liab*>(smem + P.s_newle);    // liability entry appended this round per core
-    int16_t* s_exec = reinterpret_cast<int16_t*>(smem + P.s_exec);  // per core: executed offer's slot, -1 none
-    int16_t* s_key = reinterpret_cast<int16_t*>(smem + P.s_key);    // execution order key
-    int8_t* s_by_rank = reinterpret_cast<int8_t*>(smem + P.s_rank); // cores in execution order
-    int8_t* s_fresh = reinterpret_cast<int8_t*>(smem + P.s_fresh);  // s_newle[c] is the chain's newest entry
-    int16_t* s_auct = reinterpret_cast<int16_t*>(smem + P.s_auct);  // auctioneer action per core
-    int32_t* s_agent_r = reinterpret_cast<int32_t*>(smem + P.s_agentr);  // agentReward
-    int32_t* s_auct_r = reinterpret_cast<int32_t*>(smem + P.s_auctr);    // auctioneerReward
-    int32_t* s_credit = reinterpret_cast<int32_t*>(smem + P.s_credit);   // chain credits per recipient
-    uint32_t& s_flags = *reinterpret_cast<uint32_t*>(smem + P.s_misc);
-    int& s_n_exec = *reinterpret_cast<int*>(smem + P.s_misc + 4);
+    uint8_t* smem = smem_all + (lane / LPE) * g.s_total;
+    M128* s_mc = reinterpret_cast<M128*>(smem + g.s_mc);          // offers per core
+    M128* s_mr = reinterpret_cast<M128*>(smem + g.s_mr);          // offers per recipient (0 = auctioneer)
+    Liab* s_newle = reinterpret_cast<Liab*>(smem + g.s_newle);    // liability entry appended this round per core
+    int16_t* s_exec = reinterpret_cast<int16_t*>(smem + g.s_exec);  // per core: executed offer's slot, -1 none
+    int16_t* s_key = reinterpret_cast<int16_t*>(smem + g.s_key);    // execution order key
+    int8_t* s_by_rank = reinterpret_cast<int8_t*>(smem + g.s_rank); // cores in execution order
+    int8_t* s_fresh = reinterpret_cast<int8_t*>(smem + g.s_fresh);  // s_newle[c] is the chain's newest entry
+    int16_t* s_auct = reinterpret_cast<int16_t*>(smem + g.s_auct);  // auctioneer action per core
+    int32_t* s_agent_r = reinterpret_cast<int32_t*>(smem + g.s_agentr);  // agentReward
+    int32_t* s_auct_r = reinterpret_cast<int32_t*>(smem + g.s_auctr);    // auctioneerReward
+    int32_t* s_credit = reinterpret_cast<int32_t*>(smem + g.s_credit);   // chain credits per recipient
+    uint32_t& s_flags = *reinterpret_cast<uint32_t*>(smem + g.s_misc);
+    int& s_n_exec = *reinterpret_cast<int*>(smem + g.s_misc + 4);
 
-    const int N = P.N, C = P.C, L = P.L, NL = P.NL, O = P.O;
+    const int N = g.N, C = g.C, L = g.L, NL = g.NL, O = g.O;
 #ifdef MS_PHASE_TIMING
     uint64_t t_prev = __builtin_amdgcn_s_memtime();
     uint64_t t_acc[16] = {};
 #endif
 
-    uint8_t* rec = smem + P.s_rec;
-    int8_t* a_acc = reinterpret_cast<int8_t*>(smem + P.s_act_acc);
-    int8_t* a_off = reinterpret_cast<int8_t*>(smem + P.s_act_off);
-    int8_t* a_price = reinterpret_cast<int8_t*>(smem + P.s_act_price);
-    int8_t* a_auct = reinterpret_cast<int8_t*>(smem + P.s_act_auct);
-    int32_t* acc_r = reinterpret_cast<int32_t*>(smem + P.s_accr);
-    float* off_r = reinterpret_cast<float*>(smem + P.s_offr);
-    float* price_r = reinterpret_cast<float*>(smem + P.s_pricer);
-    int8_t* spawn_kind = reinterpret_cast<int8_t*>(smem + P.s_spawn_kind);
-    uint8_t* scratch = smem + P.s_scratch;
+    uint8_t* rec = smem + g.s_rec;
+    int8_t* a_acc = reinterpret_cast<int8_t*>(smem + g.s_act_acc);
+    int8_t* a_off = reinterpret_cast<int8_t*>(smem + g.s_act_off);
+    int8_t* a_price = reinterpret_cast<int8_t*>(smem + g.s_act_price);
+    int8_t* a_auct = reinterpret_cast<int8_t*>(smem + g.s_act_auct);
+    int32_t* acc_r = reinterpret_cast<int32_t*>(smem + g.s_accr);
+    float* off_r = reinterpret_cast<float*>(smem + g.s_offr);
+    float* price_r = reinterpret_cast<float*>(smem + g.s_pricer);
+    int8_t* spawn_kind = reinterpret_cast<int8_t*>(smem + g.s_spawn_kind);
+    uint8_t* scratch = smem + g.s_scratch;
 
     // ---- stage state and actions in LDS; the successor MT blocks of the envs that crossed into
     //      theirs last round are made while the staged words wait in registers (whole wave in LDS)
     __shared__ int32_t s_kt[48];
     {
         // the record and the dword-aligned action arrays: one batch of loads, then the LDS stores
-        const uint32_t* src_rec = reinterpret_cast<const uint32_t*>(recs + e * (int64_t)P.rec_bytes);
-        const int rec_dw = P.rec_bytes / 4;
+        const uint32_t* src_rec = reinterpret_cast<const uint32_t*>(recs + e * (int64_t)g.rec_bytes);
+        const int rec_dw = g.rec_bytes / 4;
         const int8_t* a_src[4] = {io.act_acc ? io.act_acc + e * N * C : nullptr, io.act_off ? io.act_off + e * NL : nullptr,
                                   io.act_price ? io.act_price + e * NL : nullptr,
                                   io.act_auct ? io.act_auct + e * C : nullptr};
@@ -1068,7 +1089,7 @@ __device__ __forceinline__ void env_round(const Params& P, int64_t E, uint8_t* r
     }
     wave_sync();
     MS_MARK(1);
-    Rec R{rec, &P, s_kt};
+    Rec R{rec, &g, s_kt};
     const int round = R.round();
     int8_t* c_owner = R.core_owner();
     int8_t* c_kind = R.core_kind();
@@ -1098,7 +1119,7 @@ __device__ __forceinline__ void env_round(const Params& P, int64_t E, uint8_t* r
     rs.init(mt + e * 2 * kMtN, R.mt_sel(), R.mti(), active);
     rs.load(0, 0, Lg);
     // the scratch is free until the executions: per core, "an offer to it has one round left"
-    build_masks<LPE>(R, P, s_mc, s_mr, gl, scratch);
+    build_masks<LPE>(R, g, s_mc, s_mr, gl, scratch);
     Liab pf[kLiabPrefetch];
     int pf_n = 0;
     if (gl < C) {
@@ -1117,11 +1138,11 @@ __device__ __forceinline__ void env_round(const Params& P, int64_t E, uint8_t* r
     // ---- auctioneer actions: HardcodedAuctioneerAcceptor (HardcodedModules.py:54-78), asked by the
     //      driver before env.step (trainPPO.py:162); ties broken with random.sample -> _randbelow
     if (HC) {  // HardcodedFixPriceEnvironment: the agents' actions come from the kernel
-        hardcoded_agents<LPE>(R, P, s_mc, s_mr, rs, a_acc, a_off, Lg);
+        hardcoded_agents<LPE>(R, g, s_mc, s_mr, rs, a_acc, a_off, Lg);
         wave_sync();
     }
     if (!io.act_auct) {
-        hardcoded_auctioneer<LPE>(R, P, s_mc, s_mr, rs, s_auct, Lg);
+        hardcoded_auctioneer<LPE>(R, g, s_mc, s_mr, rs, s_auct, Lg);
     } else {
         for (int c = gl; c < C; c += LPE) s_auct[c] = a_auct[c];
     }
@@ -1530,8 +1551,8 @@ __device__ __forceinline__ void env_round(const Params& P, int64_t E, uint8_t* r
 
     // ---- outputs: state record, rewards, observations of the new offer set
     if (active) {
-        copy_out<LPE>(WtOut(recs, E * P.rec_bytes), e * P.rec_bytes, reinterpret_cast<uint32_t*>(recs + e * (int64_t)P.rec_bytes),
-                      reinterpret_cast<const uint32_t*>(rec), P.rec_bytes / 4, gl);
+        copy_out<LPE>(WtOut(recs, E * g.rec_bytes), e * g.rec_bytes, reinterpret_cast<uint32_t*>(recs + e * (int64_t)g.rec_bytes),
+                      reinterpret_cast<const uint32_t*>(rec), g.rec_bytes / 4, gl);
         // rewards: write-through (consumed by the update, rounds later)
         auto rew = [&](void* base, int per_env, const void* src) {
             if (!base) return;
@@ -1579,9 +1600,9 @@ __device__ __forceinline__ void env_round(const Params& P, int64_t E, uint8_t* r
         }
     }
     MS_MARK(10);
-    build_masks<LPE>(R, P, s_mc, s_mr, gl);
+    build_masks<LPE>(R, g, s_mc, s_mr, gl);
     MS_MARK(11);
-    emit_obs<LPE>(R, P, s_mc, s_mr, scratch, CMP ? nullptr : io.obs_acc, io.obs_off, io.obs_auct,
+    emit_obs<LPE>(R, g, s_mc, s_mr, scratch, CMP ? nullptr : io.obs_acc, io.obs_off, io.obs_auct,
                   (EXT || CMP) ? io.obs_crow : nullptr, (EXT || CMP) ? io.obs_cown : nullptr, e, E, active, gl);
     MS_MARK(12);
 #ifdef MS_PHASE_TIMING
@@ -1593,7 +1614,7 @@ __device__ __forceinline__ void env_round(const Params& P, int64_t E, uint8_t* r
 // One round for the 64 / LPE envs of wave slot blockIdx.x. (A persistent loop over several slots
 // per wave would let one slot's observation stores drain under the next slot's compute, but the
 // compiler then keeps the whole round's state live across iterations: 3x the VGPRs.)
-template <int LPE, bool EXT, bool CMP>
+template <int LPE, bool EXT, bool CMP, class SH>
 __global__ void __launch_bounds__(64, 4) k_env_step(Params P, int64_t E, uint8_t* recs, uint32_t* mt, Liab* liab,
                                                  StepIO io) {
 #ifdef MS_PHASE_TIMING
@@ -1602,7 +1623,7 @@ __global__ void __launch_bounds__(64, 4) k_env_step(Params P, int64_t E, uint8_t
     // per-wave start / end for the bench's launch span (optional; plain stores, no shared address,
     // nothing held across the round: the kernel sits at 4 waves per SIMD with no register to spare)
     if (io.span && threadIdx.x == 0) io.span[2 * blockIdx.x] = __builtin_amdgcn_s_memrealtime();
-    env_round<LPE, EXT, CMP>(P, E, recs, mt, liab, io, blockIdx.x);
+    env_round<LPE, EXT, CMP, SH>(P, E, recs, mt, liab, io, blockIdx.x);
     if (io.span && threadIdx.x == 0) io.span[2 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime();
 #ifdef MS_PHASE_TIMING
     if (threadIdx.x == 0) {
@@ -1727,17 +1748,43 @@ static int lanes_per_env(const Params& P) {
     return lpe;
 }
 
-template <int LPE>
-static hipError_t launch_step_t(const Params& P, int64_t E, uint8_t* recs, uint32_t* mt, Liab* liab, const StepIO& io,
-                                hipStream_t s) {
+template <int LPE, class SH>
+static hipError_t launch_step_sh(const Params& P, int64_t E, uint8_t* recs, uint32_t* mt, Liab* liab, const StepIO& io,
+                                 hipStream_t s) {
     constexpr int G = kWave / LPE;
     const int64_t blocks = (E + G - 1) / G;
     const size_t lds = (size_t)P.s_total * G > 4 * kMtN ? (size_t)P.s_total * G : 4 * kMtN;  // >= one MT block
     const bool compact = io.obs_crow != nullptr || io.obs_cown != nullptr;
     const bool ext = io.act_acc == nullptr || io.metrics != nullptr || (compact && io.obs_acc != nullptr);
-    auto kern = ext ? k_env_step<LPE, true, false> : (compact ? k_env_step<LPE, false, true> : k_env_step<LPE, false, false>);
+    auto kern = ext ? k_env_step<LPE, true, false, DynShape>
+                    : (compact ? k_env_step<LPE, false, true, SH> : k_env_step<LPE, false, false, SH>);
     hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(kWave), lds, s, P, E, recs, mt, liab, io);
     return hipGetLastError();
+}
+
+template <int N, int C, int L, int J>
+static bool is_shape(const Params& P) {
+    return P.N == N && P.C == C && P.L == L && P.new_jobs == J;
+}
+
+// The BASELINE shapes (cfg2 4x4x3, cfg3 8x8x3, cfg4 16x16x3, cfg5 32x32x3, one new job per agent and
+// round) run the kernel compiled for their geometry; every other shape the generic one.
+template <int LPE>
+static hipError_t launch_step_t(const Params& P, int64_t E, uint8_t* recs, uint32_t* mt, Liab* liab, const StepIO& io,
+                                hipStream_t s) {
+#ifndef MS_NO_FIXED_SHAPES
+    if constexpr (LPE == 16) {
+        if (is_shape<8, 8, 3, 1>(P)) return launch_step_sh<LPE, FixShape<8, 8, 3, 1>>(P, E, recs, mt, liab, io, s);
+        if (is_shape<4, 4, 3, 1>(P)) return launch_step_sh<LPE, FixShape<4, 4, 3, 1>>(P, E, recs, mt, liab, io, s);
+    }
+    if constexpr (LPE == 32) {
+        if (is_shape<16, 16, 3, 1>(P)) return launch_step_sh<LPE, FixShape<16, 16, 3, 1>>(P, E, recs, mt, liab, io, s);
+    }
+    if constexpr (LPE == 64) {
+        if (is_shape<32, 32, 3, 1>(P)) return launch_step_sh<LPE, FixShape<32, 32, 3, 1>>(P, E, recs, mt, liab, io, s);
+    }
+#endif
+    return launch_step_sh<LPE, DynShape>(P, E, recs, mt, liab, io, s);
 }
 
 hipError_t launch_env_step(const Params& P, int64_t E, uint8_t* recs, uint32_t* mt, Liab* liab, const StepIO& io,

@@ -31,24 +31,26 @@ struct Liab {  // one liabilityList entry (world.py:285-289)
     int32_t round;
 };
 
-struct Params {
+inline constexpr int32_t align4(int32_t x) { return (x + 3) & ~3; }
+inline constexpr int32_t align16(int32_t x) { return (x + 15) & ~15; }
+// w / d == umulhi(w, magic_div(d)) for every w < 2^32 / d and d >= 2 (d == 1 is the emitters'
+// special case: the quotient is w).
+inline constexpr uint32_t magic_div(uint32_t d) { return d < 2 ? 0u : (uint32_t)(0x100000000ull / d + 1); }
+
+// The shape-derived part of the launch parameters: sizes, the record layout and the LDS plan. It
+// depends only on (N, C, L, newJobsPerRound), so the env kernels can take it either from the
+// kernel arguments or, for the BASELINE shapes, as a compile-time constant (make_geom in a
+// constexpr context): every offset then folds into the instructions' immediates and every loop
+// over agents / cores / slots has a constant trip count.
+struct Geom {
     // shapes
-    int32_t N, C, L, NL, O, K, cap;
+    int32_t N, C, L, NL, O;
     int32_t d_acc, acc_stride, d_off, off_stride;
     // record byte offsets
     int32_t o_core_owner, o_core_kind, o_core_rem, o_liab_n, o_core_birth;
     int32_t o_slot_kind, o_slot_rem, o_slot_wait, o_offer_core, o_offer_recip, o_offer_price,
         o_slot_birth;
     int32_t rec_bytes;
-    // config (world.py:211-246, Reward.py)
-    int32_t prio[MS_MAX_KINDS];
-    int32_t len[MS_MAX_KINDS];
-    double acc[MS_MAX_KINDS];
-    int32_t fix[MS_MAX_KINDS];
-    int32_t n_fix;
-    int32_t free_prices, commercial, new_jobs, mult;
-    int32_t ep_len;  // episodeLength (world.py:243): the metrics slot of a round
-    float net_zero;
     // LDS carve-up (byte offsets into dynamic shared memory), sized to the config so that
     // small envs keep many waves per CU in flight
     int32_t s_rec, s_act_acc, s_act_off, s_act_price, s_act_auct, s_accr, s_offr, s_pricer,
@@ -60,6 +62,81 @@ struct Params {
     int32_t scratch_bytes, s_rowsel, s_otmpl, s_slotpair;
     // w / nw == umulhi(w, mag) for the dword counts of one env's acceptor / offer rows
     uint32_t mag_acc, mag_off;
+};
+
+inline constexpr Geom make_geom(int32_t n_agents, int32_t n_cores, int32_t coll_len, int32_t new_jobs) {
+    Geom p{};
+    p.N = n_agents;
+    p.C = n_cores;
+    p.L = coll_len;
+    p.NL = p.N * p.L;
+    p.O = p.NL;
+    p.d_acc = 3 + 2 * p.O;
+    p.acc_stride = align4(p.d_acc);
+    p.d_off = 2 * p.C + 2;
+    p.off_stride = align4(p.d_off);
+    int32_t o = 16;
+    p.o_core_owner = o; o += align4(p.C);
+    p.o_core_kind = o; o += align4(p.C);
+    p.o_core_rem = o; o += align4(p.C);
+    p.o_liab_n = o; o += align4(p.C);
+    p.o_core_birth = o; o += 4 * p.C;
+    p.o_slot_kind = o; o += align4(p.NL);
+    p.o_slot_rem = o; o += align4(p.NL);
+    p.o_slot_wait = o; o += align4(p.NL);
+    p.o_offer_core = o; o += align4(p.NL);
+    p.o_offer_recip = o; o += align4(p.NL);
+    p.o_offer_price = o; o += align4(p.NL);
+    p.o_slot_birth = o; o += 4 * p.NL;
+    p.rec_bytes = align16(o);
+    // LDS plan
+    int32_t s = 0;
+    p.s_rec = s; s += p.rec_bytes;
+    p.s_act_acc = s; s += align4(p.N * p.C);
+    p.s_act_off = s; s += align4(p.NL);
+    p.s_act_price = s; s += align4(p.NL);
+    p.s_act_auct = s; s += align4(p.C);
+    p.s_accr = s; s += 4 * p.N * p.C;          // acceptorNetRewards int32
+    p.s_offr = s; s += 4 * p.NL;               // offer / coreChooser rewards f32
+    p.s_pricer = s; s += 4 * p.NL;             // priceChooser rewards f32
+    p.s_spawn_kind = s; s += align4(p.N * (new_jobs > 0 ? new_jobs : 1));
+    s = align16(s);
+    p.s_mc = s; s += 16 * p.C;                 // offer masks per core (M128)
+    p.s_mr = s; s += 16 * (p.N + 1);           // offer masks per recipient
+    p.s_newle = s; s += 8 * p.C;               // this round's liability entry per core
+    p.s_agentr = s; s += 4 * p.N;              // agentReward
+    p.s_credit = s; s += 4 * p.N;              // chain credits received (aggregated acceptor rewards)
+    p.s_auctr = s; s += 4 * p.C;               // auctioneerReward
+    p.s_exec = s; s += align4(2 * p.C);        // executed slot per core
+    p.s_key = s; s += align4(2 * p.C);         // execution order key
+    p.s_auct = s; s += align4(2 * p.C);        // auctioneer action per core
+    p.s_rank = s; s += align4(p.C);            // cores in execution order
+    p.s_fresh = s; s += align4(p.C);           // s_newle[c] is the chain's newest entry
+    p.s_misc = s; s += 16;                     // flags, n_exec
+    s = align16(s);
+    p.s_scratch = s;
+    p.s_rowsel = (p.C + 1) * p.acc_stride;
+    p.s_otmpl = align4(p.s_rowsel + 2 * p.N * p.C);
+    p.s_slotpair = p.s_otmpl + p.off_stride;
+    p.scratch_bytes = align16(p.s_slotpair + 2 * p.NL);
+    s += p.scratch_bytes;
+    p.s_total = s;
+    p.mag_acc = magic_div(p.acc_stride / 4);
+    p.mag_off = magic_div(p.off_stride / 4);
+    return p;
+}
+
+struct Params : Geom {
+    int32_t K, cap;
+    // config (world.py:211-246, Reward.py)
+    int32_t prio[MS_MAX_KINDS];
+    int32_t len[MS_MAX_KINDS];
+    double acc[MS_MAX_KINDS];
+    int32_t fix[MS_MAX_KINDS];
+    int32_t n_fix;
+    int32_t free_prices, commercial, new_jobs, mult;
+    int32_t ep_len;  // episodeLength (world.py:243): the metrics slot of a round
+    float net_zero;
 };
 
 // device pointers of one ms_env_step call
@@ -113,40 +190,12 @@ struct RegenArgs {
     int N, C, L, d_acc, acc_stride, acc_ld, off_ld;
 };
 
-inline int32_t align4(int32_t x) { return (x + 3) & ~3; }
-inline int32_t align16(int32_t x) { return (x + 15) & ~15; }
-// w / d == umulhi(w, magic_div(d)) for every w < 2^32 / d and d >= 2 (d == 1 is the emitters'
-// special case: the quotient is w).
-inline uint32_t magic_div(uint32_t d) { return d < 2 ? 0u : (uint32_t)(0x100000000ull / d + 1); }
-
 // Build the record layout and LDS plan for a validated config.
 inline Params make_params(const ms_config& c, int32_t cap) {
     Params p{};
-    p.N = c.n_agents;
-    p.C = c.n_cores;
-    p.L = c.collection_length;
-    p.NL = p.N * p.L;
-    p.O = p.NL;
+    static_cast<Geom&>(p) = make_geom(c.n_agents, c.n_cores, c.collection_length, c.new_jobs_per_round);
     p.K = c.n_kinds;
     p.cap = cap;
-    p.d_acc = 3 + 2 * p.O;
-    p.acc_stride = align4(p.d_acc);
-    p.d_off = 2 * p.C + 2;
-    p.off_stride = align4(p.d_off);
-    int32_t o = 16;
-    p.o_core_owner = o; o += align4(p.C);
-    p.o_core_kind = o; o += align4(p.C);
-    p.o_core_rem = o; o += align4(p.C);
-    p.o_liab_n = o; o += align4(p.C);
-    p.o_core_birth = o; o += 4 * p.C;
-    p.o_slot_kind = o; o += align4(p.NL);
-    p.o_slot_rem = o; o += align4(p.NL);
-    p.o_slot_wait = o; o += align4(p.NL);
-    p.o_offer_core = o; o += align4(p.NL);
-    p.o_offer_recip = o; o += align4(p.NL);
-    p.o_offer_price = o; o += align4(p.NL);
-    p.o_slot_birth = o; o += 4 * p.NL;
-    p.rec_bytes = align16(o);
     for (int i = 0; i < MS_MAX_KINDS; i++) {
         p.prio[i] = c.job_priority[i];
         p.len[i] = c.job_length[i];
@@ -160,42 +209,7 @@ inline Params make_params(const ms_config& c, int32_t cap) {
     p.mult = c.reward_multiplier;
     p.ep_len = c.episode_length > 0 ? c.episode_length : 1;
     p.net_zero = (float)c.net_zero_offer_reward;
-    // LDS plan
-    int32_t s = 0;
-    p.s_rec = s; s += p.rec_bytes;
-    p.s_act_acc = s; s += align4(p.N * p.C);
-    p.s_act_off = s; s += align4(p.NL);
-    p.s_act_price = s; s += align4(p.NL);
-    p.s_act_auct = s; s += align4(p.C);
-    p.s_accr = s; s += 4 * p.N * p.C;          // acceptorNetRewards int32
-    p.s_offr = s; s += 4 * p.NL;               // offer / coreChooser rewards f32
-    p.s_pricer = s; s += 4 * p.NL;             // priceChooser rewards f32
-    p.s_spawn_kind = s; s += align4(p.N * (p.new_jobs > 0 ? p.new_jobs : 1));
-    s = align16(s);
-    p.s_mc = s; s += 16 * p.C;                 // offer masks per core (M128)
-    p.s_mr = s; s += 16 * (p.N + 1);           // offer masks per recipient
-    p.s_newle = s; s += 8 * p.C;               // this round's liability entry per core
-    p.s_agentr = s; s += 4 * p.N;              // agentReward
-    p.s_credit = s; s += 4 * p.N;              // chain credits received (aggregated acceptor rewards)
-    p.s_auctr = s; s += 4 * p.C;               // auctioneerReward
-    p.s_exec = s; s += align4(2 * p.C);        // executed slot per core
-    p.s_key = s; s += align4(2 * p.C);         // execution order key
-    p.s_auct = s; s += align4(2 * p.C);        // auctioneer action per core
-    p.s_rank = s; s += align4(p.C);            // cores in execution order
-    p.s_fresh = s; s += align4(p.C);           // s_newle[c] is the chain's newest entry
-    p.s_misc = s; s += 16;                     // flags, n_exec
-    s = align16(s);
-    p.s_scratch = s;
-    p.s_rowsel = (p.C + 1) * p.acc_stride;
-    p.s_otmpl = align4(p.s_rowsel + 2 * p.N * p.C);
-    p.s_slotpair = p.s_otmpl + p.off_stride;
-    p.scratch_bytes = align16(p.s_slotpair + 2 * p.NL);
-    s += p.scratch_bytes;
-    p.s_total = s;
-    p.mag_acc = magic_div(p.acc_stride / 4);
-    p.mag_off = magic_div(p.off_stride / 4);
     return p;
 }
-
 
 }  // namespace ms

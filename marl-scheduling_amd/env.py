@@ -15,13 +15,14 @@ import numpy as np
 import torch
 
 from . import abi
-from ._lib import check, lib, ptr, stream_ptr
+from ._lib import check, drain_released, lib, ptr, release, stream_ptr
 
 
 class BatchedEnv:
     def __init__(self, cfg: abi.MsConfig, n_envs: int, seed: int = 0, device=None):
         if not torch.cuda.is_available():
             raise RuntimeError("BatchedEnv needs a HIP device (no CPU fallback)")
+        drain_released()  # frees deferred by a capture that was not a hip_capture
         self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
         self.cfg = cfg
         self.E = int(n_envs)
@@ -36,9 +37,10 @@ class BatchedEnv:
         self.free_prices = bool(cfg.free_prices)
 
     def close(self):
+        """ms_env_destroy (deferred to the end of an open HIP-graph capture, _lib.release)."""
         if getattr(self, "_h", None):
-            lib.ms_env_destroy(self._h)
-            self._h = None
+            h, self._h = self._h, None
+            release(lib.ms_env_destroy, h)
 
     def __del__(self):
         try:

@@ -20,6 +20,7 @@ exactly the reference.
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes as ct
 
 import torch
@@ -28,6 +29,8 @@ from torch.distributions import Categorical
 
 from . import abi
 from ._lib import check, lib, ptr, stream_ptr
+
+MS_EINVAL = 22  # include/marlsched.h
 
 HIDDEN = 16  # numberOfNeurons of every divided / shared net (PPOmodules.py:241,259,276,456,475,604,623)
 
@@ -383,6 +386,11 @@ class HipAdam:
                                    self.betas[1], self.eps, stream_ptr(stream)))
 
 
+def _on_stream(stream):
+    """torch.cuda.stream(stream), or no change for stream None (the current stream)."""
+    return torch.cuda.stream(stream) if stream is not None else contextlib.nullcontext()
+
+
 class PPOGroup:
     """Policy / policy_old pair + Adam for one unit type (PPOmodules.py:75-174). The torch-autograd
     ``update`` steps torch.optim.Adam; ``update_fused`` steps the HIP Adam (HipAdam)."""
@@ -461,16 +469,23 @@ class PPOGroup:
         a = pol.mlp_params()
         c = pol.critic_mlp_params()
         ws_bytes = lib.ms_wide_workspace_bytes(ct.byref(a), R)
-        ws = torch.empty(((ws_bytes + 3) // 4,), dtype=torch.float32, device=dev)
+        if ws_bytes == 0:
+            check(MS_EINVAL)  # raises with ms_last_error()
+        # the workspace is cached across updates (same rows / net shape: same plan)
+        ws = getattr(self, "_wide_ws", None)
+        if ws is None or ws.device != dev or ws.numel() * 4 < ws_bytes:
+            ws = self._wide_ws = torch.empty(((ws_bytes + 3) // 4,), dtype=torch.float32, device=dev)
         batch = abi.MsWideBatch(ptr(states_i8), ptr(actions_i32), ptr(old_logprobs), ptr(returns_gr), stride, R)
         grads = abi.MsPpoGrads(*[ptr(getattr(pol, k).grad) for k in ACTOR_KEYS + CRITIC_KEYS], ptr(loss_buf))
         keep = (states_i8, actions_i32, old_logprobs, returns_gr, ws, loss_buf)  # the structs' pointees
 
         def run():
             assert keep
-            check(lib.ms_wide_grad(ct.byref(a), ct.byref(c), ct.byref(batch), ct.c_float(self.eps_clip), ptr(ws),
-                                   ws_bytes, ct.byref(grads), stream_ptr(stream)))
-            return loss_buf[:, 0] + 0.5 * loss_buf[:, 1] - 0.01 * loss_buf[:, 2]
+            # the loss combination reads loss_buf after the kernel: both on the kernel's stream
+            with _on_stream(stream):
+                check(lib.ms_wide_grad(ct.byref(a), ct.byref(c), ct.byref(batch), ct.c_float(self.eps_clip), ptr(ws),
+                                       ws_bytes, ct.byref(grads), stream_ptr(stream)))
+                return loss_buf[:, 0] + 0.5 * loss_buf[:, 1] - 0.01 * loss_buf[:, 2]
 
         return run
 
@@ -479,14 +494,16 @@ class PPOGroup:
         of each group's mean loss from ms_wide_grad (HIP), all-reduced across ranks when set, then
         the HIP Adam. states_i8 [R, G, stride] int8 rows, actions [R, G] int32, old_logprobs [R, G]
         f32, returns [G, R] f32 normalised (discounted_returns). Returns the K per-group losses."""
-        epoch = self.wide_epoch(states_i8, actions_i32, old_logprobs, returns_gr, stream)
         losses = []
-        for _ in range(self.K):
-            loss = epoch()
-            if self.allreduce is not None:
-                self.allreduce(self.policy.parameters())
-            self.hip_optimizer.step(stream)
-            losses.append(loss)
+        # the gradient zero-init, the kernel, the all-reduce and Adam in one stream order
+        with _on_stream(stream):
+            epoch = self.wide_epoch(states_i8, actions_i32, old_logprobs, returns_gr, stream)
+            for _ in range(self.K):
+                loss = epoch()
+                if self.allreduce is not None:
+                    self.allreduce(self.policy.parameters())
+                self.hip_optimizer.step(stream)
+                losses.append(loss)
         self.last_losses = losses
         return losses
 

@@ -246,6 +246,7 @@ class Trainer:
         self.use_graph = use_graph
         self.graph = None
         self.rounds_done = 0
+        self._policy_version = 0  # bumped by update(); the acting tables record the version they saw
         self.iterations = 0
         for env, e0, e1 in self.env.parts:
             env.reset(dict(self._acc_out(0, e0, e1), offer=self.off_obs[0][e0:e1]))
@@ -301,9 +302,23 @@ class Trainer:
         return [u for u in (self.acc, self.off, self.price) if u is not None]
 
     # ---- rollout
+    def _prepare_acting(self):
+        """The acting kernels' per-rollout tables from policy_old: the price chooser's table of its
+        possible inputs and the act weight fragments (ms_act_prepare). They are rebuilt at the start
+        of every rollout (inside the rollout graph) and by round() after an update changed
+        policy_old (sync_old bumps _policy_version)."""
+        if self.price_table is not None:
+            self.price_table.build(self.price.group.policy_old)
+        if self.off_frag is not None:
+            self.off_frag.build(self.off.group.policy_old)
+            self.acc_frag.build(self.acc.group.policy_old)
+        self._acting_version = self._policy_version
+
     def round(self, t: int):
         """getActionForAllAgents + env.step + saveRewards for round t of the iteration
         (trainPPO.py:160-167), part by part: part k's launches go to stream k."""
+        if getattr(self, "_acting_version", -1) != self._policy_version:
+            self._prepare_acting()
         for k in range(len(self.env.parts)):
             self._round_part(t, k)
 
@@ -399,11 +414,7 @@ class Trainer:
         cur = torch.cuda.current_stream(self.device)
         if self.span_every:
             self.spans[:: self.span_every].zero_()
-        if self.price_table is not None:
-            self.price_table.build(self.price.group.policy_old)
-        if self.off_frag is not None:
-            self.off_frag.build(self.off.group.policy_old)
-            self.acc_frag.build(self.acc.group.policy_old)
+        self._prepare_acting()
         for s in self.streams[1:]:  # fork: the side streams start after everything queued so far
             s.wait_stream(cur)
         for t in range(self.T):
@@ -466,6 +477,7 @@ class Trainer:
         first. One rank: one graph. Several ranks: one graph per stretch between two gradient
         all-reduces, the RCCL calls eager in between (_capture_update). The returned losses are
         copies of the graph's own tensors."""
+        self._policy_version += 1  # policy_old changes: round() rebuilds the acting tables
         if self.use_graph and self.fused:
             return self._update_graphed()
         sel = self._draws()
@@ -528,6 +540,15 @@ class Trainer:
     def _capture_update(self, views):
         """Capture the fused update: segment i = the kernels between all-reduce i-1 and i (one
         segment on one rank), all in one memory pool. Returns the graph's loss tensors."""
+        if self.world_size == 1 and self.update_streams:
+            # MS_UPDATE_STREAMS on one rank: the per-unit-type streams are recorded into the graph
+            # (fork / join on the capture stream), so replays run the same concurrent form the
+            # eager first update ran
+            g = torch.cuda.CUDAGraph()
+            with hip_capture(g):
+                losses = self._fused_update_streams(views, self._sel_counts)
+            self.update_graph, self._graph_params = [g], []
+            return losses
         out, graphs, params = {}, [], []
         phases = self._fused_phases(views, self._sel_counts, out)
         pool = None

@@ -90,6 +90,46 @@ class PyWorld:
         self.dwell = []
         self.spawn_edge = 0
 
+    @classmethod
+    def from_state(cls, cfg: Config, st: dict, mt_words, mt_index):
+        """A world in a given state (the KAT fixture's form, tests/golden/make_kats.py): cores, slots,
+        the pending offer of each slot (IDs in slot order, made last round), the liability deques
+        newest first, the CPython random state. formerCorePrios/Lengths are the cores' jobs as the
+        previous step left them (SchedulingEnvironment.py:64-66), i.e. this state's."""
+        w = cls(cfg, 0)
+        N, C, L = w.N, w.C, w.L
+        rnd = int(st["round"])
+        w.round = rnd
+        for c in range(C):
+            k = int(st["core_kind"][c])
+            if k >= 0:
+                w.core_job[c] = Job(False, int(st["core_owner"][c]), cfg.priorities[k], int(st["core_rem"][c]),
+                                    cfg.lengths[k], int(st["core_birth"][c]), k)
+            w.core_owner[c] = int(st["core_owner"][c])
+        w.former_prio = [j.prio for j in w.core_job]
+        w.former_len = [j.rem for j in w.core_job]
+        for a in range(N):
+            for q in range(L):
+                k = int(st["slot_kind"][a][q])
+                if k >= 0:
+                    w.coll[a][q] = Job(False, a + 1, cfg.priorities[k], int(st["slot_rem"][a][q]), cfg.lengths[k],
+                                       int(st["slot_birth"][a][q]), k, bool(st["slot_wait"][a][q]))
+            w.free[a] = sum(1 for j in w.coll[a] if j.empty)
+        oid = 1
+        for a in range(N):
+            for q in range(L):
+                c = int(st["offer_core"][a][q])
+                if c >= 0:
+                    j = w.coll[a][q]
+                    w.offers.append(Offer(oid, a + 1, int(st["offer_recip"][a][q]), c + 1, q,
+                                          int(st["offer_price"][a][q]), j.rem, j.prio, j.kind, rnd - 1))
+                    oid += 1
+        for c, chain in enumerate(st["liab"]):
+            w.liab[c] = deque(Offer(0, int(e[0]), int(e[1]), c + 1, 0, int(e[2]), int(e[3]), 0, -1, int(e[4]))
+                              for e in chain)
+        w.rng.setstate((3, tuple(int(x) for x in mt_words) + (int(mt_index),), None))
+        return w
+
     # ---- collections (world.py:123-141)
     def _insert(self, a, job):
         if self.free[a] <= 0:

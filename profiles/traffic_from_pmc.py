@@ -8,6 +8,7 @@ streaming stores (the observation / record / reward stores of the kernel). The r
 average over the profiled launches; bench.py reads it as roofline.traffic.
 """
 import csv
+import datetime
 import json
 import sys
 
@@ -28,7 +29,9 @@ def main():
     d = {"kernel": "k_env_step", "bytes": total, "fetch_bytes_raw": fetch, "fetch_bytes_corrected": 2.0 * fetch,
          "write_bytes": write, "launches": [nf, nw], "algorithmic_bytes": alg, "vs_algorithmic": total / alg,
          "correction": "FETCH_SIZE x2 (gfx950 wide-read tally), WRITE_SIZE as reported; KiB -> bytes",
-         "variant": variant}
+         "variant": variant,
+         # bench.py's committed_traffic picks the newest measurement of a workload by this stamp
+         "measured_at": datetime.datetime.now(datetime.timezone.utc).isoformat(timespec="seconds")}
     with open(out, "w") as f:
         json.dump(d, f, indent=1)
     print(json.dumps(d))

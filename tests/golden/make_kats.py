@@ -532,14 +532,152 @@ def kat_liability_overflow():
         ])
 
 
+def kat_aggregated_chain_rewards():
+    """Reward.py:92-143 getAggregatedFixedPricesReward, written out by hand next to the divided
+    Reward.py:146-212 of the same round. Round 10, fixed prices. Core 1 (agent 1, prio 10, one round
+    left) ends this round, TS = 11; its chain newest first: e1 (1 -> agent 2, price 7, necT 3,
+    round 8), e2 (2 -> auctioneer, price 2, necT 6, round 4). Agent 3's pending offer (slot 0, kind 0,
+    rem 5, to core 2 held by the auctioneer, price fixPrices[0] = 2) is accepted by the auctioneer.
+      aggregated offer (:95-101): offerRewards[offerer] += prio1 -> agent 3: 3
+      termination (:121-122): acceptorRewards[1] += 10, agentReward[1] += 10
+      e1: T = 11-8 = 3, round(fl(7/3)*3) = round(7.000000000000001) = 7 (:130-131):
+          acceptorRewards[1] -= 7, agentReward[1] -= 7; recipient 2 > 0: agentReward[2] += 7 only
+          (:136-137: no acceptor credit, unlike the divided :203-205)
+      e2: T = 3 + (8-4) = 7, round(fl(2/6)*7) = round(2.333...) = 2: acceptorRewards[2] -= 2,
+          agentReward[2] -= 2; recipient 0: auctioneerReward[1] = 2
+    -> aggregated acceptor [3, -2, 0], offer [0, 0, 3], agent [3, 5, 0], auctioneer [2, 0].
+    The divided acceptor rewards of the same round credit the recipient: [[3, 0], [5, 0], [0, 0]].
+    Spawn: agent 1 (no core, one free slot) draws one job; agent 2 (full) and agent 3 (owns core 2,
+    one free slot: 1 + 1 > 1) do not."""
+    N, C, L = 3, 2, 2
+    st = empty_state(N, C, L, 10)
+    st.update(core_owner=[1, 0], core_kind=[1, -1], core_rem=[1, -1], core_birth=[7, -1])
+    st["slot_kind"] = [[0, -1], [1, 0], [0, 1]]
+    st["slot_rem"] = [[6, -1], [3, 6], [5, 3]]
+    st["slot_birth"] = [[9, -1], [6, 9], [9, 5]]
+    st["slot_wait"] = [[0, 0], [0, 0], [1, 0]]
+    st["offer_core"] = [[-1, -1], [-1, -1], [1, -1]]
+    st["offer_recip"] = [[0, 0], [0, 0], [0, 0]]
+    st["offer_price"] = [[0, 0], [0, 0], [2, 0]]
+    st["liab"] = [[[1, 2, 7, 3, 8], [2, 0, 2, 6, 4]], []]
+    assert round(7 / 3 * 3) == 7 and round(2 / 6 * 7) == 2
+    words, idx = mt_state(2718)
+    r = rng_at(words, idx)
+    u = r.random()
+    kind = 0 if u < 0.8 else 1
+    return dict(
+        name="aggregated_chain_rewards", cites=["Reward.py:92-143", "Reward.py:146-212", "world.py:378-389"],
+        config=dict(n_agents=N, n_cores=C, collection_length=L, **README_JOBS),
+        state=st, mt_words=words, mt_index=idx, note="spawn u = %r -> kind %d" % (u, kind),
+        steps=[
+            dict(acc=[[6, 6]] * 3, off=[[2, 2]] * 3, price=None, auct=[6, 0],
+                 expect=dict(state=dict(round=11, core_owner=[0, 3], core_kind=[-1, 0], core_rem=[-1, 4],
+                                        core_birth=[-1, 9],
+                                        slot_kind=[[0, kind], [1, 0], [-1, 1]],
+                                        slot_rem=[[6, [6, 3][kind]], [3, 6], [-1, 3]],
+                                        slot_birth=[[9, 10], [6, 9], [-1, 5]], slot_wait=[[0, 0]] * 3,
+                                        offer_core=[[-1, -1]] * 3, liab=[[], [[3, 0, 2, 5, 10]]]),
+                             rewards=dict(aggregated_offer=[0, 0, 3], aggregated_acceptor=[3, -2, 0],
+                                          agent=[3, 5, 0], auctioneer=[2, 0],
+                                          acceptor=[[3, 0], [5, 0], [0, 0]], offer=[[0, 0], [0, 0], [3, 0]]),
+                             termination_revenue=10, mt_index=r.getstate()[1][624])),
+        ])
+
+
+def kat_acception_quality():
+    """SchedulingEnvironment.py:174-192 calculateAverageAcceptionQuality: for every accepted offer
+    whose recipient is an agent, 10 * (offeredReward / necessaryTime - formerCorePrio /
+    formerCoreLength), the former values being the core's job when the previous step ended
+    (:64-66: after that round's tick, i.e. the state this round starts from; 0 for an empty core).
+    Round 20, fixed prices, N = 2, C = 2, L = 3. Core 1: agent 1, prio 3, rem 4; core 2: agent 2,
+    prio 10, rem 2. Offer IDs (slot order): 1 = agent 1 slot 0 (kind 1, rem 3, price 7) to core 2
+    (recipient 2); 2 = agent 2 slot 0 (kind 0, rem 6, price 2) and 3 = agent 2 slot 1 (kind 1,
+    rem 3, price 7) to core 1 (recipient 1). Agent 1's core-1 acceptor takes index 1 = offer 3, agent
+    2's core-2 acceptor index 0 = offer 1; executions in agent order (world.py:391-404):
+      offer 3: 10 * (7/3 - 3/4)  = 10 * (2.3333333333333335 - 0.75)
+      offer 1: 10 * (7/3 - 10/2) = 10 * (2.3333333333333335 - 5.0)
+    the round's value is statistics.mean of the two, amount 2. Each old core job goes to its
+    owner's first empty slot (agent 1 slot 1, agent 2 slot 1); agent 1 then spawns into slot 0."""
+    import statistics
+
+    N, C, L = 2, 2, 3
+    st = empty_state(N, C, L, 20)
+    st.update(core_owner=[1, 2], core_kind=[0, 1], core_rem=[4, 2], core_birth=[15, 17])
+    st["slot_kind"] = [[1, -1, -1], [0, 1, -1]]
+    st["slot_rem"] = [[3, -1, -1], [6, 3, -1]]
+    st["slot_birth"] = [[16, -1, -1], [19, 18, -1]]
+    st["slot_wait"] = [[1, 0, 0], [1, 1, 0]]
+    st["offer_core"] = [[1, -1, -1], [0, 0, -1]]
+    st["offer_recip"] = [[2, 0, 0], [1, 1, 0]]
+    st["offer_price"] = [[7, 0, 0], [2, 7, 0]]
+    q3 = (7 / 3 - 3 / 4) * 10
+    q1 = (7 / 3 - 10 / 2) * 10
+    words, idx = mt_state(31415)
+    r = rng_at(words, idx)
+    u = r.random()
+    kind = 0 if u < 0.8 else 1
+    return dict(
+        name="acception_quality", cites=["SchedulingEnvironment.py:64-66", "SchedulingEnvironment.py:174-192",
+                                         "world.py:391-404", "world.py:123-133"],
+        config=dict(n_agents=N, n_cores=C, collection_length=L, **README_JOBS),
+        state=st, mt_words=words, mt_index=idx, note="spawn u = %r -> kind %d" % (u, kind),
+        steps=[
+            dict(acc=[[1, 6], [6, 0]], off=[[2, 2, 2], [2, 2, 2]], price=None, auct=[6, 6],
+                 expect=dict(state=dict(round=21, core_owner=[2, 1], core_kind=[1, 1], core_rem=[2, 2],
+                                        core_birth=[18, 16],
+                                        slot_kind=[[kind, 0, -1], [0, 1, -1]],
+                                        slot_rem=[[[6, 3][kind], 4, -1], [6, 2, -1]],
+                                        slot_birth=[[20, 15, -1], [19, 17, -1]], slot_wait=[[0, 0, 0]] * 2,
+                                        offer_core=[[-1, -1, -1]] * 2,
+                                        liab=[[[2, 1, 7, 3, 20]], [[1, 2, 7, 3, 20]]]),
+                             rewards=dict(offer=[[10, 0, 0], [0, 10, 0]], acceptor=[[0, 0], [0, 0]],
+                                          agent=[0, 0], auctioneer=[0, 0]),
+                             quality=[q3, q1], quality_mean=statistics.mean([q3, q1]),
+                             mt_index=r.getstate()[1][624])),
+        ])
+
+
+def codec_cases():
+    """numberToNDimensionalAction (Agent.py:644-666) as the aggregated agents use it (Agent.py:373-380:
+    acceptor number -> C digits in base O+1, offer number -> L digits in base C+1; fully aggregated
+    Agent.py:469-473: acceptor = a // (C+1)^L, offer = a % (C+1)^L), written out by hand for N = C = L
+    = 2 (O = 4: bases 5 and 3). The loop takes the most significant digit first and reverses, so
+    digit i (action of core / slot i) is the base^i digit:
+      acceptor 13: dimension 1: 13 // 5 = 2, rest 3; dimension 0: 3 -> [2, 3] reversed = [3, 2]
+      offer 7: 7 // 3 = 2, rest 1 -> [1, 2]
+      fully 124 = 13 * 9 + 7 -> acceptor 13, offer 7
+    A number outside [0, base^dim) raises ValueError("Illegal Argument") (:651-652)."""
+    return dict(
+        name="codec", cites=["Agent.py:644-666", "Agent.py:373-380", "Agent.py:469-473"],
+        config=dict(n_agents=2, n_cores=2, collection_length=2, **README_JOBS),
+        plain=[dict(number=0, base=5, dim=2, digits=[0, 0]), dict(number=13, base=5, dim=2, digits=[3, 2]),
+               dict(number=24, base=5, dim=2, digits=[4, 4]), dict(number=5, base=5, dim=2, digits=[0, 1]),
+               dict(number=7, base=3, dim=2, digits=[1, 2]), dict(number=8, base=3, dim=2, digits=[2, 2]),
+               dict(number=26, base=3, dim=3, digits=[2, 2, 2]), dict(number=4, base=5, dim=1, digits=[4]),
+               dict(number=0, base=1, dim=3, digits=[0, 0, 0]),
+               dict(number=25, base=5, dim=2, error="ValueError"), dict(number=-1, base=5, dim=2, error="ValueError"),
+               dict(number=9, base=3, dim=2, error="ValueError"), dict(number=1, base=1, dim=3, error="ValueError")],
+        # device form (ms_decode_aggregated): per agent (acceptor number, offer number) -> actions; an
+        # illegal number decodes as reject-all (O = 4) / offer-nothing (C = 2) and is counted as bad
+        aggregated=[dict(acceptor=13, offer=7, acc=[3, 2], off=[1, 2]),
+                    dict(acceptor=24, offer=0, acc=[4, 4], off=[0, 0]),
+                    dict(acceptor=25, offer=8, acc=[4, 4], off=[2, 2], bad=1),
+                    dict(acceptor=0, offer=9, acc=[0, 0], off=[2, 2], bad=1)],
+        fully=[dict(number=124, acc=[3, 2], off=[1, 2]), dict(number=224, acc=[4, 4], off=[2, 2]),
+               dict(number=0, acc=[0, 0], off=[0, 0]), dict(number=225, acc=[4, 4], off=[2, 2], bad=1)])
+
+
 def main():
     kats = [kat_wait_alternation(), kat_free_price_action0(), kat_auctioneer_ties(), kat_spawn_edge(),
             kat_self_offer_first_empty(), kat_mixed_chain(), kat_settlement_double_product(),
             kat_net_zero_offer_reward(), kat_noncommercial_price_reward(), kat_two_jobs_first_empty(),
-            kat_hardcoded_agent_ties(), kat_liability_overflow()]
+            kat_hardcoded_agent_ties(), kat_liability_overflow(), kat_aggregated_chain_rewards(),
+            kat_acception_quality()]
     with open(os.path.join(HERE, "kats.json"), "w") as f:
         json.dump(kats, f)
-    print("wrote %d scenarios" % len(kats))
+    with open(os.path.join(HERE, "kats_codec.json"), "w") as f:
+        json.dump(codec_cases(), f)
+    print("wrote %d scenarios + the codec cases" % len(kats))
 
 
 if __name__ == "__main__":

@@ -14,6 +14,9 @@ import pytest
 HERE = os.path.dirname(os.path.abspath(__file__))
 with open(os.path.join(HERE, "golden", "kats.json")) as f:
     KATS = json.load(f)
+with open(os.path.join(HERE, "golden", "kats_codec.json")) as f:
+    CODEC = json.load(f)
+AGG_KEYS = ("aggregated_offer", "aggregated_acceptor")
 IDS = [k["name"] for k in KATS]
 
 
@@ -78,6 +81,7 @@ def test_kat_fixture_is_current():
         open(p, "w").write(src)
         subprocess.check_call([sys.executable, p], stdout=subprocess.DEVNULL)
         assert json.load(open(os.path.join(d, "kats.json"))) == KATS
+        assert json.load(open(os.path.join(d, "kats_codec.json"))) == CODEC
 
 
 @pytest.mark.parametrize("kat", KATS, ids=IDS)
@@ -101,13 +105,109 @@ def test_kat_oracle(oracle, kat):
             assert int(got["mt_index"]) == exp["mt_index"], where
         ob = env.observe()
         check_obs(ob["acceptor"], ob["offer"], ob["auctioneer"], exp.get("obs", {}), s, where)
-        check_rewards(r, exp.get("rewards", {}), where)
+        # the C oracle has no aggregated outputs: those are checked by test_kat_pyref and on the device
+        check_rewards(r, {k: v for k, v in exp.get("rewards", {}).items() if k not in AGG_KEYS}, where)
         if "termination_revenue" in exp:
             assert r["termination_revenue"] == exp["termination_revenue"], where
+        check_quality(list(r["quality"]), exp, where)
         if "flags_set" in exp:
             assert env.flags & exp["flags_set"] == exp["flags_set"], where
         else:
             assert env.flags == 0, where
+
+
+def check_quality(q, exp, where):
+    """The accepted offers' acception qualities in execution order (SchedulingEnvironment.py:174-192)
+    and their statistics.mean."""
+    import statistics
+
+    if "quality" in exp:
+        assert q == exp["quality"], where
+        assert statistics.mean(q) == exp["quality_mean"], where
+
+
+@pytest.mark.parametrize("kat", KATS, ids=IDS)
+def test_kat_pyref(kat):
+    """The same scenarios through the object-faithful restatement (oracle/pyref.py), including the
+    aggregated rewards (Reward.py:92-143) that only it and the device compute."""
+    from oracle import pyref
+
+    if kat.get("device_only") or any(st["acc"] is None for st in kat["steps"]):
+        pytest.skip("device-only scenario (hard-coded agents / liability cap)")
+    import dataclasses
+
+    fields = {f.name for f in dataclasses.fields(pyref.Config)}
+    if set(kat["config"]) - fields:  # e.g. liability_cap: the restatement's deques have no cap
+        pytest.skip("config keys the restatement does not model: %s" % sorted(set(kat["config"]) - fields))
+    cfg = pyref.Config(**kat["config"])
+    w = pyref.PyWorld.from_state(cfg, kat["state"], kat["mt_words"], kat["mt_index"])
+    for i, step in enumerate(kat["steps"]):
+        where = "%s step %d (pyref)" % (kat["name"], i)
+        exp = step["expect"]
+        if "error" in exp:
+            continue
+        off = step["off"]
+        if cfg.free_prices:
+            off = [[(o, p) for o, p in zip(ro, rp)] for ro, rp in zip(step["off"], step["price"])]
+        (acc_o, off_o, auct_o), rewards, quality, _ = w.step(step["acc"], off, step["auct"])
+        st = w.state()
+        got = {k: v for k, v in st.items() if k not in ("liab", "mt_state")}
+        got["liab"] = st["liab"]
+        for k, v in exp.get("state", {}).items():
+            if k == "liab":
+                for c, chain in enumerate(v):
+                    assert [list(e) for e in reversed(st["liab"][c])] == chain, "%s liab core %d" % (where, c)
+            else:
+                np.testing.assert_array_equal(np.asarray(got[k]).reshape(np.shape(v)), np.asarray(v),
+                                              err_msg="%s %s" % (where, k))
+        if exp.get("mt_index") is not None:
+            assert st["mt_state"][1][624] == exp["mt_index"], where
+        offer_r, acc_r, auct_r, agent_r, term_rev = rewards
+        got_r = dict(acceptor=acc_r[..., 0], auctioneer=auct_r, agent=agent_r,
+                     aggregated_offer=w.last_aggregated[0][:, 0], aggregated_acceptor=w.last_aggregated[1][:, 0])
+        if cfg.free_prices:
+            got_r.update(offer=offer_r[0][..., 0], price=offer_r[1][..., 0])
+        else:
+            got_r["offer"] = offer_r[..., 0]
+        check_rewards(got_r, exp.get("rewards", {}), where)
+        if "termination_revenue" in exp:
+            assert term_rev == exp["termination_revenue"], where
+        check_quality(quality, exp, where)
+        s = dict(acc_obs_dim=3 + 2 * w.O, off_obs_dim=2 * w.C + 2)
+        check_obs(acc_o, off_o, auct_o, exp.get("obs", {}), s, where)
+
+
+def test_codec_pyref():
+    """numberToNDimensionalAction cases (tests/golden/kats_codec.json) through the restatement."""
+    from oracle import pyref
+
+    for c in CODEC["plain"]:
+        if "error" in c:
+            with pytest.raises(ValueError):
+                pyref.number_to_nd_action(c["number"], c["base"], c["dim"])
+        else:
+            assert pyref.number_to_nd_action(c["number"], c["base"], c["dim"]) == c["digits"], c
+
+
+@pytest.mark.gpu
+def test_codec_device(ms):
+    """The same cases through ms_decode_aggregated (E = 1 env per case, N = 2 agents: agent 0 the case,
+    agent 1 all zeros), the aggregated and the fully aggregated form."""
+    import torch
+
+    cfg = ms.abi.make_config(**CODEC["config"])
+    env = ms.BatchedEnv(cfg, 1, seed=0)
+    for fully, cases in ((False, CODEC["aggregated"]), (True, CODEC["fully"])):
+        for c in cases:
+            if fully:
+                nums = torch.tensor([[c["number"], 0]], dtype=torch.int32, device=env.device)
+            else:
+                nums = torch.tensor([[[c["acceptor"], 0]], [[c["offer"], 0]]], dtype=torch.int32, device=env.device)
+            bad = torch.zeros(1, dtype=torch.int32, device=env.device)
+            acc, off = env.decode_aggregated(nums.contiguous(), fully, n_bad=bad)
+            assert acc[0, 0].tolist() == c["acc"] and off[0, 0].tolist() == c["off"], c
+            assert acc[0, 1].tolist() == [0, 0] and off[0, 1].tolist() == [0, 0], c
+            assert int(bad.item()) == c.get("bad", 0), c
 
 
 @pytest.mark.gpu
@@ -135,7 +235,14 @@ def test_kat_device(ms, kat):
                 env.step(acc, off, pr, auctioneer=auct, obs=env.obs_buffers(auctioneer=True))
             assert ei.value.code == exp["error"], where
             continue
-        obs, rew, _ = env.step(acc, off, pr, auctioneer=auct, obs=env.obs_buffers(auctioneer=True))
+        want_agg = any(k in exp.get("rewards", {}) for k in AGG_KEYS)
+        ev = {"metrics": env.metrics_buffer(1)} if "quality_mean" in exp else None
+        obs, rew, _ = env.step(acc, off, pr, auctioneer=auct, obs=env.obs_buffers(auctioneer=True),
+                               rewards=env.reward_buffers(aggregated=want_agg), events=ev)
+        if ev is not None:  # ms_env_metrics: the round's mean acception quality and the amount
+            m = ms.metrics.view(ev["metrics"].cpu().numpy())[0, 0]
+            assert int(m["quality_rounds"]) == 1 and int(m["acception_amount"]) == len(exp["quality"]), where
+            assert abs(float(m["quality_sum"]) - exp["quality_mean"]) <= 1e-12 * abs(exp["quality_mean"]), where
         got = {k: v[0] for k, v in env.export_state().items()}
         check_state(got, exp.get("state", {}), where)
         if exp.get("mt_index") is not None:
