@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define MS_ABI_VERSION 13
+#define MS_ABI_VERSION 14
 
 #define MS_MAX_KINDS 16
 #define MS_MAX_AGENTS 64
@@ -609,6 +609,37 @@ int ms_bdqn_layer1_compact(const ms_bdqn_params* q, const void* workspace, const
  * segs = 1). explore may be NULL (all greedy). action: [n_rows][ac_dim] int8. */
 int ms_bdqn_act(const ms_bdqn_params* q, const float* h1, const int8_t* x, int32_t x_stride, const void* workspace,
                 int64_t n_rows, const uint8_t* explore, const int8_t* rand_action, int8_t* action, void* stream);
+
+/* ---- Branching DQN update (BranchingDQN.update_policy, BranchingDQNModules.py:125-164) ----
+ * One role's minibatch of `batch` (<= 128) transitions: int8 observation rows of the states and
+ * next states ([batch][ld]), the taken action of every branch ([batch][actions_ld] int8), rewards
+ * and masks (0 at an episode end) [batch] f32. */
+typedef struct ms_bdqn_batch {
+    const int8_t* states;
+    const int8_t* next_states;
+    int32_t ld;
+    const int8_t* actions;
+    int32_t actions_ld;
+    const float* rewards;
+    const float* masks;
+    int32_t batch;
+} ms_bdqn_batch;
+
+/* The online net's gradient tensors (the layout of ms_bdqn_params) and the loss [1]. */
+typedef struct ms_bdqn_grads {
+    float *w1, *b1, *w2, *b2, *wv, *bv, *wa, *ba;
+    float* loss;
+} ms_bdqn_grads;
+
+size_t ms_bdqn_update_workspace_bytes(const ms_bdqn_params* q, int32_t batch);
+
+/* The gradient of update_policy on one minibatch: current = q(s) at the taken actions (:135),
+ * argmax = the first maximum of q(s') per branch, max_next = mean over the branches of target(s') at
+ * argmax (:139-142), expected = r + max_next * gamma * mask (:144), loss = mse_loss(expected, current)
+ * over [batch, ac_dim] (:145), every gradient element clamped to [-grad_clip, grad_clip] (:157-158)
+ * and written to grads (the Adam step is ms_adam_step / ms_adam_step_dev). Deterministic. */
+int ms_bdqn_update(const ms_bdqn_params* q, const ms_bdqn_params* target, const ms_bdqn_batch* batch, float gamma,
+                   float grad_clip, void* workspace, size_t workspace_bytes, const ms_bdqn_grads* grads, void* stream);
 
 const char* ms_last_error(void);
 int ms_abi_version(void);

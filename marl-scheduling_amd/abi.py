@@ -209,6 +209,16 @@ class MsBdqnParams(ct.Structure):
                 ("obs", ct.c_int32), ("ac_dim", ct.c_int32), ("n", ct.c_int32)]
 
 
+class MsBdqnBatch(ct.Structure):
+    """ms_bdqn_batch: one role's minibatch for ms_bdqn_update."""
+    _fields_ = [("states", ct.c_void_p), ("next_states", ct.c_void_p), ("ld", ct.c_int32), ("actions", ct.c_void_p),
+                ("actions_ld", ct.c_int32), ("rewards", ct.c_void_p), ("masks", ct.c_void_p), ("batch", ct.c_int32)]
+
+
+class MsBdqnGrads(ct.Structure):
+    _fields_ = [(k, ct.c_void_p) for k in ("w1", "b1", "w2", "b2", "wv", "bv", "wa", "ba", "loss")]
+
+
 class MsDqnBatch(ct.Structure):
     _fields_ = [("states", ct.c_void_p), ("next_states", ct.c_void_p), ("actions", ct.c_void_p),
                 ("rewards", ct.c_void_p), ("samples", ct.c_void_p), ("stride", ct.c_int32), ("n_units", ct.c_int32),

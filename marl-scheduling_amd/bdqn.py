@@ -32,7 +32,10 @@ of N dense [C*D]-wide ones (32x fewer flops at cfg5), on the bf16 MFMA with exac
 (ms_bdqn_act): trunk, value head, every advantage head, the per-branch q = value + adv - mean and
 its first argmax, and the epsilon-greedy pick, on exact-f32 MFMA products; only the int8 actions
 leave it (the library-GEMM version materialised 3.25 GB of advantages per frame and read them back
-for the argmax). The update (batch 128 per role) runs in torch autograd with the HIP Adam.
+for the argmax). The update (batch 128 per role, drawn without replacement like random.sample) runs
+on ms_bdqn_update (bdqn_update_kernels.hip: the three forwards, the double-DQN target, the MSE
+backward and the clamp in four launches) and the HIP Adam; one frame's updates of all roles are
+captured into one HIP graph and replayed.
 """
 from __future__ import annotations
 
@@ -153,6 +156,7 @@ class BDQNConfig:
     learning_starts: int = 4
     grad_clip: float = 1.0
     graph_updates: bool = True   # BranchingRole updates replayed from a captured HIP graph
+    hip_updates: bool = True     # update_policy on ms_bdqn_update (else torch autograd, the reference form)
 
     def epsilon_by_frame(self, i):
         return self.epsilon_final + (self.epsilon_start - self.epsilon_final) * math.exp(-1.0 * i / self.epsilon_decay)
@@ -195,9 +199,48 @@ class BranchingRole:
         self.opt.step()
         return loss.detach()
 
+    def hip_update(self, states_i8, next_i8, actions_i8, rewards, masks, stream=None):
+        """update_policy (BranchingDQNModules.py:125-164) on the HIP kernels (ms_bdqn_update: the three
+        forwards, the double-DQN target, the MSE backward and the clamp in four launches) and the HIP
+        Adam: states / next states [B, ld] int8 observation rows, actions [B, >= ac_dim] int8, rewards /
+        masks [B] f32. Capturable (no host sync). Returns the loss tensor [1] (overwritten by the
+        next update)."""
+        B = states_i8.shape[0]
+        for x in (states_i8, next_i8, actions_i8):
+            assert x.dtype == torch.int8 and x.is_contiguous() and x.shape[0] == B
+        assert rewards.dtype == torch.float32 and masks.dtype == torch.float32
+        assert rewards.is_contiguous() and masks.is_contiguous() and rewards.numel() == masks.numel() == B
+        q = self.q
+        if getattr(self, "_upd_ws", None) is None:
+            nb = int(lib.ms_bdqn_update_workspace_bytes(ct.byref(q.hip_params()), 128))
+            self._upd_ws = torch.empty(((nb + 3) // 4,), dtype=torch.float32, device=states_i8.device)
+            self._upd_loss = torch.zeros((1,), dtype=torch.float32, device=states_i8.device)
+            for prm in q.parameters():
+                if prm.grad is None:
+                    prm.grad = torch.zeros_like(prm)
+        qp, tp = q.hip_params(), self.target.hip_params()
+        bt = abi.MsBdqnBatch(ptr(states_i8), ptr(next_i8), states_i8.shape[1], ptr(actions_i8), actions_i8.shape[1],
+                             ptr(rewards), ptr(masks), B)
+        gr = abi.MsBdqnGrads(*[ptr(getattr(q, k).grad) for k in KEYS], ptr(self._upd_loss))
+        check(lib.ms_bdqn_update(ct.byref(qp), ct.byref(tp), ct.byref(bt), ct.c_float(self.cfg.gamma),
+                                 ct.c_float(self.cfg.grad_clip), ptr(self._upd_ws), self._upd_ws.numel() * 4,
+                                 ct.byref(gr), stream_ptr(stream)))
+        self.opt.step(stream)
+        return self._upd_loss
+
+    def count_update(self):
+        """update_counter and the target sync of update_policy (:161-164), on the host."""
+        self.update_counter += 1
+        if self.update_counter % self.cfg.target_net_update_freq == 0:
+            self.update_counter = 0
+            with torch.no_grad():
+                for k in KEYS:
+                    getattr(self.target, k).copy_(getattr(self.q, k))
+
     def update(self, states, actions, rewards, next_states, masks):
-        """update_policy (BranchingDQNModules.py:125-164) on a drawn batch: states / next_states [B, obs]
-        float, actions [B, ac_dim] long, rewards / masks [B]. Returns the loss."""
+        """update_policy (BranchingDQNModules.py:125-164) in torch autograd (the numerical reference of
+        hip_update) on a drawn batch: states / next_states [B, obs] float, actions [B, ac_dim] long,
+        rewards / masks [B]. Returns the loss."""
         if not self.graph:
             loss = self._body(states, actions, rewards, next_states, masks)
         elif self._g is None:
@@ -237,6 +280,7 @@ class BDQNTrainer:
             cfg = abi.MsConfig.from_buffer_copy(cfg)
             cfg.episode_length = int(episode_length)
         self.cfg, self.E, self.b = cfg, int(n_envs), bcfg or BDQNConfig()
+        self.seed = int(seed)
         self.env = BatchedEnv(cfg, self.E, seed=seed, device=self.device)
         s = self.env.shape
         N, C, L, O = s.n_agents, s.n_cores, s.collection_length, s.max_offers
@@ -395,7 +439,30 @@ class BDQNTrainer:
         a = (j % N).to(torch.int32)
         return slot, e, a
 
+    def _sample_host(self):
+        """batch_size transitions drawn without replacement from the stored frames' E x N transitions,
+        as random.sample(memory, batch_size) (BranchingDQNModules.py:53-55) on a host random.Random:
+        [4][B] int64 (ring record, next record, agent, ring slot), 0 = the newest stored frame."""
+        import random
+
+        E, N, B = self.E, self.N, self.b.batch_size
+        if getattr(self, "_py_rng", None) is None:
+            self._py_rng = random.Random(self.seed + 29)
+        js = self._py_rng.sample(range(self.stored * E * N), B)
+        out = [[0] * B for _ in range(4)]
+        for i, j in enumerate(js):
+            age, rest = divmod(j, E * N)
+            e, a = divmod(rest, N)
+            slot = (self.head - 1 - age) % self.n_slots
+            out[0][i] = slot * E + e
+            out[1][i] = ((slot + 1) % self.n_slots) * E + e
+            out[2][i] = a
+            out[3][i] = slot
+        return out
+
     def _learn(self):
+        if self.b.hip_updates:
+            return self._learn_hip()
         slot, e, a = self._sample()
         nslot = (slot + 1) % self.n_slots
         rec, nrec = slot * self.E + e, nslot * self.E + e
@@ -415,6 +482,56 @@ class BDQNTrainer:
             r = self.rew[k][slot, e, a.long()]
             losses[k] = role.update(s, acts, r, s1, masks)
         self.last_losses = losses
+
+    def _learn_body(self):
+        """One frame's updates from the drawn indices in self._sel (device): the minibatch's rows
+        regenerated from the compact frames (ms_regen_agent_rows), the actions / rewards / masks
+        gathered, then every role's ms_bdqn_update + HIP Adam. No host sync: captured once, replayed."""
+        C, N, L = self.C, self.N, self.L
+        rec, nrec, a, slot = self._sel[0], self._sel[1], self._sel[2], self._sel[3]
+        a32 = a.to(torch.int32)
+        cr = self.core_rows.view(-1, C, self.stride)
+        co = self.core_owner.view(-1, C)
+        sp = self.slot_pairs.view(-1, N, L, 2)
+        acc_s, off_s = self.env.regen_agent_rows(cr, co, sp, rec, a32)
+        acc_n, off_n = self.env.regen_agent_rows(cr, co, sp, nrec, a32)
+        xs = dict(acc=(acc_s, acc_n), off=(off_s, off_n))
+        xs["price"] = xs["off"]
+        masks = self.mask[slot]
+        flat = rec * N + a
+        losses = {}
+        for k, role in self.roles.items():
+            s, s1 = xs[k]
+            acts = self.act[k].view(-1, role.q.ac_dim)[flat]
+            r = self.rew[k].view(-1)[flat]
+            losses[k] = role.hip_update(s, s1, acts, r, masks)
+        return losses
+
+    def _learn_hip(self):
+        B = self.b.batch_size
+        if getattr(self, "_sel", None) is None:
+            self._sel_host = torch.empty((4, B), dtype=torch.int64, pin_memory=True)
+            self._sel = torch.empty((4, B), dtype=torch.int64, device=self.device)
+            self._sel_event = torch.cuda.Event()
+            self._learn_graph = None
+        self._sel_event.synchronize()  # the previous frame's copy out of the pinned buffer is done
+        self._sel_host.copy_(torch.tensor(self._sample_host(), dtype=torch.int64))
+        self._sel.copy_(self._sel_host, non_blocking=True)
+        self._sel_event.record()
+        if not self.b.graph_updates:
+            self.last_losses = self._learn_body()
+        elif self._learn_graph is None:
+            self.last_losses = self._learn_body()  # this frame's updates (and the capture's warm-up)
+            torch.cuda.synchronize(self.device)
+            g = torch.cuda.CUDAGraph()
+            with hip_capture(g):
+                self._graph_losses = self._learn_body()
+            self._learn_graph = g
+        else:
+            self._learn_graph.replay()
+            self.last_losses = self._graph_losses
+        for role in self.roles.values():
+            role.count_update()
 
     def flags(self) -> int:
         return self.env.flags()

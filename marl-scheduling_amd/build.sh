@@ -17,7 +17,7 @@ HEADERS=("${HERE}/csrc/ms_layout.h" "${HERE}/csrc/ms_ppo.h" "${HERE}/csrc/ms_dqn
 CCVER="$("${HIPCC}" --version 2>/dev/null | head -3 | tr '\n' ' ')"
 objs=()
 pids=()
-for src in env_kernels.hip policy_kernels.hip act_pair_kernels.hip returns_kernels.hip ppo_kernels.hip agg_kernels.hip dqn_kernels.hip bdqn_kernels.hip wide_kernels.hip capi.cpp; do
+for src in env_kernels.hip policy_kernels.hip act_pair_kernels.hip returns_kernels.hip ppo_kernels.hip agg_kernels.hip dqn_kernels.hip bdqn_kernels.hip bdqn_update_kernels.hip wide_kernels.hip capi.cpp; do
   obj="${OBJDIR}/${src%.*}.o"
   # the env round reproduces Python's float64 arithmetic: no contraction there; the policy
   # and PPO kernels follow torch's f32 (which fuses freely) within tolerance: fma allowed

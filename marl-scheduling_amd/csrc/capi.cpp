@@ -20,6 +20,7 @@
 #include "ms_ppo.h"
 
 namespace ms {
+hipError_t launch_bdqn_update(const BdqnUpd&, hipStream_t);
 hipError_t launch_env_init(const Params&, int64_t, uint8_t*, uint32_t*, Liab*, uint64_t, hipStream_t);
 hipError_t launch_env_reset(const Params&, int64_t, const uint8_t*, int8_t*, int8_t*, int8_t*, int8_t*, int8_t*,
                             hipStream_t);
@@ -648,10 +649,33 @@ static size_t ppo_partials_bytes(const ms_mlp_params* a, int64_t rows) {
                     ms::ppo_param_count(a->in_dim, a->n_actions) * sizeof(float));  // one vector per block
 }
 
+// k_own_scan's buffers (compact acceptor rows of >= kOwnMinGroups groups): the groups' row masks,
+// the scan blocks' int64 sums, the scan waves' float sums, the common-row forward table and sums
+struct OwnWs {
+    size_t mask, part, wpart, cfwd, csum;
+    int words, nb;
+    size_t total() const { return KeyWs::align256(mask) + KeyWs::align256(part) + KeyWs::align256(wpart) +
+                                  KeyWs::align256(cfwd) + KeyWs::align256(csum); }
+};
+static bool ppo_ownable(const ms_mlp_params* a) { return a->n_groups >= ms::kOwnMinGroups && a->in_dim >= 16; }
+static OwnWs own_ws(const ms_mlp_params* a, int64_t rows) {
+    const size_t G = (size_t)a->n_groups, A = (size_t)a->n_actions, KA = 16 * ((A + 15) / 16);
+    OwnWs w{};
+    w.words = (int)((rows + 31) / 32);
+    w.nb = (int)((rows + 4 * ms::kOwnScanRows - 1) / (4 * ms::kOwnScanRows));
+    w.mask = G * (size_t)w.words * 4;
+    w.part = G * (size_t)w.nb * A * 8;
+    w.wpart = G * 4 * (size_t)w.nb * 8 * 4;
+    w.cfwd = G * (KA + 4) * 4;
+    w.csum = G * (KA + 8) * 4;
+    return w;
+}
+
 size_t ms_ppo_workspace_bytes(const ms_mlp_params* a, int64_t rows) {
     if (!a || rows < 1 || a->n_groups < 1) return 0;
     size_t b = ppo_partials_bytes(a, rows);
     if (ppo_keyable(a)) b += key_ws(a, rows).total();
+    if (ppo_ownable(a)) b += own_ws(a, rows).total();
     return b;
 }
 
@@ -726,6 +750,24 @@ int ms_ppo_grad(const ms_mlp_params* a, const ms_mlp_params* c, const ms_ppo_bat
         p.key_cap = (147 * 1024) / ((16 * ((a->n_actions + 15) / 16) + 1) * 8 + 4);
         // |term| * kKeyFx * R < 2^62: a slot's int64 sum cannot overflow
         p.key_bound = (float)std::min(1e30, std::ldexp(1.0, 62) / ms::kKeyFx / (double)R);
+    }
+    if (ppo_ownable(a) && b->core_owner) {
+        const OwnWs o = own_ws(a, R);
+        uint8_t* w = (uint8_t*)ws + ppo_partials_bytes(a, R) + (ppo_keyable(a) ? key_ws(a, R).total() : 0);
+        auto take = [&w](size_t bytes) {
+            uint8_t* q = w;
+            w += KeyWs::align256(bytes);
+            return q;
+        };
+        p.own_mask = (uint32_t*)take(o.mask);
+        p.own_part = (long long*)take(o.part);
+        p.own_wpart = (float*)take(o.wpart);
+        p.own_cfwd = (float*)take(o.cfwd);
+        p.own_csum = (float*)take(o.csum);
+        p.own_words = o.words;
+        p.own_nb = o.nb;
+        // |term| * 2^28 * R < 2^63: the group's int64 sum over all its rows cannot overflow
+        p.own_qbound = (float)std::min(1e30, std::ldexp(1.0, 35) / (double)R);
     }
     ms::GradOut go{g->w1, g->b1, g->w2, g->b2, g->w3, g->b3, g->cw1, g->cb1, g->cw2, g->cb2, g->cw3, g->cb3, g->loss};
     HIP_TRY(ms::launch_ppo_grad(p, go, (hipStream_t)stream));
@@ -987,6 +1029,72 @@ static int bdqn_check(const ms_bdqn_params* q, const char* who) {
 
 static ms::BdqnNet bdqn_net(const ms_bdqn_params* q) {
     return ms::BdqnNet{q->w1, q->b1, q->w2, q->b2, q->wv, q->bv, q->wa, q->ba, q->obs, q->ac_dim, q->n};
+}
+
+// update_policy workspace (bdqn_update_kernels.hip): layer-1 partials [3][nK][128][128], then the rows'
+// activations / pre-activation gradients [4][128][128], advantage gradients [128][Mn], dv and losses
+struct BdqnUpdWs {
+    int nK;
+    size_t l1p, rows, dadv, small, total;
+};
+static BdqnUpdWs bdqn_upd_ws(const ms_bdqn_params* q) {
+    BdqnUpdWs w{};
+    w.nK = (q->obs + 127) / 128;
+    w.l1p = align256(sizeof(float) * 3 * (size_t)w.nK * 128 * 128);
+    w.rows = align256(sizeof(float) * 4 * 128 * 128);
+    w.dadv = align256(sizeof(float) * 128 * (size_t)q->ac_dim * q->n);
+    w.small = align256(sizeof(float) * 2 * 128);
+    w.total = w.l1p + w.rows + w.dadv + w.small;
+    return w;
+}
+
+size_t ms_bdqn_update_workspace_bytes(const ms_bdqn_params* q, int32_t batch) {
+    if (!q || batch < 1 || batch > 128 || q->obs < 1 || q->ac_dim < 1 || q->n < 1) return 0;
+    return bdqn_upd_ws(q).total;
+}
+
+int ms_bdqn_update(const ms_bdqn_params* q, const ms_bdqn_params* target, const ms_bdqn_batch* b, float gamma,
+                   float grad_clip, void* ws, size_t ws_bytes, const ms_bdqn_grads* g, void* stream) {
+    if (int rc = bdqn_check(q, "ms_bdqn_update")) return rc;
+    if (int rc = bdqn_check(target, "ms_bdqn_update (target)")) return rc;
+    if (!b || !g || !ws) return fail(MS_EINVAL, "ms_bdqn_update: NULL argument");
+    if (target->obs != q->obs || target->ac_dim != q->ac_dim || target->n != q->n)
+        return fail(MS_EINVAL, "ms_bdqn_update: target shape differs from the online net");
+    if (q->ac_dim > 32) return fail(MS_EINVAL, "ms_bdqn_update: ac_dim %d > 32", q->ac_dim);
+    if (b->batch < 1 || b->batch > 128 || !b->states || !b->next_states || !b->actions || !b->rewards || !b->masks ||
+        b->ld < q->obs || b->actions_ld < q->ac_dim)
+        return fail(MS_EINVAL, "ms_bdqn_update: bad batch (1..128 rows, ld >= obs, actions_ld >= ac_dim)");
+    if (!g->w1 || !g->b1 || !g->w2 || !g->b2 || !g->wv || !g->bv || !g->wa || !g->ba || !g->loss)
+        return fail(MS_EINVAL, "ms_bdqn_update: NULL gradient tensor");
+    const BdqnUpdWs w = bdqn_upd_ws(q);
+    if (ws_bytes < w.total) return fail(MS_EINVAL, "ms_bdqn_update: workspace too small (%zu < %zu)", ws_bytes, w.total);
+    ms::BdqnUpd p{};
+    p.q = bdqn_net(q);
+    p.t = bdqn_net(target);
+    p.xs = b->states;
+    p.xn = b->next_states;
+    p.ld = b->ld;
+    p.act = b->actions;
+    p.act_ld = b->actions_ld;
+    p.rew = b->rewards;
+    p.mask = b->masks;
+    p.B = b->batch;
+    p.gamma = gamma;
+    p.clip = grad_clip > 0.f ? grad_clip : 3.0e38f;
+    p.nK = w.nK;
+    char* base = (char*)ws;
+    p.l1p = (float*)base;
+    float* rows = (float*)(base + w.l1p);
+    p.out1 = rows;
+    p.out2 = rows + 128 * 128;
+    p.dpre2 = rows + 2 * 128 * 128;
+    p.dpre1 = rows + 3 * 128 * 128;
+    p.dadv = (float*)(base + w.l1p + w.rows);
+    p.dv = (float*)(base + w.l1p + w.rows + w.dadv);
+    p.lossb = p.dv + 128;
+    p.g = ms::BdqnGrads{g->w1, g->b1, g->w2, g->b2, g->wv, g->bv, g->wa, g->ba, g->loss};
+    HIP_TRY(ms::launch_bdqn_update(p, (hipStream_t)stream));
+    return MS_OK;
 }
 
 int ms_bdqn_prepare(const ms_bdqn_params* q, int32_t seg, int32_t segs, void* workspace, size_t workspace_bytes,

@@ -38,4 +38,29 @@ struct BdqnAct {
     int8_t* action;          // [rows][ac_dim]
 };
 
+// update_policy of one role (bdqn_update_kernels.hip)
+struct BdqnGrads {
+    float *w1, *b1, *w2, *b2, *wv, *bv, *wa, *ba;  // clamped gradients of the online net
+    float* loss;                                   // [1]
+};
+struct BdqnUpd {
+    BdqnNet q, t;             // online and target nets
+    const int8_t* xs;         // [B][ld] state rows (int8 observations)
+    const int8_t* xn;         // [B][ld] next-state rows
+    int ld;
+    const int8_t* act;        // [B][act_ld] the taken actions, one per branch
+    int act_ld;
+    const float* rew;         // [B]
+    const float* mask;        // [B] 0 at an episode end
+    int B;                    // <= 128
+    float gamma, clip;
+    int nK;                   // layer-1 K chunks of 128 inputs
+    float* l1p;               // [3][nK][128][128] layer-1 partial sums of the three forwards
+    float *out1, *out2;       // [B][128] ReLU outputs of q(s)
+    float *dpre2, *dpre1;     // [B][128] d loss / d pre-activations of layers 2 and 1
+    float* dadv;              // [B][ac_dim * n]
+    float *dv, *lossb;        // [B]
+    BdqnGrads g;
+};
+
 }  // namespace ms

@@ -47,7 +47,21 @@ struct PpoArgs {
     float key_bound;       // a larger |term| sends the group to the tile path (keeps the sums in int64)
     int key_nbs;           // scan blocks per group
     int key_cap;           // ranks per scan pass (LDS)
+    // compact acceptor rows of many groups (G >= kOwnMinGroups, the divided acceptors): k_own_scan
+    // reads every row once for 64 groups at a time (lane = group), sums the common rows' loss
+    // derivatives and marks the rest; the tile kernel (kMaskRow) runs only the marked rows
+    uint32_t* own_mask;    // [G][own_words] bit r of word w: row 32w + r goes to the tiles
+    int own_words;         // ceil(R / 32)
+    int own_nb;            // scan blocks per group (kOwnScanRows * 4 rows each)
+    long long* own_part;   // [G][own_nb][A] int64 fixed-point sums of d min(surr)/d ratio * ratio
+    float* own_wpart;      // [G][4 * own_nb][8] per scan wave: sum of (V - G)/R, count, loss sums
+    float* own_cfwd;       // [G][16*NT + 4] the common row's clamped log-probs, V, entropy
+    float* own_csum;       // [G][16*NT + 8] the group's common-row sums (k_own_common)
+    float own_qbound;      // a larger |term| marks the row for the tiles (|sum| * 2^28 < 2^63)
 };
+
+constexpr int kOwnMinGroups = 64;     // groups from which compact rows take k_own_scan + kMaskRow
+constexpr int kOwnScanRows = 1024;    // rows per scan wave (a multiple of 32: whole mask words)
 
 // row (r, u) of the rollout arrays (states rows, actions, old log-probs): [R][U] or unit-major
 __device__ __forceinline__ size_t ru_index(const PpoArgs& p, long long r, int u) {

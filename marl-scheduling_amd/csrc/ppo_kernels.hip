@@ -128,7 +128,12 @@ struct BoolC {
 // kernel modes: every row on its own; rows equal to one common row (found by comparing the rows, or
 // from the core owners of compact acceptor observations); keyed rows (the backward and the forward
 // of a group's distinct rows, k_key_scan sums the rows' loss derivatives in between)
-enum GradMode { kPlain = 0, kCommonRow = 1, kOwnerRow = 2, kKeyBack = 3, kKeyFwd = 4 };
+enum GradMode { kPlain = 0, kCommonRow = 1, kOwnerRow = 2, kKeyBack = 3, kKeyFwd = 4, kMaskRow = 5, kCommonFwd = 6 };
+// kMaskRow: compact acceptor rows of many groups (the divided acceptors), the common rows already
+// summed by k_own_scan / k_own_common: each wave runs the tiles of the rows its group's own-row mask
+// lists, and one wave per group the common rows' virtual tile. kCommonFwd: the forward of the
+// common row of every group (k_own_scan's table).
+constexpr int kMaskList = 1024 + 64;  // LDS list of one wave in kMaskRow: < 16 carried + 32 mask words
 
 #ifdef MS_GRAD_PROBE
 // Probe build only (tools/grad_probe.py): per wave of the last common/owner-row launch, s_memrealtime
@@ -140,6 +145,7 @@ __device__ unsigned long long g_grad_probe[kGradProbeWaves][4];
 template <int NQ, int NT, int MODE>
 struct GradLds {
     static constexpr bool CM = MODE == kCommonRow || MODE == kOwnerRow;
+    static constexpr bool ML = MODE == kMaskRow;
     static constexpr int S1 = (NQ + 1) / 2;           // 32-input k-steps of layer 1 (16*NQ inputs)
     static constexpr int W1B = 32 * S1 + 8;           // bf16 pitch of a split W1 row (+16 B: no conflicts)
     static constexpr int XPD = (NQ & 1) ? 4 * NQ + 6 : 4 * NQ + 2;  // staged input row pitch (dwords)
@@ -152,7 +158,7 @@ struct GradLds {
     // per wave: d1 / e1 transposes over a tile pair, the per-tile transposes, 32 staged input rows
     // (common-row path: the common row's clamped logs, V, entropy, the list of the other rows,
     //  and the wave's int64 fixed-point sums of d min(surr)/d ratio * ratio per action [16*NT])
-    static constexpr int CMF = CM ? 16 * NT + 4 + seg_rows<MODE>() + 64 + 2 * 16 * NT : 0;
+    static constexpr int CMF = CM ? 16 * NT + 4 + seg_rows<MODE>() + 64 + 2 * 16 * NT : (ML ? kMaskList : 0);
     static constexpr int wave_floats = 2 * 16 * TP2 + NTR * 16 * TP + 32 * XPD + CMF;
     // waves per block: 4 when they fit the 160 KB of LDS, else 2 (each wave then walks two chunks)
     static constexpr int WPB = shared_floats + 4 * wave_floats <= 40960 ? 4 : 2;
@@ -271,10 +277,11 @@ __global__ void __launch_bounds__((64 * GradLds<NQ, NT, MODE>::WPB), ((NQ * NT >
     const int one_dw = D >> 2;
     const uint32_t one_bit = 1u << (8 * (D & 3));
     // compact acceptor rows: unit u = agent u / C, core u % C reads core row (r, u % C)
-    const int own_c = MODE == kOwnerRow ? u % p.owner_C : 0;
-    const int8_t own_me = MODE == kOwnerRow ? (int8_t)(u / p.owner_C + 1) : 0;
+    constexpr bool OWNROWS = MODE == kOwnerRow || MODE == kMaskRow;  // rows are compact core rows
+    const int own_c = OWNROWS ? u % p.owner_C : 0;
+    const int8_t own_me = OWNROWS ? (int8_t)(u / p.owner_C + 1) : 0;
     auto row_src = [&](int r) {
-        if constexpr (MODE == kOwnerRow)
+        if constexpr (OWNROWS)
             return reinterpret_cast<const uint32_t*>(p.states + ((size_t)r * p.owner_C + own_c) * p.stride);
         else
             return reinterpret_cast<const uint32_t*>(p.states + ru_index(p, r, u) * p.stride);
@@ -381,6 +388,37 @@ __global__ void __launch_bounds__((64 * GradLds<NQ, NT, MODE>::WPB), ((NQ * NT >
         f.ent = ent;  // this lane's part: the row's entropy is xsum4g(f.ent) (ent_of)
     };
     auto ent_of = [&](const Fwd& f) { return xsum4g(f.ent); };
+
+    if constexpr (MODE == kCommonFwd) {
+        // the common row's forward values of this group: clamped log-probs [16*NT], V, entropy (the
+        // table k_own_scan reads; the same forward as the tiles and the virtual tile)
+        if (wave == 0) {
+            const uint32_t* crow = reinterpret_cast<const uint32_t*>(p.common);
+            uint32_t xw[S1][2];
+#pragma unroll
+            for (int s = 0; s < S1; s++)
+#pragma unroll
+                for (int h = 0; h < 2; h++) {
+                    const int cc = 8 * s + 2 * g4 + h;
+                    xw[s][h] = cc < stride4 ? crow[cc] : 0u;
+                }
+            Fwd f;
+            forward(xw, f);
+            const float ent_row = ent_of(f);
+            float* dst = p.own_cfwd + (size_t)grp * (16 * NT + 4);
+            if (j == 0) {
+#pragma unroll
+                for (int t = 0; t < NT; t++)
+#pragma unroll
+                    for (int q = 0; q < 4; q++) dst[16 * t + 4 * g4 + q] = f.cl[t][q];
+                if (g4 == 0) {
+                    dst[16 * NT] = f.V;
+                    dst[16 * NT + 1] = ent_row;
+                }
+            }
+        }
+        return;
+    }
 
     // ---- one 16-row tile: forward, per-row loss derivatives, backward, weight gradients.
     //      xr = the rows' raw dwords (B-fragment layout), act/olp/G/valid = row j's scalars.
@@ -656,10 +694,10 @@ __global__ void __launch_bounds__((64 * GradLds<NQ, NT, MODE>::WPB), ((NQ * NT >
     uint32_t pre[S1][2];
     int pre_act = 0;
     float pre_olp = 0.f, pre_G = 0.f;
-    const int st_rb = (MODE == kOwnerRow ? p.owner_C : (int)p.rrs) * p.stride;  // bytes between rows
+    const int st_rb = (OWNROWS ? p.owner_C : (int)p.rrs) * p.stride;  // bytes between rows
     const int ac_rb = (int)p.rrs, lp_rb = 4 * (int)p.rrs, rt_rb = 4 * p.ret_ld;
     const int8_t* st_base =
-        MODE == kOwnerRow ? p.states + (size_t)own_c * p.stride : p.states + (size_t)u * (size_t)p.rus * p.stride;
+        OWNROWS ? p.states + (size_t)own_c * p.stride : p.states + (size_t)u * (size_t)p.rus * p.stride;
     const int8_t* ac_base = p.actions + (size_t)u * (size_t)p.rus;
     const float* lp_base = p.old_lp + (size_t)u * (size_t)p.rus;
     const float* rt_base = p.ret + grp;
@@ -806,7 +844,104 @@ __global__ void __launch_bounds__((64 * GradLds<NQ, NT, MODE>::WPB), ((NQ * NT >
             tile_step(BoolC<false>{}, xr, act, olp, G, valid, half, half == 1 || tile + 1 == tile_end, zero_vs, 0.f,
                       0.f);
         }
-    } else if (tile0 < tile_end) {
+    } else if constexpr (MODE == kMaskRow) {
+        // ---- the rows the group's own-row mask lists (k_own_scan: bit r of word w = row 32w + r is
+        //      the owner's row, or a common row whose term the fixed-point sums could not hold), in
+        //      16-row tiles; this wave's chunk is a contiguous range of mask words. The common rows'
+        //      summed derivatives (k_own_common) run through one virtual tile, on wave 0 of block 0.
+        const int wpc = (p.own_words + p.n_chunks - 1) / p.n_chunks;
+        const int w0 = min(chunk * wpc, p.own_words), w1 = min(w0 + CPW * wpc, p.own_words);
+        const int rb = 32 * w0;
+        int32_t* list = reinterpret_cast<int32_t*>(sCm);
+        const uint32_t* mask = p.own_mask + (size_t)grp * p.own_words;
+        const RowBufs wb = row_bufs(rb);
+        int n_list = 0, otile = 0;
+        auto list_tiles = [&](int cnt) {
+            auto pf = [&](int t0) { prefetch_rel(wb, (uint32_t)(list[t0 + (t0 + j < cnt ? j : 0)] - rb)); };
+            pf(0);
+            for (int t0 = 0; t0 < cnt; t0 += 16) {
+                uint32_t xr[S1][2];
+#pragma unroll
+                for (int s = 0; s < S1; s++) xr[s][0] = pre[s][0], xr[s][1] = pre[s][1];
+                const int act = pre_act;
+                const float olp = pre_olp, G = pre_G;
+                const bool valid = t0 + j < cnt;
+                if (t0 + 16 < cnt) pf(t0 + 16);
+                const int half = otile & 1;
+                tile_step(BoolC<false>{}, xr, act, olp, G, valid, half, half == 1, zero_vs, 0.f, 0.f);
+                otile++;
+            }
+        };
+        for (int wbase = w0; wbase < w1; wbase += 32) {
+            // 32 mask words (1024 rows) per step: lane k < 32 expands word wbase + k into its rows, at
+            // its exclusive prefix count of listed rows (rows stay in increasing order)
+            const int w = wbase + lane;
+            uint32_t m = (lane < 32 && w < w1) ? mask[w] : 0u;
+            const int c = __popc(m);
+            int incl = c;
+#pragma unroll
+            for (int d = 1; d < 32; d <<= 1) {
+                const int v = __shfl_up(incl, d);
+                if (lane >= d) incl += v;
+            }
+            const int total = __shfl(incl, 31);
+            int pos = n_list + incl - c;
+            while (m) {
+                list[pos++] = 32 * w + __ffs(m) - 1;
+                m &= m - 1;
+            }
+            n_list += total;
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            const int full = n_list & ~15;
+            if (full > 0) list_tiles(full);
+            const int rest = n_list - full;
+            const int mv = lane < rest ? list[full + lane] : 0;
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            if (lane < rest) list[lane] = mv;
+            n_list = rest;
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        }
+        if (n_list > 0) list_tiles(n_list);
+        if (blk == 0 && wave == 0) {
+            // the common rows of the whole group: column 0 of the virtual tile carries their summed
+            // derivatives (k_own_common: per action, then sum of V - G, count, loss sums)
+            const float* cs = p.own_csum + (size_t)grp * (16 * NT + 8);
+            uint32_t txr[S1][2];
+            const uint32_t* crow = reinterpret_cast<const uint32_t*>(p.common);
+#pragma unroll
+            for (int s = 0; s < S1; s++)
+#pragma unroll
+                for (int h = 0; h < 2; h++) {
+                    const int cc = 8 * s + 2 * g4 + h;
+                    txr[s][h] = crow[cc < stride4 ? cc : stride4 - 1];
+                }
+            float vsum[NT][4];
+#pragma unroll
+            for (int t = 0; t < NT; t++)
+#pragma unroll
+                for (int q = 0; q < 4; q++) vsum[t][q] = j == 0 ? cs[16 * t + 4 * g4 + q] : 0.f;
+            const float gv = cs[16 * NT], cnt = cs[16 * NT + 1];
+            tile_step(BoolC<true>{}, txr, 0, 0.f, 0.f, true, otile & 1, true, vsum,
+                      j == 0 ? -0.01f * p.inv_R * cnt : 0.f, j == 0 ? gv : 0.f);
+            if (lane == 0) {
+                l_min += cs[16 * NT + 2];
+                l_mse += cs[16 * NT + 3];
+                l_ent += cs[16 * NT + 4];
+            }
+        } else if (otile & 1) {  // the last pair's second half: a tile of zero derivatives
+            uint32_t xr[S1][2];
+#pragma unroll
+            for (int s = 0; s < S1; s++) xr[s][0] = xr[s][1] = 0u;
+            tile_step(BoolC<true>{}, xr, 0, 0.f, 0.f, true, 1, true, zero_vs, 0.f, 0.f);
+        }
+    } else if constexpr (L::CM) {
+    if (tile0 < tile_end) {
         // ---- rows equal to the common row (acceptor rows of cores the agent does not own) share
         //      one forward pass: the wave scans its rows one per lane, accumulates their loss
         //      derivatives by action, and lists the other rows for the MFMA tiles; the summed
@@ -1007,6 +1142,7 @@ __global__ void __launch_bounds__((64 * GradLds<NQ, NT, MODE>::WPB), ((NQ * NT >
             l_ent += e_tot;
         }
     }
+    }
 
     // ---- the block's partial gradient: the 4 waves' vectors summed in LDS in wave order
     //      (deterministic), then one coalesced store per block
@@ -1082,6 +1218,159 @@ __global__ void __launch_bounds__((64 * GradLds<NQ, NT, MODE>::WPB), ((NQ * NT >
         }
     }
 #endif
+}
+
+// ---- compact acceptor rows of many groups (the divided acceptors of cfg4: 256 nets, each on its own
+//      1.6 M rows, of which ~5 % are its own rows). PPOmodules.py:127-174 per group; Agent.py:167-212:
+//      an acceptor row is its core's owner row when the agent owns the core, else the constant
+//      common (foreign) row, whose forward is the same for every such row of a group.
+// k_own_scan: one pass over the rows for 64 groups at a time, lane = group (the [R][U] rollout rows
+// of 64 consecutive units are 64 contiguous bytes / floats, so every load is one coalesced segment;
+// the per-group scans of the tile kernel read 1-4 bytes of each row's line). For a common row the
+// lane adds the tile path's d min(surr)/d ratio * ratio to its group's int64 fixed-point sum of the
+// row's action (LDS, [A][64]: no two lanes share an address), and (V - G)/R, the count and the loss
+// terms to its registers; every other row (the owner's, or a term beyond own_qbound) gets its bit in
+// the group's mask for the tiles. Block = 4 waves on consecutive kOwnScanRows-row chunks of the same
+// 64 groups; the block's sums go to own_part, each wave's floats to own_wpart (fixed order later).
+__global__ void __launch_bounds__(256) k_own_scan(PpoArgs p) {
+    extern __shared__ __align__(16) long long own_sh[];
+    const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int A = p.A, KA = 16 * ((A + 15) / 16);
+    const int g = blockIdx.y * 64 + lane;
+    const bool gok = g < p.G;
+    long long* sums = own_sh;                                   // [A][64]
+    float* cl = reinterpret_cast<float*>(own_sh + A * 64);      // [A][64]
+    float* vt = cl + A * 64;                                    // [2][64]: V, entropy of the common row
+    for (int i = tid; i < A * 64; i += 256) {
+        const int a = i >> 6, gg = blockIdx.y * 64 + (i & 63);
+        sums[i] = 0;
+        cl[i] = gg < p.G ? p.own_cfwd[(size_t)gg * (KA + 4) + a] : 0.f;
+    }
+    if (tid < 128) {
+        const int gg = blockIdx.y * 64 + (tid & 63);
+        vt[tid] = gg < p.G ? p.own_cfwd[(size_t)gg * (KA + 4) + KA + (tid >> 6)] : 0.f;
+    }
+    __syncthreads();
+    const int u = gok ? p.unit_of_group[g] : 0;
+    const int own_c = u % p.owner_C;
+    const int own_me = u / p.owner_C + 1;
+    const float Vc = vt[lane], ent_c = vt[64 + lane];
+    const int wc = blockIdx.x * 4 + wave;  // this wave's chunk of rows
+    const long long r0 = (long long)wc * kOwnScanRows;
+    const int nrow = (int)max(0LL, min((long long)kOwnScanRows, p.R - r0));
+    // the chunk's rows as raw buffers from row r0: the wave-uniform row offset goes in soffset, the
+    // lane's column in voffset (no per-row address arithmetic)
+    auto mk = [&](const void* base, long long step) {
+        return __builtin_amdgcn_make_buffer_rsrc(
+            const_cast<void*>(reinterpret_cast<const void*>(reinterpret_cast<const int8_t*>(base) + r0 * step)), 0,
+            (int)(nrow * step), 0x00020000);
+    };
+    const __amdgpu_buffer_rsrc_t b_ac = mk(p.actions, p.rrs), b_lp = mk(p.old_lp, 4 * p.rrs),
+                                 b_rt = mk(p.ret, 4LL * p.ret_ld), b_ow = mk(p.owner, p.owner_C);
+    const int c_ac = (int)(u * p.rus), c_lp = 4 * c_ac, c_rt = 4 * g, c_ow = own_c;
+    const int s_ac = (int)p.rrs, s_lp = 4 * (int)p.rrs, s_rt = 4 * p.ret_ld, s_ow = p.owner_C;
+    const float qb = p.own_qbound, eps_lo = 1.f - p.eps_clip, eps_hi = 1.f + p.eps_clip;
+    float sgv = 0.f, sl_min = 0.f, sl_mse = 0.f, sl_ent = 0.f;
+    int scnt = 0;
+    uint32_t* mrow = p.own_mask + (size_t)g * p.own_words + (size_t)r0 / 32;
+    constexpr int U8 = 8;  // rows per batch of loads
+    for (int w = 0; 32 * w < nrow; w++) {
+        uint32_t bits = 0;
+#pragma unroll
+        for (int k8 = 0; k8 < 32; k8 += U8) {
+            int act[U8], ow[U8];
+            float olp[U8], G[U8];
+#pragma unroll
+            for (int k = 0; k < U8; k++) {
+                // rows past the chunk load the last row again (a wave-uniform clamp: soffset is not
+                // part of the buffer's range check); the `in` test below drops them
+                const int rr = min(32 * w + k8 + k, nrow - 1);
+                act[k] = (int8_t)__builtin_amdgcn_raw_buffer_load_b8(b_ac, c_ac, rr * s_ac, 0);
+                olp[k] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(b_lp, c_lp, rr * s_lp, 0));
+                G[k] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(b_rt, c_rt, rr * s_rt, 0));
+                ow[k] = (int8_t)__builtin_amdgcn_raw_buffer_load_b8(b_ow, c_ow, rr * s_ow, 0);
+            }
+#pragma unroll
+            for (int k = 0; k < U8; k++) {
+                const int rr = 32 * w + k8 + k;
+                const bool in = gok && rr < nrow;
+                bool common = in && ow[k] != own_me;
+                float qd = 0.f, sur1 = 0.f, sur2 = 0.f;
+                if (common) {
+                    // the tile path's per-row derivatives with the common row's forward values
+                    const float lp = (unsigned)act[k] < (unsigned)A ? cl[act[k] * 64 + lane] : 0.f;
+                    const float ratio = fast_exp(lp - olp[k]);
+                    const float adv = G[k] - Vc;
+                    sur1 = ratio * adv;
+                    const float rc = fminf(fmaxf(ratio, eps_lo), eps_hi);
+                    sur2 = rc * adv;
+                    const float inr = (ratio >= eps_lo && ratio <= eps_hi) ? 1.f : 0.f;
+                    const float dmin = sur1 < sur2 ? adv : (sur2 < sur1 ? adv * inr : 0.5f * adv + 0.5f * adv * inr);
+                    qd = dmin * ratio;
+                    common = fabsf(qd) <= qb;  // NaN or huge: the tile path
+                }
+                if (common) {
+                    if ((unsigned)act[k] < (unsigned)A)
+                        atomicAdd(reinterpret_cast<unsigned long long*>(sums + act[k] * 64 + lane),
+                                  (unsigned long long)__float2ll_rn(qd * 268435456.f));
+                    sgv += (Vc - G[k]) * p.inv_R;
+                    scnt++;
+                    sl_min += -fminf(sur1, sur2);
+                    sl_mse += (Vc - G[k]) * (Vc - G[k]);
+                    sl_ent += ent_c;
+                }
+                if (in && !common) bits |= 1u << (k8 + k);
+            }
+        }
+        if (gok) mrow[w] = bits;
+    }
+    if (gok) {
+        float* wp = p.own_wpart + ((size_t)g * 4 * p.own_nb + wc) * 8;
+        wp[0] = sgv;
+        wp[1] = (float)scnt;
+        wp[2] = sl_min;
+        wp[3] = sl_mse;
+        wp[4] = sl_ent;
+    }
+    __syncthreads();
+    for (int i = tid; i < A * 64; i += 256) {
+        const int a = i >> 6, gg = blockIdx.y * 64 + (i & 63);
+        if (gg < p.G) p.own_part[((size_t)gg * p.own_nb + blockIdx.x) * A + a] = sums[i];
+    }
+}
+
+// k_own_common: per group, the scan blocks' int64 sums (exact, order-free) and the scan waves' float
+// sums (a fixed order: thread t takes waves t, t + 256, ..., then a fixed tree) -> own_csum:
+// [16*NT] d loss / d log p of the common rows per action (= -sum / R, column 0 of the virtual tile),
+// then sum of (V - G)/R, the count, and the three loss sums.
+__global__ void __launch_bounds__(256) k_own_common(PpoArgs p) {
+    __shared__ long long ps[2][128];
+    __shared__ float pf[5][256];
+    const int g = blockIdx.x, tid = threadIdx.x, A = p.A, KA = 16 * ((A + 15) / 16);
+    const int a = tid & 127, part = tid >> 7;  // actions a (< 128) over two halves of the blocks
+    long long s = 0;
+    if (a < A)
+        for (int b = part; b < p.own_nb; b += 2) s += p.own_part[((size_t)g * p.own_nb + b) * A + a];
+    ps[part][a] = s;
+    float f[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int wv = tid; wv < 4 * p.own_nb; wv += 256) {
+        const float* wp = p.own_wpart + ((size_t)g * 4 * p.own_nb + wv) * 8;
+#pragma unroll
+        for (int k = 0; k < 5; k++) f[k] += wp[k];
+    }
+#pragma unroll
+    for (int k = 0; k < 5; k++) pf[k][tid] = f[k];
+    __syncthreads();
+    for (int h = 128; h > 0; h >>= 1) {
+        if (tid < h)
+#pragma unroll
+            for (int k = 0; k < 5; k++) pf[k][tid] += pf[k][tid + h];
+        __syncthreads();
+    }
+    float* cs = p.own_csum + (size_t)g * (KA + 8);
+    const double fx_lp = -(double)p.inv_R / 268435456.0;
+    if (tid < KA) cs[tid] = tid < A ? (float)((double)(ps[0][tid] + ps[1][tid]) * fx_lp) : 0.f;
+    if (tid < 5) cs[KA + tid] = pf[tid][0];
 }
 
 // Sum the blocks' partial vectors (fixed order: 4 interleaved row sets, then a fixed tree) and
@@ -1345,6 +1634,20 @@ __global__ void __launch_bounds__(1024) k_key_scan(PpoArgs p) {
     if (tid < 3) p.key_ploss[pb * 4 + tid] = red[tid][0];
 }
 
+// compact rows of many groups: the common row's forward per group, the row scan over all groups,
+// the common sums per group, then the tiles of the marked rows (+ the virtual tile)
+template <int NQ, int NT>
+static hipError_t launch_own(const PpoArgs& a, unsigned nb, hipStream_t st) {
+    hipError_t e;
+    if ((e = launch_grad_cm<NQ, NT, kCommonFwd>(a, 1, st)) != hipSuccess) return e;
+    const size_t lds = (size_t)a.A * 64 * (8 + 4) + 2 * 64 * 4;
+    hipLaunchKernelGGL(k_own_scan, dim3((unsigned)a.own_nb, (unsigned)((a.G + 63) / 64)), dim3(256), lds, st, a);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    hipLaunchKernelGGL(k_own_common, dim3((unsigned)a.G), dim3(256), 0, st, a);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    return launch_grad_cm<NQ, NT, kMaskRow>(a, nb, st);
+}
+
 // the common-row path for inputs up to 128 bytes (its scan holds a row per lane in registers)
 template <int NQ, int NT>
 static hipError_t launch_grad_t(const PpoArgs& a0, hipStream_t st) {
@@ -1380,6 +1683,7 @@ static hipError_t launch_grad_t(const PpoArgs& a0, hipStream_t st) {
         if (a.common && a.stride >= 16) {
             using L = GradLds<NQ, NT, kCommonRow>;
             if (sizeof(float) * L::lds_floats <= 160 * 1024) {
+                if (a.owner && a.own_mask && a.G >= kOwnMinGroups) return launch_own<NQ, NT>(a, nb, st);
                 if (a.owner) return launch_grad_cm<NQ, NT, kOwnerRow>(a, nb, st);
                 return launch_grad_cm<NQ, NT, kCommonRow>(a, nb, st);
             }

@@ -251,3 +251,105 @@ def test_bdqn_trainer_cfg5(ms):
     assert tr.flags() == 0 and tr.env.round == 9 and tr.stored == 6
     assert set(tr.last_losses) >= {"acc", "off"}
     assert all(torch.isfinite(v) for v in tr.last_losses.values())
+
+
+@pytest.mark.parametrize("obs,ac,n,B", [(70, 3, 33, 128), (6240, 32, 97, 128), (130, 32, 13, 77)])
+def test_hip_update_matches_reference(ms, obs, ac, n, B):
+    """ms_bdqn_update + HIP Adam (BranchingRole.hip_update) against the torch restatement of
+    update_policy (oracle/bdqn_ref.py: the three forwards, the double-DQN target averaged over the
+    branches, the broadcast MSE, the clamp, Adam) over three updates with a target sync after the
+    second; the cfg5 acceptor shape (6240 inputs, 32 branches of 97) and a partial batch included."""
+    bdqn = _bdqn()
+    torch.manual_seed(3)
+    cfg = bdqn.BDQNConfig(target_net_update_freq=2)
+    role = bdqn.BranchingRole(obs, ac, n, cfg, "cuda")
+    ref_q, ref_t = RefBranchingQNetwork(obs, ac, n), RefBranchingQNetwork(obs, ac, n)
+    ref_q.load_stacked({k: getattr(role.q, k).detach().cpu() for k in bdqn.KEYS})
+    ref_t.load_stacked({k: getattr(role.target, k).detach().cpu() for k in bdqn.KEYS})
+    adam = torch.optim.Adam(ref_q.parameters(), lr=1e-4)
+    g = torch.Generator().manual_seed(4)
+    for step in range(3):
+        s = torch.randint(-5, 13, (B, obs), generator=g, dtype=torch.int8)
+        s1 = torch.randint(-5, 13, (B, obs), generator=g, dtype=torch.int8)
+        a = torch.randint(0, n, (B, ac), generator=g)
+        r = torch.randint(-30, 30, (B,), generator=g).float()
+        m = (torch.rand((B,), generator=g) > 0.1).float()
+        lg = role.hip_update(s.cuda(), s1.cuda(), a.to(torch.int8).cuda(), r.cuda(), m.cuda())
+        role.count_update()
+        lr_ = update_policy_reference(ref_q, ref_t, adam, s.float(), a, r, s1.float(), m)
+        assert abs(float(lg) - float(lr_)) <= 1e-4 * max(1.0, abs(float(lr_))), (step, float(lg), float(lr_))
+        if step == 1:  # target_net_update_freq = 2
+            ref_t.load_state_dict(ref_q.state_dict())
+    want = ref_q.stacked()
+    for k in bdqn.KEYS:
+        np.testing.assert_allclose(getattr(role.q, k).detach().cpu().numpy(), want[k].detach().numpy(),
+                                   rtol=1e-3, atol=1e-6, err_msg=k)
+    tw = ref_t.stacked()
+    for k in bdqn.KEYS:
+        np.testing.assert_allclose(getattr(role.target, k).detach().cpu().numpy(), tw[k].detach().numpy(),
+                                   rtol=1e-3, atol=1e-6, err_msg=k)
+
+
+def test_hip_update_gradient_matches_autograd(ms):
+    """One ms_bdqn_update's clamped gradient against torch autograd of the same update_policy loss
+    (before Adam), element by element, and bit-identical on a repeat."""
+    bdqn = _bdqn()
+    obs, ac, n, B = 200, 4, 9, 128
+    torch.manual_seed(5)
+    cfg = bdqn.BDQNConfig(grad_clip=0.05)  # a small clamp: some elements hit it
+    role = bdqn.BranchingRole(obs, ac, n, cfg, "cuda")
+    with torch.no_grad():
+        for k in bdqn.KEYS:  # a target different from the online net
+            getattr(role.target, k).add_(0.01 * torch.randn_like(getattr(role.target, k)))
+    g = torch.Generator().manual_seed(6)
+    s = torch.randint(-5, 13, (B, obs), generator=g, dtype=torch.int8).cuda()
+    s1 = torch.randint(-5, 13, (B, obs), generator=g, dtype=torch.int8).cuda()
+    a = torch.randint(0, n, (B, ac), generator=g).cuda()
+    r = torch.randint(-30, 30, (B,), generator=g).float().cuda()
+    m = (torch.rand((B,), generator=g) > 0.1).float().cuda()
+    # autograd of the loss on the current weights
+    q = role.q
+    current = q(s.float()).gather(2, a.unsqueeze(2)).squeeze(-1)
+    with torch.no_grad():
+        am = torch.argmax(q(s1.float()), dim=2)
+        mx = role.target(s1.float()).gather(2, am.unsqueeze(2)).squeeze(-1).mean(1, keepdim=True)
+    expected = r.view(-1, 1) + mx * 0.99 * m.view(-1, 1)
+    loss = ((expected - current) ** 2).mean()
+    want = torch.autograd.grad(loss, [getattr(q, k) for k in bdqn.KEYS])
+    want = {k: w.clamp(-0.05, 0.05) for k, w in zip(bdqn.KEYS, want)}
+    lr0 = role.opt.param_groups[0]["lr"]
+    role.opt.param_groups[0]["lr"] = 0.0  # keep the weights: compare the gradient only
+    l1 = role.hip_update(s, s1, a.to(torch.int8), r, m).clone()
+    g1 = {k: getattr(q, k).grad.clone() for k in bdqn.KEYS}
+    l2 = role.hip_update(s, s1, a.to(torch.int8), r, m).clone()
+    role.opt.param_groups[0]["lr"] = lr0
+    assert abs(float(l1) - float(loss)) <= 1e-5 * abs(float(loss))
+    assert torch.equal(l1, l2)
+    for k in bdqn.KEYS:
+        assert torch.equal(g1[k], getattr(q, k).grad), k
+        scale = want[k].abs().max().item() + 1e-12
+        err = (g1[k] - want[k]).abs().max().item()
+        assert err <= 1e-4 * scale + 1e-7, (k, err, scale)
+
+
+def test_bdqn_trainer_hip_graph_equals_eager(ms):
+    """The trainer's HIP learn step replayed from its captured graph == the same steps eager (same
+    seeds, same draws), bit for bit, and the minibatch drawn without replacement."""
+    bdqn = _bdqn()
+    cfg = ms.abi.named_config("cfg5")
+    trs = []
+    for graph in (False, True):
+        b = bdqn.BDQNConfig(memory_frames=5, learning_starts=2, batch_size=128, graph_updates=graph,
+                            target_net_update_freq=3)
+        trs.append(bdqn.BDQNTrainer(cfg, n_envs=40, bcfg=b, seed=2, episode_length=4))
+    for _ in range(8):
+        for tr in trs:
+            tr.step()
+        sel = trs[1]._sel_host[0] * trs[1].N + trs[1]._sel_host[2]
+        assert len(set(sel.tolist())) == 128
+    assert trs[1]._learn_graph is not None
+    for k in trs[0].roles:
+        for key in bdqn.KEYS:
+            assert torch.equal(getattr(trs[0].roles[k].q, key), getattr(trs[1].roles[k].q, key)), (k, key)
+            assert torch.equal(getattr(trs[0].roles[k].target, key), getattr(trs[1].roles[k].target, key)), (k, key)
+        assert torch.equal(trs[0].last_losses[k], trs[1].last_losses[k]), k

@@ -399,6 +399,58 @@ def test_fused_grad_compact_rows_bit_identical(ms, G, T, E, N, C, O, K):
         assert torch.equal(res[0][1][k], res[1][1][k]), k
 
 
+@pytest.mark.parametrize("N,C,G,T,E,K,shuffle", [(8, 8, 64, 6, 1700, 2, False), (10, 10, 70, 3, 2999, 1, True),
+                                                  (16, 16, 256, 4, 1100, 1, False)])
+def test_fused_grad_compact_many_groups_matches_autograd(ms, N, C, G, T, E, K, shuffle):
+    """ms_ppo_grad on compact acceptor rows with >= 64 groups (the divided acceptors, cfg4: k_own_scan
+    sums the common rows of 64 groups per pass, the tiles run the marked rows) against torch autograd
+    of PPO.update on the regenerated rows (Agent.py:167-212), including a unit map that is not the
+    identity, a group count that leaves a partial lane block, and R over several scan blocks with a
+    partial last chunk; and twice in a row for bit-identical gradients."""
+    ppo = _ppo(ms)
+    O = 3 * N
+    D, A = 3 + 2 * O, O + 1
+    stride = (D + 3) // 4 * 4
+    R, U = T * E, N * C
+    gen = torch.Generator().manual_seed(31)
+    rows = torch.zeros((R, C, stride), dtype=torch.int8)
+    rows[..., :D] = torch.randint(-5, 13, (R, C, D), generator=gen, dtype=torch.int8)
+    owner = torch.randint(0, N + 1, (R, C), generator=gen, dtype=torch.int8)
+    actions = torch.randint(0, A, (R, U), generator=gen).to(torch.int8)
+    old_lp = -torch.rand((R, U), generator=gen) * 3
+    ret = torch.randn((T, E, G), generator=gen)
+    u_sel = (torch.randperm(U, generator=gen)[:G] if shuffle else torch.arange(G)).to(torch.int32)
+    crow = _common_row(D, stride, O).cuda()
+    rows, owner = rows.cuda(), owner.cuda()
+    full = ppo.regen_acceptor_rows(rows, owner, crow, N).contiguous()
+    us = u_sel.long().cuda()
+    x = full[:, us, :D].permute(1, 0, 2).float()
+    a = actions.cuda()[:, us].T.long()
+    lp = old_lp.cuda()[:, us].T.contiguous()
+    rt = ret.cuda().permute(2, 0, 1).reshape(G, R)
+    torch.manual_seed(25)
+    ref = ppo.PPOGroup(G, D, A, 0.003, 0.01, 0.9, 0.2, K, device="cuda")
+    ref_losses = ref.update(x, a, lp, rt)
+    ref_grads = {k: getattr(ref.policy, k).grad.clone() for k in ppo.ACTOR_KEYS + ppo.CRITIC_KEYS}
+    del x, full
+    runs = []
+    for _ in range(2):
+        torch.manual_seed(25)
+        fus = ppo.PPOGroup(G, D, A, 0.003, 0.01, 0.9, 0.2, K, device="cuda")
+        losses = fus.update_fused(rows, actions.cuda(), old_lp.cuda(), ret.cuda(), u_sel.cuda(), T, E,
+                                  common_row=crow, core_owner=owner)
+        runs.append((losses, {k: getattr(fus.policy, k).grad.clone() for k in ref_grads}))
+    for rl, fl in zip(ref_losses, runs[0][0]):
+        np.testing.assert_allclose(fl.cpu().numpy(), rl.cpu().numpy(), rtol=1e-5, atol=1e-6)
+    for k, g in ref_grads.items():
+        fg = runs[0][1][k]
+        scale = g.abs().amax(dim=tuple(range(1, g.dim())), keepdim=True) + 1e-12  # per group
+        err = (fg - g).abs()
+        assert (err <= 1e-4 * scale + 1e-7).all(), (k, (err / scale).max().item())
+    for k in ref_grads:
+        assert torch.equal(runs[0][1][k], runs[1][1][k]), k
+
+
 @pytest.mark.parametrize("N,C,L,O,E", [(8, 8, 3, 24, 2048), (4, 4, 3, 12, 301), (16, 16, 3, 48, 97)])
 def test_act_round_free_matches_separate_calls(ms, N, C, L, O, E):
     """ms_act_round_free (offer units + compact acceptor units in one launch; the paired kernel for
