@@ -290,7 +290,9 @@ def bench_other(args):
               "vs_baseline": None, "dtype": "int8/f32", "data": "synthetic (reference spawn sampler, random-init nets)",
               "config": {"workload": "%s: %s; one step = %d rounds%s" % (args.config, spec["what"], T,
                                                                        " + update" if args.config != "cfg5" else ""),
-                         "replicas_per_gpu": E, "rounds_per_step": T}}
+                         "replicas_per_gpu": E, "rounds_per_step": T,
+                         "world_size": dist.get_world_size() if world > 1 else 1,
+                         "replicas_total": E * world}}
     tm = dict(tr.timings)
     result["breakdown_ms_per_step"] = {k: v / args.steps * 1e3 for k, v in tm.items()}
     if args.config == "cfg5":

@@ -510,14 +510,20 @@ class BDQNTrainer:
     def _learn_hip(self):
         B = self.b.batch_size
         if getattr(self, "_sel", None) is None:
-            self._sel_host = torch.empty((4, B), dtype=torch.int64, pin_memory=True)
+            # two pinned staging buffers, alternating: a frame waits only for the copy of two frames
+            # ago (long done), so the host never stalls behind the device here
+            self._sel_hosts = [torch.empty((4, B), dtype=torch.int64, pin_memory=True) for _ in range(2)]
+            self._sel_events = [torch.cuda.Event() for _ in range(2)]
+            self._sel_flip = 0
             self._sel = torch.empty((4, B), dtype=torch.int64, device=self.device)
-            self._sel_event = torch.cuda.Event()
             self._learn_graph = None
-        self._sel_event.synchronize()  # the previous frame's copy out of the pinned buffer is done
+        i = self._sel_flip
+        self._sel_flip ^= 1
+        self._sel_events[i].synchronize()
+        self._sel_host = self._sel_hosts[i]
         self._sel_host.copy_(torch.tensor(self._sample_host(), dtype=torch.int64))
         self._sel.copy_(self._sel_host, non_blocking=True)
-        self._sel_event.record()
+        self._sel_events[i].record()
         if not self.b.graph_updates:
             self.last_losses = self._learn_body()
         elif self._learn_graph is None:

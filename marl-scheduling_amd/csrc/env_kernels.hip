@@ -18,6 +18,7 @@
 // /root/reference/src) are cited per phase; the CPU restatement that checks
 // this kernel bit-for-bit is oracle/ms_oracle.c.
 #include <hip/hip_runtime.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include "ms_layout.h"
@@ -1741,10 +1742,21 @@ hipError_t launch_env_reset(const Params& P, int64_t E, const uint8_t* recs, int
 #ifndef MS_MIN_LPE
 #define MS_MIN_LPE 16
 #endif
-static int lanes_per_env(const Params& P) {
+// A launch of >= 1024 replicas in fewer than MS_ENV_MIN_WAVES waves (env variable, default 2048: two per
+// SIMD) widens the lane groups up to that many waves, so the chip's SIMDs each hold two waves
+// whose waits can hide each other: cfg2 (4096 replicas, 4 x 4) runs 32 lanes per env, 2048 waves,
+// instead of 16 lanes, 1024 waves (one per SIMD, every wait exposed).
+static int lanes_per_env(const Params& P, int64_t E) {
     int need = P.C > P.N ? P.C : P.N;
     int lpe = MS_MIN_LPE;
     while (lpe < need) lpe *= 2;
+    static const long long min_waves = [] {
+        const char* v = getenv("MS_ENV_MIN_WAVES");
+        return v ? atoll(v) : 2048LL;
+    }();
+    while (E >= 1024 && lpe < kWave && (E * lpe + kWave - 1) / kWave < min_waves &&
+           (E * 2 * lpe + kWave - 1) / kWave <= min_waves)
+        lpe *= 2;
     return lpe;
 }
 
@@ -1775,12 +1787,10 @@ static hipError_t launch_step_t(const Params& P, int64_t E, uint8_t* recs, uint3
 #ifndef MS_NO_FIXED_SHAPES
     if constexpr (LPE == 16) {
         if (is_shape<8, 8, 3, 1>(P)) return launch_step_sh<LPE, FixShape<8, 8, 3, 1>>(P, E, recs, mt, liab, io, s);
-        if (is_shape<4, 4, 3, 1>(P)) return launch_step_sh<LPE, FixShape<4, 4, 3, 1>>(P, E, recs, mt, liab, io, s);
-    }
-    if constexpr (LPE == 32) {
         if (is_shape<16, 16, 3, 1>(P)) return launch_step_sh<LPE, FixShape<16, 16, 3, 1>>(P, E, recs, mt, liab, io, s);
     }
-    if constexpr (LPE == 64) {
+    if constexpr (LPE == 32) {
+        if (is_shape<4, 4, 3, 1>(P)) return launch_step_sh<LPE, FixShape<4, 4, 3, 1>>(P, E, recs, mt, liab, io, s);
         if (is_shape<32, 32, 3, 1>(P)) return launch_step_sh<LPE, FixShape<32, 32, 3, 1>>(P, E, recs, mt, liab, io, s);
     }
 #endif
@@ -1789,7 +1799,7 @@ static hipError_t launch_step_t(const Params& P, int64_t E, uint8_t* recs, uint3
 
 hipError_t launch_env_step(const Params& P, int64_t E, uint8_t* recs, uint32_t* mt, Liab* liab, const StepIO& io,
                            hipStream_t s) {
-    switch (lanes_per_env(P)) {
+    switch (lanes_per_env(P, E)) {
 #if MS_MIN_LPE <= 8
         case 8: return launch_step_t<8>(P, E, recs, mt, liab, io, s);
 #endif

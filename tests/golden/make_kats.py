@@ -657,12 +657,14 @@ def codec_cases():
                dict(number=0, base=1, dim=3, digits=[0, 0, 0]),
                dict(number=25, base=5, dim=2, error="ValueError"), dict(number=-1, base=5, dim=2, error="ValueError"),
                dict(number=9, base=3, dim=2, error="ValueError"), dict(number=1, base=1, dim=3, error="ValueError")],
-        # device form (ms_decode_aggregated): per agent (acceptor number, offer number) -> actions; an
-        # illegal number decodes as reject-all (O = 4) / offer-nothing (C = 2) and is counted as bad
+        # device form (ms_decode_aggregated): per agent (acceptor number, offer number) -> actions. In
+        # the reference one illegal number raises out of getActions (Agent.py:368-382), so the agent
+        # takes no action at all: the device decodes such an agent as reject-all (O = 4) and
+        # offer-nothing (C = 2), whichever of its two numbers was illegal, and counts it as bad
         aggregated=[dict(acceptor=13, offer=7, acc=[3, 2], off=[1, 2]),
                     dict(acceptor=24, offer=0, acc=[4, 4], off=[0, 0]),
                     dict(acceptor=25, offer=8, acc=[4, 4], off=[2, 2], bad=1),
-                    dict(acceptor=0, offer=9, acc=[0, 0], off=[2, 2], bad=1)],
+                    dict(acceptor=0, offer=9, acc=[4, 4], off=[2, 2], bad=1)],
         fully=[dict(number=124, acc=[3, 2], off=[1, 2]), dict(number=224, acc=[4, 4], off=[2, 2]),
                dict(number=0, acc=[0, 0], off=[0, 0]), dict(number=225, acc=[4, 4], off=[2, 2], bad=1)])
 

@@ -280,14 +280,20 @@ def test_hip_update_matches_reference(ms, obs, ac, n, B):
         assert abs(float(lg) - float(lr_)) <= 1e-4 * max(1.0, abs(float(lr_))), (step, float(lg), float(lr_))
         if step == 1:  # target_net_update_freq = 2
             ref_t.load_state_dict(ref_q.state_dict())
+    # Adam moves an element by about lr per step whatever its gradient's size, so an element whose
+    # gradient sits at the f32 noise floor may move either way: at most 2 * lr * steps apart, and few
+    def close(got, want, k):
+        got, want = got.detach().cpu(), want.detach().cpu()
+        off = ~torch.isclose(got, want, rtol=1e-3, atol=1e-6)
+        assert int(off.sum()) <= max(2, off.numel() // 10000), (k, int(off.sum()))
+        assert ((got - want)[off].abs() <= 2 * 1e-4 * 3 + 1e-6).all(), k
+
     want = ref_q.stacked()
     for k in bdqn.KEYS:
-        np.testing.assert_allclose(getattr(role.q, k).detach().cpu().numpy(), want[k].detach().numpy(),
-                                   rtol=1e-3, atol=1e-6, err_msg=k)
+        close(getattr(role.q, k), want[k], k)
     tw = ref_t.stacked()
     for k in bdqn.KEYS:
-        np.testing.assert_allclose(getattr(role.target, k).detach().cpu().numpy(), tw[k].detach().numpy(),
-                                   rtol=1e-3, atol=1e-6, err_msg=k)
+        close(getattr(role.target, k), tw[k], k)
 
 
 def test_hip_update_gradient_matches_autograd(ms):
@@ -345,8 +351,9 @@ def test_bdqn_trainer_hip_graph_equals_eager(ms):
     for _ in range(8):
         for tr in trs:
             tr.step()
-        sel = trs[1]._sel_host[0] * trs[1].N + trs[1]._sel_host[2]
-        assert len(set(sel.tolist())) == 128
+        if trs[1].frame > b.learning_starts:  # a minibatch was drawn this frame
+            sel = trs[1]._sel_host[0] * trs[1].N + trs[1]._sel_host[2]
+            assert len(set(sel.tolist())) == 128
     assert trs[1]._learn_graph is not None
     for k in trs[0].roles:
         for key in bdqn.KEYS:

@@ -55,7 +55,7 @@ def test_env_released_inside_capture_is_deferred(ms):
     assert torch.equal(obs["acceptor"], o_tw["acceptor"]) and torch.equal(obs["offer"], o_tw["offer"])
     for k in ("offer", "acceptor", "auctioneer", "agent"):
         assert torch.equal(rew[k], r_tw[k]), k
-    assert env.round() == twin.round() == T + 1
+    assert env.round == twin.round == T + 1
     # later captures on the same process still work (round 3 saw CaptureUnsupported cascades)
     g2 = torch.cuda.CUDAGraph()
     x = torch.zeros(16, device=env.device)

@@ -74,14 +74,21 @@ def test_rank_env_seeds_are_disjoint():
             assert spans[i][1] <= spans[j][0] or spans[j][1] <= spans[i][0]
 
 
-def _trainer_rank(rank, world, port, out_dir, use_graph=False, iters=2):
+def _trainer_rank(rank, world, port, out_dir, use_graph=False, iters=2, backend="gloo"):
     import torch.distributed as dist
 
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC only on these hosts (RCCL)
+    device = None
+    if backend == "nccl":  # one device per rank, RCCL over xGMI
+        device = "cuda:%d" % rank
+        torch.cuda.set_device(rank)
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device(device))
+    else:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
     tr = importlib.import_module("marl-scheduling_amd.trainer")
     t = tr.Trainer.from_named("cfg3", n_envs=32, update_step=12, seed=3, rank=rank, world_size=world,
-                              use_graph=use_graph)
+                              use_graph=use_graph, device=device)
     for _ in range(iters):
         t.iteration()
     out = {}
@@ -89,7 +96,8 @@ def _trainer_rank(rank, world, port, out_dir, use_graph=False, iters=2):
         for k, v in u.group.policy.named_parameters():
             out[u.name + "." + k] = v.detach().cpu().clone()
     out["flags"] = torch.tensor(t.flags())
-    torch.save(out, os.path.join(out_dir, "trainer%s%d.pt" % ("_graph" if use_graph else "", rank)))
+    torch.save(out, os.path.join(out_dir, "trainer%s%s%d.pt" % ("_" + backend if backend != "gloo" else "",
+                                                              "_graph" if use_graph else "", rank)))
     dist.destroy_process_group()
 
 
@@ -117,3 +125,33 @@ def test_two_rank_graphed_update_equals_eager(tmp_path):
         assert int(g.pop("flags")) == 0 and int(e.pop("flags")) == 0
         for k in e:
             assert torch.equal(g[k], e[k]), (r, k)
+
+
+def _device_count():
+    try:
+        return torch.cuda.device_count()
+    except Exception:
+        return 0
+
+
+@pytest.mark.gpu
+@pytest.mark.skipif(_device_count() < 2, reason="needs 2 GPUs (the RCCL path runs one rank per device)")
+@pytest.mark.parametrize("use_graph", [False, True])
+def test_two_rank_rccl_trainer(tmp_path, use_graph):
+    """The multi-GPU path as bench.py --gpus N runs it: two ranks on two devices, the gradient
+    all-reduce on the nccl (RCCL over xGMI) backend, eager and graph-replayed updates
+    (SchedulingEnvironment.py:314-329 / PPOmodules.py:548-597 shared nets). Both ranks must end with
+    bit-identical weights, and the graphed update must equal the eager one."""
+    mp.spawn(_trainer_rank, args=(2, _free_port(), str(tmp_path), use_graph, 3, "nccl"), nprocs=2, join=True)
+    tag = "_nccl" + ("_graph" if use_graph else "")
+    w0 = torch.load(tmp_path / ("trainer%s0.pt" % tag), weights_only=True)
+    w1 = torch.load(tmp_path / ("trainer%s1.pt" % tag), weights_only=True)
+    assert int(w0.pop("flags")) == 0 and int(w1.pop("flags")) == 0
+    for k in w0:
+        assert torch.equal(w0[k], w1[k]), k
+    if use_graph:  # the same ranks eager: identical weights
+        mp.spawn(_trainer_rank, args=(2, _free_port(), str(tmp_path), False, 3, "nccl"), nprocs=2, join=True)
+        e0 = torch.load(tmp_path / "trainer_nccl0.pt", weights_only=True)
+        e0.pop("flags")
+        for k in e0:
+            assert torch.equal(w0[k], e0[k]), k
