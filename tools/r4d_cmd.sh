@@ -1,0 +1,16 @@
+# round-4 check (via gpurun): the GPU suite, smoke, the default bench line, the other configs' lines,
+# the profile of the cfg3 bench (kernel trace + env PMC traffic) and the cfg2 / cfg4 env traffic
+set -o pipefail
+O=gpurun_out/r4d
+mkdir -p $O
+timeout -k 10 600 python -u -m pytest tests -m gpu -q --timeout 120 --timeout-method thread -p no:cacheprovider \
+  > $O/gputest.log 2>&1; echo "pytest rc=$?" >> $O/gputest.log
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || exit 1
+timeout -k 10 400 python bench.py > $O/bench.json 2> $O/bench.err || exit 1
+for c in cfg2 cfg4 cfg5; do
+  timeout -k 10 300 python bench.py --config $c --no-cpu-baseline > $O/$c.json 2> $O/$c.err || exit 1
+done
+bash profiles/run_profile.sh r4d > $O/profile.log 2>&1 || exit 1
+bash profiles/run_profile.sh r4d cfg2 > $O/profile_cfg2.log 2>&1 || exit 1
+bash profiles/run_profile.sh r4d cfg4 > $O/profile_cfg4.log 2>&1 || exit 1
+echo done > $O/done
