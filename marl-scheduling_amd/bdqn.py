@@ -500,11 +500,21 @@ class BDQNTrainer:
         masks = self.mask[slot]
         flat = rec * N + a
         losses = {}
+        # the roles' updates are independent chains of small launches (a 128-row batch): one stream
+        # each, forked from and joined back into the current stream (captured as parallel branches)
+        main = torch.cuda.current_stream(self.device)
+        if getattr(self, "_role_streams", None) is None:
+            self._role_streams = {k: torch.cuda.Stream(device=self.device) for k in self.roles}
         for k, role in self.roles.items():
-            s, s1 = xs[k]
-            acts = self.act[k].view(-1, role.q.ac_dim)[flat]
-            r = self.rew[k].view(-1)[flat]
-            losses[k] = role.hip_update(s, s1, acts, r, masks)
+            st = self._role_streams[k]
+            st.wait_stream(main)
+            with torch.cuda.stream(st):
+                s, s1 = xs[k]
+                acts = self.act[k].view(-1, role.q.ac_dim)[flat]
+                r = self.rew[k].view(-1)[flat]
+                losses[k] = role.hip_update(s, s1, acts, r, masks)
+        for st in self._role_streams.values():
+            main.wait_stream(st)
         return losses
 
     def _learn_hip(self):

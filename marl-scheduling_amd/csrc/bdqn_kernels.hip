@@ -55,6 +55,25 @@ __device__ __forceinline__ uint32_t pack_hi(float lo, float hi) {
 __device__ __forceinline__ uint32_t pack_i(int a, int b) { return pack_hi((float)a, (float)b); }
 __device__ __forceinline__ float trunc_bf16(float x) { return __uint_as_float(__float_as_uint(x) & 0xffff0000u); }
 
+// eight f32 values as three exact bf16 terms (hi + mid + lo == v: each term keeps 8 significant bits)
+__device__ __forceinline__ void split8(const float (&v)[8], u4v& hi, u4v& mid, u4v& lo) {
+#pragma unroll
+    for (int t = 0; t < 4; t++) {
+        float h[2], m[2], l[2];
+#pragma unroll
+        for (int u = 0; u < 2; u++) {
+            const float x = v[2 * t + u];
+            h[u] = trunc_bf16(x);
+            const float r = x - h[u];
+            m[u] = trunc_bf16(r);
+            l[u] = r - m[u];
+        }
+        hi[t] = pack_hi(h[0], h[1]);
+        mid[t] = pack_hi(m[0], m[1]);
+        lo[t] = pack_hi(l[0], l[1]);
+    }
+}
+
 // the foreign acceptor row F (Agent.py:167-212): [0, -1, -1, (-2, -2) * O]; zero past D
 __device__ __forceinline__ int foreign(int k, int D) { return k == 0 ? 0 : (k <= 2 ? -1 : (k < D ? -2 : 0)); }
 
@@ -175,187 +194,303 @@ __global__ void __launch_bounds__(256) k_bdqn_l1_gather(BdqnL1Compact p) {
     *reinterpret_cast<f4*>(p.h1 + (size_t)r * kBH + 4 * h4) = v;
 }
 
-// ---- the fused trunk + heads + argmax. Block = 8 waves x 16 rows; lane (j, g4): row j of its wave's
-//      tile, k-group / accumulator-row group g4.
+// ---- the fused trunk + heads + argmax. Block = 8 waves x 32 rows: two 16-row column tiles per wave;
+//      lane (j, g4): row j of each of its wave's tiles, k-group / accumulator-row group g4.
+//      Heads on v_mfma_f32_16x16x32_bf16 with both operands as three exact bf16 terms (W = a1 + a2 + a3,
+//      out = b1 + b2 + b3, each term 8 significant bits): the six products down to 2^-16 of the leading
+//      one (a1 b1; a1 b2, a2 b1; a1 b3, a2 b2, a3 b1) are exact in the f32 accumulator, the three
+//      dropped ones are below 2^-23 of it, so a q value differs from the f32 product sum by about f32
+//      rounding (3 MFMA passes of 16 cycles per 32 inputs instead of 8 of 32 on v_mfma_f32_16x16x4_f32).
+//      K permutation of the heads: k-step s, lane group g4, element e <-> hidden unit
+//      16 (2 s + e / 4) + 4 g4 + e % 4, so a lane's B fragment is its own trunk outputs out[2s], out[2s+1]
+//      and the staged Wa rows are stored permuted to match.
+constexpr int kAPitch = 136;    // bf16 pitch of a staged term row (272 B: 16 rows' b128 reads spread over the banks)
+// hidden units 4 k4 .. 4 k4 + 3 (= 16 kt + 4 g + 0..3) of a 128-wide weight row m as three bf16 terms,
+// stored at positions 32 (kt / 2) + 8 g + 4 (kt % 2) + 0..3 of term rows [3][rows][kAPitch]: the
+// permuted K order whose k-step s, lane group g4, element e is hidden unit 16 (2 s + e / 4) + 4 g4 + e % 4
+__device__ __forceinline__ void put_terms(uint16_t* base, int rows, int m, int k4, const f4& v4) {
+    const int kt = k4 >> 2, g = k4 & 3;
+    const int pos = 32 * (kt >> 1) + 8 * g + 4 * (kt & 1);
+    uint32_t t3[3][2];
+#pragma unroll
+    for (int e2 = 0; e2 < 2; e2++) {
+        float hh[2], mm[2], ll[2];
+#pragma unroll
+        for (int u2 = 0; u2 < 2; u2++) {
+            const float v = v4[2 * e2 + u2];
+            hh[u2] = trunc_bf16(v);
+            const float r = v - hh[u2];
+            mm[u2] = trunc_bf16(r);
+            ll[u2] = r - mm[u2];
+        }
+        t3[0][e2] = pack_hi(hh[0], hh[1]);
+        t3[1][e2] = pack_hi(mm[0], mm[1]);
+        t3[2][e2] = pack_hi(ll[0], ll[1]);
+    }
+#pragma unroll
+    for (int t = 0; t < 3; t++)
+        *reinterpret_cast<uint2*>(base + ((size_t)t * rows + m) * kAPitch + pos) = make_uint2(t3[t][0], t3[t][1]);
+}
+// six products of the three-term operands into one accumulator (the three below 2^-23 of the leading
+// product dropped)
+__device__ __forceinline__ f4 mfma_split6(const u4v& a1, const u4v& a2, const u4v& a3, const u4v (&b)[3], f4 c) {
+    c = mfma_bf16(a1, b[0], c);
+    c = mfma_bf16(a1, b[1], c);
+    c = mfma_bf16(a2, b[0], c);
+    c = mfma_bf16(a1, b[2], c);
+    c = mfma_bf16(a2, b[1], c);
+    c = mfma_bf16(a3, b[0], c);
+    return c;
+}
+
 constexpr int kActWaves = 8;
+constexpr int kActTiles = 2;    // 16-row column tiles per wave
 
 template <int NMT, bool L1>
 __global__ void __launch_bounds__(64 * kActWaves) k_bdqn_act(BdqnAct p) {
     constexpr int ROWS_W = 16 * NMT;                   // staged Wa rows per branch
-    constexpr int PF = (ROWS_W * 32 + 64 * kActWaves - 1) / (64 * kActWaves);  // f4 per thread per branch
-    extern __shared__ __align__(16) float sm[];        // [128][kBPitch] W2, then [ROWS_W][kBPitch] Wa + ba
+    constexpr int NTH = 64 * kActWaves;
+    constexpr int NC = kActTiles;
+    extern __shared__ __align__(16) float sm[];        // [128][kBPitch] W2, then [3][ROWS_W][kAPitch] bf16 Wa + ba
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int j = lane & 15, g4 = lane >> 4;
     const int n = p.q.n, A = p.q.ac_dim;
-    const long long row0 = ((long long)blockIdx.x * kActWaves + w) * 16;
-    const long long row = row0 + j;
-    const bool rv = row < p.rows;
-    const long long rc = rv ? row : p.rows - 1;
-
-    // stage W2 (rows m, pitch kBPitch)
-    for (int x = tid; x < kBH * 32; x += 64 * kActWaves) {
-        const int m = x >> 5, k4 = x & 31;
-        *reinterpret_cast<f4*>(sm + m * kBPitch + 4 * k4) = *reinterpret_cast<const f4*>(p.q.w2 + (size_t)m * kBH + 4 * k4);
+    const long long row0 = ((long long)blockIdx.x * kActWaves + w) * 16 * NC;
+    long long row[NC], rc[NC];
+    bool rv[NC];
+#pragma unroll
+    for (int c = 0; c < NC; c++) {
+        row[c] = row0 + 16 * c + j;
+        rv[c] = row[c] < p.rows;
+        rc[c] = rv[c] ? row[c] : p.rows - 1;
     }
 
-    // ---- layer-1 pre-activations in the trunk's B layout: h[kt][q] = h1[row j][16 kt + 4 g4 + q]
-    float h[8][4];
-    if constexpr (!L1) {
+    // stage W2 as three bf16 terms in the permuted K order ([3][128][kAPitch])
+    uint16_t* sW2 = reinterpret_cast<uint16_t*>(sm);
+    for (int x = tid; x < kBH * 32; x += NTH) {
+        const int m = x >> 5, k4 = x & 31;
+        put_terms(sW2, kBH, m, k4, *reinterpret_cast<const f4*>(p.q.w2 + (size_t)m * kBH + 4 * k4));
+    }
+
+    // ---- trunk: out = ReLU(W2 h + b2) of row j (three-term bf16 MFMA, as the heads), the value head, then
+    //      out as the heads' B fragments: bf[c][s][t] = term t of (out[2s][0..3], out[2s+1][0..3])
+    __syncthreads();  // W2 staged
+    u4v bf[NC][4][3];
+    float value[NC];
 #pragma unroll
-        for (int kt = 0; kt < 8; kt++) {
-            const f4 v = *reinterpret_cast<const f4*>(p.h1 + (size_t)rc * kBH + 16 * kt + 4 * g4);
+    for (int c = 0; c < NC; c++) {
+        // layer-1 pre-activations in the trunk's B layout: h[kt][q] = h1[row j of tile c][16 kt + 4 g4 + q]
+        float h[8][4];
+        if constexpr (!L1) {
 #pragma unroll
-            for (int q = 0; q < 4; q++) h[kt][q] = v[q];
-        }
-    } else {
-        // W1 x on the bf16 MFMA: int8 inputs exact, W1 three exact bf16 terms; D layout = B layout
-        const int S = p.Kp / 32;
-        const int x4 = p.x_stride >> 2;
-        const uint32_t* xr = reinterpret_cast<const uint32_t*>(p.x + (size_t)rc * p.x_stride);
-        const size_t tsz = (size_t)kBH * p.Kp;
-        f4 acc1[8];
+            for (int kt = 0; kt < 8; kt++) {
+                const f4 v = *reinterpret_cast<const f4*>(p.h1 + (size_t)rc[c] * kBH + 16 * kt + 4 * g4);
 #pragma unroll
-        for (int mt = 0; mt < 8; mt++) acc1[mt] = (f4){0, 0, 0, 0};
-        for (int s = 0; s < S; s++) {
-            const int d0 = 8 * s + 2 * g4;
-            const uint32_t x0 = d0 < x4 ? xr[d0] : 0u, x1 = d0 + 1 < x4 ? xr[d0 + 1] : 0u;
-            u4v xb;
-            xb[0] = pack_i((int8_t)x0, (int8_t)(x0 >> 8));
-            xb[1] = pack_i((int8_t)(x0 >> 16), (int8_t)(x0 >> 24));
-            xb[2] = pack_i((int8_t)x1, (int8_t)(x1 >> 8));
-            xb[3] = pack_i((int8_t)(x1 >> 16), (int8_t)(x1 >> 24));
-#pragma unroll
-            for (int mt = 0; mt < 8; mt++) {
-                const uint16_t* wp = p.w1s + (size_t)(16 * mt + j) * p.Kp + 32 * s + 8 * g4;
-#pragma unroll
-                for (int t = 0; t < 3; t++) acc1[mt] = mfma_bf16(*reinterpret_cast<const u4v*>(wp + t * tsz), xb, acc1[mt]);
+                for (int q = 0; q < 4; q++) h[kt][q] = v[q];
             }
+        } else {
+            // W1 x on the bf16 MFMA: int8 inputs exact, W1 three exact bf16 terms; D layout = B layout
+            const int S = p.Kp / 32;
+            const int x4 = p.x_stride >> 2;
+            const uint32_t* xr = reinterpret_cast<const uint32_t*>(p.x + (size_t)rc[c] * p.x_stride);
+            const size_t tsz = (size_t)kBH * p.Kp;
+            f4 acc1[8];
+#pragma unroll
+            for (int mt = 0; mt < 8; mt++) acc1[mt] = (f4){0, 0, 0, 0};
+            for (int s = 0; s < S; s++) {
+                const int d0 = 8 * s + 2 * g4;
+                const uint32_t x0 = d0 < x4 ? xr[d0] : 0u, x1 = d0 + 1 < x4 ? xr[d0 + 1] : 0u;
+                u4v xb;
+                xb[0] = pack_i((int8_t)x0, (int8_t)(x0 >> 8));
+                xb[1] = pack_i((int8_t)(x0 >> 16), (int8_t)(x0 >> 24));
+                xb[2] = pack_i((int8_t)x1, (int8_t)(x1 >> 8));
+                xb[3] = pack_i((int8_t)(x1 >> 16), (int8_t)(x1 >> 24));
+#pragma unroll
+                for (int mt = 0; mt < 8; mt++) {
+                    const uint16_t* wp = p.w1s + (size_t)(16 * mt + j) * p.Kp + 32 * s + 8 * g4;
+#pragma unroll
+                    for (int t = 0; t < 3; t++) acc1[mt] = mfma_bf16(*reinterpret_cast<const u4v*>(wp + t * tsz), xb, acc1[mt]);
+                }
+            }
+#pragma unroll
+            for (int kt = 0; kt < 8; kt++)
+#pragma unroll
+                for (int q = 0; q < 4; q++) h[kt][q] = acc1[kt][q] + p.q.b1[16 * kt + 4 * g4 + q];
         }
 #pragma unroll
         for (int kt = 0; kt < 8; kt++)
 #pragma unroll
-            for (int q = 0; q < 4; q++) h[kt][q] = acc1[kt][q] + p.q.b1[16 * kt + 4 * g4 + q];
-    }
-#pragma unroll
-    for (int kt = 0; kt < 8; kt++)
-#pragma unroll
-        for (int q = 0; q < 4; q++) h[kt][q] = fmaxf(h[kt][q], 0.f);
-    __syncthreads();
+            for (int q = 0; q < 4; q++) h[kt][q] = fmaxf(h[kt][q], 0.f);
 
-    // ---- trunk: out[mt][q] = ReLU(W2 h + b2)[16 mt + 4 g4 + q] of row j
-    float out[8][4];
-    {
+        u4v hb[4][3];
+#pragma unroll
+        for (int s = 0; s < 4; s++) {
+            float v[8];
+#pragma unroll
+            for (int e = 0; e < 4; e++) {
+                v[e] = h[2 * s][e];
+                v[4 + e] = h[2 * s + 1][e];
+            }
+            split8(v, hb[s][0], hb[s][1], hb[s][2]);
+        }
         f4 acc[8];
 #pragma unroll
-        for (int mt = 0; mt < 8; mt++) acc[mt] = (f4){0, 0, 0, 0};
+        for (int mt = 0; mt < 8; mt++) {
+            acc[mt] = (f4){0, 0, 0, 0};
 #pragma unroll
-        for (int kt = 0; kt < 8; kt++) {
-#pragma unroll
-            for (int mt = 0; mt < 8; mt++) {
-                const f4 a4 = *reinterpret_cast<const f4*>(sm + (16 * mt + j) * kBPitch + 16 * kt + 4 * g4);
-#pragma unroll
-                for (int q = 0; q < 4; q++) acc[mt] = mfma4(a4[q], h[kt][q], acc[mt]);
+            for (int s = 0; s < 4; s++) {
+                const uint16_t* ap = sW2 + (size_t)(16 * mt + j) * kAPitch + 32 * s + 8 * g4;
+                acc[mt] = mfma_split6(*reinterpret_cast<const u4v*>(ap), *reinterpret_cast<const u4v*>(ap + kBH * kAPitch),
+                                      *reinterpret_cast<const u4v*>(ap + 2 * kBH * kAPitch), hb[s], acc[mt]);
             }
         }
+        float out[8][4];
 #pragma unroll
         for (int mt = 0; mt < 8; mt++)
 #pragma unroll
             for (int q = 0; q < 4; q++) out[mt][q] = fmaxf(acc[mt][q] + p.q.b2[16 * mt + 4 * g4 + q], 0.f);
-    }
-    // value head: sum over the row's 128 features (lane partials in feature order, then the 4 groups)
-    float vp = 0.f;
+        // value head: sum over the row's 128 features (lane partials in feature order, then the 4 groups)
+        float vp = 0.f;
 #pragma unroll
-    for (int mt = 0; mt < 8; mt++)
+        for (int mt = 0; mt < 8; mt++)
 #pragma unroll
-        for (int q = 0; q < 4; q++) vp = fmaf(p.q.wv[16 * mt + 4 * g4 + q], out[mt][q], vp);
-    const float value = rows_sum(vp) + p.q.bv[0];
-    const bool explore = p.explore && rv && p.explore[row] != 0;
-
-    // ---- heads, one branch at a time: Wa rows b*n + m (m < ROWS_W; zero rows past n) in LDS
-    float* sWa = sm;                       // [ROWS_W][kBPitch]
-    float* sba = sm + ROWS_W * kBPitch;    // [ROWS_W]
-    f4 pf[PF];
-    float pfb = 0.f;
-    auto fetch = [&](int b) {  // branch b's rows into registers
+            for (int q = 0; q < 4; q++) vp = fmaf(p.q.wv[16 * mt + 4 * g4 + q], out[mt][q], vp);
+        value[c] = rows_sum(vp) + p.q.bv[0];
 #pragma unroll
-        for (int u = 0; u < PF; u++) {
-            const int x = tid + u * 64 * kActWaves;
-            const int m = x >> 5, k4 = x & 31;
-            pf[u] = (x < ROWS_W * 32 && m < n) ? *reinterpret_cast<const f4*>(p.q.wa + ((size_t)b * n + m) * kBH + 4 * k4)
-                                               : (f4){0, 0, 0, 0};
+        for (int s = 0; s < 4; s++) {
+            float v[8];
+#pragma unroll
+            for (int e = 0; e < 4; e++) {
+                v[e] = out[2 * s][e];
+                v[4 + e] = out[2 * s + 1][e];
+            }
+            split8(v, bf[c][s][0], bf[c][s][1], bf[c][s][2]);
         }
-        pfb = (tid < ROWS_W && tid < n) ? p.q.ba[(size_t)b * n + tid] : 0.f;
+    }
+    bool explore[NC];
+#pragma unroll
+    for (int c = 0; c < NC; c++) explore[c] = p.explore && rv[c] && p.explore[row[c]] != 0;
+
+    // ---- heads, one branch at a time: Wa rows b*n + m (m < ROWS_W; zero rows past n) in LDS as three
+    //      bf16 terms in the permuted K order. The next branch's f32 rows stream into an LDS staging
+    //      area by LDS-DMA (global_load_lds_dwordx4, no registers) while the current one's MFMAs run;
+    //      the split into terms happens between two barriers. (NMT = 8 does not fit the staging area in
+    //      160 KB: it prefetches through registers.)
+    constexpr bool GLDS = 3 * ROWS_W * kAPitch * 2 + ROWS_W * 4 + ROWS_W * kBH * 4 <= 160 * 1024;
+    uint16_t* sWa = reinterpret_cast<uint16_t*>(sm);                        // [3][ROWS_W][kAPitch]
+    float* sba = sm + (3 * ROWS_W * kAPitch) / 2;                          // [ROWS_W]
+    float* sF = sba + ROWS_W;                                               // [ROWS_W][128] f32 staging (GLDS)
+    constexpr int PF = GLDS ? 1 : (ROWS_W * 32 + NTH - 1) / NTH;            // f4 per thread per branch (registers)
+    f4 pf[PF];
+    auto fetch = [&](int b) {  // branch b's rows: LDS staging (GLDS) or registers
+        if constexpr (GLDS) {
+            typedef __attribute__((address_space(3))) void* lds_vp;
+            typedef __attribute__((address_space(1))) void* glb_vp;
+            // wave-instruction i: rows 2i, 2i + 1 (1 KB, lane-linear); rows past n read row n - 1 (zeroed at the split)
+            for (int i = w; i < ROWS_W / 2; i += kActWaves) {
+                const int m = 2 * i + (lane >> 5), mc = m < n ? m : n - 1;
+                const float* src = p.q.wa + ((size_t)b * n + mc) * kBH + 4 * (lane & 31);
+                __builtin_amdgcn_global_load_lds((glb_vp)src, (lds_vp)(sF + 256 * i), 16, 0, 0);
+            }
+        } else {
+#pragma unroll
+            for (int u = 0; u < PF; u++) {
+                const int x = tid + u * NTH;
+                const int m = x >> 5, k4 = x & 31;
+                pf[u] = (x < ROWS_W * 32 && m < n) ? *reinterpret_cast<const f4*>(p.q.wa + ((size_t)b * n + m) * kBH + 4 * k4)
+                                                   : (f4){0, 0, 0, 0};
+            }
+        }
     };
+    __syncthreads();  // everyone is done with W2 (the staging area overlaps it)
     fetch(0);
     const float inv_n = 1.0f / (float)n;
     for (int b = 0; b < A; b++) {
-        __syncthreads();  // everyone is done with the previous branch's rows (and with W2)
+        __syncthreads();  // branch b's rows have landed; everyone is done with the previous branch's terms
+        if constexpr (GLDS) {
+            for (int x = tid; x < ROWS_W * 32; x += NTH) {
+                const int m = x >> 5, k4 = x & 31;
+                const f4 v4 = m < n ? *reinterpret_cast<const f4*>(sF + m * kBH + 4 * k4) : (f4){0, 0, 0, 0};
+                put_terms(sWa, ROWS_W, m, k4, v4);
+            }
+        } else {
 #pragma unroll
-        for (int u = 0; u < PF; u++) {
-            const int x = tid + u * 64 * kActWaves;
-            if (x < ROWS_W * 32) *reinterpret_cast<f4*>(sWa + (x >> 5) * kBPitch + 4 * (x & 31)) = pf[u];
+            for (int u = 0; u < PF; u++) {
+                const int x = tid + u * NTH;
+                if (x < ROWS_W * 32) put_terms(sWa, ROWS_W, x >> 5, x & 31, pf[u]);
+            }
         }
-        if (tid < ROWS_W) sba[tid] = pfb;
+        if (tid < ROWS_W) sba[tid] = tid < n ? p.q.ba[(size_t)b * n + tid] : 0.f;
         __syncthreads();
         if (b + 1 < A) fetch(b + 1);
-        f4 acc[NMT];
+        f4 acc[NC][NMT];
 #pragma unroll
-        for (int mt = 0; mt < NMT; mt++) acc[mt] = (f4){0, 0, 0, 0};
+        for (int c = 0; c < NC; c++)
 #pragma unroll
-        for (int kt = 0; kt < 8; kt++) {
+            for (int mt = 0; mt < NMT; mt++) acc[c][mt] = (f4){0, 0, 0, 0};
 #pragma unroll
-            for (int mt = 0; mt < NMT; mt++) {
-                const f4 a4 = *reinterpret_cast<const f4*>(sWa + (16 * mt + j) * kBPitch + 16 * kt + 4 * g4);
+        for (int mt = 0; mt < NMT; mt++) {
 #pragma unroll
-                for (int q = 0; q < 4; q++) acc[mt] = mfma4(a4[q], out[kt][q], acc[mt]);
+            for (int s = 0; s < 4; s++) {
+                const uint16_t* ap = sWa + (size_t)(16 * mt + j) * kAPitch + 32 * s + 8 * g4;
+                const u4v a1 = *reinterpret_cast<const u4v*>(ap);
+                const u4v a2 = *reinterpret_cast<const u4v*>(ap + ROWS_W * kAPitch);
+                const u4v a3 = *reinterpret_cast<const u4v*>(ap + 2 * ROWS_W * kAPitch);
+#pragma unroll
+                for (int c = 0; c < NC; c++) acc[c][mt] = mfma_split6(a1, a2, a3, bf[c][s], acc[c][mt]);
             }
         }
-        // q = (value + adv) - mean(adv) over the branch's n actions; the first maximum
-        // (lane (j, g4) holds actions 16 mt + 4 g4 + q of row j, increasing in (mt, q))
-        float adv[NMT][4];
-        float sum = 0.f;
 #pragma unroll
-        for (int mt = 0; mt < NMT; mt++)
+        for (int c = 0; c < NC; c++) {
+            // q = (value + adv) - mean(adv) over the branch's n actions; the first maximum
+            // (lane (j, g4) holds actions 16 mt + 4 g4 + q of row j, increasing in (mt, q))
+            float adv[NMT][4];
+            float sum = 0.f;
 #pragma unroll
-            for (int q = 0; q < 4; q++) {
-                const int m = 16 * mt + 4 * g4 + q;
-                adv[mt][q] = acc[mt][q] + sba[m];
-                if (m < n) sum += adv[mt][q];
-            }
-        const float mean = rows_sum(sum) * inv_n;
-        float best = -INFINITY;
-        int bidx = 0x7fffffff;
+            for (int mt = 0; mt < NMT; mt++)
 #pragma unroll
-        for (int mt = 0; mt < NMT; mt++)
+                for (int q = 0; q < 4; q++) {
+                    const int m = 16 * mt + 4 * g4 + q;
+                    adv[mt][q] = acc[c][mt][q] + sba[m];
+                    if (m < n) sum += adv[mt][q];
+                }
+            const float mean = rows_sum(sum) * inv_n;
+            float best = -INFINITY;
+            int bidx = 0x7fffffff;
 #pragma unroll
-            for (int q = 0; q < 4; q++) {
-                const int m = 16 * mt + 4 * g4 + q;
-                const float qv = (value + adv[mt][q]) - mean;
-                if (m < n && (qv > best || bidx == 0x7fffffff)) {
-                    best = qv;
-                    bidx = m;
+            for (int mt = 0; mt < NMT; mt++)
+#pragma unroll
+                for (int q = 0; q < 4; q++) {
+                    const int m = 16 * mt + 4 * g4 + q;
+                    const float qv = (value[c] + adv[mt][q]) - mean;
+                    if (m < n && (qv > best || bidx == 0x7fffffff)) {
+                        best = qv;
+                        bidx = m;
+                    }
+                }
+            // across the 4 lane groups: the larger q, ties to the smaller index
+#pragma unroll
+            for (int sh = 16; sh <= 32; sh <<= 1) {
+                const float ob = __shfl_xor(best, sh);
+                const int oi = __shfl_xor(bidx, sh);
+                if (ob > best || (ob == best && oi < bidx)) {
+                    best = ob;
+                    bidx = oi;
                 }
             }
-        // across the 4 lane groups: the larger q, ties to the smaller index
-#pragma unroll
-        for (int sh = 16; sh <= 32; sh <<= 1) {
-            const float ob = __shfl_xor(best, sh);
-            const int oi = __shfl_xor(bidx, sh);
-            if (ob > best || (ob == best && oi < bidx)) {
-                best = ob;
-                bidx = oi;
+            if (rv[c] && g4 == (b & 3)) {
+                const int8_t act = explore[c] ? p.rnd[(size_t)row[c] * A + b] : (int8_t)bidx;
+                p.action[(size_t)row[c] * A + b] = act;
             }
-        }
-        if (rv && g4 == (b & 3)) {
-            const int8_t act = explore ? p.rnd[(size_t)row * A + b] : (int8_t)bidx;
-            p.action[(size_t)row * A + b] = act;
         }
     }
 }
 
 size_t bdqn_act_lds(int nmt) {
-    const size_t heads = sizeof(float) * ((size_t)16 * nmt * kBPitch + 16 * nmt);
-    const size_t trunk = sizeof(float) * (size_t)kBH * kBPitch;
+    const size_t rows = (size_t)16 * nmt;
+    size_t heads = sizeof(uint16_t) * 3 * rows * kAPitch + sizeof(float) * rows;
+    if (heads + sizeof(float) * rows * kBH <= 160 * 1024) heads += sizeof(float) * rows * kBH;  // f32 staging (GLDS)
+    const size_t trunk = sizeof(uint16_t) * 3 * (size_t)kBH * kAPitch;
     return heads > trunk ? heads : trunk;
 }
 
@@ -394,7 +529,8 @@ hipError_t launch_bdqn_l1_compact(const BdqnL1Compact& p, hipStream_t st) {
 
 hipError_t launch_bdqn_act(const BdqnAct& p, hipStream_t st) {
     const int nmt = (p.q.n + 15) / 16;
-    const unsigned blocks = (unsigned)((p.rows + 16 * kActWaves - 1) / (16 * kActWaves));
+    const long long rpb = 16 * kActWaves * kActTiles;  // rows per block
+    const unsigned blocks = (unsigned)((p.rows + rpb - 1) / rpb);
     const bool l1 = p.h1 == nullptr;
 #define MS_BDQN_CASE(T)                                                                                  \
     if (nmt <= T) {                                                                                      \

@@ -1031,20 +1031,24 @@ static ms::BdqnNet bdqn_net(const ms_bdqn_params* q) {
     return ms::BdqnNet{q->w1, q->b1, q->w2, q->b2, q->wv, q->bv, q->wa, q->ba, q->obs, q->ac_dim, q->n};
 }
 
-// update_policy workspace (bdqn_update_kernels.hip): layer-1 partials [3][nK][128][128], then the rows'
-// activations / pre-activation gradients [4][128][128], advantage gradients [128][Mn], dv and losses
+// update_policy workspace (bdqn_update_kernels.hip): layer-1 partials [3][nK][128][128]; the rows'
+// activations and pre-activation gradients [6][128][128] (out1, out2 x 3, dpre2, dpre1); head outputs
+// [3][128][Mp]; head gradients [128][Mp]; d out2 partials [Mp/64][128][128]; the rows' losses
 struct BdqnUpdWs {
-    int nK;
-    size_t l1p, rows, dadv, small, total;
+    int nK, Mp;
+    size_t l1p, rows, q3, dq, d2p, small, total;
 };
 static BdqnUpdWs bdqn_upd_ws(const ms_bdqn_params* q) {
     BdqnUpdWs w{};
     w.nK = (q->obs + 127) / 128;
+    w.Mp = (q->ac_dim * q->n + 1 + 63) / 64 * 64;
     w.l1p = align256(sizeof(float) * 3 * (size_t)w.nK * 128 * 128);
-    w.rows = align256(sizeof(float) * 4 * 128 * 128);
-    w.dadv = align256(sizeof(float) * 128 * (size_t)q->ac_dim * q->n);
-    w.small = align256(sizeof(float) * 2 * 128);
-    w.total = w.l1p + w.rows + w.dadv + w.small;
+    w.rows = align256(sizeof(float) * 6 * 128 * 128);
+    w.q3 = align256(sizeof(float) * 3 * 128 * (size_t)w.Mp);
+    w.dq = align256(sizeof(float) * 128 * (size_t)w.Mp);
+    w.d2p = align256(sizeof(float) * (size_t)(w.Mp / 64) * 128 * 128);
+    w.small = align256(sizeof(float) * 128);
+    w.total = w.l1p + w.rows + w.q3 + w.dq + w.d2p + w.small;
     return w;
 }
 
@@ -1067,6 +1071,9 @@ int ms_bdqn_update(const ms_bdqn_params* q, const ms_bdqn_params* target, const 
     if (!g->w1 || !g->b1 || !g->w2 || !g->b2 || !g->wv || !g->bv || !g->wa || !g->ba || !g->loss)
         return fail(MS_EINVAL, "ms_bdqn_update: NULL gradient tensor");
     const BdqnUpdWs w = bdqn_upd_ws(q);
+    if (w.Mp > ms::kUpdMaxHeadRows)
+        return fail(MS_EINVAL, "ms_bdqn_update: ac_dim * n + 1 = %d head rows > %d", q->ac_dim * q->n + 1,
+                    ms::kUpdMaxHeadRows);
     if (ws_bytes < w.total) return fail(MS_EINVAL, "ms_bdqn_update: workspace too small (%zu < %zu)", ws_bytes, w.total);
     ms::BdqnUpd p{};
     p.q = bdqn_net(q);
@@ -1082,16 +1089,22 @@ int ms_bdqn_update(const ms_bdqn_params* q, const ms_bdqn_params* target, const 
     p.gamma = gamma;
     p.clip = grad_clip > 0.f ? grad_clip : 3.0e38f;
     p.nK = w.nK;
+    p.Mp = w.Mp;
     char* base = (char*)ws;
     p.l1p = (float*)base;
     float* rows = (float*)(base + w.l1p);
     p.out1 = rows;
     p.out2 = rows + 128 * 128;
-    p.dpre2 = rows + 2 * 128 * 128;
-    p.dpre1 = rows + 3 * 128 * 128;
-    p.dadv = (float*)(base + w.l1p + w.rows);
-    p.dv = (float*)(base + w.l1p + w.rows + w.dadv);
-    p.lossb = p.dv + 128;
+    p.dpre2 = rows + 4 * 128 * 128;
+    p.dpre1 = rows + 5 * 128 * 128;
+    size_t off = w.l1p + w.rows;
+    p.q3 = (float*)(base + off);
+    off += w.q3;
+    p.dq = (float*)(base + off);
+    off += w.dq;
+    p.d2p = (float*)(base + off);
+    off += w.d2p;
+    p.lossb = (float*)(base + off);
     p.g = ms::BdqnGrads{g->w1, g->b1, g->w2, g->b2, g->wv, g->bv, g->wa, g->ba, g->loss};
     HIP_TRY(ms::launch_bdqn_update(p, (hipStream_t)stream));
     return MS_OK;

@@ -55,12 +55,17 @@ struct BdqnUpd {
     int B;                    // <= 128
     float gamma, clip;
     int nK;                   // layer-1 K chunks of 128 inputs
+    int Mp;                   // head rows (ac_dim * n advantage rows, then the value row) padded to 64
     float* l1p;               // [3][nK][128][128] layer-1 partial sums of the three forwards
-    float *out1, *out2;       // [B][128] ReLU outputs of q(s)
-    float *dpre2, *dpre1;     // [B][128] d loss / d pre-activations of layers 2 and 1
-    float* dadv;              // [B][ac_dim * n]
-    float *dv, *lossb;        // [B]
+    float* out1;              // [128][128] ReLU output of layer 1 of q(s)
+    float* out2;              // [3][128][128] ReLU outputs of layer 2 of q(s), q(s'), target(s')
+    float* q3;                // [3][128][Mp] head outputs (advantages, then the value) of the three forwards
+    float* dq;                // [128][Mp] d loss / d head outputs of q(s) (zero rows past B)
+    float* d2p;               // [Mp / 64][128][128] d out2 partial sums per chunk of 64 head rows
+    float *dpre2, *dpre1;     // [128][128] d loss / d pre-activations of layers 2 and 1
+    float* lossb;             // [128] squared errors of a row (summed over the branches)
     BdqnGrads g;
 };
+constexpr int kUpdMaxHeadRows = 5440;  // Mp * 3 floats of one row's head outputs in 64 KB of LDS
 
 }  // namespace ms

@@ -1,0 +1,8 @@
+# the BDQN update on MFMA tiles: its tests, the cfg5 bench line and frame breakdown
+set -o pipefail
+O=gpurun_out/r4h
+mkdir -p $O
+timeout -k 10 400 python -u -m pytest tests/test_bdqn_gpu.py -m gpu -v --timeout 120 --timeout-method thread -p no:cacheprovider > $O/tests.log 2>&1 || { echo "tests rc=$?" >> $O/tests.log; exit 1; }
+timeout -k 10 300 python bench.py --config cfg5 --no-cpu-baseline > $O/cfg5.json 2> $O/cfg5.err || exit 1
+bash tools/trace_cfg5.sh r4h > $O/trace5.log 2>&1 || exit 1
+echo done > $O/done
