@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define MS_ABI_VERSION 14
+#define MS_ABI_VERSION 15
 
 #define MS_MAX_KINDS 16
 #define MS_MAX_AGENTS 64
@@ -609,6 +609,15 @@ int ms_bdqn_layer1_compact(const ms_bdqn_params* q, const void* workspace, const
  * segs = 1). explore may be NULL (all greedy). action: [n_rows][ac_dim] int8. */
 int ms_bdqn_act(const ms_bdqn_params* q, const float* h1, const int8_t* x, int32_t x_stride, const void* workspace,
                 int64_t n_rows, const uint8_t* explore, const int8_t* rand_action, int8_t* action, void* stream);
+
+/* ms_bdqn_layer1_compact + ms_bdqn_act in two launches without the h1 rows: the P rows of every
+ * (replica, core) go to scratch and the act kernel adds an agent's owned cores' rows to base itself
+ * (the same sum in the same order, so the actions equal those of ms_bdqn_act on
+ * ms_bdqn_layer1_compact's h1). Rows e * n_agents + a; arguments as those two functions'. */
+int ms_bdqn_act_compact(const ms_bdqn_params* q, const void* workspace, const float* base, const int8_t* core_rows,
+                        const int8_t* core_owner, int64_t n_envs, int32_t n_agents, int32_t n_cores, int32_t acc_dim,
+                        int32_t acc_stride, void* scratch, size_t scratch_bytes, const uint8_t* explore,
+                        const int8_t* rand_action, int8_t* action, void* stream);
 
 /* ---- Branching DQN update (BranchingDQN.update_policy, BranchingDQNModules.py:125-164) ----
  * One role's minibatch of `batch` (<= 128) transitions: int8 observation rows of the states and

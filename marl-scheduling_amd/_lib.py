@@ -27,7 +27,7 @@ class MarlSchedError(RuntimeError):
         self.code = code
 
 
-ABI_VERSION = 14  # include/marlsched.h MS_ABI_VERSION
+ABI_VERSION = 15  # include/marlsched.h MS_ABI_VERSION
 
 
 def _load():
@@ -95,6 +95,8 @@ def _load():
         "ms_bdqn_layer1_compact": (ct.c_int, [ct.POINTER(abi.MsBdqnParams), P, P, P, P, i64, i32, i32, i32, i32, P,
                                               ct.c_size_t, P, P]),
         "ms_bdqn_act": (ct.c_int, [ct.POINTER(abi.MsBdqnParams), P, P, i32, P, i64, P, P, P, P]),
+        "ms_bdqn_act_compact": (ct.c_int, [ct.POINTER(abi.MsBdqnParams), P, P, P, P, i64, i32, i32, i32, i32, P,
+                                           ct.c_size_t, P, P, P, P]),
         "ms_bdqn_update_workspace_bytes": (ct.c_size_t, [ct.POINTER(abi.MsBdqnParams), i32]),
         "ms_bdqn_update": (ct.c_int, [ct.POINTER(abi.MsBdqnParams), ct.POINTER(abi.MsBdqnParams),
                                       ct.POINTER(abi.MsBdqnBatch), ct.c_float, ct.c_float, P, ct.c_size_t,
@@ -107,11 +109,12 @@ def _load():
     }
     L.ms_abi_version.restype = ct.c_int
     version = L.ms_abi_version()
-    # ABI 14 added ms_bdqn_update*; a 13 library (an A/B variant built before it) loads without them
-    if version not in (13, ABI_VERSION):
+    # ABI 14 added ms_bdqn_update*, 15 ms_bdqn_act_compact; an older library (an A/B variant built
+    # before them) loads without them
+    if version not in (13, 14, ABI_VERSION):
         raise ImportError("libmarlsched.so ABI version mismatch (%d, want %d)" % (version, ABI_VERSION))
     for name, (res, args) in sig.items():
-        if version < 14 and name.startswith("ms_bdqn_update"):
+        if (version < 14 and name.startswith("ms_bdqn_update")) or (version < 15 and name == "ms_bdqn_act_compact"):
             continue
         fn = getattr(L, name)
         fn.restype = res
@@ -131,7 +134,7 @@ EXPORTED = (
     "ms_ppo_workspace_bytes", "ms_ppo_grad", "ms_adam_step", "ms_adam_step_dev",
     "ms_aggregate_obs", "ms_decode_aggregated", "ms_dqn_act", "ms_dqn_workspace_bytes", "ms_dqn_grad",
     "ms_regen_agent_rows", "ms_bdqn_workspace_bytes", "ms_bdqn_prepare", "ms_bdqn_layer1_scratch_bytes", "ms_bdqn_layer1_compact",
-    "ms_bdqn_act", "ms_bdqn_update_workspace_bytes", "ms_bdqn_update", "ms_wide_act", "ms_wide_workspace_bytes",
+    "ms_bdqn_act", "ms_bdqn_act_compact", "ms_bdqn_update_workspace_bytes", "ms_bdqn_update", "ms_wide_act", "ms_wide_workspace_bytes",
     "ms_wide_grad",
 )
 

@@ -29,13 +29,15 @@ owns core c and the constant foreign row F elsewhere, so
 one [D, 128] product per (replica, core) added to its owner's row: C of them per replica instead
 of N dense [C*D]-wide ones (32x fewer flops at cfg5), on the bf16 MFMA with exact products
 (ms_bdqn_layer1_compact, bdqn_kernels.hip). Acting is one fused HIP kernel per role
-(ms_bdqn_act): trunk, value head, every advantage head, the per-branch q = value + adv - mean and
-its first argmax, and the epsilon-greedy pick, on exact-f32 MFMA products; only the int8 actions
-leave it (the library-GEMM version materialised 3.25 GB of advantages per frame and read them back
-for the argmax). The update (batch 128 per role, drawn without replacement like random.sample) runs
-on ms_bdqn_update (bdqn_update_kernels.hip: the three forwards, the double-DQN target, the MSE
-backward and the clamp in four launches) and the HIP Adam; one frame's updates of all roles are
-captured into one HIP graph and replayed.
+(ms_bdqn_act; the acceptor role ms_bdqn_act_compact, which also adds the owned cores' layer-1 rows
+itself): trunk, value head, every advantage head, the per-branch q = value + adv - mean and its
+first argmax, and the epsilon-greedy pick, on the bf16 MFMA with both operands as three exact bf16
+terms (six products: f32-level sums); only the int8 actions leave it (the library-GEMM version
+materialised 3.25 GB of advantages per frame and read them back for the argmax). The update (batch
+128 per role, drawn without replacement like random.sample) runs on ms_bdqn_update
+(bdqn_update_kernels.hip: the three forwards, the double-DQN target, the MSE backward and the clamp
+in eight tile launches) and the HIP Adam, the roles on parallel streams; one frame's updates of all
+roles are captured into one HIP graph and replayed.
 """
 from __future__ import annotations
 
@@ -117,6 +119,28 @@ class HipActor:
         check(lib.ms_bdqn_layer1_compact(ct.byref(p), ptr(self.ws), ptr(self.base), ptr(core_rows), ptr(core_owner), E,
                                          n_agents, C, self.seg, stride, ptr(self._scratch), self._scratch.numel() * 4,
                                          ptr(out), stream_ptr(stream)))
+        return out
+
+    def act_compact(self, core_rows, core_owner, n_agents: int, explore=None, rand_action=None, out=None, stream=None):
+        """ms_bdqn_act_compact: the acceptor role's actions [E * N, ac_dim] int8 straight from the compact
+        observations (layer 1 summed in the act kernel, no h1 rows); equal to act(h1=layer1_compact(...))."""
+        E, C, stride = core_rows.shape
+        assert self.compact and C == self.segs and core_rows.dtype == torch.int8 and core_owner.dtype == torch.int8
+        assert core_rows.is_contiguous() and core_owner.is_contiguous() and core_owner.shape == (E, C)
+        rows = E * n_agents
+        if explore is not None:
+            assert explore.dtype == torch.uint8 and explore.numel() == rows
+            assert rand_action.dtype == torch.int8 and rand_action.shape == (rows, self.q.ac_dim)
+            assert rand_action.is_contiguous()
+        if out is None:
+            out = torch.empty((rows, self.q.ac_dim), dtype=torch.int8, device=core_rows.device)
+        sb = int(lib.ms_bdqn_layer1_scratch_bytes(E, C))
+        if getattr(self, "_scratch", None) is None or self._scratch.numel() * 4 < sb:
+            self._scratch = torch.empty(((sb + 3) // 4,), dtype=torch.float32, device=core_rows.device)
+        p = self.q.hip_params()
+        check(lib.ms_bdqn_act_compact(ct.byref(p), ptr(self.ws), ptr(self.base), ptr(core_rows), ptr(core_owner), E,
+                                      n_agents, C, self.seg, stride, ptr(self._scratch), self._scratch.numel() * 4,
+                                      ptr(explore), ptr(rand_action), ptr(out), stream_ptr(stream)))
         return out
 
     def act(self, h1=None, x=None, explore=None, rand_action=None, out=None, stream=None):
@@ -301,7 +325,6 @@ class BDQNTrainer:
         # roles' on the aggregated offer rows inside the act kernel
         self.actors = {k: (HipActor(r.q, self.d_acc, C, dev, compact=True) if k == "acc"
                            else HipActor(r.q, self.d_off, 1, dev)) for k, r in self.roles.items()}
-        self._h1 = torch.empty((self.E * N, 128), dtype=torch.float32, device=dev)
         # compact replay ring: states of frames 0..F (slot F + 1 holds the next state of the newest frame)
         Fm = self.b.memory_frames
         self.n_slots = Fm + 1
@@ -351,20 +374,20 @@ class BDQNTrainer:
     @torch.no_grad()
     def _actions(self, slot, eps):
         """get_action (BranchingDQNModules.py:117-123) of every agent, epsilon-greedy per agent (:181-186):
-        one fused HIP act kernel per role (ms_bdqn_act)."""
+        one fused HIP act kernel per role (ms_bdqn_act; the acceptor role ms_bdqn_act_compact)."""
         E, N = self.E, self.N
         for a in self.actors.values():
             a.prepare()  # the weights changed in the last update
-        ea = self.actors["acc"]
-        h1 = ea.layer1_compact(self.core_rows[slot], self.core_owner[slot], N, out=self._h1)
         x_off = self._offer_rows_i8(slot)
         explore = (torch.rand((E * N,), generator=self.gen, device=self.device) <= eps).to(torch.uint8)
         out = {}
         for k, actor in self.actors.items():
             q = actor.q
             rnd = torch.randint(0, q.n, (E * N, q.ac_dim), generator=self.gen, device=self.device).to(torch.int8)
-            a = actor.act(h1=h1, explore=explore, rand_action=rnd) if k == "acc" else \
-                actor.act(x=x_off, explore=explore, rand_action=rnd)
+            if k == "acc":  # layer 1 from the compact frame, summed inside the act kernel
+                a = actor.act_compact(self.core_rows[slot], self.core_owner[slot], N, explore=explore, rand_action=rnd)
+            else:
+                a = actor.act(x=x_off, explore=explore, rand_action=rnd)
             out[k] = a.view(E, N, -1)
         return out
 

@@ -144,17 +144,24 @@ __global__ void __launch_bounds__(256) k_bdqn_l1_cores(BdqnL1Compact p) {
 #pragma unroll
         for (int t = 0; t < 3; t++) aw[s][t] = *reinterpret_cast<const u4v*>(wp0 + t * tsz + 32 * s);
     const long long t0 = ch * kL1TilesPerWave, t1 = min(t0 + kL1TilesPerWave, rtiles);
-    for (long long rt = t0; rt < t1; rt++) {
+    // register prefetch: the next replica tile's row dwords are loaded before this tile's MFMAs
+    auto load_tile = [&](long long rt, uint32_t (&xw)[S][2]) {
         const long long e = rt * 16 + i;
-        const bool ev = e < p.E;
-        const uint32_t* row = reinterpret_cast<const uint32_t*>(p.core_rows + ((size_t)(ev ? e : 0) * C + c) * p.stride);
-        uint32_t xw[S][2];
+        const uint32_t* row = reinterpret_cast<const uint32_t*>(p.core_rows + ((size_t)(e < p.E ? e : 0) * C + c) * p.stride);
 #pragma unroll
         for (int s = 0; s < S; s++) {
             const int d0 = 8 * s + 2 * g4;
             xw[s][0] = d0 < stride4 ? row[d0] : 0u;
             xw[s][1] = d0 + 1 < stride4 ? row[d0 + 1] : 0u;
         }
+    };
+    uint32_t cur[S][2];
+    load_tile(t0, cur);
+    for (long long rt = t0; rt < t1; rt++) {
+        const long long e = rt * 16 + i;
+        const bool ev = e < p.E;
+        uint32_t nxt[S][2];
+        if (rt + 1 < t1) load_tile(rt + 1, nxt);
         f4 acc = {0, 0, 0, 0};
 #pragma unroll
         for (int s = 0; s < S; s++) {
@@ -162,7 +169,7 @@ __global__ void __launch_bounds__(256) k_bdqn_l1_cores(BdqnL1Compact p) {
             u4v xb;
 #pragma unroll
             for (int t = 0; t < 4; t++) {
-                const uint32_t dw = xw[s][t >> 1];
+                const uint32_t dw = cur[s][t >> 1];
                 const int sh = 16 * (t & 1);
                 const int ka = k0 + 2 * t, kb = ka + 1;
                 const int va = ka < D ? (int)(int8_t)(dw >> sh) - foreign(ka, D) : 0;
@@ -175,6 +182,10 @@ __global__ void __launch_bounds__(256) k_bdqn_l1_cores(BdqnL1Compact p) {
         }
         // lane (replica i, g4) holds P_c[hidden 16 ht + 4 g4 + q] of replica e
         if (ev) *reinterpret_cast<f4*>(p.P + ((size_t)e * C + c) * kBH + 16 * ht + 4 * g4) = acc;
+        if (rt + 1 < t1) {
+#pragma unroll
+            for (int s = 0; s < S; s++) cur[s][0] = nxt[s][0], cur[s][1] = nxt[s][1];
+        }
     }
 }
 
@@ -282,12 +293,40 @@ __global__ void __launch_bounds__(64 * kActWaves) k_bdqn_act(BdqnAct p) {
         // layer-1 pre-activations in the trunk's B layout: h[kt][q] = h1[row j of tile c][16 kt + 4 g4 + q]
         float h[8][4];
         if constexpr (!L1) {
+            f4 hv[8];
+            if (p.P) {
+                // compact acceptor rows: base + the owned cores' P rows in core order (= k_bdqn_l1_gather)
+                const long long e = rc[c] / p.N;
+                const int a1 = (int)(rc[c] - e * p.N) + 1;
 #pragma unroll
-            for (int kt = 0; kt < 8; kt++) {
-                const f4 v = *reinterpret_cast<const f4*>(p.h1 + (size_t)rc[c] * kBH + 16 * kt + 4 * g4);
+                for (int kt = 0; kt < 8; kt++) hv[kt] = *reinterpret_cast<const f4*>(p.base + 16 * kt + 4 * g4);
+                const int8_t* own = p.core_owner + (size_t)e * p.C;
+                const float* prow = p.P + (size_t)e * p.C * kBH + 4 * g4;
+                for (int c4 = 0; c4 < p.C; c4 += 4) {
+                    uint32_t ow;
+                    if ((p.C & 3) == 0) {
+                        ow = *reinterpret_cast<const uint32_t*>(own + c4);
+                    } else {
+                        ow = 0;
+                        for (int u = 0; u < 4 && c4 + u < p.C; u++) ow |= (uint32_t)(uint8_t)own[c4 + u] << (8 * u);
+                    }
 #pragma unroll
-                for (int q = 0; q < 4; q++) h[kt][q] = v[q];
+                    for (int u = 0; u < 4; u++) {
+                        if ((int)(int8_t)(ow >> (8 * u)) == a1 && c4 + u < p.C) {
+                            const float* pr = prow + (size_t)(c4 + u) * kBH;
+#pragma unroll
+                            for (int kt = 0; kt < 8; kt++) hv[kt] += *reinterpret_cast<const f4*>(pr + 16 * kt);
+                        }
+                    }
+                }
+            } else {
+#pragma unroll
+                for (int kt = 0; kt < 8; kt++) hv[kt] = *reinterpret_cast<const f4*>(p.h1 + (size_t)rc[c] * kBH + 16 * kt + 4 * g4);
             }
+#pragma unroll
+            for (int kt = 0; kt < 8; kt++)
+#pragma unroll
+                for (int q = 0; q < 4; q++) h[kt][q] = hv[kt][q];
         } else {
             // W1 x on the bf16 MFMA: int8 inputs exact, W1 three exact bf16 terms; D layout = B layout
             const int S = p.Kp / 32;
@@ -521,7 +560,7 @@ hipError_t launch_bdqn_l1_compact(const BdqnL1Compact& p, hipStream_t st) {
         default: return hipErrorInvalidValue;
     }
     hipError_t e = hipGetLastError();
-    if (e != hipSuccess) return e;
+    if (e != hipSuccess || !p.h1) return e;  // (h1 NULL: the act kernel sums the P rows itself)
     const long long thr = p.E * p.N * 32;
     hipLaunchKernelGGL(k_bdqn_l1_gather, dim3((unsigned)((thr + 255) / 256)), dim3(256), 0, st, p);
     return hipGetLastError();
@@ -531,7 +570,7 @@ hipError_t launch_bdqn_act(const BdqnAct& p, hipStream_t st) {
     const int nmt = (p.q.n + 15) / 16;
     const long long rpb = 16 * kActWaves * kActTiles;  // rows per block
     const unsigned blocks = (unsigned)((p.rows + rpb - 1) / rpb);
-    const bool l1 = p.h1 == nullptr;
+    const bool l1 = p.h1 == nullptr && p.P == nullptr;
 #define MS_BDQN_CASE(T)                                                                                  \
     if (nmt <= T) {                                                                                      \
         const size_t lds = bdqn_act_lds(T);                                                              \

@@ -1156,6 +1156,48 @@ int ms_bdqn_layer1_compact(const ms_bdqn_params* q, const void* workspace, const
     return MS_OK;
 }
 
+int ms_bdqn_act_compact(const ms_bdqn_params* q, const void* workspace, const float* base, const int8_t* core_rows,
+                        const int8_t* core_owner, int64_t n_envs, int32_t n_agents, int32_t n_cores, int32_t acc_dim,
+                        int32_t acc_stride, void* scratch, size_t scratch_bytes, const uint8_t* explore,
+                        const int8_t* rand_action, int8_t* action, void* stream) {
+    if (int rc = bdqn_check(q, "ms_bdqn_act_compact")) return rc;
+    if (!workspace || !base || !core_rows || !core_owner || !scratch || !action)
+        return fail(MS_EINVAL, "ms_bdqn_act_compact: NULL argument");
+    if (explore && !rand_action) return fail(MS_EINVAL, "ms_bdqn_act_compact: explore needs rand_action");
+    if (n_envs < 1 || n_agents < 1 || n_agents > 127 || n_cores < 1 || acc_dim < 4 || acc_dim > 256 ||
+        acc_stride < acc_dim || (acc_stride & 3) || (int64_t)acc_dim * n_cores != q->obs)
+        return fail(MS_EINVAL, "ms_bdqn_act_compact: bad shape (obs must be n_cores * acc_dim)");
+    if (scratch_bytes < ms_bdqn_layer1_scratch_bytes(n_envs, n_cores))
+        return fail(MS_EINVAL, "ms_bdqn_act_compact: scratch too small");
+    ms::BdqnL1Compact l{};
+    l.w1s = (const uint16_t*)workspace;
+    l.base = base;
+    l.core_rows = core_rows;
+    l.core_owner = core_owner;
+    l.E = n_envs;
+    l.N = n_agents;
+    l.C = n_cores;
+    l.D = acc_dim;
+    l.Dp = bdqn_pad(acc_dim);
+    l.stride = acc_stride;
+    l.P = (float*)scratch;
+    l.h1 = nullptr;  // the act kernel sums the P rows
+    HIP_TRY(ms::launch_bdqn_l1_compact(l, (hipStream_t)stream));
+    ms::BdqnAct p{};
+    p.q = bdqn_net(q);
+    p.rows = n_envs * n_agents;
+    p.explore = explore;
+    p.rnd = rand_action;
+    p.action = action;
+    p.P = l.P;
+    p.base = base;
+    p.core_owner = core_owner;
+    p.N = n_agents;
+    p.C = n_cores;
+    HIP_TRY(ms::launch_bdqn_act(p, (hipStream_t)stream));
+    return MS_OK;
+}
+
 int ms_bdqn_act(const ms_bdqn_params* q, const float* h1, const int8_t* x, int32_t x_stride, const void* workspace,
                 int64_t n_rows, const uint8_t* explore, const int8_t* rand_action, int8_t* action, void* stream) {
     if (int rc = bdqn_check(q, "ms_bdqn_act")) return rc;

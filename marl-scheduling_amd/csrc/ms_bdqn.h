@@ -36,6 +36,12 @@ struct BdqnAct {
     const uint8_t* explore;  // [rows] nonzero: take rnd (or NULL)
     const int8_t* rnd;       // [rows][ac_dim]
     int8_t* action;          // [rows][ac_dim]
+    // compact acceptor rows (P != NULL, h1 == NULL): layer 1 of agent row r = e * N + a is
+    // base + the P rows of the cores agent a owns, in core order (k_bdqn_l1_gather's sum, in the kernel)
+    const float* P;            // [E][C][128] W1_c (R_c - F)
+    const float* base;         // [128]
+    const int8_t* core_owner;  // [E][C]
+    int N, C;
 };
 
 // update_policy of one role (bdqn_update_kernels.hip)

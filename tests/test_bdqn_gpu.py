@@ -187,6 +187,29 @@ def test_act_kernel_is_the_argmax_of_q(ms, role):
     assert torch.equal(got.cpu()[~ex], greedy.cpu()[~ex])
 
 
+def test_act_compact_equals_layer1_then_act(ms):
+    """ms_bdqn_act_compact (the owned cores' P rows summed inside the act kernel) == ms_bdqn_layer1_compact
+    followed by ms_bdqn_act on its h1, bit for bit, greedy and epsilon-greedy."""
+    bdqn = _bdqn()
+    E = 80
+    env, comp, s = _cfg5_compact(ms, E, steps=9, seed=5)
+    N, C, D = s["N"], s["C"], s["acc_obs_dim"]
+    torch.manual_seed(13)
+    net = bdqn.BranchingQ(C * D, C, s["O"] + 1).cuda()
+    actor = bdqn.HipActor(net, D, C, "cuda", compact=True)
+    actor.prepare()
+    rows = E * N
+    g = torch.Generator(device="cuda").manual_seed(9)
+    explore = (torch.rand((rows,), generator=g, device="cuda") < 0.3).to(torch.uint8)
+    rnd = torch.randint(0, net.n, (rows, C), generator=g, device="cuda").to(torch.int8)
+    h1 = actor.layer1_compact(comp["core_rows"], comp["core_owner"], N)
+    for ex, rn in ((None, None), (explore, rnd)):
+        want = actor.act(h1=h1, explore=ex, rand_action=rn)
+        got = actor.act_compact(comp["core_rows"], comp["core_owner"], N, explore=ex, rand_action=rn)
+        assert torch.equal(got, want)
+    assert (comp["core_owner"] > 0).sum().item() > 0
+
+
 def test_update_matches_reference(ms):
     bdqn = _bdqn()
     torch.manual_seed(3)
