@@ -580,11 +580,12 @@ typedef struct ms_bdqn_params {
 } ms_bdqn_params;
 
 /* Bytes of the prepared layer 1 (three exact bf16 terms of W1 over `segs` input segments of `seg`
- * values, each padded to a multiple of 32). */
+ * values, each padded to a multiple of 32; then the segments' products W1_c F, segs x 128 floats). */
 size_t ms_bdqn_workspace_bytes(int32_t seg, int32_t segs);
 
 /* Prepares W1 for ms_bdqn_layer1_compact / ms_bdqn_act (once per weight change; seg * segs must be
- * obs). With base != NULL also writes base[128] = b1 + sum_c W1_c F, F the foreign acceptor row of
+ * obs). With base != NULL also writes W1_c F of every segment c into the workspace and
+ * base[128] = b1 + sum_c W1_c F (in segment order), F the foreign acceptor row of
  * seg = D_acc values [0, -1, -1, (-2, -2) * O] (Agent.py:167-212). */
 int ms_bdqn_prepare(const ms_bdqn_params* q, int32_t seg, int32_t segs, void* workspace, size_t workspace_bytes,
                     float* base, void* stream);

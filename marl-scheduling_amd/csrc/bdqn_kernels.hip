@@ -95,25 +95,33 @@ __global__ void __launch_bounds__(256) k_bdqn_w1split(const float* __restrict__ 
     }
 }
 
-// ---- base[h] = b1[h] + sum_c sum_k W1[h][c*D + k] F[k]: block h, a fixed-order tree over its 256 threads
-__global__ void __launch_bounds__(256) k_bdqn_l1_base(const float* __restrict__ w1, const float* __restrict__ b1, int D,
-                                                      int C, float* __restrict__ base) {
+// ---- cF[c][h] = sum_k W1[h][c*D + k] F[k] (block (h, c), a fixed-order tree over its 256 threads), then
+//      base[h] = b1[h] + sum_c cF[c][h] in core order
+__global__ void __launch_bounds__(256) k_bdqn_l1_cf(const float* __restrict__ w1, int D, int C, float* __restrict__ cF) {
     __shared__ float red[256];
-    const int h = blockIdx.x, t = threadIdx.x;
-    const int K = C * D;
+    const int h = blockIdx.x, c = blockIdx.y, t = threadIdx.x;
     float s = 0.f;
-    for (int i = t; i < K; i += 256) s = fmaf(w1[(size_t)h * K + i], (float)foreign(i % D, D), s);
+    for (int k = t; k < D; k += 256) s = fmaf(w1[(size_t)h * C * D + (size_t)c * D + k], (float)foreign(k, D), s);
     red[t] = s;
     __syncthreads();
     for (int d = 128; d > 0; d >>= 1) {
         if (t < d) red[t] += red[t + d];
         __syncthreads();
     }
-    if (t == 0) base[h] = b1[h] + red[0];
+    if (t == 0) cF[(size_t)c * kBH + h] = red[0];
+}
+__global__ void __launch_bounds__(128) k_bdqn_l1_base(const float* __restrict__ cF, const float* __restrict__ b1, int C,
+                                                      float* __restrict__ base) {
+    const int h = threadIdx.x;
+    float s = 0.f;
+    for (int c = 0; c < C; c++) s += cF[(size_t)c * kBH + h];
+    base[h] = b1[h] + s;
 }
 
 // ---- layer 1 from compact observations, two passes.
-//      k_bdqn_l1_cores: P[e][c] = W1_c (R_ec - F) for every (replica, core). A wave owns one (core,
+//      k_bdqn_l1_cores: P[e][c] = W1_c R_ec - W1_c F for every (replica, core): the accumulator starts
+//      at -cF[c] (ms_bdqn_prepare) and the int8 row bytes go to the bf16 B operand as they are (exact;
+//      the split W1 is zero past D, so the row's padding bytes add nothing). A wave owns one (core,
 //      16 hidden) tile and holds its A fragments (three bf16 terms of every k-step) in registers
 //      while it walks replica tiles of 16: only the int8 rows stream in and P streams out.
 //      k_bdqn_l1_gather: h1[e*N + a] = base + the P rows of the cores agent a owns, in core order (an
@@ -155,6 +163,7 @@ __global__ void __launch_bounds__(256) k_bdqn_l1_cores(BdqnL1Compact p) {
             xw[s][1] = d0 + 1 < stride4 ? row[d0 + 1] : 0u;
         }
     };
+    const f4 ncf = -*reinterpret_cast<const f4*>(p.cF + (size_t)c * kBH + 16 * ht + 4 * g4);
     uint32_t cur[S][2];
     load_tile(t0, cur);
     for (long long rt = t0; rt < t1; rt++) {
@@ -162,20 +171,14 @@ __global__ void __launch_bounds__(256) k_bdqn_l1_cores(BdqnL1Compact p) {
         const bool ev = e < p.E;
         uint32_t nxt[S][2];
         if (rt + 1 < t1) load_tile(rt + 1, nxt);
-        f4 acc = {0, 0, 0, 0};
+        f4 acc = ncf;
 #pragma unroll
         for (int s = 0; s < S; s++) {
-            const int k0 = 32 * s + 8 * g4;
             u4v xb;
-#pragma unroll
-            for (int t = 0; t < 4; t++) {
-                const uint32_t dw = cur[s][t >> 1];
-                const int sh = 16 * (t & 1);
-                const int ka = k0 + 2 * t, kb = ka + 1;
-                const int va = ka < D ? (int)(int8_t)(dw >> sh) - foreign(ka, D) : 0;
-                const int vb = kb < D ? (int)(int8_t)(dw >> (sh + 8)) - foreign(kb, D) : 0;
-                xb[t] = pack_i(va, vb);
-            }
+            xb[0] = pack_i((int8_t)cur[s][0], (int8_t)(cur[s][0] >> 8));
+            xb[1] = pack_i((int8_t)(cur[s][0] >> 16), (int8_t)(cur[s][0] >> 24));
+            xb[2] = pack_i((int8_t)cur[s][1], (int8_t)(cur[s][1] >> 8));
+            xb[3] = pack_i((int8_t)(cur[s][1] >> 16), (int8_t)(cur[s][1] >> 24));
             acc = mfma_bf16(aw[s][0], xb, acc);
             acc = mfma_bf16(aw[s][1], xb, acc);
             acc = mfma_bf16(aw[s][2], xb, acc);
@@ -540,8 +543,11 @@ hipError_t launch_bdqn_w1split(const float* w1, int seg, int segs, int Dp, uint1
     return hipGetLastError();
 }
 
-hipError_t launch_bdqn_l1_base(const float* w1, const float* b1, int D, int C, float* base, hipStream_t st) {
-    hipLaunchKernelGGL(k_bdqn_l1_base, dim3(kBH), dim3(256), 0, st, w1, b1, D, C, base);
+hipError_t launch_bdqn_l1_base(const float* w1, const float* b1, int D, int C, float* cF, float* base, hipStream_t st) {
+    hipLaunchKernelGGL(k_bdqn_l1_cf, dim3(kBH, C), dim3(256), 0, st, w1, D, C, cF);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_bdqn_l1_base, dim3(1), dim3(kBH), 0, st, cF, b1, C, base);
     return hipGetLastError();
 }
 

@@ -55,7 +55,7 @@ hipError_t launch_dqn_act(const DqnActArgs&, hipStream_t);
 hipError_t launch_regen_agent_rows(const RegenArgs&, hipStream_t);
 hipError_t launch_dqn_grad(const DqnGradArgs&, const DqnReduceArgs&, hipStream_t);
 hipError_t launch_bdqn_w1split(const float*, int, int, int, uint16_t*, hipStream_t);
-hipError_t launch_bdqn_l1_base(const float*, const float*, int, int, float*, hipStream_t);
+hipError_t launch_bdqn_l1_base(const float*, const float*, int, int, float*, float*, hipStream_t);
 hipError_t launch_bdqn_l1_compact(const BdqnL1Compact&, hipStream_t);
 hipError_t launch_bdqn_act(const BdqnAct&, hipStream_t);
 hipError_t launch_wide_act(const WideAct&, hipStream_t);
@@ -1014,9 +1014,13 @@ int ms_regen_agent_rows(const ms_config* cfg, const int8_t* core_rows, const int
 // ---- Branching DQN acting (bdqn_kernels.hip)
 static int bdqn_pad(int seg) { return (seg + 31) & ~31; }
 
+// prepared layer 1: the split W1 [3][128][segs][Dp] bf16, then cF [segs][128] f32 (W1_c F, compact acting)
+static size_t bdqn_split_bytes(int32_t seg, int32_t segs) {
+    return (size_t)3 * ms::kBH * segs * bdqn_pad(seg) * sizeof(uint16_t);
+}
 size_t ms_bdqn_workspace_bytes(int32_t seg, int32_t segs) {
     if (seg < 1 || segs < 1) return 0;
-    return (size_t)3 * ms::kBH * segs * bdqn_pad(seg) * sizeof(uint16_t);
+    return bdqn_split_bytes(seg, segs) + (size_t)segs * ms::kBH * sizeof(float);
 }
 
 static int bdqn_check(const ms_bdqn_params* q, const char* who) {
@@ -1118,7 +1122,9 @@ int ms_bdqn_prepare(const ms_bdqn_params* q, int32_t seg, int32_t segs, void* wo
     if (!workspace || workspace_bytes < ms_bdqn_workspace_bytes(seg, segs))
         return fail(MS_EINVAL, "ms_bdqn_prepare: workspace too small");
     HIP_TRY(ms::launch_bdqn_w1split(q->w1, seg, segs, bdqn_pad(seg), (uint16_t*)workspace, (hipStream_t)stream));
-    if (base) HIP_TRY(ms::launch_bdqn_l1_base(q->w1, q->b1, seg, segs, base, (hipStream_t)stream));
+    if (base)
+        HIP_TRY(ms::launch_bdqn_l1_base(q->w1, q->b1, seg, segs, (float*)((char*)workspace + bdqn_split_bytes(seg, segs)),
+                                        base, (hipStream_t)stream));
     return MS_OK;
 }
 
@@ -1142,6 +1148,7 @@ int ms_bdqn_layer1_compact(const ms_bdqn_params* q, const void* workspace, const
     ms::BdqnL1Compact p{};
     p.w1s = (const uint16_t*)workspace;
     p.base = base;
+    p.cF = (const float*)((const char*)workspace + bdqn_split_bytes(acc_dim, n_cores));
     p.core_rows = core_rows;
     p.core_owner = core_owner;
     p.E = n_envs;
@@ -1172,6 +1179,7 @@ int ms_bdqn_act_compact(const ms_bdqn_params* q, const void* workspace, const fl
     ms::BdqnL1Compact l{};
     l.w1s = (const uint16_t*)workspace;
     l.base = base;
+    l.cF = (const float*)((const char*)workspace + bdqn_split_bytes(acc_dim, n_cores));
     l.core_rows = core_rows;
     l.core_owner = core_owner;
     l.E = n_envs;

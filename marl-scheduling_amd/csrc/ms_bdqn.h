@@ -18,6 +18,7 @@ struct BdqnNet {  // one BranchingQNetwork, heads stacked (head b = rows b*n .. 
 struct BdqnL1Compact {
     const uint16_t* w1s;       // [3][128][C][Dp] bf16 bit patterns: W1 = hi + mid + lo exactly, zero for k >= D
     const float* base;         // [128]: b1 + sum_c W1_c F
+    const float* cF;           // [C][128]: W1_c F
     const int8_t* core_rows;   // [E][C][stride]
     const int8_t* core_owner;  // [E][C]
     long long E;
