@@ -384,10 +384,12 @@ class BDQNTrainer:
         for k, actor in self.actors.items():
             q = actor.q
             rnd = torch.randint(0, q.n, (E * N, q.ac_dim), generator=self.gen, device=self.device).to(torch.int8)
+            dst = self.act[k][slot].view(E * N, q.ac_dim)  # written in place: the ring slot of this frame
             if k == "acc":  # layer 1 from the compact frame, summed inside the act kernel
-                a = actor.act_compact(self.core_rows[slot], self.core_owner[slot], N, explore=explore, rand_action=rnd)
+                a = actor.act_compact(self.core_rows[slot], self.core_owner[slot], N, explore=explore, rand_action=rnd,
+                                      out=dst)
             else:
-                a = actor.act(x=x_off, explore=explore, rand_action=rnd)
+                a = actor.act(x=x_off, explore=explore, rand_action=rnd, out=dst)
             out[k] = a.view(E, N, -1)
         return out
 
@@ -428,8 +430,6 @@ class BDQNTrainer:
         ev[0].record()
         acts = self._actions(cur, eps)
         ev[1].record()
-        for k, a in acts.items():
-            self.act[k][cur].copy_(a)
         obs = self._observe_into(nxt)
         price = acts["price"].contiguous() if self.free else None
         rew = dict(self.rbuf)
@@ -468,20 +468,16 @@ class BDQNTrainer:
         [4][B] int64 (ring record, next record, agent, ring slot), 0 = the newest stored frame."""
         import random
 
+        import numpy as np
+
         E, N, B = self.E, self.N, self.b.batch_size
         if getattr(self, "_py_rng", None) is None:
             self._py_rng = random.Random(self.seed + 29)
-        js = self._py_rng.sample(range(self.stored * E * N), B)
-        out = [[0] * B for _ in range(4)]
-        for i, j in enumerate(js):
-            age, rest = divmod(j, E * N)
-            e, a = divmod(rest, N)
-            slot = (self.head - 1 - age) % self.n_slots
-            out[0][i] = slot * E + e
-            out[1][i] = ((slot + 1) % self.n_slots) * E + e
-            out[2][i] = a
-            out[3][i] = slot
-        return out
+        js = np.array(self._py_rng.sample(range(self.stored * E * N), B), dtype=np.int64)
+        age, rest = np.divmod(js, E * N)
+        e, a = np.divmod(rest, N)
+        slot = (self.head - 1 - age) % self.n_slots
+        return np.stack([slot * E + e, ((slot + 1) % self.n_slots) * E + e, a, slot])
 
     def _learn(self):
         if self.b.hip_updates:
@@ -554,7 +550,7 @@ class BDQNTrainer:
         self._sel_flip ^= 1
         self._sel_events[i].synchronize()
         self._sel_host = self._sel_hosts[i]
-        self._sel_host.copy_(torch.tensor(self._sample_host(), dtype=torch.int64))
+        self._sel_host.copy_(torch.from_numpy(self._sample_host()))
         self._sel.copy_(self._sel_host, non_blocking=True)
         self._sel_events[i].record()
         if not self.b.graph_updates:
