@@ -611,10 +611,12 @@ int ms_bdqn_layer1_compact(const ms_bdqn_params* q, const void* workspace, const
 int ms_bdqn_act(const ms_bdqn_params* q, const float* h1, const int8_t* x, int32_t x_stride, const void* workspace,
                 int64_t n_rows, const uint8_t* explore, const int8_t* rand_action, int8_t* action, void* stream);
 
-/* ms_bdqn_layer1_compact + ms_bdqn_act in two launches without the h1 rows: the P rows of every
- * (replica, core) go to scratch and the act kernel adds an agent's owned cores' rows to base itself
- * (the same sum in the same order, so the actions equal those of ms_bdqn_act on
- * ms_bdqn_layer1_compact's h1). Rows e * n_agents + a; arguments as those two functions'. */
+/* ms_bdqn_layer1_compact + ms_bdqn_act without the h1 rows: the P rows of every (replica, core) go to
+ * scratch and the act kernel adds an agent's owned cores' rows to base itself (the same sum in the
+ * same order, so the actions equal those of ms_bdqn_act on ms_bdqn_layer1_compact's h1). Only the
+ * rows of agents that own a core run through the heads; an agent owning none has layer 1 = base, and
+ * all of those take the greedy actions of that one common row (or their random ones where explored).
+ * Rows e * n_agents + a, n_agents <= 64; arguments as those two functions'. */
 int ms_bdqn_act_compact(const ms_bdqn_params* q, const void* workspace, const float* base, const int8_t* core_rows,
                         const int8_t* core_owner, int64_t n_envs, int32_t n_agents, int32_t n_cores, int32_t acc_dim,
                         int32_t acc_stride, void* scratch, size_t scratch_bytes, const uint8_t* explore,

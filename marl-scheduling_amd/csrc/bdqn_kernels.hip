@@ -164,30 +164,51 @@ __global__ void __launch_bounds__(256) k_bdqn_l1_cores(BdqnL1Compact p) {
         }
     };
     const f4 ncf = -*reinterpret_cast<const f4*>(p.cF + (size_t)c * kBH + 16 * ht + 4 * g4);
-    uint32_t cur[S][2];
-    load_tile(t0, cur);
-    for (long long rt = t0; rt < t1; rt++) {
-        const long long e = rt * 16 + i;
-        const bool ev = e < p.E;
-        uint32_t nxt[S][2];
-        if (rt + 1 < t1) load_tile(rt + 1, nxt);
-        f4 acc = ncf;
+    // two replica tiles per step, one accumulator per (tile, W1 term): six independent MFMA chains, and the
+    // next pair's rows in flight during this pair's MFMAs
+    uint32_t cur[2][S][2];
+    load_tile(t0, cur[0]);
+    load_tile(t0 + 1 < t1 ? t0 + 1 : t0, cur[1]);
+    for (long long rt = t0; rt < t1; rt += 2) {
+        uint32_t nxt[2][S][2];
+        if (rt + 2 < t1) {
+            load_tile(rt + 2, nxt[0]);
+            load_tile(rt + 3 < t1 ? rt + 3 : rt + 2, nxt[1]);
+        }
+        f4 acc[2][3];
+#pragma unroll
+        for (int u = 0; u < 2; u++) {
+            acc[u][0] = ncf;
+            acc[u][1] = acc[u][2] = (f4){0, 0, 0, 0};
+        }
 #pragma unroll
         for (int s = 0; s < S; s++) {
-            u4v xb;
-            xb[0] = pack_i((int8_t)cur[s][0], (int8_t)(cur[s][0] >> 8));
-            xb[1] = pack_i((int8_t)(cur[s][0] >> 16), (int8_t)(cur[s][0] >> 24));
-            xb[2] = pack_i((int8_t)cur[s][1], (int8_t)(cur[s][1] >> 8));
-            xb[3] = pack_i((int8_t)(cur[s][1] >> 16), (int8_t)(cur[s][1] >> 24));
-            acc = mfma_bf16(aw[s][0], xb, acc);
-            acc = mfma_bf16(aw[s][1], xb, acc);
-            acc = mfma_bf16(aw[s][2], xb, acc);
+            u4v xb[2];
+#pragma unroll
+            for (int u = 0; u < 2; u++) {
+                xb[u][0] = pack_i((int8_t)cur[u][s][0], (int8_t)(cur[u][s][0] >> 8));
+                xb[u][1] = pack_i((int8_t)(cur[u][s][0] >> 16), (int8_t)(cur[u][s][0] >> 24));
+                xb[u][2] = pack_i((int8_t)cur[u][s][1], (int8_t)(cur[u][s][1] >> 8));
+                xb[u][3] = pack_i((int8_t)(cur[u][s][1] >> 16), (int8_t)(cur[u][s][1] >> 24));
+            }
+#pragma unroll
+            for (int t = 0; t < 3; t++)
+#pragma unroll
+                for (int u = 0; u < 2; u++) acc[u][t] = mfma_bf16(aw[s][t], xb[u], acc[u][t]);
         }
         // lane (replica i, g4) holds P_c[hidden 16 ht + 4 g4 + q] of replica e
-        if (ev) *reinterpret_cast<f4*>(p.P + ((size_t)e * C + c) * kBH + 16 * ht + 4 * g4) = acc;
-        if (rt + 1 < t1) {
 #pragma unroll
-            for (int s = 0; s < S; s++) cur[s][0] = nxt[s][0], cur[s][1] = nxt[s][1];
+        for (int u = 0; u < 2; u++) {
+            const long long e = (rt + u) * 16 + i;
+            if (rt + u < t1 && e < p.E)
+                *reinterpret_cast<f4*>(p.P + ((size_t)e * C + c) * kBH + 16 * ht + 4 * g4) =
+                    (acc[u][0] + acc[u][1]) + acc[u][2];
+        }
+        if (rt + 2 < t1) {
+#pragma unroll
+            for (int u = 0; u < 2; u++)
+#pragma unroll
+                for (int s2 = 0; s2 < S; s2++) cur[u][s2][0] = nxt[u][s2][0], cur[u][s2][1] = nxt[u][s2][1];
         }
     }
 }
@@ -206,6 +227,79 @@ __global__ void __launch_bounds__(256) k_bdqn_l1_gather(BdqnL1Compact p) {
     for (int c = 0; c < p.C; c++)
         if (own[c] == a1) v += *reinterpret_cast<const f4*>(p.P + ((size_t)e * p.C + c) * kBH + 4 * h4);
     *reinterpret_cast<f4*>(p.h1 + (size_t)r * kBH + 4 * h4) = v;
+}
+
+// ---- the rows of agents that own a core (the others' acceptor row is the common row F everywhere, so
+//      their layer 1 is base and their greedy actions are the common row's). k_bdqn_own_mask: per replica
+//      the bitmask of agents owning a core (N <= 64); k_bdqn_own_list: one atomic per wave (ballot +
+//      prefix count) appends the owning rows; the list order varies from run to run, each row's result
+//      does not. Entry 0 is the common row itself (-1).
+__global__ void __launch_bounds__(256) k_bdqn_own_mask(BdqnAct p, unsigned long long* mask) {
+    const long long e = (long long)blockIdx.x * 256 + threadIdx.x;
+    if (e >= p.rows / p.N) return;
+    const int8_t* own = p.core_owner + (size_t)e * p.C;
+    unsigned long long m = 0;
+    if ((p.C & 15) == 0) {
+        for (int c = 0; c < p.C; c += 16) {
+            const uint4 v = *reinterpret_cast<const uint4*>(own + c);
+            const uint32_t d[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+            for (int k = 0; k < 16; k++) {
+                const int o = (int)(int8_t)(d[k >> 2] >> (8 * (k & 3)));
+                if (o > 0) m |= 1ull << (o - 1);
+            }
+        }
+    } else {
+        for (int c = 0; c < p.C; c++) {
+            const int o = own[c];
+            if (o > 0) m |= 1ull << (o - 1);
+        }
+    }
+    mask[e] = m;
+}
+constexpr int kOwnListThreads = 1024;  // rows per block of k_bdqn_own_list: one atomic per block
+__global__ void __launch_bounds__(kOwnListThreads) k_bdqn_own_list(BdqnAct p, const unsigned long long* mask,
+                                                                   int32_t* list, int32_t* count) {
+    __shared__ int wcount[kOwnListThreads / 64];
+    __shared__ int bbase;
+    const long long r = (long long)blockIdx.x * kOwnListThreads + threadIdx.x;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    bool owns = false;
+    if (r < p.rows) {
+        const long long e = r / p.N;
+        owns = (mask[e] >> (int)(r - e * p.N)) & 1ull;
+    }
+    const unsigned long long m = __ballot(owns);
+    if (lane == 0) wcount[w] = __popcll(m);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int tot = 0;
+        for (int k = 0; k < kOwnListThreads / 64; k++) {
+            const int c = wcount[k];
+            wcount[k] = tot;  // exclusive offsets of the waves
+            tot += c;
+        }
+        bbase = tot ? atomicAdd(count, tot) : 0;
+    }
+    __syncthreads();
+    if (owns) list[1 + bbase + wcount[w] + __popcll(m & ((1ull << lane) - 1))] = (int32_t)r;
+    if (r == 0) list[0] = -1;
+}
+
+// ---- rows of agents owning no core: the common row's greedy actions (or the row's random ones)
+__global__ void __launch_bounds__(256) k_bdqn_common_fill(BdqnAct p, const unsigned long long* mask) {
+    const long long r = (long long)blockIdx.x * 256 + threadIdx.x;
+    if (r >= p.rows) return;
+    const long long e = r / p.N;
+    if ((mask[e] >> (int)(r - e * p.N)) & 1ull) return;
+    const int A = p.q.ac_dim;
+    const int8_t* src = (p.explore && p.explore[r] != 0) ? p.rnd + (size_t)r * A : p.common;
+    int8_t* dst = p.action + (size_t)r * A;
+    if ((A & 15) == 0) {
+        for (int b = 0; b < A; b += 16) *reinterpret_cast<uint4*>(dst + b) = *reinterpret_cast<const uint4*>(src + b);
+    } else {
+        for (int b = 0; b < A; b++) dst[b] = src[b];
+    }
 }
 
 // ---- the fused trunk + heads + argmax. Block = 8 waves x 32 rows: two 16-row column tiles per wave;
@@ -271,12 +365,28 @@ __global__ void __launch_bounds__(64 * kActWaves) k_bdqn_act(BdqnAct p) {
     const int n = p.q.n, A = p.q.ac_dim;
     const long long row0 = ((long long)blockIdx.x * kActWaves + w) * 16 * NC;
     long long row[NC], rc[NC];
-    bool rv[NC];
+    bool rv[NC], virt[NC];
+    if (p.list) {
+        // row list: positions past 1 + *n_owning exit (the whole block: before any barrier)
+        const long long nl = 1 + (long long)__builtin_amdgcn_readfirstlane(*p.n_owning);
+        if ((long long)blockIdx.x * kActWaves * 16 * NC >= nl) return;
 #pragma unroll
-    for (int c = 0; c < NC; c++) {
-        row[c] = row0 + 16 * c + j;
-        rv[c] = row[c] < p.rows;
-        rc[c] = rv[c] ? row[c] : p.rows - 1;
+        for (int c = 0; c < NC; c++) {
+            const long long lp = row0 + 16 * c + j;
+            const int r = p.list[lp < nl ? lp : nl - 1];
+            virt[c] = lp < nl && r < 0;
+            rv[c] = lp < nl && r >= 0;
+            row[c] = r < 0 ? 0 : r;
+            rc[c] = row[c];
+        }
+    } else {
+#pragma unroll
+        for (int c = 0; c < NC; c++) {
+            row[c] = row0 + 16 * c + j;
+            rv[c] = row[c] < p.rows;
+            virt[c] = false;
+            rc[c] = rv[c] ? row[c] : p.rows - 1;
+        }
     }
 
     // stage W2 as three bf16 terms in the permuted K order ([3][128][kAPitch])
@@ -300,7 +410,7 @@ __global__ void __launch_bounds__(64 * kActWaves) k_bdqn_act(BdqnAct p) {
             if (p.P) {
                 // compact acceptor rows: base + the owned cores' P rows in core order (= k_bdqn_l1_gather)
                 const long long e = rc[c] / p.N;
-                const int a1 = (int)(rc[c] - e * p.N) + 1;
+                const int a1 = virt[c] ? -1 : (int)(rc[c] - e * p.N) + 1;  // the common row: no owned core
 #pragma unroll
                 for (int kt = 0; kt < 8; kt++) hv[kt] = *reinterpret_cast<const f4*>(p.base + 16 * kt + 4 * g4);
                 const int8_t* own = p.core_owner + (size_t)e * p.C;
@@ -450,8 +560,10 @@ __global__ void __launch_bounds__(64 * kActWaves) k_bdqn_act(BdqnAct p) {
     for (int b = 0; b < A; b++) {
         __syncthreads();  // branch b's rows have landed; everyone is done with the previous branch's terms
         if constexpr (GLDS) {
-            for (int x = tid; x < ROWS_W * 32; x += NTH) {
-                const int m = x >> 5, k4 = x & 31;
+            static_assert(NTH % 32 == 0, "a thread keeps its hidden-unit group across rows");
+            const int k4 = tid & 31;  // the same 4 hidden units (and term positions) for every row it splits
+#pragma unroll
+            for (int m = tid >> 5; m < ROWS_W; m += NTH / 32) {
                 const f4 v4 = m < n ? *reinterpret_cast<const f4*>(sF + m * kBH + 4 * k4) : (f4){0, 0, 0, 0};
                 put_terms(sWa, ROWS_W, m, k4, v4);
             }
@@ -486,6 +598,7 @@ __global__ void __launch_bounds__(64 * kActWaves) k_bdqn_act(BdqnAct p) {
         for (int c = 0; c < NC; c++) {
             // q = (value + adv) - mean(adv) over the branch's n actions; the first maximum
             // (lane (j, g4) holds actions 16 mt + 4 g4 + q of row j, increasing in (mt, q))
+            // (tiles mt < NMT - 1 hold only valid actions: n > 16 (NMT - 1); only the last tile is masked)
             float adv[NMT][4];
             float sum = 0.f;
 #pragma unroll
@@ -494,18 +607,28 @@ __global__ void __launch_bounds__(64 * kActWaves) k_bdqn_act(BdqnAct p) {
                 for (int q = 0; q < 4; q++) {
                     const int m = 16 * mt + 4 * g4 + q;
                     adv[mt][q] = acc[c][mt][q] + sba[m];
-                    if (m < n) sum += adv[mt][q];
+                    if (mt < NMT - 1 || m < n) sum += adv[mt][q];
                 }
             const float mean = rows_sum(sum) * inv_n;
             float best = -INFINITY;
             int bidx = 0x7fffffff;
+            if constexpr (NMT >= 2) {
+                // the lane's first action (4 g4 < 16 < n) starts the scan, as the first valid one
+                best = (value[c] + adv[0][0]) - mean;
+                bidx = 4 * g4;
+            }
 #pragma unroll
             for (int mt = 0; mt < NMT; mt++)
 #pragma unroll
                 for (int q = 0; q < 4; q++) {
                     const int m = 16 * mt + 4 * g4 + q;
                     const float qv = (value[c] + adv[mt][q]) - mean;
-                    if (m < n && (qv > best || bidx == 0x7fffffff)) {
+                    if constexpr (NMT >= 2) {
+                        if ((mt > 0 || q > 0) && (mt < NMT - 1 || m < n) && qv > best) {
+                            best = qv;
+                            bidx = m;
+                        }
+                    } else if (m < n && (qv > best || bidx == 0x7fffffff)) {
                         best = qv;
                         bidx = m;
                     }
@@ -524,6 +647,7 @@ __global__ void __launch_bounds__(64 * kActWaves) k_bdqn_act(BdqnAct p) {
                 const int8_t act = explore[c] ? p.rnd[(size_t)row[c] * A + b] : (int8_t)bidx;
                 p.action[(size_t)row[c] * A + b] = act;
             }
+            if (virt[c] && g4 == (b & 3)) p.common[b] = (int8_t)bidx;  // the common row's greedy action
         }
     }
 }
@@ -575,7 +699,20 @@ hipError_t launch_bdqn_l1_compact(const BdqnL1Compact& p, hipStream_t st) {
 hipError_t launch_bdqn_act(const BdqnAct& p, hipStream_t st) {
     const int nmt = (p.q.n + 15) / 16;
     const long long rpb = 16 * kActWaves * kActTiles;  // rows per block
-    const unsigned blocks = (unsigned)((p.rows + rpb - 1) / rpb);
+    const unsigned blocks = (unsigned)((p.rows + (p.list ? 1 : 0) + rpb - 1) / rpb);
+    if (p.list) {
+        if (p.N > 64) return hipErrorInvalidValue;
+        hipError_t e = hipMemsetAsync(const_cast<int32_t*>(p.n_owning), 0, sizeof(int32_t), st);
+        if (e != hipSuccess) return e;
+        const long long E = p.rows / p.N;
+        hipLaunchKernelGGL(k_bdqn_own_mask, dim3((unsigned)((E + 255) / 256)), dim3(256), 0, st, p, p.own_mask);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+        hipLaunchKernelGGL(k_bdqn_own_list, dim3((unsigned)((p.rows + kOwnListThreads - 1) / kOwnListThreads)),
+                           dim3(kOwnListThreads), 0, st, p,
+                           (const unsigned long long*)p.own_mask, const_cast<int32_t*>(p.list),
+                           const_cast<int32_t*>(p.n_owning));
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+    }
     const bool l1 = p.h1 == nullptr && p.P == nullptr;
 #define MS_BDQN_CASE(T)                                                                                  \
     if (nmt <= T) {                                                                                      \
@@ -584,6 +721,10 @@ hipError_t launch_bdqn_act(const BdqnAct& p, hipStream_t st) {
             hipLaunchKernelGGL((k_bdqn_act<T, true>), dim3(blocks), dim3(64 * kActWaves), lds, st, p);   \
         else                                                                                             \
             hipLaunchKernelGGL((k_bdqn_act<T, false>), dim3(blocks), dim3(64 * kActWaves), lds, st, p);  \
+        hipError_t e = hipGetLastError();                                                                \
+        if (e != hipSuccess || !p.list) return e;                                                        \
+        hipLaunchKernelGGL(k_bdqn_common_fill, dim3((unsigned)((p.rows + 255) / 256)), dim3(256), 0, st, p,  \
+                           (const unsigned long long*)p.own_mask);                                        \
         return hipGetLastError();                                                                        \
     }
     MS_BDQN_CASE(1) MS_BDQN_CASE(3) MS_BDQN_CASE(7) MS_BDQN_CASE(8)

@@ -1128,9 +1128,15 @@ int ms_bdqn_prepare(const ms_bdqn_params* q, int32_t seg, int32_t segs, void* wo
     return MS_OK;
 }
 
+// compact layer-1 scratch: P [E][C][128] f32, then (ms_bdqn_act_compact) the owning-row count, the
+// common row's actions and the row list [1 + E * 127] int32
+static size_t bdqn_p_bytes(int64_t n_envs, int32_t n_cores) {
+    return align256(sizeof(float) * (size_t)n_envs * n_cores * ms::kBH);
+}
 size_t ms_bdqn_layer1_scratch_bytes(int64_t n_envs, int32_t n_cores) {
     if (n_envs < 1 || n_cores < 1) return 0;
-    return sizeof(float) * (size_t)n_envs * n_cores * ms::kBH;
+    return bdqn_p_bytes(n_envs, n_cores) + 256 + 256 + align256(sizeof(uint64_t) * (size_t)n_envs) +
+           sizeof(int32_t) * (1 + (size_t)n_envs * 127);
 }
 
 int ms_bdqn_layer1_compact(const ms_bdqn_params* q, const void* workspace, const float* base, const int8_t* core_rows,
@@ -1171,6 +1177,7 @@ int ms_bdqn_act_compact(const ms_bdqn_params* q, const void* workspace, const fl
     if (!workspace || !base || !core_rows || !core_owner || !scratch || !action)
         return fail(MS_EINVAL, "ms_bdqn_act_compact: NULL argument");
     if (explore && !rand_action) return fail(MS_EINVAL, "ms_bdqn_act_compact: explore needs rand_action");
+    if (n_agents > 64) return fail(MS_EINVAL, "ms_bdqn_act_compact: %d agents > 64", n_agents);
     if (n_envs < 1 || n_agents < 1 || n_agents > 127 || n_cores < 1 || acc_dim < 4 || acc_dim > 256 ||
         acc_stride < acc_dim || (acc_stride & 3) || (int64_t)acc_dim * n_cores != q->obs)
         return fail(MS_EINVAL, "ms_bdqn_act_compact: bad shape (obs must be n_cores * acc_dim)");
@@ -1202,6 +1209,12 @@ int ms_bdqn_act_compact(const ms_bdqn_params* q, const void* workspace, const fl
     p.core_owner = core_owner;
     p.N = n_agents;
     p.C = n_cores;
+    // only the rows of agents owning a core run the kernel; the others take the common row's actions
+    char* tail = (char*)scratch + bdqn_p_bytes(n_envs, n_cores);
+    p.n_owning = (const int32_t*)tail;
+    p.common = (int8_t*)(tail + 256);
+    p.own_mask = (unsigned long long*)(tail + 512);
+    p.list = (const int32_t*)(tail + 512 + align256(sizeof(uint64_t) * (size_t)n_envs));
     HIP_TRY(ms::launch_bdqn_act(p, (hipStream_t)stream));
     return MS_OK;
 }

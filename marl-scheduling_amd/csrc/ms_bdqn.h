@@ -43,6 +43,13 @@ struct BdqnAct {
     const float* base;         // [128]
     const int8_t* core_owner;  // [E][C]
     int N, C;
+    // with a row list (list != NULL, compact rows): the kernel runs rows list[0 .. 1 + *n_owning) only,
+    // entry -1 being the common row (an agent owning no core: layer 1 = base), whose greedy actions go
+    // to common[ac_dim]; k_bdqn_common_fill then writes them to every row of an agent owning no core
+    const int32_t* list;
+    const int32_t* n_owning;
+    int8_t* common;
+    unsigned long long* own_mask;  // [E] agents owning a core, bit a (N <= 64)
 };
 
 // update_policy of one role (bdqn_update_kernels.hip)
