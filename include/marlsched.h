@@ -590,7 +590,8 @@ size_t ms_bdqn_workspace_bytes(int32_t seg, int32_t segs);
 int ms_bdqn_prepare(const ms_bdqn_params* q, int32_t seg, int32_t segs, void* workspace, size_t workspace_bytes,
                     float* base, void* stream);
 
-/* Scratch bytes of ms_bdqn_layer1_compact (n_envs * n_cores * 128 floats). */
+/* Scratch bytes of ms_bdqn_layer1_compact / ms_bdqn_act_compact: n_envs * n_cores * 128 floats of
+ * per-(replica, core) layer-1 products, then (act_compact) the owning-agent masks and row list. */
 size_t ms_bdqn_layer1_scratch_bytes(int64_t n_envs, int32_t n_cores);
 
 /* Layer-1 pre-activations of every agent's aggregated acceptor row (Agent.py:82-124: its C acceptor

@@ -363,7 +363,9 @@ class BDQNTrainer:
         """The aggregated offer rows [E * N, ld_off] int8 of every (replica, agent) of ring slot `slot`
         (ms_regen_agent_rows)."""
         E, N = self.E, self.N
-        frame = (torch.arange(E, device=self.device, dtype=torch.int64) + slot * E).repeat_interleave(N)
+        if getattr(self, "_frame_base", None) is None:
+            self._frame_base = torch.arange(E, device=self.device, dtype=torch.int64).repeat_interleave(N)
+        frame = self._frame_base + slot * E
         _, off = self.env.regen_agent_rows(self.core_rows.view(-1, self.C, self.stride),
                                            self.core_owner.view(-1, self.C), self.slot_pairs.view(-1, N, self.L, 2),
                                            frame, self._agent_idx,
@@ -379,11 +381,11 @@ class BDQNTrainer:
         for a in self.actors.values():
             a.prepare()  # the weights changed in the last update
         x_off = self._offer_rows_i8(slot)
-        explore = (torch.rand((E * N,), generator=self.gen, device=self.device) <= eps).to(torch.uint8)
+        explore = torch.empty((E * N,), dtype=torch.uint8, device=self.device).bernoulli_(eps, generator=self.gen)
         out = {}
         for k, actor in self.actors.items():
             q = actor.q
-            rnd = torch.randint(0, q.n, (E * N, q.ac_dim), generator=self.gen, device=self.device).to(torch.int8)
+            rnd = torch.randint(0, q.n, (E * N, q.ac_dim), generator=self.gen, device=self.device, dtype=torch.int8)
             dst = self.act[k][slot].view(E * N, q.ac_dim)  # written in place: the ring slot of this frame
             if k == "acc":  # layer 1 from the compact frame, summed inside the act kernel
                 a = actor.act_compact(self.core_rows[slot], self.core_owner[slot], N, explore=explore, rand_action=rnd,
