@@ -414,11 +414,12 @@ class BDQNTrainer:
             self._timings["act"] += ev[0].elapsed_time(ev[1]) / 1e3
             self._timings["env"] += ev[1].elapsed_time(ev[2]) / 1e3
             self._timings["learn"] += ev[2].elapsed_time(ev[3]) / 1e3
-            self._pending_events.pop(0)
+            self._event_pool.append(self._pending_events.pop(0))  # reused: no new HIP events per frame
 
     @timings.setter
     def timings(self, value):
         self._pending_events = []
+        self._event_pool = []
         self._timings = dict(act=0.0, env=0.0, learn=0.0)
 
     def step(self):
@@ -428,7 +429,13 @@ class BDQNTrainer:
         cur = self.head
         nxt = (cur + 1) % self.n_slots
         eps = b.epsilon_by_frame(self.frame)
-        ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+        ev = self._event_pool.pop() if self._event_pool else [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+        if self.frame + 1 > b.learning_starts and b.hip_updates and not getattr(self, "_staged", False):
+            # this frame's minibatch (after this frame's store: stored + 1 frames, head nxt); from the
+            # second learning frame on it was drawn at the end of the previous step, while the device ran
+            # that step's learn
+            self._stage_sample(min(self.stored + 1, b.memory_frames), nxt)
+            self._staged = True
         ev[0].record()
         acts = self._actions(cur, eps)
         ev[1].record()
@@ -450,6 +457,11 @@ class BDQNTrainer:
         if self.frame > b.learning_starts:
             self._learn()
         ev[3].record()
+        self._staged = False
+        if self.frame + 1 > b.learning_starts and b.hip_updates:
+            # the next frame's minibatch now: the host samples while the device runs this frame's learn
+            self._stage_sample(min(self.stored + 1, b.memory_frames), (self.head + 1) % self.n_slots)
+            self._staged = True
         self._pending_events.append(ev)
         self._fold_events(block=False, keep=32)
         return done
@@ -464,7 +476,7 @@ class BDQNTrainer:
         a = (j % N).to(torch.int32)
         return slot, e, a
 
-    def _sample_host(self):
+    def _sample_host(self, stored=None, head=None):
         """batch_size transitions drawn without replacement from the stored frames' E x N transitions,
         as random.sample(memory, batch_size) (BranchingDQNModules.py:53-55) on a host random.Random:
         [4][B] int64 (ring record, next record, agent, ring slot), 0 = the newest stored frame."""
@@ -475,10 +487,12 @@ class BDQNTrainer:
         E, N, B = self.E, self.N, self.b.batch_size
         if getattr(self, "_py_rng", None) is None:
             self._py_rng = random.Random(self.seed + 29)
-        js = np.array(self._py_rng.sample(range(self.stored * E * N), B), dtype=np.int64)
+        stored = self.stored if stored is None else stored
+        head = self.head if head is None else head
+        js = np.array(self._py_rng.sample(range(stored * E * N), B), dtype=np.int64)
         age, rest = np.divmod(js, E * N)
         e, a = np.divmod(rest, N)
-        slot = (self.head - 1 - age) % self.n_slots
+        slot = (head - 1 - age) % self.n_slots
         return np.stack([slot * E + e, ((slot + 1) % self.n_slots) * E + e, a, slot])
 
     def _learn(self):
@@ -538,7 +552,9 @@ class BDQNTrainer:
             main.wait_stream(st)
         return losses
 
-    def _learn_hip(self):
+    def _stage_sample(self, stored, head):
+        """Draw the frame's minibatch on the host and queue its copy to the device index buffer (stream
+        order puts it after the previous frame's learn, which read the buffer)."""
         B = self.b.batch_size
         if getattr(self, "_sel", None) is None:
             # two pinned staging buffers, alternating: a frame waits only for the copy of two frames
@@ -552,9 +568,11 @@ class BDQNTrainer:
         self._sel_flip ^= 1
         self._sel_events[i].synchronize()
         self._sel_host = self._sel_hosts[i]
-        self._sel_host.copy_(torch.from_numpy(self._sample_host()))
+        self._sel_host.copy_(torch.from_numpy(self._sample_host(stored, head)))
         self._sel.copy_(self._sel_host, non_blocking=True)
         self._sel_events[i].record()
+
+    def _learn_hip(self):
         if not self.b.graph_updates:
             self.last_losses = self._learn_body()
         elif self._learn_graph is None:

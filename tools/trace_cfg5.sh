@@ -29,6 +29,15 @@ with open(o + "/frame_breakdown.txt", "w") as out:
     out.write("per frame: wall %.1f us, kernel busy %.1f us, %d dispatches\n" % (wall, busy, len(span) / 4))
     for k, v in sorted(tot.items(), key=lambda x: -x[1])[:40]:
         out.write("%-90s %5.1f calls %9.1f us/frame\n" % (k, cnt[k] / 4, v / 4))
+    # idle gaps between consecutive dispatches (device idle: the host had not queued the next one)
+    gaps = collections.defaultdict(float)
+    for p_, n_ in zip(span, span[1:]):
+        g = (int(n_["Start_Timestamp"]) - int(p_["End_Timestamp"])) / 1e3
+        if g > 0:
+            gaps[(p_["Kernel_Name"][:50], n_["Kernel_Name"][:50])] += g
+    out.write("\nidle gaps per frame (previous -> next dispatch):\n")
+    for (a_, b_), g in sorted(gaps.items(), key=lambda x: -x[1])[:15]:
+        out.write("%8.1f us  %s  ->  %s\n" % (g / 4, a_, b_))
 PY
 rm -rf "$O/trace5"
 echo "trace_cfg5 done"
