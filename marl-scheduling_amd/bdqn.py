@@ -84,9 +84,14 @@ class BranchingQ(nn.Module):
         return self.head(F_.linear(x, self.w1, self.b1))
 
     def hip_params(self) -> abi.MsBdqnParams:
-        """ms_bdqn_params of this net (raw device pointers: the parameters change in place)."""
-        return abi.MsBdqnParams(ptr(self.w1), ptr(self.b1), ptr(self.w2), ptr(self.b2), ptr(self.wv), ptr(self.bv),
-                                ptr(self.wa), ptr(self.ba), self.obs, self.ac_dim, self.n)
+        """ms_bdqn_params of this net (raw device pointers: the parameters change in place, so the struct
+        is built once and rebuilt only when the storage moved, e.g. after .to())."""
+        key = tuple(getattr(self, k).data_ptr() for k in ("w1", "wa", "ba"))
+        if getattr(self, "_hip_key", None) != key:
+            self._hip_p = abi.MsBdqnParams(ptr(self.w1), ptr(self.b1), ptr(self.w2), ptr(self.b2), ptr(self.wv),
+                                           ptr(self.bv), ptr(self.wa), ptr(self.ba), self.obs, self.ac_dim, self.n)
+            self._hip_key = key
+        return self._hip_p
 
 
 class HipActor:
