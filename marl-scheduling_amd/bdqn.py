@@ -437,13 +437,18 @@ class BDQNTrainer:
         ev = self._event_pool.pop() if self._event_pool else [torch.cuda.Event(enable_timing=True) for _ in range(4)]
         if self.frame + 1 > b.learning_starts and b.hip_updates and not getattr(self, "_staged", False):
             # this frame's minibatch (after this frame's store: stored + 1 frames, head nxt); from the
-            # second learning frame on it was drawn at the end of the previous step, while the device ran
-            # that step's learn
-            self._stage_sample(min(self.stored + 1, b.memory_frames), nxt)
+            # second learning frame on it was drawn during the previous step
+            self._draw_sample(min(self.stored + 1, b.memory_frames), nxt)
+            self._queue_sample()
             self._staged = True
         ev[0].record()
         acts = self._actions(cur, eps)
         ev[1].record()
+        if self.frame + 2 > b.learning_starts and b.hip_updates:
+            # the next frame's minibatch drawn on the host now, while the device runs this frame's
+            # acting; its copy is queued after this frame's learn (which still reads the index buffer)
+            self._draw_sample(min(min(self.stored + 1, b.memory_frames) + 1, b.memory_frames),
+                              (nxt + 1) % self.n_slots)
         obs = self._observe_into(nxt)
         price = acts["price"].contiguous() if self.free else None
         rew = dict(self.rbuf)
@@ -463,9 +468,8 @@ class BDQNTrainer:
             self._learn()
         ev[3].record()
         self._staged = False
-        if self.frame + 1 > b.learning_starts and b.hip_updates:
-            # the next frame's minibatch now: the host samples while the device runs this frame's learn
-            self._stage_sample(min(self.stored + 1, b.memory_frames), (self.head + 1) % self.n_slots)
+        if getattr(self, "_drawn", None) is not None:
+            self._queue_sample()
             self._staged = True
         self._pending_events.append(ev)
         self._fold_events(block=False, keep=32)
@@ -557,13 +561,11 @@ class BDQNTrainer:
             main.wait_stream(st)
         return losses
 
-    def _stage_sample(self, stored, head):
-        """Draw the frame's minibatch on the host and queue its copy to the device index buffer (stream
-        order puts it after the previous frame's learn, which read the buffer)."""
+    def _draw_sample(self, stored, head):
+        """Draw a frame's minibatch on the host into the next pinned staging buffer (two alternate: the
+        buffer's previous copy, two frames ago, is long done)."""
         B = self.b.batch_size
         if getattr(self, "_sel", None) is None:
-            # two pinned staging buffers, alternating: a frame waits only for the copy of two frames
-            # ago (long done), so the host never stalls behind the device here
             self._sel_hosts = [torch.empty((4, B), dtype=torch.int64, pin_memory=True) for _ in range(2)]
             self._sel_events = [torch.cuda.Event() for _ in range(2)]
             self._sel_flip = 0
@@ -574,8 +576,15 @@ class BDQNTrainer:
         self._sel_events[i].synchronize()
         self._sel_host = self._sel_hosts[i]
         self._sel_host.copy_(torch.from_numpy(self._sample_host(stored, head)))
-        self._sel.copy_(self._sel_host, non_blocking=True)
+        self._drawn = i
+
+    def _queue_sample(self):
+        """Queue the drawn minibatch's copy to the device index buffer the learn graph reads (stream order
+        puts it after the previous learn)."""
+        i = self._drawn
+        self._sel.copy_(self._sel_hosts[i], non_blocking=True)
         self._sel_events[i].record()
+        self._drawn = None
 
     def _learn_hip(self):
         if not self.b.graph_updates:
