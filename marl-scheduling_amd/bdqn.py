@@ -339,7 +339,10 @@ class BDQNTrainer:
         self.slot_pairs = torch.zeros((self.n_slots, E, N, L, 2), dtype=torch.int8, device=dev)
         self.act = {k: torch.zeros((self.n_slots, E, N, r.q.ac_dim), dtype=torch.int8, device=dev)
                     for k, r in self.roles.items()}
-        self.rew = {k: torch.zeros((self.n_slots, E, N), dtype=torch.float32, device=dev) for k in self.roles}
+        # the aggregated acceptor / offer rewards are int32 (Reward.py:92-143) and the env kernel writes
+        # them straight into the ring slot; the price role's float sums are copied in
+        self.rew = {k: torch.zeros((self.n_slots, E, N), dtype=torch.float32 if k == "price" else torch.int32,
+                                   device=dev) for k in self.roles}
         self.mask = torch.ones(self.n_slots, dtype=torch.float32, device=dev)
         self.off_rows = torch.zeros((E, N, L, s.off_obs_stride), dtype=torch.int8, device=dev)
         self.rbuf = self.env.reward_buffers(aggregated=True)
@@ -452,11 +455,11 @@ class BDQNTrainer:
         obs = self._observe_into(nxt)
         price = acts["price"].contiguous() if self.free else None
         rew = dict(self.rbuf)
+        rew["aggregated_acceptor"] = self.rew["acc"][cur]  # written in place by the step kernel
+        rew["aggregated_offer"] = self.rew["off"][cur]
         self.env.step(acts["acc"].contiguous(), acts["off"].contiguous(), price, obs=obs, rewards=rew)
         self._store_slot_pairs(nxt)
         done = self.env.round % self.cfg.episode_length == 0
-        self.rew["acc"][cur].copy_(rew["aggregated_acceptor"].float())
-        self.rew["off"][cur].copy_(rew["aggregated_offer"].float())
         if self.free:
             self.rew["price"][cur].copy_(rew["price"].sum(2))
         self.mask[cur] = 0.0 if done else 1.0
@@ -523,7 +526,7 @@ class BDQNTrainer:
         for k, role in self.roles.items():
             s, s1 = xs[k]
             acts = self.act[k][slot, e, a.long()].long()
-            r = self.rew[k][slot, e, a.long()]
+            r = self.rew[k][slot, e, a.long()].float()
             losses[k] = role.update(s, acts, r, s1, masks)
         self.last_losses = losses
 
@@ -555,7 +558,7 @@ class BDQNTrainer:
             with torch.cuda.stream(st):
                 s, s1 = xs[k]
                 acts = self.act[k].view(-1, role.q.ac_dim)[flat]
-                r = self.rew[k].view(-1)[flat]
+                r = self.rew[k].view(-1)[flat].float()
                 losses[k] = role.hip_update(s, s1, acts, r, masks)
         for st in self._role_streams.values():
             main.wait_stream(st)
