@@ -398,6 +398,40 @@ __global__ void __launch_bounds__(64 * kActWaves) k_bdqn_act(BdqnAct p) {
 
     // ---- trunk: out = ReLU(W2 h + b2) of row j (three-term bf16 MFMA, as the heads), the value head, then
     //      out as the heads' B fragments: bf[c][s][t] = term t of (out[2s][0..3], out[2s+1][0..3])
+    // L1: layer 1 of both tiles in one pass over the k-steps (each W1 fragment loaded once for both)
+    f4 hl[L1 ? NC : 1][8];
+    if constexpr (L1) {
+        const int S = p.Kp / 32;
+        const int x4 = p.x_stride >> 2;
+        const size_t tsz = (size_t)kBH * p.Kp;
+#pragma unroll
+        for (int c = 0; c < NC; c++)
+#pragma unroll
+            for (int mt = 0; mt < 8; mt++) hl[c][mt] = (f4){0, 0, 0, 0};
+        for (int s = 0; s < S; s++) {
+            const int d0 = 8 * s + 2 * g4;
+            u4v xb[NC];
+#pragma unroll
+            for (int c = 0; c < NC; c++) {
+                const uint32_t* xr = reinterpret_cast<const uint32_t*>(p.x + (size_t)rc[c] * p.x_stride);
+                const uint32_t x0 = d0 < x4 ? xr[d0] : 0u, x1 = d0 + 1 < x4 ? xr[d0 + 1] : 0u;
+                xb[c][0] = pack_i((int8_t)x0, (int8_t)(x0 >> 8));
+                xb[c][1] = pack_i((int8_t)(x0 >> 16), (int8_t)(x0 >> 24));
+                xb[c][2] = pack_i((int8_t)x1, (int8_t)(x1 >> 8));
+                xb[c][3] = pack_i((int8_t)(x1 >> 16), (int8_t)(x1 >> 24));
+            }
+#pragma unroll
+            for (int mt = 0; mt < 8; mt++) {
+                const uint16_t* wp = p.w1s + (size_t)(16 * mt + j) * p.Kp + 32 * s + 8 * g4;
+#pragma unroll
+                for (int t = 0; t < 3; t++) {
+                    const u4v wf = *reinterpret_cast<const u4v*>(wp + t * tsz);
+#pragma unroll
+                    for (int c = 0; c < NC; c++) hl[c][mt] = mfma_bf16(wf, xb[c], hl[c][mt]);
+                }
+            }
+        }
+    }
     __syncthreads();  // W2 staged
     u4v bf[NC][4][3];
     float value[NC];
@@ -441,33 +475,10 @@ __global__ void __launch_bounds__(64 * kActWaves) k_bdqn_act(BdqnAct p) {
 #pragma unroll
                 for (int q = 0; q < 4; q++) h[kt][q] = hv[kt][q];
         } else {
-            // W1 x on the bf16 MFMA: int8 inputs exact, W1 three exact bf16 terms; D layout = B layout
-            const int S = p.Kp / 32;
-            const int x4 = p.x_stride >> 2;
-            const uint32_t* xr = reinterpret_cast<const uint32_t*>(p.x + (size_t)rc[c] * p.x_stride);
-            const size_t tsz = (size_t)kBH * p.Kp;
-            f4 acc1[8];
-#pragma unroll
-            for (int mt = 0; mt < 8; mt++) acc1[mt] = (f4){0, 0, 0, 0};
-            for (int s = 0; s < S; s++) {
-                const int d0 = 8 * s + 2 * g4;
-                const uint32_t x0 = d0 < x4 ? xr[d0] : 0u, x1 = d0 + 1 < x4 ? xr[d0 + 1] : 0u;
-                u4v xb;
-                xb[0] = pack_i((int8_t)x0, (int8_t)(x0 >> 8));
-                xb[1] = pack_i((int8_t)(x0 >> 16), (int8_t)(x0 >> 24));
-                xb[2] = pack_i((int8_t)x1, (int8_t)(x1 >> 8));
-                xb[3] = pack_i((int8_t)(x1 >> 16), (int8_t)(x1 >> 24));
-#pragma unroll
-                for (int mt = 0; mt < 8; mt++) {
-                    const uint16_t* wp = p.w1s + (size_t)(16 * mt + j) * p.Kp + 32 * s + 8 * g4;
-#pragma unroll
-                    for (int t = 0; t < 3; t++) acc1[mt] = mfma_bf16(*reinterpret_cast<const u4v*>(wp + t * tsz), xb, acc1[mt]);
-                }
-            }
 #pragma unroll
             for (int kt = 0; kt < 8; kt++)
 #pragma unroll
-                for (int q = 0; q < 4; q++) h[kt][q] = acc1[kt][q] + p.q.b1[16 * kt + 4 * g4 + q];
+                for (int q = 0; q < 4; q++) h[kt][q] = hl[c][kt][q] + p.q.b1[16 * kt + 4 * g4 + q];
         }
 #pragma unroll
         for (int kt = 0; kt < 8; kt++)
