@@ -230,7 +230,7 @@ class BranchingRole:
 
     def hip_update(self, states_i8, next_i8, actions_i8, rewards, masks, stream=None):
         """update_policy (BranchingDQNModules.py:125-164) on the HIP kernels (ms_bdqn_update: the three
-        forwards, the double-DQN target, the MSE backward and the clamp in four launches) and the HIP
+        forwards, the double-DQN target, the MSE backward and the clamp in eight tile launches) and the HIP
         Adam: states / next states [B, ld] int8 observation rows, actions [B, >= ac_dim] int8, rewards /
         masks [B] f32. Capturable (no host sync). Returns the loss tensor [1] (overwritten by the
         next update)."""
