@@ -9,25 +9,29 @@
 //
 //   k_bdqn_w1split    W1 as three bf16 terms (hi + mid + lo = W1 exactly), zero-padded per input
 //                     segment, once per weight update;
-//   k_bdqn_l1_base    b1 + sum_c W1_c F (F = the foreign acceptor row, Agent.py:167-212);
+//   k_bdqn_l1_cf /    W1_c F per core c (F = the foreign acceptor row, Agent.py:167-212) and
+//   k_bdqn_l1_base    base = b1 + sum_c W1_c F, once per weight update;
 //   k_bdqn_l1_cores   layer 1 of all N agents' aggregated acceptor rows from the compact
 //   k_bdqn_l1_gather  observations: an agent's row is R_c on the cores it owns and F elsewhere, so
-//                     W1 x_a + b1 = base + sum_{c owned by a} W1_c (R_c - F). P_c = W1_c (R_c - F)
-//                     of every (replica, core) on v_mfma_f32_16x16x32_bf16: R_c - F is a small
-//                     integer (exact in bf16) and W1 is three exact bf16 terms, so every product is
-//                     exact and only the f32 accumulation rounds; then every agent row adds its
-//                     owned cores' P rows in core order (deterministic);
+//                     W1 x_a + b1 = base + sum_{c owned by a} P_c, P_c = W1_c R_c - W1_c F of every
+//                     (replica, core) on v_mfma_f32_16x16x32_bf16 (the int8 row bytes are exact in
+//                     bf16 and W1 is three exact bf16 terms: exact products, f32 accumulation); the
+//                     gather adds an agent's owned cores' P rows to base in core order (the h1 rows of
+//                     ms_bdqn_layer1_compact; ms_bdqn_act_compact does that sum inside k_bdqn_act);
+//   k_bdqn_own_mask / the compact acting's row list: only agents that own a core run the heads, the
+//   k_bdqn_own_list / others (layer 1 = base) take the one common row's greedy actions (fill);
+//   k_bdqn_common_fill
 //   k_bdqn_act        the trunk, the value head and every advantage head fused with the per-branch
 //                     mean, q and first-maximum argmax, then the epsilon-greedy pick: nothing but
 //                     the int8 actions leaves the kernel. Trunk and heads run on
-//                     v_mfma_f32_16x16x4_f32 (exact f32 products, f32 accumulation; no bf16 in
-//                     the q values, so a greedy action differs from the fp32 reference only where
-//                     two q values are within f32 rounding). The batch is on the MFMA column axis
-//                     and every layer's accumulator is the next layer's B operand unchanged (the
-//                     K order permuted to match); a block of 8 waves (128 rows) stages W2, then
-//                     one branch's Wa rows at a time, in LDS (register prefetch of the next
-//                     branch during the current one's MFMAs). With h1 == NULL layer 1 runs in the
-//                     kernel on int8 rows (the offerer / price roles).
+//                     v_mfma_f32_16x16x32_bf16 with both operands as three exact bf16 terms and six
+//                     products (the f32 product sum within about f32 rounding, see the comment at the
+//                     kernel). The batch is on the MFMA column axis and every layer's accumulator is
+//                     the next layer's B operand (the K order permuted to match); a block of 8 waves
+//                     (256 rows, two 16-row tiles per wave) stages W2's terms, then one branch's Wa
+//                     rows at a time in LDS (the next branch's f32 rows arrive by LDS-DMA during the
+//                     current one's MFMAs). With h1 == NULL and P == NULL layer 1 runs in the kernel
+//                     on int8 rows (the offerer / price roles).
 #include <hip/hip_runtime.h>
 #include <math.h>
 #include <stdint.h>
