@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define MS_ABI_VERSION 15
+#define MS_ABI_VERSION 16
 
 #define MS_MAX_KINDS 16
 #define MS_MAX_AGENTS 64
@@ -294,6 +294,12 @@ typedef struct ms_mlp_params {
      * fragment block whose header does not match the call's shape is ignored. Rebuild it whenever
      * the weights change (like ms_price_table_build). Other entry points ignore the field. */
     const void* act_frag;
+    /* ABI 16: the Philox row counter of this call's row r (= e * n_units + u) is row_base + r. A caller
+     * stepping replicas [e0, e0 + E) of a larger set passes row_base = e0 * n_units, so every replica
+     * draws the numbers it would draw in one call over the whole set (a rank's shard, a stream's part).
+     * For the single-net acceptor rule (word (i >> 6) & 1 of item i's draw) this holds when
+     * e0 * units_per_group is a multiple of 128. 0 for a standalone call; ignored outside acting. */
+    int64_t row_base;
 } ms_mlp_params;
 
 /* Bytes of the act fragment block of net p acting on rows of obs_stride bytes. */
@@ -649,7 +655,8 @@ size_t ms_bdqn_update_workspace_bytes(const ms_bdqn_params* q, int32_t batch);
 /* The gradient of update_policy on one minibatch: current = q(s) at the taken actions (:135),
  * argmax = the first maximum of q(s') per branch, max_next = mean over the branches of target(s') at
  * argmax (:139-142), expected = r + max_next * gamma * mask (:144), loss = mse_loss(expected, current)
- * over [batch, ac_dim] (:145), every gradient element clamped to [-grad_clip, grad_clip] (:157-158)
+ * over [batch, ac_dim] (:145), every gradient element clamped to [-grad_clip, grad_clip] (:157-158;
+ * grad_clip <= 0: no clamp, as ms_dqn_grad)
  * and written to grads (the Adam step is ms_adam_step / ms_adam_step_dev). Deterministic. */
 int ms_bdqn_update(const ms_bdqn_params* q, const ms_bdqn_params* target, const ms_bdqn_batch* batch, float gamma,
                    float grad_clip, void* workspace, size_t workspace_bytes, const ms_bdqn_grads* grads, void* stream);

@@ -27,7 +27,7 @@ class MarlSchedError(RuntimeError):
         self.code = code
 
 
-ABI_VERSION = 15  # include/marlsched.h MS_ABI_VERSION
+ABI_VERSION = 16  # include/marlsched.h MS_ABI_VERSION
 
 
 def _load():
@@ -109,9 +109,11 @@ def _load():
     }
     L.ms_abi_version.restype = ct.c_int
     version = L.ms_abi_version()
-    # ABI 14 added ms_bdqn_update*, 15 ms_bdqn_act_compact; an older library (an A/B variant built
-    # before them) loads without them
-    if version not in (13, 14, ABI_VERSION):
+    # ABI 14 added ms_bdqn_update*, 15 ms_bdqn_act_compact, 16 ms_mlp_params.row_base (a trailing field an
+    # older library does not read: its acting draws are those of row_base 0). An older library (an A/B variant built
+    # before them, tools/ab_variant.sh) loads without them only when MARLSCHED_LENIENT_ABI=1 asks for it
+    lenient = os.environ.get("MARLSCHED_LENIENT_ABI") == "1" and version in (13, 14, 15)
+    if version != ABI_VERSION and not lenient:
         raise ImportError("libmarlsched.so ABI version mismatch (%d, want %d)" % (version, ABI_VERSION))
     for name, (res, args) in sig.items():
         if (version < 14 and name.startswith("ms_bdqn_update")) or (version < 15 and name == "ms_bdqn_act_compact"):

@@ -194,6 +194,7 @@ class MsMlpParams(ct.Structure):
         ("n_actions", ct.c_int32),
         ("n_groups", ct.c_int32),
         ("act_frag", ct.c_void_p),  # ms_act_prepare's block, or NULL
+        ("row_base", ct.c_int64),   # the Philox row counter of row r is row_base + r (ABI 16)
     ]
 
 

@@ -223,8 +223,9 @@ class BranchingRole:
             if p.grad is not None:
                 p.grad.zero_()
         loss.backward()
-        for p in self.q.parameters():
-            p.grad.data.clamp_(-self.cfg.grad_clip, self.cfg.grad_clip)
+        if self.cfg.grad_clip > 0:  # grad_clip <= 0: no clamp (the ms_bdqn_update convention)
+            for p in self.q.parameters():
+                p.grad.data.clamp_(-self.cfg.grad_clip, self.cfg.grad_clip)
         self.opt.step()
         return loss.detach()
 

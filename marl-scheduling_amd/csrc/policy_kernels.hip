@@ -569,18 +569,21 @@ __device__ __forceinline__ void act_tiles(const ActArgs& a, int block) {
     // Philox uniforms, computed for 4 tiles at a time: lane (j, g4) draws for row j of tile
     // base + g4 (counter = the obs row index, so the values do not depend on the tiling)
     uint32_t rnd0 = 0, rnd1 = 0, rb0[4] = {0, 0, 0, 0}, rb1[4] = {0, 0, 0, 0};
+    // the counter's row is global across launches (ms_mlp_params.row_base: this call's first replica's
+    // first row), so a replica draws the same numbers whichever rank or replica split steps it
+    const uint32_t rbase = (uint32_t)a.n1.row_base;
     // With a price net the row's two words are its two uniforms. A single net's row takes word
     // (i >> 6) & 1 of the draw countered by the row of item i & ~64: the rule of k_act_common's scan
     // (one draw per two 64-item steps there), so both kernels sample a row alike.
     auto draw4 = [&](int base) {
         if (NT2 > 0) {
             const int r = base + g4 < t1 ? row_of_lane(base + g4, j) : -1;
-            philox2((uint32_t)r, off, a.seed, rnd0, rnd1);
+            philox2((uint32_t)r + rbase, off, a.seed, rnd0, rnd1);
             rows_bcast(rnd1, rb1);
         } else {
             const int i = (base + g4) * 16 + j;
             const int r = base + g4 < t1 ? row_of_lane(0, i & ~64) : -1;
-            philox2((uint32_t)r, off, a.seed, rnd0, rnd1);
+            philox2((uint32_t)r + rbase, off, a.seed, rnd0, rnd1);
             if (i & 64) rnd0 = rnd1;
         }
         rows_bcast(rnd0, rb0);  // tile base + k takes row k's draws
@@ -904,7 +907,7 @@ __device__ __forceinline__ void act_common_rows(const ActArgs& a, int block) {
         if ((i0 & 64) && i0 > i_begin) return u24(u_other);
         const int ib = (i0 & ~64) + lane;
         uint32_t r0, r1;
-        philox2((uint32_t)row_of_item(ib), off, a.seed, r0, r1);
+        philox2((uint32_t)row_of_item(ib) + (uint32_t)a.n1.row_base, off, a.seed, r0, r1);
         u_other = r1;
         return u24((i0 & 64) ? r1 : r0);
     };

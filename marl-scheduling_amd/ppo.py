@@ -132,13 +132,15 @@ class GroupedActorCritic(nn.Module):
         dist = Categorical(self.actor_probs(x))
         return dist.log_prob(actions), self.critic(x), dist.entropy()
 
-    def mlp_params(self, frag: "ActFrag | None" = None) -> abi.MsMlpParams:
-        """The actor's ms_mlp_params; frag: an ActFrag built for the current weights (acting only)."""
+    def mlp_params(self, frag: "ActFrag | None" = None, row_base: int = 0) -> abi.MsMlpParams:
+        """The actor's ms_mlp_params; frag: an ActFrag built for the current weights (acting only);
+        row_base: the Philox row counter of the call's first row (acting only)."""
         for k in ACTOR_KEYS:
             t = getattr(self, k)
             assert t.is_cuda and t.is_contiguous() and t.dtype == torch.float32
         return abi.MsMlpParams(ptr(self.w1), ptr(self.b1), ptr(self.w2), ptr(self.b2), ptr(self.w3), ptr(self.b3),
-                               self.D, self.H, self.A, self.G, ptr(frag.buf) if frag is not None else None)
+                               self.D, self.H, self.A, self.G, ptr(frag.buf) if frag is not None else None,
+                               int(row_base))
 
     def critic_mlp_params(self) -> abi.MsMlpParams:
         return abi.MsMlpParams(ptr(self.cw1), ptr(self.cb1), ptr(self.cw2), ptr(self.cb2), ptr(self.cw3),
@@ -146,11 +148,12 @@ class GroupedActorCritic(nn.Module):
 
     @torch.no_grad()
     def act(self, obs_i8, n_units: int, seed: int, offset: int, uniforms=None, action=None, logprob=None, stream=None,
-            offset_dev=None, common_row=None, frag: "ActFrag | None" = None):
+            offset_dev=None, common_row=None, frag: "ActFrag | None" = None, replica_base: int = 0):
         """ActorCritic.act (PPOmodules.py:53-63) for obs [E, n_units, stride] int8 on the HIP kernel.
         Unit u uses group u // (n_units // G). Returns (action int8 [E, U], logprob f32 [E, U]).
         common_row (int8 [stride] on the device, optional): rows equal to it share one forward pass
-        (``ms_policy_act_common``; same outputs)."""
+        (``ms_policy_act_common``; same outputs). replica_base: the global index of obs's first replica
+        (its Philox rows start at replica_base * n_units: a shard draws what the whole set would)."""
         E, U, stride = obs_i8.shape
         assert U == n_units and U % self.G == 0 and obs_i8.dtype == torch.int8 and obs_i8.is_contiguous()
         dev = obs_i8.device
@@ -158,7 +161,7 @@ class GroupedActorCritic(nn.Module):
             action = torch.empty((E, U), dtype=torch.int8, device=dev)
         if logprob is None:
             logprob = torch.empty((E, U), dtype=torch.float32, device=dev)
-        p = self.mlp_params(frag)
+        p = self.mlp_params(frag, replica_base * U)
         if common_row is not None:
             assert common_row.dtype == torch.int8 and common_row.numel() == stride and common_row.device == dev
             check(lib.ms_policy_act_common(ct.byref(p), ptr(obs_i8), stride, E, U, U // self.G, ptr(common_row),
@@ -172,7 +175,8 @@ class GroupedActorCritic(nn.Module):
 
     @torch.no_grad()
     def act_compact(self, core_rows, core_owner, n_units: int, seed: int, offset: int, common_row, uniforms=None,
-                    action=None, logprob=None, stream=None, offset_dev=None, frag: "ActFrag | None" = None):
+                    action=None, logprob=None, stream=None, offset_dev=None, frag: "ActFrag | None" = None,
+                    replica_base: int = 0):
         """``act`` with common_row on compact acceptor observations (ms_policy_act_compact):
         core_rows [E, C, stride], core_owner [E, C] int8; unit u = a*C + c acts on core row c when
         core_owner == a + 1, else on common_row. Same outputs as ``act`` on the regenerated rows."""
@@ -184,7 +188,7 @@ class GroupedActorCritic(nn.Module):
             action = torch.empty((E, n_units), dtype=torch.int8, device=dev)
         if logprob is None:
             logprob = torch.empty((E, n_units), dtype=torch.float32, device=dev)
-        p = self.mlp_params(frag)
+        p = self.mlp_params(frag, replica_base * n_units)
         check(lib.ms_policy_act_compact(ct.byref(p), ptr(core_rows), ptr(core_owner), stride, E, n_units,
                                         n_units // self.G, C, ptr(common_row), ct.c_uint64(seed), ct.c_uint64(offset),
                                         ptr(offset_dev), ptr(uniforms), ptr(action), ptr(logprob), stream_ptr(stream)))
@@ -247,7 +251,8 @@ class ActFrag:
 def act_round_free(core: GroupedActorCritic, price: GroupedActorCritic, off_obs, acc: GroupedActorCritic, core_rows,
                    core_owner, common_row, n_cores: int, seed: int, off_offset: int, acc_offset: int, out: dict,
                    acc_action, acc_logprob, offset_dev=None, stream=None, price_table: PriceTable | None = None,
-                   price_unit_stride: int = 0, core_frag: "ActFrag | None" = None, acc_frag: "ActFrag | None" = None):
+                   price_unit_stride: int = 0, core_frag: "ActFrag | None" = None, acc_frag: "ActFrag | None" = None,
+                   replica_base: int = 0):
     """``offer_act_free`` + ``act_compact`` of one free-price round in one launch (ms_act_round_free):
     getActionForAllAgents (SchedulingEnvironment.py:150-172); outputs identical to the two calls.
     price_table: the price chooser samples from it (built for the current weights).
@@ -258,7 +263,8 @@ def act_round_free(core: GroupedActorCritic, price: GroupedActorCritic, off_obs,
     U_acc = acc_action.shape[1]
     assert off_obs.is_contiguous() and core_rows.is_contiguous() and core_owner.is_contiguous()
     _check_price_out(out, E, U_off, price_unit_stride)
-    pc, pp, pa = core.mlp_params(core_frag), price.mlp_params(), acc.mlp_params(acc_frag)
+    pc, pp = core.mlp_params(core_frag, replica_base * U_off), price.mlp_params()
+    pa = acc.mlp_params(acc_frag, replica_base * U_acc)
     check(lib.ms_act_round_free(ct.byref(pc), ct.byref(pp), ptr(off_obs), off_stride, U_off, U_off // core.G,
                                 ct.byref(pa), ptr(core_rows), ptr(core_owner), acc_stride, U_acc, U_acc // acc.G,
                                 n_cores, ptr(common_row), E, ct.c_uint64(seed), ct.c_uint64(off_offset),
@@ -295,7 +301,7 @@ def regen_acceptor_rows(core_rows, core_owner, common_row, n_agents: int):
 @torch.no_grad()
 def offer_act_free(core: GroupedActorCritic, price: GroupedActorCritic, obs_i8, n_cores: int, seed: int, offset: int,
                    out: dict, uniforms=None, offset_dev=None, stream=None, price_unit_stride: int = 0,
-                   core_frag: "ActFrag | None" = None):
+                   core_frag: "ActFrag | None" = None, replica_base: int = 0):
     """FreePriceOfferPPO.selectAction (PPOmodules.py:312-332) for obs [E, U, stride] int8 in one launch.
     out: core_action/price_action/env_price int8 [E, U], core_logprob/price_logprob f32 [E, U],
     price_state int8 [E, U, 4]. price_unit_stride > 0: price_state / price_action / price_logprob are
@@ -303,7 +309,7 @@ def offer_act_free(core: GroupedActorCritic, price: GroupedActorCritic, obs_i8, 
     E, U, stride = obs_i8.shape
     assert obs_i8.dtype == torch.int8 and obs_i8.is_contiguous() and U % core.G == 0
     _check_price_out(out, E, U, price_unit_stride)
-    pc, pp = core.mlp_params(core_frag), price.mlp_params()
+    pc, pp = core.mlp_params(core_frag, replica_base * U), price.mlp_params()
     check(lib.ms_offer_act_free(ct.byref(pc), ct.byref(pp), ptr(obs_i8), stride, E, U, U // core.G, n_cores,
                                 ct.c_uint64(seed), ct.c_uint64(offset), ptr(offset_dev), ptr(uniforms),
                                 ptr(out["core_action"]), ptr(out["core_logprob"]), ptr(out["price_state"]),

@@ -331,9 +331,12 @@ class Trainer:
         env, e0, e1 = self.env.parts[k]
         st = self.streams[k]
         E, N, C, L = e1 - e0, self.N, self.C, self.L
-        # Philox key per rank and part (part 0 keeps the unsplit key); offsets: static per round +
-        # the device counter (advanced per rollout)
-        seed = self.seed * 7919 + self.rank + k * 0x9E3779B1
+        # one Philox key for every rank and part; the counter's row is global (replica_base = this
+        # part's first replica in the whole job, rank-major), so a replica draws the same numbers on
+        # any number of ranks or parts (when rank * E * units per group is a multiple of 128, ms_mlp_params)
+        # offsets: static per round + the device counter (advanced per rollout)
+        seed = self.seed * 7919
+        rb = self.rank * self.E + e0
         base = 8 * t
         sl = lambda x: x[e0:e1]
         # per agent: offer units then acceptors (Agent.py:504-515); separate streams per unit type
@@ -353,27 +356,28 @@ class Trainer:
                                self.acc.group.policy_old, sl(self.acc_rows[t]), sl(self.acc_owner[t]), self.acc_common,
                                C, seed, base + 1, base + 3, out, sl(self.acc.actions[t]), sl(self.acc.logprobs[t]),
                                offset_dev=self.rng_ctr, stream=st, price_table=self.price_table,
-                               price_unit_stride=pus, core_frag=self.off_frag, acc_frag=self.acc_frag)
+                               price_unit_stride=pus, core_frag=self.off_frag, acc_frag=self.acc_frag,
+                               replica_base=rb)
             else:
                 offer_act_free(self.off.group.policy_old, self.price.group.policy_old, sl(self.off_obs[t]), C, seed,
                                base + 1, out, offset_dev=self.rng_ctr, stream=st, price_unit_stride=pus,
-                               core_frag=self.off_frag)
+                               core_frag=self.off_frag, replica_base=rb)
         else:
             self.off.group.policy_old.act(sl(self.off_obs[t]), N * L, seed, base + 1, action=sl(self.off.actions[t]),
                                           logprob=sl(self.off.logprobs[t]), offset_dev=self.rng_ctr, stream=st,
-                                          frag=self.off_frag)
+                                          frag=self.off_frag, replica_base=rb)
         if self.compact and self.free:
             pass  # acted above with the offers
         elif self.compact:
             self.acc.group.policy_old.act_compact(sl(self.acc_rows[t]), sl(self.acc_owner[t]), N * C, seed, base + 3,
                                                   self.acc_common, action=sl(self.acc.actions[t]),
                                                   logprob=sl(self.acc.logprobs[t]), offset_dev=self.rng_ctr, stream=st,
-                                                  frag=self.acc_frag)
+                                                  frag=self.acc_frag, replica_base=rb)
         else:
             self.acc.group.policy_old.act(sl(self.acc_obs[t]), N * C, seed, base + 3, action=sl(self.acc.actions[t]),
                                           logprob=sl(self.acc.logprobs[t]), offset_dev=self.rng_ctr,
                                           common_row=self.acc_common if self.common_rows else None, stream=st,
-                                          frag=self.acc_frag)
+                                          frag=self.acc_frag, replica_base=rb)
 
     def _step_part(self, t: int, k: int):
         """env.step + saveRewards of round t for replica part k (on stream k)."""

@@ -57,20 +57,24 @@ class RefPPO:
         t = torch.tensor(out, dtype=torch.float32)
         return (t - t.mean()) / (t.std() + 1e-7)
 
+    def epoch(self, states, actions, old_logprobs, rewards_norm):
+        """One K-epoch step of PPOmodules.py:144-168: the clipped-surrogate loss, its gradient, the Adam
+        step. Returns (mean loss, {name: the gradient before the step})."""
+        logprobs, values, entropy = self.policy.evaluate(states, actions)
+        ratios = torch.exp(logprobs - old_logprobs.detach())
+        adv = rewards_norm - values.detach()
+        s1 = ratios * adv
+        s2 = torch.clamp(ratios, 1 - self.eps_clip, 1 + self.eps_clip) * adv
+        loss = -torch.min(s1, s2) + 0.5 * self.mse(values, rewards_norm) - 0.01 * entropy
+        self.optimizer.zero_grad()
+        loss.mean().backward()
+        grads = {k: v.grad.detach().clone() for k, v in self.policy.flat().items()}
+        self.optimizer.step()
+        return float(loss.mean().detach()), grads
+
     def update(self, states, actions, old_logprobs, rewards_norm):
         """PPOmodules.py:144-171 on given tensors; returns the per-epoch mean losses."""
-        losses = []
-        for _ in range(self.K):
-            logprobs, values, entropy = self.policy.evaluate(states, actions)
-            ratios = torch.exp(logprobs - old_logprobs.detach())
-            adv = rewards_norm - values.detach()
-            s1 = ratios * adv
-            s2 = torch.clamp(ratios, 1 - self.eps_clip, 1 + self.eps_clip) * adv
-            loss = -torch.min(s1, s2) + 0.5 * self.mse(values, rewards_norm) - 0.01 * entropy
-            self.optimizer.zero_grad()
-            loss.mean().backward()
-            self.optimizer.step()
-            losses.append(float(loss.mean().detach()))
+        losses = [self.epoch(states, actions, old_logprobs, rewards_norm)[0] for _ in range(self.K)]
         self.policy_old.load_state_dict(self.policy.state_dict())
         return losses
 

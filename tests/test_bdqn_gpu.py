@@ -187,6 +187,32 @@ def test_act_kernel_is_the_argmax_of_q(ms, role):
     assert torch.equal(got.cpu()[~ex], greedy.cpu()[~ex])
 
 
+@pytest.mark.parametrize("n", [17, 33, 50, 65, 100])
+def test_act_kernel_masks_padded_action_tiles(ms, n):
+    """Branch widths whose tile count is not an instantiated NMT (n = 17: NMT 3 for 2 tiles; 50, 65,
+    100: NMT 7 for 4..6 tiles; 33 is exact) on int8 rows (layer 1 in the kernel): the zero-padded
+    rows past n join neither the mean nor the argmax, so every action is < n and the greedy ones are
+    the first argmax of the fp32 reference's q (BranchingDQNModules.py:88-101). The advantage biases
+    are shifted so the mean advantage is negative, where a padded row would win."""
+    bdqn = _bdqn()
+    obs, ac, rows = 40, 3, 3000
+    torch.manual_seed(n)
+    net = bdqn.BranchingQ(obs, ac, n).cuda()
+    with torch.no_grad():
+        net.ba.sub_(0.5)
+    actor = bdqn.HipActor(net, obs, 1, "cuda")
+    actor.prepare()
+    g = torch.Generator(device="cuda").manual_seed(n)
+    x = torch.randint(-5, 14, (rows, 40), generator=g, device="cuda").to(torch.int8)
+    got = actor.act(x=x)
+    assert int(got.min()) >= 0 and int(got.max()) < n
+    ref = RefBranchingQNetwork(obs, ac, n)
+    ref.load_stacked({k: getattr(net, k).detach().cpu() for k in bdqn.KEYS})
+    with torch.no_grad():
+        q = ref(x.cpu().float())
+    assert _check_greedy(q, got.cpu()) > 0.995
+
+
 def test_act_compact_equals_layer1_then_act(ms):
     """ms_bdqn_act_compact (the owned cores' P rows summed inside the act kernel) == ms_bdqn_layer1_compact
     followed by ms_bdqn_act on its h1, bit for bit, greedy and epsilon-greedy."""

@@ -127,6 +127,77 @@ def test_two_rank_graphed_update_equals_eager(tmp_path):
             assert torch.equal(g[k], e[k]), (r, k)
 
 
+_UNION = dict(name="cfg3", E=64, T=12, iters=2, seed=3)
+
+
+def _ring_views(t):
+    """Every per-replica rollout ring of a trainer, replica axis 1 ([T(+1)][E]...)."""
+    out = {"off_obs": t.off_obs, "acc_rows": t.acc_rows, "acc_owner": t.acc_owner}
+    if t.price_obs is not None:
+        out["price_obs"] = t.price_obs
+    for u in t.units():
+        for k in ("actions", "logprobs", "rewards"):
+            out["%s.%s" % (u.name, k)] = getattr(u, k)
+    return out
+
+
+def _union_rank(rank, world, port, out_dir):
+    """One rank of a world-size-`world` run over E / world replicas (rank r = replicas
+    [r E / world, (r + 1) E / world) of the union: env seeds env_seed(seed, r, E / world) = base + r E / world,
+    Philox rows from replica_base r E / world), or the single process over all E (world 1)."""
+    import torch.distributed as dist
+
+    c = _UNION
+    if world > 1:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    tr = importlib.import_module("marl-scheduling_amd.trainer")
+    t = tr.Trainer.from_named(c["name"], n_envs=c["E"] // world, update_step=c["T"], seed=c["seed"], rank=rank,
+                              world_size=world, use_graph=False)
+    out = {}
+    for it in range(c["iters"]):
+        t.rollout()
+        for k, v in _ring_views(t).items():
+            out["it%d.%s" % (it, k)] = v[: c["T"]].detach().cpu().clone()
+        losses = t.update()
+        for k, v in losses.items():
+            out["it%d.loss.%s" % (it, k)] = v.detach().cpu().clone()
+        for u in t.units():
+            for k, v in u.group.policy.named_parameters():
+                out["it%d.w.%s.%s" % (it, u.name, k)] = v.detach().cpu().clone()
+    out["flags"] = torch.tensor(t.flags())
+    torch.save(out, os.path.join(out_dir, "union_w%d_r%d.pt" % (world, rank)))
+    if world > 1:
+        dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_two_rank_shards_equal_one_rank_on_the_union(tmp_path):
+    """§8(e): 2 ranks x E/2 replicas == 1 rank x E replicas (SchedulingEnvironment.py:314-329, PPOmodules.py:548-597
+    shared nets, gradient all-reduce mean). Replica e's env seed and Philox rows are functions of its
+    global index, so every per-replica ring of iteration 1 (observations, actions, log-probs, rewards)
+    is bit-identical to the union's. The union's loss is the mean of the two ranks' (equal shards),
+    and the weights after each iteration agree within 1e-5 (the all-reduce sums the two halves' f32
+    gradients in another order than one rank's reduction). Iteration 2 acts on those weights; its
+    rings are compared bit for bit too: a sampled action flips only if a uniform lies within ~1e-7 of a
+    CDF boundary."""
+    mp.spawn(_union_rank, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True)
+    mp.spawn(_union_rank, args=(1, 0, str(tmp_path)), nprocs=1, join=True)
+    one = torch.load(tmp_path / "union_w1_r0.pt", weights_only=True)
+    two = [torch.load(tmp_path / ("union_w2_r%d.pt" % r), weights_only=True) for r in range(2)]
+    assert int(one.pop("flags")) == 0 and all(int(x.pop("flags")) == 0 for x in two)
+    h = _UNION["E"] // 2
+    for k, v in one.items():
+        if ".w." in k:
+            assert torch.equal(two[0][k], two[1][k]), k  # lockstep
+            torch.testing.assert_close(two[0][k], v, rtol=1e-5, atol=1e-6, msg=k)
+        elif ".loss." in k:
+            torch.testing.assert_close((two[0][k] + two[1][k]) / 2, v, rtol=1e-5, atol=1e-6, msg=k)
+        else:
+            for r in range(2):
+                assert torch.equal(two[r][k], v[:, r * h:(r + 1) * h]), (k, r)
+
+
 def _device_count():
     try:
         return torch.cuda.device_count()

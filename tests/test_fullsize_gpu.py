@@ -11,10 +11,16 @@
 * cfg5 (8192 x 32 x 32, Branching DQN): a few frames, finite losses, no flags, and two replicas'
   trajectories vs the C oracle from the trainer's action ring.
 
+* Every (draw, epoch) step of both PPO trainers re-synced (cfg3: all three unit types, agents 0 and 5;
+  cfg4: one acceptor, one offer and one price unit): before each step the reference takes the HIP
+  path's current weights and Adam state, so each step's own loss is held to the north star's 1e-5
+  relative, its gradient to 1e-4 of the tensor's scale, and the HIP Adam's new weights to torch's
+  Adam formula applied to the HIP gradient.
+
 Returns are per replica (E = 1 semantics of PPOmodules.py:548-560), rows r = t * E + e.
-Tolerances: the first draw's loss 1e-5 relative (north star); after an Adam step the weights
-agree within 1e-4 relative (Adam divides by sqrt(v), which amplifies last-ulp gradient order
-differences), so later draws' losses are held to 1e-4."""
+Tolerances of the whole-update comparisons (no re-sync): the first draw's loss 1e-5 relative; after
+an Adam step the weights agree within 1e-4 relative (Adam divides by sqrt(v), which amplifies last-ulp
+gradient order differences), so later draws' losses there are held to 1e-4."""
 import importlib
 import random
 
@@ -24,6 +30,7 @@ import torch
 
 from oracle import pyoracle
 from oracle.ppo_ref import RefPPO
+from tests.replay import oracle_replay as _oracle_replay
 
 pytestmark = pytest.mark.gpu
 
@@ -144,44 +151,123 @@ def test_cfg3_fullsize_iteration_losses_match_refppo(ms):
                                "%s agent %d %s" % (u.name, a, k))
 
 
-def _oracle_replay(tr, replicas, base_seed, T):
-    """Step the C oracle of replicas e with the actions the trainer's rings hold and compare its
-    observations and rewards with the rings (slot t + 1 = the observation after round t)."""
-    cfg = tr.cfg
-    s = pyoracle.abi.config_shape(cfg)
-    N, C, L, D_acc, D_off = s["N"], s["C"], s["L"], s["acc_obs_dim"], s["off_obs_dim"]
-    idx = torch.tensor(list(replicas), device=tr.acc_rows.device)
-    acc_all = _ppo().regen_acceptor_rows(tr.acc_rows.index_select(1, idx).contiguous(),
-                                         tr.acc_owner.index_select(1, idx).contiguous(), tr.acc_common,
-                                         tr.N).cpu().numpy()                # [T+1, n, N*C, stride]
-    off_all = tr.off_obs[:, list(replicas)].cpu().numpy()
-    aa = tr.acc.actions[:, list(replicas)].cpu().numpy()
-    ao = tr.off.actions[:, list(replicas)].cpu().numpy()
-    ap = tr.price.actions[:, list(replicas)].cpu().numpy() if tr.free else None
-    ra = tr.acc.rewards[:, list(replicas)].cpu().numpy()
-    ro = tr.off.rewards[:, list(replicas)].cpu().numpy()
-    rp = tr.price.rewards[:, list(replicas)].cpu().numpy() if tr.free else None
-    for i, e in enumerate(replicas):
-        env = pyoracle.OracleEnv(cfg, base_seed + e)
-        o = env.observe()
-        assert np.array_equal(acc_all[0, i, :, :D_acc].reshape(N, C, D_acc), o["acceptor"]), e
-        for t in range(T):
-            core = ao[t, i].reshape(N, L)
-            price = np.where(core == 0, -5, ap[t, i].reshape(N, L)) if tr.free else None
-            r = env.step(aa[t, i].reshape(N, C), core, price)
-            o = env.observe()
-            assert np.array_equal(acc_all[t + 1, i, :, :D_acc].reshape(N, C, D_acc), o["acceptor"]), (e, t)
-            assert np.array_equal(off_all[t + 1, i, :, :D_off].reshape(N, L, D_off), o["offer"]), (e, t)
-            assert np.array_equal(ra[t, i].reshape(N, C), r["acceptor"]), (e, t)
-            assert np.array_equal(ro[t, i].reshape(N, L), r["offer"]), (e, t)
-            if tr.free:
-                assert np.array_equal(rp[t, i].reshape(N, L), r["price"]), (e, t)
-
-
 def _cfg4_run(seed):
     tr = _tr().Trainer.from_named("cfg4", n_envs=8192, seed=seed, device="cuda:0")
     assert tr.arch == "divided" and tr.E == 8192 and tr.N == 16 and tr.C == 16
     return tr
+
+
+def _resync_ref(tr, u, g):
+    """A one-epoch RefPPO holding group g's current weights and HipAdam state (exp_avg, exp_avg_sq, step)."""
+    hp = tr.hp
+    ref = RefPPO(u.D, u.group.policy.A, hp.lr_actor, hp.lr_critic, u.group.gamma, hp.eps_clip, 1)
+    flat = ref.policy.flat()
+    with torch.no_grad():
+        for k, v in flat.items():
+            v.copy_(getattr(u.group.policy, k)[g].detach().cpu())
+    ref.policy.cuda()
+    opt = u.group.hip_optimizer
+    for k, v in flat.items():
+        st = opt.state[getattr(u.group.policy, k)]
+        ref.optimizer.state[v] = dict(step=torch.tensor(float(opt.step_count)), exp_avg=st["exp_avg"][g].clone(),
+                                      exp_avg_sq=st["exp_avg_sq"][g].clone())
+    return ref
+
+
+def _adam_replay(tr, k, w0, grad, m0, v0, step):
+    """torch.optim.Adam's step (PPOmodules.py:100-105 param groups) of one tensor from (w0, m0, v0, step)
+    with the given gradient: the weights the HIP Adam must produce from the HIP gradient."""
+    p = torch.nn.Parameter(w0.clone())
+    p.grad = grad.clone()
+    lr = tr.hp.lr_critic if k.startswith("c") else tr.hp.lr_actor
+    opt = torch.optim.Adam([p], lr=lr, foreach=False)
+    opt.state[p] = dict(step=torch.tensor(float(step)), exp_avg=m0.clone(), exp_avg_sq=v0.clone())
+    opt.step()
+    return p.detach()
+
+
+def _resynced_update(tr, picks, report):
+    """The trainer's fused update run step by step: the closures Trainer._epochs builds (the kernels the
+    update graph replays) and the HIP Adam. Before every (draw, epoch) step, group g of picks[name]
+    is re-synced into a RefPPO that takes the same step on the same rows (PPOmodules.py:144-168,
+    548-597): the step's loss within 1e-5 relative, its gradient within 1e-4 of each tensor's scale,
+    the HIP Adam's weights == torch's Adam formula on the HIP gradient (1e-6 relative), and the
+    weight delta against the reference's (1e-4 relative + 1e-4 lr absolute for at least 99 % of
+    the elements; the rest are near-cancelled gradients whose Adam step sign is noise, none beyond
+    2 lr)."""
+    ppo = _ppo()
+    keys = ppo.ACTOR_KEYS + ppo.CRITIC_KEYS
+    T = tr.T
+    sel = tr._draws()
+    all_sel = {k: torch.cat(v).to(torch.int32) for k, v in sel.items()}
+    counts = {k: [x.numel() for x in v] for k, v in sel.items()}
+    for u in tr.units():
+        seq = tr._epochs(u, all_sel[u.name], counts[u.name])
+        K = u.group.K
+        opt = u.group.hip_optimizer
+        pol = u.group.policy
+        for s, ep in enumerate(seq):
+            d = s // K
+            step0 = opt.step_count
+            before = {g: {k: (getattr(pol, k)[g].detach().clone(), opt.state[getattr(pol, k)]["exp_avg"][g].clone(),
+                              opt.state[getattr(pol, k)]["exp_avg_sq"][g].clone()) for k in keys}
+                      for g in picks[u.name]}
+            refs = {g: _resync_ref(tr, u, g) for g in picks[u.name]}
+            loss = ep().cpu()
+            grads = {g: {k: getattr(pol, k).grad[g].detach().clone() for k in keys} for g in picks[u.name]}
+            opt.step()
+            torch.cuda.synchronize()
+            for g in picks[u.name]:
+                unit = int(sel[u.name][d][g])
+                x, act, lp, rw = _unit_rows(tr, u, unit, T)
+                want, rgrad = refs[g].epoch(x, act, lp, _returns(rw, u.group.gamma).cuda())
+                tag = "%s group %d step %d" % (u.name, g, s)
+                rel = abs(float(loss[g]) - want) / max(abs(want), 1e-30)
+                np.testing.assert_allclose(float(loss[g]), want, rtol=1e-5, atol=1e-6, err_msg=tag)
+                gerr, dfrac = 0.0, 0.0
+                for k in keys:
+                    w0, m0, v0 = before[g][k]
+                    sc = rgrad[k].abs().max().item()
+                    e = (grads[g][k] - rgrad[k]).abs().max().item()
+                    gerr = max(gerr, e / max(sc, 1e-30))
+                    assert e <= 1e-4 * sc + 1e-9, (tag, k, e, sc)
+                    w1 = getattr(pol, k)[g].detach()
+                    want_w = _adam_replay(tr, k, w0, grads[g][k], m0, v0, step0)
+                    torch.testing.assert_close(w1, want_w, rtol=1e-6, atol=1e-9, msg=tag + " adam " + k)
+                    lr = tr.hp.lr_critic if k.startswith("c") else tr.hp.lr_actor
+                    dg, dr = w1 - w0, refs[g].policy.flat()[k].detach() - w0
+                    dd = (dg - dr).abs()
+                    loose = dd > 1e-4 * dr.abs() + 1e-4 * lr
+                    dfrac = max(dfrac, loose.float().mean().item())
+                    assert loose.float().mean().item() <= 0.01, (tag, k, int(loose.sum()))
+                    assert dd.max().item() <= 2 * lr + 1e-7, (tag, k, dd.max().item())
+                report.append("%s: loss %.6g rel err %.2e, grad err %.2e of scale, delta loose frac %.4f"
+                              % (tag, want, rel, gerr, dfrac))
+        u.group.last_losses = []
+        u.group.sync_old()
+    tr._carry_last_observation()
+
+
+def test_cfg3_every_update_step_resynced(ms):
+    tr = _tr().Trainer.from_named("cfg3", seed=9, device="cuda:0")
+    tr.rollout()
+    torch.cuda.synchronize()
+    assert tr.flags() == 0
+    report = []
+    _resynced_update(tr, {u.name: (0, 5) for u in tr.units()}, report)
+    print("\n".join(report))
+    assert len(report) == 2 * sum(tr.hp.centralisation_sample * u.group.K for u in tr.units())
+
+
+def test_cfg4_every_update_step_resynced(ms):
+    tr = _cfg4_run(13)
+    tr.rollout()
+    torch.cuda.synchronize()
+    assert tr.flags() == 0
+    report = []
+    _resynced_update(tr, dict(acceptor=(37,), offer=(5,), price=(20,)), report)
+    print("\n".join(report))
+    assert len(report) == sum(u.group.K for u in tr.units())
 
 
 def test_cfg4_fullsize_iteration(ms):
