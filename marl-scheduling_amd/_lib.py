@@ -111,7 +111,7 @@ def _load():
     version = L.ms_abi_version()
     # ABI 14 added ms_bdqn_update*, 15 ms_bdqn_act_compact, 16 ms_mlp_params.row_base (a trailing field an
     # older library does not read: its acting draws are those of row_base 0). An older library (an A/B variant built
-    # before them, tools/ab_variant.sh) loads without them only when MARLSCHED_LENIENT_ABI=1 asks for it
+    # before them, tools/gpu_job.sh ab step) loads without them only when MARLSCHED_LENIENT_ABI=1 asks for it
     lenient = os.environ.get("MARLSCHED_LENIENT_ABI") == "1" and version in (13, 14, 15)
     if version != ABI_VERSION and not lenient:
         raise ImportError("libmarlsched.so ABI version mismatch (%d, want %d)" % (version, ABI_VERSION))

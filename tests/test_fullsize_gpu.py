@@ -158,20 +158,36 @@ def _cfg4_run(seed):
 
 
 def _resync_ref(tr, u, g):
-    """A one-epoch RefPPO holding group g's current weights and HipAdam state (exp_avg, exp_avg_sq, step)."""
+    """A one-epoch RefPPO in float64 holding group g's current weights and HipAdam state (exp_avg,
+    exp_avg_sq, step): its loss and gradient carry no rounding error of their own at this scale."""
     hp = tr.hp
     ref = RefPPO(u.D, u.group.policy.A, hp.lr_actor, hp.lr_critic, u.group.gamma, hp.eps_clip, 1)
+    ref.policy.double()
     flat = ref.policy.flat()
     with torch.no_grad():
         for k, v in flat.items():
-            v.copy_(getattr(u.group.policy, k)[g].detach().cpu())
+            v.copy_(getattr(u.group.policy, k)[g].detach().cpu().double())
     ref.policy.cuda()
     opt = u.group.hip_optimizer
     for k, v in flat.items():
         st = opt.state[getattr(u.group.policy, k)]
-        ref.optimizer.state[v] = dict(step=torch.tensor(float(opt.step_count)), exp_avg=st["exp_avg"][g].clone(),
-                                      exp_avg_sq=st["exp_avg_sq"][g].clone())
+        ref.optimizer.state[v] = dict(step=torch.tensor(float(opt.step_count)), exp_avg=st["exp_avg"][g].double(),
+                                      exp_avg_sq=st["exp_avg_sq"][g].double())
     return ref
+
+
+def _assert_resynced(report):
+    """The per-step bars of _resynced_update over every recorded step."""
+    for st in report:
+        tag = st["tag"]
+        np.testing.assert_allclose(st["loss"], st["want"], rtol=1e-5, atol=1e-6, err_msg=tag)
+        net_scale = max(sc for _, sc in st["grad"].values())
+        for k, (e, sc) in st["grad"].items():
+            assert e <= 1e-4 * net_scale, (tag, k, e, sc, net_scale)
+        for k, v in st["adam"].items():
+            assert v[0] <= 1e-6 * max(abs(v[1]), 1e-3), (tag, k) + v
+        for k, (frac, dmax, lr) in st["delta"].items():
+            assert frac <= 0.01 and dmax <= 2 * lr + 1e-7, (tag, k, frac, dmax)
 
 
 def _adam_replay(tr, k, w0, grad, m0, v0, step):
@@ -220,29 +236,36 @@ def _resynced_update(tr, picks, report):
             for g in picks[u.name]:
                 unit = int(sel[u.name][d][g])
                 x, act, lp, rw = _unit_rows(tr, u, unit, T)
-                want, rgrad = refs[g].epoch(x, act, lp, _returns(rw, u.group.gamma).cuda())
+                want, rgrad = refs[g].epoch(x.double(), act, lp.double(), _returns(rw, u.group.gamma).cuda().double())
                 tag = "%s group %d step %d" % (u.name, g, s)
                 rel = abs(float(loss[g]) - want) / max(abs(want), 1e-30)
-                np.testing.assert_allclose(float(loss[g]), want, rtol=1e-5, atol=1e-6, err_msg=tag)
-                gerr, dfrac = 0.0, 0.0
+                st = dict(tag=tag, loss=float(loss[g]), want=want, rel=rel, grad={}, adam={}, delta={})
                 for k in keys:
                     w0, m0, v0 = before[g][k]
                     sc = rgrad[k].abs().max().item()
-                    e = (grads[g][k] - rgrad[k]).abs().max().item()
-                    gerr = max(gerr, e / max(sc, 1e-30))
-                    assert e <= 1e-4 * sc + 1e-9, (tag, k, e, sc)
+                    e = (grads[g][k].double() - rgrad[k]).abs().max().item()
+                    st["grad"][k] = (e, sc)
                     w1 = getattr(pol, k)[g].detach()
                     want_w = _adam_replay(tr, k, w0, grads[g][k], m0, v0, step0)
-                    torch.testing.assert_close(w1, want_w, rtol=1e-6, atol=1e-9, msg=tag + " adam " + k)
+                    da = (w1 - want_w).abs()
+                    i = int(da.argmax())
+                    st["adam"][k] = (da.max().item(), float(w0.flatten()[i]), float(w1.flatten()[i]),
+                                     float(want_w.flatten()[i]), float(grads[g][k].flatten()[i]),
+                                     float(m0.flatten()[i]), float(v0.flatten()[i]), step0)
                     lr = tr.hp.lr_critic if k.startswith("c") else tr.hp.lr_actor
-                    dg, dr = w1 - w0, refs[g].policy.flat()[k].detach() - w0
+                    dg, dr = (w1 - w0).double(), refs[g].policy.flat()[k].detach() - w0.double()
                     dd = (dg - dr).abs()
                     loose = dd > 1e-4 * dr.abs() + 1e-4 * lr
-                    dfrac = max(dfrac, loose.float().mean().item())
-                    assert loose.float().mean().item() <= 0.01, (tag, k, int(loose.sum()))
-                    assert dd.max().item() <= 2 * lr + 1e-7, (tag, k, dd.max().item())
-                report.append("%s: loss %.6g rel err %.2e, grad err %.2e of scale, delta loose frac %.4f"
-                              % (tag, want, rel, gerr, dfrac))
+                    st["delta"][k] = (loose.float().mean().item(), dd.max().item(), lr)
+                report.append(st)
+                print("%s: loss %.7g want %.7g rel %.2e | grad err/scale %s | adam max %s | delta loose %s" % (
+                    tag, st["loss"], want, rel,
+                    " ".join("%s %.1e/%.1e" % (k, *v) for k, v in st["grad"].items()),
+                    " ".join("%s %.1e" % (k, v[0]) for k, v in st["adam"].items()),
+                    " ".join("%s %.4f/%.1e" % (k, v[0], v[1]) for k, v in st["delta"].items())), flush=True)
+                worst = max(st["adam"].items(), key=lambda kv: kv[1][0])
+                print("   worst adam %s: d %.3e w0 %.9g w1 %.9g want %.9g g %.3e m0 %.3e v0 %.3e step %d"
+                      % ((worst[0],) + worst[1]), flush=True)
         u.group.last_losses = []
         u.group.sync_old()
     tr._carry_last_observation()
@@ -255,7 +278,7 @@ def test_cfg3_every_update_step_resynced(ms):
     assert tr.flags() == 0
     report = []
     _resynced_update(tr, {u.name: (0, 5) for u in tr.units()}, report)
-    print("\n".join(report))
+    _assert_resynced(report)
     assert len(report) == 2 * sum(tr.hp.centralisation_sample * u.group.K for u in tr.units())
 
 
@@ -266,7 +289,7 @@ def test_cfg4_every_update_step_resynced(ms):
     assert tr.flags() == 0
     report = []
     _resynced_update(tr, dict(acceptor=(37,), offer=(5,), price=(20,)), report)
-    print("\n".join(report))
+    _assert_resynced(report)
     assert len(report) == sum(u.group.K for u in tr.units())
 
 

@@ -2,6 +2,7 @@
 # Alternating cfg3 bench lines with an environment knob set (A) and unset (B) on one box (via gpurun).
 # Usage: bash tools/ab_knob.sh <tag> "<VAR=value ...>" [rounds]
 set -euo pipefail
+export MARLSCHED_LENIENT_ABI=1  # variants built at an older ABI load without the newer entry points
 TAG="$1"; KNOB="$2"; N="${3:-2}"
 R="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
 O="$R/gpurun_out/$TAG"

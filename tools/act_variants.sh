@@ -2,6 +2,7 @@
 # tools/act_cost.py under library variants (tools/_variants/<name>/libmarlsched.so) and the in-tree
 # library, on one box (via gpurun). Usage: bash tools/act_variants.sh <tag> "<variant names>"
 set -euo pipefail
+export MARLSCHED_LENIENT_ABI=1  # variants built at an older ABI load without the newer entry points
 TAG="$1"; VARS="$2"
 R="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
 O="$R/gpurun_out/$TAG"

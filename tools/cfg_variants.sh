@@ -3,6 +3,7 @@
 # (tools/_variants/<name>/libmarlsched.so) and the in-tree library, one box (via gpurun).
 # Usage: bash tools/cfg_variants.sh <tag> <config> "<variant names>" [kernel name regex]
 set -euo pipefail
+export MARLSCHED_LENIENT_ABI=1  # variants built at an older ABI load without the newer entry points
 TAG="$1"; CFG="$2"; VARS="$3"; RX="${4:-k_ppo_grad|k_act|k_env_step}"
 R="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
 O="$R/gpurun_out/$TAG"

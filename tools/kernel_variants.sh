@@ -3,6 +3,7 @@
 # library variants (tools/_variants/<name>/libmarlsched.so) and the in-tree library, one box (via gpurun).
 # Usage: bash tools/kernel_variants.sh <tag> "<variant names>" [kernel name regex for the summary]
 set -euo pipefail
+export MARLSCHED_LENIENT_ABI=1  # variants built at an older ABI load without the newer entry points
 TAG="$1"; VARS="$2"; RX="${3:-k_ppo_grad|k_act|k_env_step|k_key|k_unit}"
 R="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
 O="$R/gpurun_out/$TAG"
