@@ -26,6 +26,34 @@
 
 namespace ms {
 
+// Profiling build only (tools/build_act_probe.sh: -DMS_ACT_PROBE): lane 0 of every wave of the paired act
+// kernel adds the shader-clock cycles between consecutive marks to a per-(half, phase) counter. The product
+// library is built without it and the marks compile to nothing.
+#if defined(MS_ACT_PROBE) && (defined(MS_ACT_PAIR_TU) || !defined(MS_SPLIT_PAIR))
+#define MS_ACT_PROBE_ON 1
+__device__ unsigned long long g_act_cycles[2][17];  // [offer / acceptor half][phase 0..15, waves]
+#define MS_AMARK(k)                                                    \
+    do {                                                               \
+        const uint64_t t_now = __builtin_amdgcn_s_memtime();          \
+        t_acc[k] += t_now - t_prev;                                    \
+        t_prev = t_now;                                                \
+    } while (0)
+#define MS_APROBE_BEGIN                                                \
+    uint64_t t_prev = __builtin_amdgcn_s_memtime();                    \
+    uint64_t t_acc[16] = {};
+#define MS_APROBE_END(half)                                            \
+    if (lane == 0) {                                                   \
+        for (int k = 0; k < 16; k++) atomicAdd(&g_act_cycles[half][k], (unsigned long long)t_acc[k]); \
+        atomicAdd(&g_act_cycles[half][16], 1ull);                      \
+    }
+#else
+#define MS_AMARK(k) \
+    do {            \
+    } while (0)
+#define MS_APROBE_BEGIN
+#define MS_APROBE_END(half)
+#endif
+
 typedef float f4 __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ f4 mfma4(float a, float b, f4 c) { return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0); }
 
@@ -509,6 +537,7 @@ __device__ __forceinline__ void act_tiles(const ActArgs& a, int block) {
     const int grp = gw / a.waves_per_group;
     const int wv = gw - grp * a.waves_per_group;
     if (grp >= a.n1.n_groups) return;
+    MS_APROBE_BEGIN
     const int j = lane & 15, g4 = lane >> 4;
     constexpr int NP = NT2 > 0 ? NT2 : 1;
     constexpr int TW = PriceTW<NP>::v;
@@ -696,6 +725,38 @@ __device__ __forceinline__ void act_tiles(const ActArgs& a, int block) {
         if (t0 + i < t1) load_rows(row[i], pre[i]);
     }
     bool any_miss = false;  // a pair with a price input outside the table: priced after the loop
+    // the tabulated price chooser of the previous pair, sampled one pair late (its table entries in registers)
+    bool pend = false;
+    int p_cur[2], p_act[2], p_pin[2], p_lnz[2];
+    float p_u2[2], p_S2[2], p_cum[2][NP][4], p_lpv[2][NP][4];
+    auto price_finish = [&]() {
+        int cnt[2], pact[2];
+        float plp[2];
+#pragma unroll
+        for (int i = 0; i < 2; i++) {
+            const float target = p_u2[i] * p_S2[i];
+            cnt[i] = 0;
+#pragma unroll
+            for (int t = 0; t < NP; t++)
+#pragma unroll
+                for (int q = 0; q < 4; q++) cnt[i] += (p_cum[i][t][q] <= target) ? 1 : 0;
+        }
+        rows_sum2_i(cnt[0], cnt[1]);
+        // the chosen action's log-prob: the one lane of the row holding it contributes it, the others 0
+        // (a sum of zeros and one value: the table entry bit for bit)
+#pragma unroll
+        for (int i = 0; i < 2; i++) {
+            pact[i] = cnt[i] >= a.n2.n_actions ? p_lnz[i] : cnt[i];
+            plp[i] = 0.f;
+#pragma unroll
+            for (int t = 0; t < NP; t++)
+#pragma unroll
+                for (int q = 0; q < 4; q++) plp[i] = (16 * t + 4 * g4 + q == pact[i]) ? p_lpv[i][t][q] : plp[i];
+        }
+        rows_sum2(plp[0], plp[1]);
+        price_out2(p_cur, p_act, p_pin, pact, plp);
+    };
+    MS_AMARK(0);  // setup: weights / fragments, the price digits, the first rows' loads issued
     for (int tile = t0; tile < t1; tile += 2) {
         uint32_t xd[2][S1][2];
         int cur[2];
@@ -710,61 +771,66 @@ __device__ __forceinline__ void act_tiles(const ActArgs& a, int block) {
             row[i] = tile + 2 + i < t1 ? row_of(tile + 2 + i) : -1;
             if (tile + 2 + i < t1) load_rows(row[i], pre[i]);
         }
+        MS_AMARK(1);  // row indices + the next pair's loads issued
         float u1[2], u2[2];
         uniforms2(tile, cur, u1, u2);
+        MS_AMARK(2);  // Philox
         int act[2];
         float lp[2];
         core2(xd, u1, act, lp);
+        MS_AMARK(3);  // core chooser (layer 1 waits for this pair's rows)
         if (NT2 > 0) {
             int pin[2], dg[2];
             price_in2(xd, cur, act, pin, dg);
             if (a.ptab && __ballot(dg[0] < 0 || dg[1] < 0) == 0ull) {
-                // every row of both tiles is tabulated: sample from the table (Head::run's arithmetic)
+                // every row of both tiles is tabulated: the table entries' loads are issued now and
+                // the pair is sampled one pair later (price_finish), so their latency overlaps the
+                // next pair's core chooser
                 rows_sum2_i(dg[0], dg[1]);
-                float cum[2][NP][4], S2[2];
-                int lnz[2], cnt[2], pact[2];
-                float plp[2];
-                uint32_t te[2];  // byte offset of the row's table entry
+                float n_cum[2][NP][4], n_lpv[2][NP][4], n_S2[2];
+                int n_lnz[2];
 #pragma unroll
                 for (int i = 0; i < 2; i++) {
-                    te[i] = __umul24((uint32_t)dg[i], 4u * TW);
+                    const uint32_t te = __umul24((uint32_t)dg[i], 4u * TW);  // byte offset of the row's entry
 #pragma unroll
                     for (int t = 0; t < NP; t++) {
-                        const auto c4 = __builtin_amdgcn_raw_buffer_load_b128(tab_b.r, (int)(te[i] + 4 * (16 * t + 4 * g4)), 0, 0);
+                        const auto c4 = __builtin_amdgcn_raw_buffer_load_b128(tab_b.r, (int)(te + 4 * (16 * t + 4 * g4)), 0, 0);
+                        const auto l4 = __builtin_amdgcn_raw_buffer_load_b128(
+                            tab_b.r, (int)(te + 4 * (16 * NP + 16 * t + 4 * g4)), 0, 0);
 #pragma unroll
-                        for (int q = 0; q < 4; q++) cum[i][t][q] = __uint_as_float(c4[q]);
+                        for (int q = 0; q < 4; q++) {
+                            n_cum[i][t][q] = __uint_as_float(c4[q]);
+                            n_lpv[i][t][q] = __uint_as_float(l4[q]);
+                        }
                     }
-                    S2[i] = tab_b.ldf(te[i] + 4 * (32 * NP));
-                    lnz[i] = (int)tab_b.ld32(te[i] + 4 * (32 * NP + 1));
+                    n_S2[i] = tab_b.ldf(te + 4 * (32 * NP));
+                    n_lnz[i] = (int)tab_b.ld32(te + 4 * (32 * NP + 1));
                 }
+                if (pend) price_finish();
+                pend = true;
 #pragma unroll
                 for (int i = 0; i < 2; i++) {
-                    const float target = u2[i] * S2[i];
-                    cnt[i] = 0;
+                    p_cur[i] = cur[i], p_act[i] = act[i], p_pin[i] = pin[i], p_u2[i] = u2[i];
+                    p_S2[i] = n_S2[i], p_lnz[i] = n_lnz[i];
 #pragma unroll
                     for (int t = 0; t < NP; t++)
 #pragma unroll
-                        for (int q = 0; q < 4; q++) cnt[i] += (cum[i][t][q] <= target) ? 1 : 0;
+                        for (int q = 0; q < 4; q++) p_cum[i][t][q] = n_cum[i][t][q], p_lpv[i][t][q] = n_lpv[i][t][q];
                 }
-                rows_sum2_i(cnt[0], cnt[1]);
-                // the chosen action's log-prob straight from its table entry (one load per row)
-#pragma unroll
-                for (int i = 0; i < 2; i++) {
-                    pact[i] = cnt[i] >= a.n2.n_actions ? lnz[i] : cnt[i];
-                    plp[i] = tab_b.ldf(te[i] + 4 * (16 * NP + pact[i]));
-                }
-                price_out2(cur, act, pin, pact, plp);
             } else {
                 any_miss = true;
             }
         }
+        MS_AMARK(4);  // price chooser: input, table entry, sample, its stores
 #pragma unroll
         for (int i = 0; i < 2; i++)
             if (cur[i] >= 0 && g4 == 0) {
                 act_b.st8((uint32_t)cur[i], act[i]);
                 lp_b.stf(4 * (uint32_t)cur[i], lp[i]);
             }
+        MS_AMARK(5);  // core chooser stores
     }
+    if (NT2 > 0 && pend) price_finish();
     if (NT2 > 0 && any_miss) {
         // the pairs the table could not serve (or every pair, without a table): the same pairs and
         // draws again, the core chooser recomputed (bit-identical), then the price net itself; its
@@ -796,6 +862,8 @@ __device__ __forceinline__ void act_tiles(const ActArgs& a, int block) {
             price_out2(cur, act, pin, pact, plp);
         }
     }
+    MS_AMARK(6);  // untabulated price inputs
+    MS_APROBE_END(0)
 }
 
 // ---------------------------------------------------------------------------
@@ -848,6 +916,7 @@ __device__ __forceinline__ void act_common_rows(const ActArgs& a, int block) {
     const int grp = gw / a.waves_per_group;
     const int wv = gw - grp * a.waves_per_group;
     if (grp >= a.n1.n_groups) return;  // whole waves only: the kernel has no block barrier
+    MS_APROBE_BEGIN
     const int j = lane & 15, g4 = lane >> 4;
     const int A = a.n1.n_actions;
     const int stride4 = a.stride >> 2;
@@ -945,7 +1014,9 @@ __device__ __forceinline__ void act_common_rows(const ActArgs& a, int block) {
     auto scan_step = [&](int i0, int row, bool in, bool common) {
         // every lane draws (the lanes of listed rows keep theirs for the tile pass: no second draw
         // there, and no lane-group-replicated one)
+        MS_AMARK(2);  // (scan bookkeeping)
         const float u = step_uniform(i0, row);
+        MS_AMARK(3);  // Philox (every other step)
         if (common) {
             const float target = u * S;
             // the number of running sums <= target (Head::run's count), by binary search
@@ -964,7 +1035,9 @@ __device__ __forceinline__ void act_common_rows(const ActArgs& a, int block) {
             ulist[n_list + __popcll(m & below)] = u;
         }
         n_list += __popcll(m);
+        MS_AMARK(4);  // table search, stores, row list
     };
+    MS_AMARK(0);  // setup: fragments, the common row's table
     if constexpr (OWN) {
         // compact rows: every step's owner byte is loaded up front (one memory round trip per wave)
         constexpr int MS = kCommonSeg / 64;
@@ -979,6 +1052,7 @@ __device__ __forceinline__ void act_common_rows(const ActArgs& a, int block) {
             own_st[st] = a.owner[cr];
             me_st[st] = (int8_t)(ag + 1);
         }
+        MS_AMARK(1);  // owner loads issued
 #pragma unroll
         for (int st = 0; st < MS; st++)
             if (i_begin + 64 * st < i_end)
@@ -1026,6 +1100,7 @@ __device__ __forceinline__ void act_common_rows(const ActArgs& a, int block) {
 #pragma unroll
     for (int i = 0; i < 2; i++)
         if (16 * i < n_list) load_tile(i, 16 * i);
+    MS_AMARK(5);  // list barrier + first tiles' loads issued
     for (int t0 = 0; t0 < n_list; t0 += 32) {
         int row[2];
         float u[2];
@@ -1048,16 +1123,20 @@ __device__ __forceinline__ void act_common_rows(const ActArgs& a, int block) {
             u[i] = t_u[i];
             if (t0 + 32 + 16 * i < n_list) load_tile(i, t0 + 32 + 16 * i);
         }
+        MS_AMARK(6);  // listed rows: layer 1 (waits for their loads), the next pair's loads issued
         int act[2];
         float lp[2];
         h1.run2(acc, A, g4, u, act, lp);
+        MS_AMARK(7);  // listed rows: layers 2-3, softmax, sample
 #pragma unroll
         for (int i = 0; i < 2; i++)
             if (row[i] >= 0 && g4 == 0) {
                 a.action[row[i]] = (int8_t)act[i];
                 a.logprob[row[i]] = lp[i];
             }
+        MS_AMARK(8);  // listed rows' stores
     }
+    MS_APROBE_END(1)
 }
 
 // launch-shape knobs for measurements (tools/); the defaults are the measured best for cfg3
@@ -1436,6 +1515,17 @@ hipError_t launch_act_round(const ms_mlp_params* core, const ms_mlp_params* pric
     hipLaunchKernelGGL((k_act_pair<1, 1, 1, 2, 2>), dim3(ob + cb), dim3(256), 0, st, o, c, (int)ob);
     return hipGetLastError();
 }
+#ifdef MS_ACT_PROBE_ON
+// profiling build only: the paired act kernel's per-phase cycles, out[2][17] (the last column: waves)
+extern "C" int ms_probe_act_cycles(unsigned long long* out, int clear) {
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_act_cycles), sizeof(g_act_cycles)) != hipSuccess) return -1;
+    if (clear) {
+        static const unsigned long long zero[2][17] = {};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(g_act_cycles), zero, sizeof(zero)) != hipSuccess) return -1;
+    }
+    return 0;
+}
+#endif
 #endif
 
 }  // namespace ms
