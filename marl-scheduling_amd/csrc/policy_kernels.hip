@@ -965,6 +965,10 @@ __device__ __forceinline__ void act_common_rows(const ActArgs& a, int block) {
         if ((e + 1) * a.S <= i) e++;
         return e * a.U + grp * a.S + (i - e * a.S);
     };
+    // the outputs as raw buffers: 32-bit row offsets, no 64-bit address arithmetic per store
+    // (act_common_fits: E * U * 4 bytes < 2^31)
+    const long long n_rows = (long long)a.E * a.U;
+    const RawBuf act_b(a.action, n_rows), lp_b(a.logprob, 4 * n_rows);
     const int i_begin = wv * a.items_per_wave;
     const int i_end = min(i_begin + a.items_per_wave, a.n_items);  // <= kCommonSeg rows
     // Item i's uniform: word (i >> 6) & 1 of the Philox draw countered by the row of item i & ~64, so
@@ -1025,8 +1029,8 @@ __device__ __forceinline__ void act_common_rows(const ActArgs& a, int block) {
             for (int step = 16 * NT; step >= 1; step >>= 1)
                 if (cnt + step <= 16 * NT && cum[cnt + step - 1] <= target) cnt += step;
             const int act = cnt >= A ? last_nz : cnt;
-            a.action[row] = (int8_t)act;
-            a.logprob[row] = s_lp[wid][act];
+            act_b.st8((uint32_t)row, act);
+            lp_b.stf(4 * (uint32_t)row, s_lp[wid][act]);
         }
         const bool other = in && !common;
         const uint64_t m = __ballot(other);
@@ -1043,14 +1047,24 @@ __device__ __forceinline__ void act_common_rows(const ActArgs& a, int block) {
         constexpr int MS = kCommonSeg / 64;
         int8_t own_st[MS], me_st[MS];
         int row_st[MS];
+        // a group of exactly one agent's C acceptors (locally shared: S == C, unit a*C + c): item i of
+        // group g is core row i (replica i / C, core i % C) and the agent is g, so the core row and the
+        // owner byte need no per-item quotient
+        const bool agent_group = a.S == a.n_cores;
+        const RawBuf own_b(a.owner, (long long)a.E * a.n_cores);
 #pragma unroll
         for (int st = 0; st < MS; st++) {
             const int i = i_begin + 64 * st + lane;
             row_st[st] = i < i_end ? row_of_item(i) : -1;
-            int ag;
-            const size_t cr = core_row_of(row_st[st] < 0 ? 0 : row_st[st], ag);
-            own_st[st] = a.owner[cr];
-            me_st[st] = (int8_t)(ag + 1);
+            if (agent_group) {
+                own_st[st] = (int8_t)own_b.ld8s((uint32_t)(i < i_end ? i : 0));
+                me_st[st] = (int8_t)(grp + 1);
+            } else {
+                int ag;
+                const size_t cr = core_row_of(row_st[st] < 0 ? 0 : row_st[st], ag);
+                own_st[st] = a.owner[cr];
+                me_st[st] = (int8_t)(ag + 1);
+            }
         }
         MS_AMARK(1);  // owner loads issued
 #pragma unroll
@@ -1131,8 +1145,8 @@ __device__ __forceinline__ void act_common_rows(const ActArgs& a, int block) {
 #pragma unroll
         for (int i = 0; i < 2; i++)
             if (row[i] >= 0 && g4 == 0) {
-                a.action[row[i]] = (int8_t)act[i];
-                a.logprob[row[i]] = lp[i];
+                act_b.st8((uint32_t)row[i], act[i]);
+                lp_b.stf(4 * (uint32_t)row[i], lp[i]);
             }
         MS_AMARK(8);  // listed rows' stores
     }
@@ -1175,8 +1189,14 @@ static unsigned act_common_blocks(ActArgs& a, long long target) {
     return (unsigned)((waves + 3) / 4);
 }
 
+// act_common_rows stores through 31-bit byte offsets (RawBuf) and reads compact owners by item index
+static bool act_common_fits(const ActArgs& a) {
+    return (long long)a.E * a.U * 4 <= 0x7fffffffll && (long long)a.E * (a.n_cores > 0 ? a.n_cores : 1) <= 0x7fffffffll;
+}
+
 template <int S1, int NT>
 static hipError_t launch_act_common_t(ActArgs& a, hipStream_t st) {
+    if (!act_common_fits(a)) return hipErrorInvalidValue;
     auto kern = a.owner ? (a.uniforms ? k_act_common<S1, NT, true, true> : k_act_common<S1, NT, false, true>)
                         : (a.uniforms ? k_act_common<S1, NT, true, false> : k_act_common<S1, NT, false, false>);
     static const long long target = env_int("MS_ACT_COMMON_WAVES", 1536);  // measured best for cfg3 alone
@@ -1503,7 +1523,7 @@ hipError_t launch_act_round(const ms_mlp_params* core, const ms_mlp_params* pric
                              acc_offset, offset_dev, nullptr, acc_action, acc_logprob);
     const bool paired = (off_stride + 31) / 32 == 1 && core->n_actions <= 16 && price->n_actions <= 16 &&
                         (acc_stride + 31) / 32 == 2 && acc->n_actions <= 32 && !env_int("MS_ACT_UNPAIRED", 0);
-    if (paired && !act_tiles_fits(o)) return hipErrorInvalidValue;
+    if (paired && (!act_tiles_fits(o) || !act_common_fits(c))) return hipErrorInvalidValue;
     if (!paired) {
         hipError_t e = dispatch_act(o, st);
         return e != hipSuccess ? e : dispatch_act(c, st);
