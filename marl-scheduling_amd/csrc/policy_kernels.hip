@@ -20,6 +20,7 @@
 #include <hip/hip_runtime.h>
 #include <math.h>
 #include <stdlib.h>
+#include <string.h>
 
 #include "../../include/marlsched.h"
 #include "ms_common.h"
@@ -31,7 +32,11 @@ namespace ms {
 // library is built without it and the marks compile to nothing.
 #if defined(MS_ACT_PROBE) && (defined(MS_ACT_PAIR_TU) || !defined(MS_SPLIT_PAIR))
 #define MS_ACT_PROBE_ON 1
-__device__ unsigned long long g_act_cycles[2][17];  // [offer / acceptor half][phase 0..15, waves]
+constexpr int kActProbeWaves = 1 << 14;
+// per wave slot [half][wave % kActProbeWaves][phase] (plain stores of lane 0: no shared address, so the
+// probe's own writes do not queue behind each other in the memory system), summed on the host
+__device__ unsigned long long g_act_cycles[2][kActProbeWaves][16];
+__device__ unsigned long long g_act_waves[2][kActProbeWaves];
 #define MS_AMARK(k)                                                    \
     do {                                                               \
         const uint64_t t_now = __builtin_amdgcn_s_memtime();          \
@@ -43,8 +48,9 @@ __device__ unsigned long long g_act_cycles[2][17];  // [offer / acceptor half][p
     uint64_t t_acc[16] = {};
 #define MS_APROBE_END(half)                                            \
     if (lane == 0) {                                                   \
-        for (int k = 0; k < 16; k++) atomicAdd(&g_act_cycles[half][k], (unsigned long long)t_acc[k]); \
-        atomicAdd(&g_act_cycles[half][16], 1ull);                      \
+        const int slot = (block * 4 + (threadIdx.x >> 6)) % kActProbeWaves; \
+        for (int k = 0; k < 16; k++) g_act_cycles[half][slot][k] += t_acc[k]; \
+        g_act_waves[half][slot] += 1ull;                               \
     }
 #else
 #define MS_AMARK(k) \
@@ -1538,10 +1544,21 @@ hipError_t launch_act_round(const ms_mlp_params* core, const ms_mlp_params* pric
 #ifdef MS_ACT_PROBE_ON
 // profiling build only: the paired act kernel's per-phase cycles, out[2][17] (the last column: waves)
 extern "C" int ms_probe_act_cycles(unsigned long long* out, int clear) {
-    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_act_cycles), sizeof(g_act_cycles)) != hipSuccess) return -1;
+    static unsigned long long cyc[2][kActProbeWaves][16], waves[2][kActProbeWaves];
+    if (hipMemcpyFromSymbol(cyc, HIP_SYMBOL(g_act_cycles), sizeof(cyc)) != hipSuccess) return -1;
+    if (hipMemcpyFromSymbol(waves, HIP_SYMBOL(g_act_waves), sizeof(waves)) != hipSuccess) return -1;
+    for (int h = 0; h < 2; h++) {
+        for (int k = 0; k < 17; k++) out[17 * h + k] = 0;
+        for (int w = 0; w < kActProbeWaves; w++) {
+            for (int k = 0; k < 16; k++) out[17 * h + k] += cyc[h][w][k];
+            out[17 * h + 16] += waves[h][w];
+        }
+    }
     if (clear) {
-        static const unsigned long long zero[2][17] = {};
-        if (hipMemcpyToSymbol(HIP_SYMBOL(g_act_cycles), zero, sizeof(zero)) != hipSuccess) return -1;
+        memset(cyc, 0, sizeof(cyc));
+        memset(waves, 0, sizeof(waves));
+        if (hipMemcpyToSymbol(HIP_SYMBOL(g_act_cycles), cyc, sizeof(cyc)) != hipSuccess) return -1;
+        if (hipMemcpyToSymbol(HIP_SYMBOL(g_act_waves), waves, sizeof(waves)) != hipSuccess) return -1;
     }
     return 0;
 }
