@@ -120,12 +120,6 @@ inline constexpr Geom make_geom(int32_t n_agents, int32_t n_cores, int32_t coll_
     p.s_slotpair = p.s_otmpl + p.off_stride;
     p.scratch_bytes = align16(p.s_slotpair + 2 * p.NL);
     s += p.scratch_bytes;
-    // The envs of one wave own LDS slices s_total bytes apart, and ds_read/write_b32 serve lanes 0-31
-    // (two 16-lane envs) together with bank = dword mod 32: a slice stride of 16 banks mod 32
-    // (s_total = 64 mod 128 bytes) keeps the two envs' 16-lane accesses of one field in distinct banks.
-#ifndef MS_ENV_NO_LDS_PAD
-    s += (64 - s % 128 + 128) % 128;
-#endif
     p.s_total = s;
     p.mag_acc = magic_div(p.acc_stride / 4);
     p.mag_off = magic_div(p.off_stride / 4);

@@ -27,6 +27,7 @@
 
 namespace ms {
 
+
 // Profiling build only (tools/build_act_probe.sh: -DMS_ACT_PROBE): lane 0 of every wave of the paired act
 // kernel adds the shader-clock cycles between consecutive marks to a per-(half, phase) counter. The product
 // library is built without it and the marks compile to nothing.
@@ -731,37 +732,6 @@ __device__ __forceinline__ void act_tiles(const ActArgs& a, int block) {
         if (t0 + i < t1) load_rows(row[i], pre[i]);
     }
     bool any_miss = false;  // a pair with a price input outside the table: priced after the loop
-    // the tabulated price chooser of the previous pair, sampled one pair late (its table entries in registers)
-    bool pend = false;
-    int p_cur[2], p_act[2], p_pin[2], p_lnz[2];
-    float p_u2[2], p_S2[2], p_cum[2][NP][4], p_lpv[2][NP][4];
-    auto price_finish = [&]() {
-        int cnt[2], pact[2];
-        float plp[2];
-#pragma unroll
-        for (int i = 0; i < 2; i++) {
-            const float target = p_u2[i] * p_S2[i];
-            cnt[i] = 0;
-#pragma unroll
-            for (int t = 0; t < NP; t++)
-#pragma unroll
-                for (int q = 0; q < 4; q++) cnt[i] += (p_cum[i][t][q] <= target) ? 1 : 0;
-        }
-        rows_sum2_i(cnt[0], cnt[1]);
-        // the chosen action's log-prob: the one lane of the row holding it contributes it, the others 0
-        // (a sum of zeros and one value: the table entry bit for bit)
-#pragma unroll
-        for (int i = 0; i < 2; i++) {
-            pact[i] = cnt[i] >= a.n2.n_actions ? p_lnz[i] : cnt[i];
-            plp[i] = 0.f;
-#pragma unroll
-            for (int t = 0; t < NP; t++)
-#pragma unroll
-                for (int q = 0; q < 4; q++) plp[i] = (16 * t + 4 * g4 + q == pact[i]) ? p_lpv[i][t][q] : plp[i];
-        }
-        rows_sum2(plp[0], plp[1]);
-        price_out2(p_cur, p_act, p_pin, pact, plp);
-    };
     MS_AMARK(0);  // setup: weights / fragments, the price digits, the first rows' loads issued
     for (int tile = t0; tile < t1; tile += 2) {
         uint32_t xd[2][S1][2];
@@ -789,40 +759,41 @@ __device__ __forceinline__ void act_tiles(const ActArgs& a, int block) {
             int pin[2], dg[2];
             price_in2(xd, cur, act, pin, dg);
             if (a.ptab && __ballot(dg[0] < 0 || dg[1] < 0) == 0ull) {
-                // every row of both tiles is tabulated: the table entries' loads are issued now and
-                // the pair is sampled one pair later (price_finish), so their latency overlaps the
-                // next pair's core chooser
+                // every row of both tiles is tabulated: sample from the table (Head::run's arithmetic)
                 rows_sum2_i(dg[0], dg[1]);
-                float n_cum[2][NP][4], n_lpv[2][NP][4], n_S2[2];
-                int n_lnz[2];
+                float cum[2][NP][4], S2[2];
+                int lnz[2], cnt[2], pact[2];
+                float plp[2];
+                uint32_t te[2];  // byte offset of the row's table entry
 #pragma unroll
                 for (int i = 0; i < 2; i++) {
-                    const uint32_t te = __umul24((uint32_t)dg[i], 4u * TW);  // byte offset of the row's entry
+                    te[i] = __umul24((uint32_t)dg[i], 4u * TW);
 #pragma unroll
                     for (int t = 0; t < NP; t++) {
-                        const auto c4 = __builtin_amdgcn_raw_buffer_load_b128(tab_b.r, (int)(te + 4 * (16 * t + 4 * g4)), 0, 0);
-                        const auto l4 = __builtin_amdgcn_raw_buffer_load_b128(
-                            tab_b.r, (int)(te + 4 * (16 * NP + 16 * t + 4 * g4)), 0, 0);
+                        const auto c4 = __builtin_amdgcn_raw_buffer_load_b128(tab_b.r, (int)(te[i] + 4 * (16 * t + 4 * g4)), 0, 0);
 #pragma unroll
-                        for (int q = 0; q < 4; q++) {
-                            n_cum[i][t][q] = __uint_as_float(c4[q]);
-                            n_lpv[i][t][q] = __uint_as_float(l4[q]);
-                        }
+                        for (int q = 0; q < 4; q++) cum[i][t][q] = __uint_as_float(c4[q]);
                     }
-                    n_S2[i] = tab_b.ldf(te + 4 * (32 * NP));
-                    n_lnz[i] = (int)tab_b.ld32(te + 4 * (32 * NP + 1));
+                    S2[i] = tab_b.ldf(te[i] + 4 * (32 * NP));
+                    lnz[i] = (int)tab_b.ld32(te[i] + 4 * (32 * NP + 1));
                 }
-                if (pend) price_finish();
-                pend = true;
 #pragma unroll
                 for (int i = 0; i < 2; i++) {
-                    p_cur[i] = cur[i], p_act[i] = act[i], p_pin[i] = pin[i], p_u2[i] = u2[i];
-                    p_S2[i] = n_S2[i], p_lnz[i] = n_lnz[i];
+                    const float target = u2[i] * S2[i];
+                    cnt[i] = 0;
 #pragma unroll
                     for (int t = 0; t < NP; t++)
 #pragma unroll
-                        for (int q = 0; q < 4; q++) p_cum[i][t][q] = n_cum[i][t][q], p_lpv[i][t][q] = n_lpv[i][t][q];
+                        for (int q = 0; q < 4; q++) cnt[i] += (cum[i][t][q] <= target) ? 1 : 0;
                 }
+                rows_sum2_i(cnt[0], cnt[1]);
+                // the chosen action's log-prob straight from its table entry (one load per row)
+#pragma unroll
+                for (int i = 0; i < 2; i++) {
+                    pact[i] = cnt[i] >= a.n2.n_actions ? lnz[i] : cnt[i];
+                    plp[i] = tab_b.ldf(te[i] + 4 * (16 * NP + pact[i]));
+                }
+                price_out2(cur, act, pin, pact, plp);
             } else {
                 any_miss = true;
             }
@@ -836,7 +807,6 @@ __device__ __forceinline__ void act_tiles(const ActArgs& a, int block) {
             }
         MS_AMARK(5);  // core chooser stores
     }
-    if (NT2 > 0 && pend) price_finish();
     if (NT2 > 0 && any_miss) {
         // the pairs the table could not serve (or every pair, without a table): the same pairs and
         // draws again, the core chooser recomputed (bit-identical), then the price net itself; its
@@ -1536,8 +1506,12 @@ hipError_t launch_act_round(const ms_mlp_params* core, const ms_mlp_params* pric
     }
     // fewer, longer waves than either launch alone: the other half's waves fill the gaps
     // (tools/sweep_act.sh: 2048 / 768 -> 2048 offer and 2048 acceptor waves at cfg3)
+    // (the targets are for cfg3's 16384 replicas; a launch over fewer replicas, e.g. one of two replica
+    //  halves stepped on two streams, takes proportionally fewer waves so the other stream's kernel fits beside)
     static const long long t_off = env_int("MS_ACT_PAIR_WAVES", 2048), t_acc = env_int("MS_ACT_PAIR_COMMON_WAVES", 768);
-    const unsigned ob = act_blocks(o, t_off), cb = act_common_blocks(c, t_acc);
+    const long long sc_off = E >= 16384 ? t_off : (t_off * E + 16383) / 16384;
+    const long long sc_acc = E >= 16384 ? t_acc : (t_acc * E + 16383) / 16384;
+    const unsigned ob = act_blocks(o, sc_off < 64 ? 64 : sc_off), cb = act_common_blocks(c, sc_acc < 64 ? 64 : sc_acc);
     hipLaunchKernelGGL((k_act_pair<1, 1, 1, 2, 2>), dim3(ob + cb), dim3(256), 0, st, o, c, (int)ob);
     return hipGetLastError();
 }

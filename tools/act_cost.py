@@ -46,6 +46,9 @@ res = {
     "paired (ms_act_round_free)": timed(lambda: ppo.act_round_free(core, price, off_obs, acc, tr.acc_rows[t], tr.acc_owner[t],
                                                                    tr.acc_common, C, 1, 1, 3, out, tr.acc.actions[t],
                                                                    tr.acc.logprobs[t], price_unit_stride=pus, price_table=pt)),
+    "paired with act fragments (the trainer's launch)": timed(lambda: ppo.act_round_free(
+        core, price, off_obs, acc, tr.acc_rows[t], tr.acc_owner[t], tr.acc_common, C, 1, 1, 3, out, tr.acc.actions[t],
+        tr.acc.logprobs[t], price_unit_stride=pus, price_table=pt, core_frag=tr.off_frag, acc_frag=tr.acc_frag)),
 }
 for k, v in res.items():
     print("%-45s %8.2f us" % (k, v))
