@@ -572,12 +572,11 @@ __global__ void __launch_bounds__(64 * kActWaves) k_bdqn_act(BdqnAct p) {
     __syncthreads();  // everyone is done with W2 (the staging area overlaps it)
     fetch(0);
     const float inv_n = 1.0f / (float)n;
-    const int nfull = n >> 4;  // action tiles holding 16 valid actions (wave-uniform)
     for (int b = 0; b < A; b++) {
-        // branch b's rows have landed: LDS-DMA completion is counted by vmcnt, and the barrier alone does not
-        // wait for it, so each issuing wave drains its own transfers before the barrier that publishes them
-        if constexpr (GLDS) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();  // ... and everyone is done with the previous branch's terms
+        // branch b's rows have landed (LDS-DMA completion is counted by vmcnt: the compiler drains it with
+        // s_waitcnt vmcnt(0) lgkmcnt(0) right before this barrier, checked in the k_bdqn_act<7, false> ISA);
+        // everyone is done with the previous branch's terms
+        __syncthreads();
         if constexpr (GLDS) {
             static_assert(NTH % 32 == 0, "a thread keeps its hidden-unit group across rows");
             const int k4 = tid & 31;  // the same 4 hidden units (and term positions) for every row it splits
@@ -617,8 +616,8 @@ __global__ void __launch_bounds__(64 * kActWaves) k_bdqn_act(BdqnAct p) {
         for (int c = 0; c < NC; c++) {
             // q = (value + adv) - mean(adv) over the branch's n actions; the first maximum
             // (lane (j, g4) holds actions 16 mt + 4 g4 + q of row j, increasing in (mt, q))
-            // (tiles mt < nfull hold only valid actions; the rest are masked per element: launch_bdqn_act runs
-            //  NMT = 3 for nmt = 2 and NMT = 7 for nmt = 4..6, so tiles past n's own count hold zero-padded rows)
+            // (tiles mt < NMT - 1 hold only valid actions: launch_bdqn_act instantiates NMT = ceil(n / 16)
+            //  exactly, so n > 16 (NMT - 1); only the last tile is masked)
             float adv[NMT][4];
             float sum = 0.f;
 #pragma unroll
@@ -627,7 +626,7 @@ __global__ void __launch_bounds__(64 * kActWaves) k_bdqn_act(BdqnAct p) {
                 for (int q = 0; q < 4; q++) {
                     const int m = 16 * mt + 4 * g4 + q;
                     adv[mt][q] = acc[c][mt][q] + sba[m];
-                    if (mt < nfull || m < n) sum += adv[mt][q];
+                    if (mt < NMT - 1 || m < n) sum += adv[mt][q];
                 }
             const float mean = rows_sum(sum) * inv_n;
             float best = -INFINITY;
@@ -644,7 +643,7 @@ __global__ void __launch_bounds__(64 * kActWaves) k_bdqn_act(BdqnAct p) {
                     const int m = 16 * mt + 4 * g4 + q;
                     const float qv = (value[c] + adv[mt][q]) - mean;
                     if constexpr (NMT >= 2) {
-                        if ((mt > 0 || q > 0) && (mt < nfull || m < n) && qv > best) {
+                        if ((mt > 0 || q > 0) && (mt < NMT - 1 || m < n) && qv > best) {
                             best = qv;
                             bidx = m;
                         }
@@ -747,7 +746,9 @@ hipError_t launch_bdqn_act(const BdqnAct& p, hipStream_t st) {
                            (const unsigned long long*)p.own_mask);                                        \
         return hipGetLastError();                                                                        \
     }
-    MS_BDQN_CASE(1) MS_BDQN_CASE(3) MS_BDQN_CASE(7) MS_BDQN_CASE(8)
+    // NMT = nmt exactly: the epilogue masks only the last action tile
+    MS_BDQN_CASE(1) MS_BDQN_CASE(2) MS_BDQN_CASE(3) MS_BDQN_CASE(4) MS_BDQN_CASE(5) MS_BDQN_CASE(6) MS_BDQN_CASE(7)
+    MS_BDQN_CASE(8)
 #undef MS_BDQN_CASE
     return hipErrorInvalidValue;
 }

@@ -1506,12 +1506,8 @@ hipError_t launch_act_round(const ms_mlp_params* core, const ms_mlp_params* pric
     }
     // fewer, longer waves than either launch alone: the other half's waves fill the gaps
     // (tools/sweep_act.sh: 2048 / 768 -> 2048 offer and 2048 acceptor waves at cfg3)
-    // (the targets are for cfg3's 16384 replicas; a launch over fewer replicas, e.g. one of two replica
-    //  halves stepped on two streams, takes proportionally fewer waves so the other stream's kernel fits beside)
     static const long long t_off = env_int("MS_ACT_PAIR_WAVES", 2048), t_acc = env_int("MS_ACT_PAIR_COMMON_WAVES", 768);
-    const long long sc_off = E >= 16384 ? t_off : (t_off * E + 16383) / 16384;
-    const long long sc_acc = E >= 16384 ? t_acc : (t_acc * E + 16383) / 16384;
-    const unsigned ob = act_blocks(o, sc_off < 64 ? 64 : sc_off), cb = act_common_blocks(c, sc_acc < 64 ? 64 : sc_acc);
+    const unsigned ob = act_blocks(o, t_off), cb = act_common_blocks(c, t_acc);
     hipLaunchKernelGGL((k_act_pair<1, 1, 1, 2, 2>), dim3(ob + cb), dim3(256), 0, st, o, c, (int)ob);
     return hipGetLastError();
 }
