@@ -373,7 +373,10 @@ int ms_price_table_build(const ms_mlp_params* price_chooser, const ms_price_tabl
  * core_owner) (offset acc_offset), same seed and offset_dev; outputs identical to the two calls.
  * The offer and acceptor waves share the CUs, so neither launch waits out its own latency alone.
  * price_table (optional, built for the current price-chooser weights): the price chooser samples
- * from it. */
+ * from it. price_chooser NULL (ABI 16): a fixed-price round (SchedulingEnvironment.py:150-172 with the
+ * offer units' ActorCritic, PPOmodules.py:53-63): core_chooser is the offer net, core_action /
+ * core_logprob its outputs, and price_state, price_action, price_logprob, env_price and price_table
+ * must be NULL; outputs identical to ms_policy_act + ms_policy_act_compact. */
 int ms_act_round_free(const ms_mlp_params* core_chooser, const ms_mlp_params* price_chooser, const int8_t* off_obs,
                       int32_t off_stride, int32_t off_units, int32_t off_units_per_group, const ms_mlp_params* acceptor,
                       const int8_t* core_rows, const int8_t* core_owner, int32_t acc_stride, int32_t acc_units,

@@ -548,17 +548,25 @@ int ms_act_round_free(const ms_mlp_params* core, const ms_mlp_params* price, con
                       int8_t* price_state, int8_t* price_action, float* price_logprob, int8_t* env_price,
                       int8_t* acc_action, float* acc_logprob, const ms_price_table* price_table,
                       int64_t price_unit_stride, void* stream) {
-    if (!off_obs || !core_rows || !core_owner || !common_row || !core_action || !core_logprob || !price_state ||
-        !price_action || !price_logprob || !env_price || !acc_action || !acc_logprob)
+    if (!off_obs || !core_rows || !core_owner || !common_row || !core_action || !core_logprob || !acc_action ||
+        !acc_logprob)
         return fail(MS_EINVAL, "NULL argument");
+    // price == NULL: a fixed-price round (the offer units' net acts alone; no price outputs)
+    if (price && (!price_state || !price_action || !price_logprob || !env_price))
+        return fail(MS_EINVAL, "NULL price output");
+    if (!price && (price_state || price_action || price_logprob || env_price || price_table))
+        return fail(MS_EINVAL, "a fixed-price round (price_chooser NULL) takes no price outputs or table");
     if (n_envs < 1) return fail(MS_EINVAL, "n_envs must be >= 1");
     int rc = check_mlp(core, off_stride, off_units, off_units_per_group);
     if (rc) return rc;
-    rc = check_mlp(price, 4, off_units, off_units_per_group);
-    if (rc) return rc;
+    if (price) {
+        rc = check_mlp(price, 4, off_units, off_units_per_group);
+        if (rc) return rc;
+    }
     rc = check_mlp(acc, acc_stride, acc_units, acc_units_per_group);
     if (rc) return rc;
-    if (price->in_dim != 4 || price->n_groups != core->n_groups) return fail(MS_EINVAL, "price chooser must be 4 -> A");
+    if (price && (price->in_dim != 4 || price->n_groups != core->n_groups))
+        return fail(MS_EINVAL, "price chooser must be 4 -> A");
     if (core->in_dim != 2 * n_cores + 2 || core->n_actions != n_cores + 1)
         return fail(MS_EINVAL, "core chooser must be (2C+2) -> C+1");
     if (n_cores < 1 || acc_units % n_cores != 0 || acc_stride < 16)

@@ -1488,6 +1488,37 @@ hipError_t launch_act_round(const ms_mlp_params* core, const ms_mlp_params* pric
                             int8_t* acc_action, float* acc_logprob, const float* ptab, const int16_t* pdigit,
                             int pkeys, int64_t pus, hipStream_t st) {
     if (!common || acc_stride < 16 || n_cores < 1 || acc_U % n_cores != 0) return hipErrorInvalidValue;
+    ActArgs c = compact_args(acc, core_rows, core_owner, acc_stride, E, acc_U, acc_S, n_cores, common, seed,
+                             acc_offset, offset_dev, nullptr, acc_action, acc_logprob);
+    if (!price) {
+        // a fixed-price round (cfg2): the offer units' one net (ActorCritic.act, k_act's single-net body) and the
+        // compact acceptors in one launch
+        ActArgs o{};
+        o.n1 = *core;
+        o.n2.n_groups = 0;
+        o.obs = off_obs;
+        o.stride = off_stride;
+        o.U = off_U;
+        o.S = off_S;
+        o.E = (int)E;
+        o.n_items = (int)(E * off_S);
+        o.seed = seed;
+        o.offset = off_offset;
+        o.offset_dev = offset_dev;
+        o.action = core_action;
+        o.logprob = core_logprob;
+        const bool paired = (off_stride + 31) / 32 == 1 && core->n_actions <= 16 && (acc_stride + 31) / 32 == 1 &&
+                            acc->n_actions <= 16 && !env_int("MS_ACT_UNPAIRED", 0);
+        if (paired && (!act_tiles_fits(o) || !act_common_fits(c))) return hipErrorInvalidValue;
+        if (!paired) {
+            hipError_t e = dispatch_act(o, st);
+            return e != hipSuccess ? e : dispatch_act(c, st);
+        }
+        static const long long f_off = env_int("MS_ACT_FIXED_WAVES", 1024), f_acc = env_int("MS_ACT_FIXED_COMMON_WAVES", 512);
+        const unsigned ob = act_blocks(o, f_off), cb = act_common_blocks(c, f_acc);
+        hipLaunchKernelGGL((k_act_pair<1, 1, 0, 1, 1>), dim3(ob + cb), dim3(256), 0, st, o, c, (int)ob);
+        return hipGetLastError();
+    }
     if (price->in_dim != 4) return hipErrorInvalidValue;
     ActArgs o = offer_free_args(core, price, off_obs, off_stride, E, off_U, off_S, n_cores, seed, off_offset,
                                 offset_dev, nullptr, core_action, core_logprob, price_state, price_action,
@@ -1495,8 +1526,6 @@ hipError_t launch_act_round(const ms_mlp_params* core, const ms_mlp_params* pric
     o.ptab = ptab;
     o.pdigit = pdigit;
     o.pkeys = pkeys;
-    ActArgs c = compact_args(acc, core_rows, core_owner, acc_stride, E, acc_U, acc_S, n_cores, common, seed,
-                             acc_offset, offset_dev, nullptr, acc_action, acc_logprob);
     const bool paired = (off_stride + 31) / 32 == 1 && core->n_actions <= 16 && price->n_actions <= 16 &&
                         (acc_stride + 31) / 32 == 2 && acc->n_actions <= 32 && !env_int("MS_ACT_UNPAIRED", 0);
     if (paired && (!act_tiles_fits(o) || !act_common_fits(c))) return hipErrorInvalidValue;

@@ -254,7 +254,8 @@ def act_round_free(core: GroupedActorCritic, price: GroupedActorCritic, off_obs,
                    price_unit_stride: int = 0, core_frag: "ActFrag | None" = None, acc_frag: "ActFrag | None" = None,
                    replica_base: int = 0):
     """``offer_act_free`` + ``act_compact`` of one free-price round in one launch (ms_act_round_free):
-    getActionForAllAgents (SchedulingEnvironment.py:150-172); outputs identical to the two calls.
+    getActionForAllAgents (SchedulingEnvironment.py:150-172); outputs identical to the two calls. price None:
+    a fixed-price round, ``core.act`` of the offer units + ``act_compact`` (out: core_action / core_logprob).
     price_table: the price chooser samples from it (built for the current weights).
     price_unit_stride: see ``offer_act_free``. core_frag / acc_frag: ActFrag blocks of the core chooser and
     the acceptor net for their current weights (bit-identical; the acting waves then skip deriving them)."""
@@ -262,15 +263,22 @@ def act_round_free(core: GroupedActorCritic, price: GroupedActorCritic, off_obs,
     _, C, acc_stride = core_rows.shape
     U_acc = acc_action.shape[1]
     assert off_obs.is_contiguous() and core_rows.is_contiguous() and core_owner.is_contiguous()
-    _check_price_out(out, E, U_off, price_unit_stride)
-    pc, pp = core.mlp_params(core_frag, replica_base * U_off), price.mlp_params()
+    pc = core.mlp_params(core_frag, replica_base * U_off)
     pa = acc.mlp_params(acc_frag, replica_base * U_acc)
-    check(lib.ms_act_round_free(ct.byref(pc), ct.byref(pp), ptr(off_obs), off_stride, U_off, U_off // core.G,
+    if price is None:  # a fixed-price round: out holds core_action / core_logprob only
+        assert price_table is None and price_unit_stride == 0
+        for k in ("core_action", "core_logprob"):
+            assert out[k].is_contiguous() and out[k].shape[:2] == (E, U_off), k
+        pp, prices = None, (None, None, None, None)
+    else:
+        _check_price_out(out, E, U_off, price_unit_stride)
+        pp = ct.byref(price.mlp_params())
+        prices = (out["price_state"], out["price_action"], out["price_logprob"], out["env_price"])
+    check(lib.ms_act_round_free(ct.byref(pc), pp, ptr(off_obs), off_stride, U_off, U_off // core.G,
                                 ct.byref(pa), ptr(core_rows), ptr(core_owner), acc_stride, U_acc, U_acc // acc.G,
                                 n_cores, ptr(common_row), E, ct.c_uint64(seed), ct.c_uint64(off_offset),
                                 ct.c_uint64(acc_offset), ptr(offset_dev), ptr(out["core_action"]),
-                                ptr(out["core_logprob"]), ptr(out["price_state"]), ptr(out["price_action"]),
-                                ptr(out["price_logprob"]), ptr(out["env_price"]), ptr(acc_action), ptr(acc_logprob),
+                                ptr(out["core_logprob"]), *[ptr(x) for x in prices], ptr(acc_action), ptr(acc_logprob),
                                 ct.byref(price_table.struct) if price_table is not None else None,
                                 int(price_unit_stride), stream_ptr(stream)))
 

@@ -362,18 +362,18 @@ class Trainer:
                 offer_act_free(self.off.group.policy_old, self.price.group.policy_old, sl(self.off_obs[t]), C, seed,
                                base + 1, out, offset_dev=self.rng_ctr, stream=st, price_unit_stride=pus,
                                core_frag=self.off_frag, replica_base=rb)
+        elif self.compact:
+            # a fixed-price round: the offer units and the compact acceptors in one launch
+            act_round_free(self.off.group.policy_old, None, sl(self.off_obs[t]), self.acc.group.policy_old,
+                           sl(self.acc_rows[t]), sl(self.acc_owner[t]), self.acc_common, C, seed, base + 1, base + 3,
+                           dict(core_action=sl(self.off.actions[t]), core_logprob=sl(self.off.logprobs[t])),
+                           sl(self.acc.actions[t]), sl(self.acc.logprobs[t]), offset_dev=self.rng_ctr, stream=st,
+                           core_frag=self.off_frag, acc_frag=self.acc_frag, replica_base=rb)
         else:
             self.off.group.policy_old.act(sl(self.off_obs[t]), N * L, seed, base + 1, action=sl(self.off.actions[t]),
                                           logprob=sl(self.off.logprobs[t]), offset_dev=self.rng_ctr, stream=st,
                                           frag=self.off_frag, replica_base=rb)
-        if self.compact and self.free:
-            pass  # acted above with the offers
-        elif self.compact:
-            self.acc.group.policy_old.act_compact(sl(self.acc_rows[t]), sl(self.acc_owner[t]), N * C, seed, base + 3,
-                                                  self.acc_common, action=sl(self.acc.actions[t]),
-                                                  logprob=sl(self.acc.logprobs[t]), offset_dev=self.rng_ctr, stream=st,
-                                                  frag=self.acc_frag, replica_base=rb)
-        else:
+        if not self.compact:  # (compact acceptors acted above, in the offers' launch)
             self.acc.group.policy_old.act(sl(self.acc_obs[t]), N * C, seed, base + 3, action=sl(self.acc.actions[t]),
                                           logprob=sl(self.acc.logprobs[t]), offset_dev=self.rng_ctr,
                                           common_row=self.acc_common if self.common_rows else None, stream=st,

@@ -451,6 +451,43 @@ def test_fused_grad_compact_many_groups_matches_autograd(ms, N, C, G, T, E, K, s
         assert torch.equal(runs[0][1][k], runs[1][1][k]), k
 
 
+@pytest.mark.parametrize("N,C,L,O,E,G", [(4, 4, 3, 12, 4096, 1), (4, 4, 3, 12, 301, 1), (8, 8, 3, 24, 513, 8),
+                                         (16, 16, 3, 48, 97, 1)])
+def test_act_round_fixed_matches_separate_calls(ms, N, C, L, O, E, G):
+    """ms_act_round_free with price_chooser NULL (a fixed-price round: the offer units' net and the compact
+    acceptors in one launch, the paired kernel for cfg2's shapes, two launches otherwise) == ms_policy_act +
+    ms_policy_act_compact, bit for bit, with and without act fragments, and with a replica base."""
+    ppo = _ppo(ms)
+    torch.manual_seed(13)
+    D_off, A_off, D_acc, A_acc = 2 * C + 2, C + 1, 3 + 2 * O, O + 1
+    s_off, s_acc = (D_off + 3) & ~3, (D_acc + 3) & ~3
+    off = ppo.GroupedActorCritic(G, D_off, A_off).cuda()
+    acc = ppo.GroupedActorCritic(G, D_acc, A_acc).cuda()
+    gen = torch.Generator().manual_seed(14)
+    off_obs = torch.zeros((E, N * L, s_off), dtype=torch.int8)
+    off_obs[..., :D_off] = torch.randint(-1, 13, (E, N * L, D_off), generator=gen, dtype=torch.int8)
+    rows = torch.zeros((E, C, s_acc), dtype=torch.int8)
+    rows[..., :D_acc] = torch.randint(-5, 13, (E, C, D_acc), generator=gen, dtype=torch.int8)
+    owner = torch.randint(0, N + 1, (E, C), generator=gen, dtype=torch.int8)
+    off_obs, rows, owner = off_obs.cuda(), rows.cuda(), owner.cuda()
+    crow = _common_row(D_acc, s_acc, O).cuda()
+    ctr = torch.tensor([24], dtype=torch.int64, device="cuda")
+    fo, fa = ppo.ActFrag(off, s_off), ppo.ActFrag(acc, s_acc, crow)
+    fo.build(off)
+    fa.build(acc)
+    for rb in (0, 64):
+        o1, l1 = off.act(off_obs, N * L, 55, 1, offset_dev=ctr, replica_base=rb)
+        a1, al1 = acc.act_compact(rows, owner, N * C, 55, 3, crow, offset_dev=ctr, replica_base=rb)
+        for of, af in ((None, None), (fo, fa)):
+            out = dict(core_action=torch.empty_like(o1), core_logprob=torch.empty_like(l1))
+            a2, al2 = torch.empty_like(a1), torch.empty_like(al1)
+            ppo.act_round_free(off, None, off_obs, acc, rows, owner, crow, C, 55, 1, 3, out, a2, al2, offset_dev=ctr,
+                               core_frag=of, acc_frag=af, replica_base=rb)
+            assert torch.equal(out["core_action"], o1) and torch.equal(a2, a1), (rb, of is None)
+            assert torch.equal(out["core_logprob"].view(torch.int32), l1.view(torch.int32))
+            assert torch.equal(al2.view(torch.int32), al1.view(torch.int32))
+
+
 @pytest.mark.parametrize("N,C,L,O,E", [(8, 8, 3, 24, 2048), (4, 4, 3, 12, 301), (16, 16, 3, 48, 97)])
 def test_act_round_free_matches_separate_calls(ms, N, C, L, O, E):
     """ms_act_round_free (offer units + compact acceptor units in one launch; the paired kernel for
