@@ -1514,7 +1514,9 @@ hipError_t launch_act_round(const ms_mlp_params* core, const ms_mlp_params* pric
             hipError_t e = dispatch_act(o, st);
             return e != hipSuccess ? e : dispatch_act(c, st);
         }
-        static const long long f_off = env_int("MS_ACT_FIXED_WAVES", 1024), f_acc = env_int("MS_ACT_FIXED_COMMON_WAVES", 512);
+        // wave split swept at cfg2 (profiles/r5g): 2048 offer / 512 acceptor target waves 8.5 us per launch (two
+        // launches: 13.4 us; 1024 / 512: 8.8, 512 / 256: 9.4, 3072 / 512: 11.6, 2048 / 256: 10.8)
+        static const long long f_off = env_int("MS_ACT_FIXED_WAVES", 2048), f_acc = env_int("MS_ACT_FIXED_COMMON_WAVES", 512);
         const unsigned ob = act_blocks(o, f_off), cb = act_common_blocks(c, f_acc);
         hipLaunchKernelGGL((k_act_pair<1, 1, 0, 1, 1>), dim3(ob + cb), dim3(256), 0, st, o, c, (int)ob);
         return hipGetLastError();
