@@ -301,6 +301,7 @@ def bench_other(args):
         launch_us = tr.launch_spans_us()
         b_round = env_round_bytes(tr.env.shape, tr.cfg.new_jobs_per_round, tr.free, tr.compact)
         result["roofline"] = env_roofline(b_round, E, launch_us, tr.compact)
+        result["roofline"]["clock_mhz"] = tr.launch_clock_mhz()
         result["act_roofline"] = act_roofline(tr, device)
     if rank == 0:
         print(json.dumps(result))
@@ -696,6 +697,9 @@ def main():
             "envs_per_launch": part_envs,
             "avg_launch_us": avg_step_s * 1e6,
             "launches_timed": len(launch_us),
+            # the env waves' shader clock over the same launches (s_memtime cycles / s_memrealtime ticks):
+            # the in-region span moves with it from box to box
+            "clock_mhz": tr.launch_clock_mhz(),
             "launch_timing": "first-wave-start to last-wave-end span (s_memrealtime, 100 MHz) of every %d-th "
                              "round's env launches in the last timed iteration (graph replay)" % SAMPLE_EVERY,
         },

@@ -196,10 +196,11 @@ typedef struct ms_env_metrics {
 typedef struct ms_event_out {
     ms_accept_rec* accepted; /* [E][C] or NULL */
     ms_term_rec* terminated; /* [E][C] or NULL */
-    /* [E][2] device u64 or NULL: per wave of the launch, its start and end on the s_memrealtime
-     * clock (100 MHz), wave b at [b][0..1] (a wave steps 64 / lanes_per_env envs, so the first
-     * ceil(E * lanes_per_env / 64) entries are written); min start to max end is the launch's span.
-     * Measurement only: two plain stores per wave. */
+    /* [E][4] device u64 or NULL: per wave of the launch, its start and end on the s_memrealtime
+     * clock (100 MHz) at [b][0..1] and on the shader clock (s_memtime) at [b][2..3] (ABI 16; a wave steps
+     * 64 / lanes_per_env envs, so the first ceil(E * lanes_per_env / 64) entries are written); min start
+     * to max end is the launch's span, shader cycles over 100 MHz ticks its clock. Measurement only:
+     * four plain stores per wave. */
     uint64_t* launch_span;
     /* [metrics_slots][E] or NULL: round r (world.round before the step) adds into slot
      * (r / episode_length) % metrics_slots */

@@ -1623,9 +1623,16 @@ __global__ void __launch_bounds__(64, 4) k_env_step(Params P, int64_t E, uint8_t
 #endif
     // per-wave start / end for the bench's launch span (optional; plain stores, no shared address,
     // nothing held across the round: the kernel sits at 4 waves per SIMD with no register to spare)
-    if (io.span && threadIdx.x == 0) io.span[2 * blockIdx.x] = __builtin_amdgcn_s_memrealtime();
+    // (with the shader clock beside the 100 MHz one: the launch's effective clock, which differs box to box)
+    if (io.span && threadIdx.x == 0) {
+        io.span[4 * blockIdx.x] = __builtin_amdgcn_s_memrealtime();
+        io.span[4 * blockIdx.x + 2] = __builtin_amdgcn_s_memtime();
+    }
     env_round<LPE, EXT, CMP, SH>(P, E, recs, mt, liab, io, blockIdx.x);
-    if (io.span && threadIdx.x == 0) io.span[2 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime();
+    if (io.span && threadIdx.x == 0) {
+        io.span[4 * blockIdx.x + 3] = __builtin_amdgcn_s_memtime();
+        io.span[4 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime();
+    }
 #ifdef MS_PHASE_TIMING
     if (threadIdx.x == 0) {
         g_wave_span[blockIdx.x % kProbeSlots][0] = rt_start;

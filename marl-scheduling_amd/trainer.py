@@ -24,6 +24,7 @@ import random
 import time
 from dataclasses import dataclass, field
 
+import numpy as np
 import torch
 
 from . import abi
@@ -397,15 +398,16 @@ class Trainer:
 
     def record_launch_spans(self, every: int):
         """Every `every`-th round's env launches record their span (first wave start, last wave end
-        on the 100 MHz s_memrealtime clock) into self.spans [T][parts][2]; read with launch_spans_us().
-        Set before the first rollout (the HIP graph captures it)."""
+        on the 100 MHz s_memrealtime clock, and each wave's shader-clock cycles) into self.spans
+        [T][parts][waves][4]; read with launch_spans_us() / launch_clock_mhz(). Set before the first
+        rollout (the HIP graph captures it)."""
         self.span_every = int(every)
         w = self.env.parts[0][2] - self.env.parts[0][1]
-        self.spans = torch.zeros((self.T, len(self.env.parts), w, 2), dtype=torch.int64, device=self.device)
+        self.spans = torch.zeros((self.T, len(self.env.parts), w, 4), dtype=torch.int64, device=self.device)
 
     def launch_spans_us(self):
         """Durations (us) of the recorded env launches of the last rollout."""
-        sp = self.spans[:: self.span_every].cpu().numpy()  # [rounds][parts][waves][2]
+        sp = self.spans[:: self.span_every].cpu().numpy()  # [rounds][parts][waves][4]
         out = []
         for r in range(sp.shape[0]):
             for k in range(sp.shape[1]):
@@ -413,6 +415,14 @@ class Trainer:
                 w = w[w[:, 1] > 0]  # the waves of the launch
                 out.append(float(w[:, 1].max() - w[:, 0].min()) / 100.0)
         return out
+
+    def launch_clock_mhz(self):
+        """Median shader clock (MHz) of the recorded env launches' waves: shader cycles over 100 MHz ticks."""
+        sp = self.spans[:: self.span_every].cpu().numpy().reshape(-1, 4)
+        sp = sp[(sp[:, 1] > sp[:, 0]) & (sp[:, 3] > sp[:, 2])]
+        if len(sp) == 0:
+            return None
+        return float(np.median((sp[:, 3] - sp[:, 2]) / (sp[:, 1] - sp[:, 0]) * 100.0))
 
     def _rollout_body(self):
         cur = torch.cuda.current_stream(self.device)
