@@ -13,7 +13,7 @@ FLAGS=(-O3 -std=c++17 -fPIC --offload-arch="${ARCH}" -Wall -Wno-unused-function
 OBJDIR="${MS_OBJDIR:-${HERE}/build}"
 [[ "${MS_CLEAN:-0}" == 1 ]] && rm -rf "${OBJDIR}"
 mkdir -p "${OBJDIR}"
-HEADERS=("${HERE}/csrc/ms_layout.h" "${HERE}/csrc/ms_ppo.h" "${HERE}/csrc/ms_dqn.h" "${HERE}/csrc/ms_bdqn.h" "${HERE}/csrc/ms_wide.h" "${HERE}/csrc/ms_common.h" "${HERE}/../include/marlsched.h")
+HEADERS=("${HERE}/csrc/ms_layout.h" "${HERE}/csrc/ms_act.h" "${HERE}/csrc/ms_ppo.h" "${HERE}/csrc/ms_dqn.h" "${HERE}/csrc/ms_bdqn.h" "${HERE}/csrc/ms_wide.h" "${HERE}/csrc/ms_common.h" "${HERE}/../include/marlsched.h")
 CCVER="$("${HIPCC}" --version 2>/dev/null | head -3 | tr '\n' ' ')"
 objs=()
 pids=()
