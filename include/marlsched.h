@@ -387,6 +387,34 @@ int ms_act_round_free(const ms_mlp_params* core_chooser, const ms_mlp_params* pr
                       float* price_logprob, int8_t* env_price, int8_t* acc_action, float* acc_logprob,
                       const ms_price_table* price_table, int64_t price_unit_stride, void* stream);
 
+/* The next round's getActionForAllAgents fused into the env round (ABI 16; SchedulingEnvironment.py:
+ * 150-172 with PPOmodules.py:53-63): after the round's observations, the wave that stepped a replica
+ * samples that replica's next actions from them (still in its LDS), so a round is one launch instead of
+ * an act launch and an env launch. For fixed-price rounds with compact acceptor observations and one
+ * offer net and one acceptor net (n_groups 1, globally shared), each net one 32-input k-step and <= 16
+ * actions, and act fragments (ms_act_prepare; the acceptor's with the common row's table). Outputs are
+ * those of ms_act_round_free(offer, NULL, ...) on the emitted observations, bit for bit: off_offset /
+ * acc_offset are that call's offsets, and each net's row_base its Philox row base. */
+typedef struct ms_fused_act {
+    ms_mlp_params offer;      /* the offer units' net, act_frag for obs rows of off_obs_stride bytes */
+    ms_mlp_params acceptor;   /* the acceptors' net, act_frag with the common row's table */
+    const int8_t* common_row; /* [acc_obs_stride] the foreign acceptor row (ms_policy_act_compact's) */
+    uint64_t seed, off_offset, acc_offset;
+    const uint64_t* offset_dev; /* may be NULL */
+    int8_t* off_action;       /* [E][N*L] */
+    float* off_logprob;       /* [E][N*L] */
+    int8_t* acc_action;       /* [E][N*C] */
+    float* acc_logprob;       /* [E][N*C] */
+} ms_fused_act;
+
+/* ms_env_step followed by the fused acting of `next` (obs must hold core_rows / core_owner and offer).
+ * MS_EINVAL when the shapes are not supported (the caller then steps and acts in two calls). */
+int ms_env_step_act(ms_env* env, const ms_actions* act, const ms_obs_out* obs, const ms_reward_out* rew,
+                    const ms_event_out* ev, const ms_fused_act* next, void* stream);
+
+/* 1 when ms_env_step_act can run this env's rounds (fixed prices, the shapes above), else 0. */
+int ms_env_step_act_supported(const ms_env* env);
+
 /* Discounted Monte-Carlo returns + per-sequence normalisation (PPOmodules.py:128-137):
  * rewards [T][M] (f32, as stored per round), for each sequence m:
  * G_t = r_t + gamma*G_{t+1} in float64, cast to f32, then

@@ -49,6 +49,10 @@ def _load():
         "ms_env_reset": (ct.c_int, [P, ct.POINTER(abi.MsObsOut), P]),
         "ms_env_step": (ct.c_int, [P, ct.POINTER(abi.MsActions), ct.POINTER(abi.MsObsOut),
                                    ct.POINTER(abi.MsRewardOut), ct.POINTER(abi.MsEventOut), P]),
+        "ms_env_step_act": (ct.c_int, [P, ct.POINTER(abi.MsActions), ct.POINTER(abi.MsObsOut),
+                                       ct.POINTER(abi.MsRewardOut), ct.POINTER(abi.MsEventOut),
+                                       ct.POINTER(abi.MsFusedAct), P]),
+        "ms_env_step_act_supported": (ct.c_int, [P]),
         "ms_env_round": (i64, [P]),
         "ms_env_flags": (ct.c_int, [P, ct.POINTER(u32), P]),
         "ms_env_randbelow": (ct.c_int, [P, i64, u32, ct.POINTER(u32), P]),
@@ -116,7 +120,8 @@ def _load():
     if version != ABI_VERSION and not lenient:
         raise ImportError("libmarlsched.so ABI version mismatch (%d, want %d)" % (version, ABI_VERSION))
     for name, (res, args) in sig.items():
-        if (version < 14 and name.startswith("ms_bdqn_update")) or (version < 15 and name == "ms_bdqn_act_compact"):
+        if (version < 14 and name.startswith("ms_bdqn_update")) or (version < 15 and name == "ms_bdqn_act_compact") \
+                or (version < 16 and name.startswith("ms_env_step_act")):
             continue
         fn = getattr(L, name)
         fn.restype = res
@@ -129,7 +134,7 @@ lib = _load()
 # every entry point include/marlsched.h declares (checked by tests)
 EXPORTED = (
     "ms_last_error", "ms_abi_version", "ms_config_shape", "ms_env_create", "ms_env_destroy", "ms_env_shape",
-    "ms_env_reset", "ms_env_step", "ms_env_round", "ms_env_flags", "ms_env_randbelow", "ms_env_auctioneer",
+    "ms_env_reset", "ms_env_step", "ms_env_step_act", "ms_env_step_act_supported", "ms_env_round", "ms_env_flags", "ms_env_randbelow", "ms_env_auctioneer",
     "ms_env_get_rng", "ms_env_set_rng", "ms_env_export",
     "ms_env_import", "ms_policy_act", "ms_policy_act_common", "ms_policy_act_compact",
     "ms_act_round_free", "ms_price_table_build", "ms_act_frag_bytes", "ms_act_prepare", "ms_offer_act_free", "ms_discounted_returns", "ms_unit_returns",

@@ -198,6 +198,13 @@ class MsMlpParams(ct.Structure):
     ]
 
 
+class MsFusedAct(ct.Structure):  # ms_fused_act (ABI 16)
+    _fields_ = [("offer", MsMlpParams), ("acceptor", MsMlpParams), ("common_row", ct.c_void_p), ("seed", ct.c_uint64),
+                ("off_offset", ct.c_uint64), ("acc_offset", ct.c_uint64), ("offset_dev", ct.c_void_p),
+                ("off_action", ct.c_void_p), ("off_logprob", ct.c_void_p), ("acc_action", ct.c_void_p),
+                ("acc_logprob", ct.c_void_p)]
+
+
 class MsQnetParams(ct.Structure):
     _fields_ = [("w1", ct.c_void_p), ("b1", ct.c_void_p), ("w2", ct.c_void_p), ("b2", ct.c_void_p),
                 ("in_dim", ct.c_int32), ("hidden", ct.c_int32), ("n_actions", ct.c_int32), ("n_groups", ct.c_int32)]

@@ -25,6 +25,9 @@ hipError_t launch_env_init(const Params&, int64_t, uint8_t*, uint32_t*, Liab*, u
 hipError_t launch_env_reset(const Params&, int64_t, const uint8_t*, int8_t*, int8_t*, int8_t*, int8_t*, int8_t*,
                             hipStream_t);
 hipError_t launch_env_step(const Params&, int64_t, uint8_t*, uint32_t*, Liab*, const StepIO&, hipStream_t);
+hipError_t launch_env_step_act(const Params&, int64_t, uint8_t*, uint32_t*, Liab*, const StepIO&, const FusedAct&,
+                               hipStream_t);
+bool env_step_act_supported(const Params&, int64_t);
 hipError_t launch_env_randbelow(const Params&, uint8_t*, uint32_t*, int64_t, uint32_t, uint32_t*, hipStream_t);
 hipError_t launch_env_auctioneer(const Params&, int64_t, uint8_t*, uint32_t*, int8_t*, hipStream_t);
 hipError_t launch_policy_act(const ms_mlp_params*, const int8_t*, int, int64_t, int, int, const int8_t*, uint64_t,
@@ -240,8 +243,48 @@ int ms_env_reset(ms_env* env, const ms_obs_out* obs, void* stream) {
     return MS_OK;
 }
 
+static int env_step_impl(ms_env* env, const ms_actions* act, const ms_obs_out* obs, const ms_reward_out* rew,
+                         const ms_event_out* ev, const ms::FusedAct* fa, void* stream);
+
 int ms_env_step(ms_env* env, const ms_actions* act, const ms_obs_out* obs, const ms_reward_out* rew,
                 const ms_event_out* ev, void* stream) {
+    return env_step_impl(env, act, obs, rew, ev, nullptr, stream);
+}
+
+int ms_env_step_act(ms_env* env, const ms_actions* act, const ms_obs_out* obs, const ms_reward_out* rew,
+                    const ms_event_out* ev, const ms_fused_act* next, void* stream) {
+    if (!env || !next) return fail(MS_EINVAL, "env/next is NULL");
+    const ms::Params& P = env->P;
+    if (env->cfg.free_prices) return fail(MS_EINVAL, "ms_env_step_act: fixed-price rounds only");
+    if (!obs || !obs->core_rows || !obs->core_owner || !obs->offer || obs->acceptor)
+        return fail(MS_EINVAL, "ms_env_step_act: needs compact acceptor observations (core_rows, core_owner) and offer rows");
+    if (!act || !act->acceptor || (ev && ev->metrics))
+        return fail(MS_EINVAL, "ms_env_step_act: the trainer's round only (actions given, no metrics)");
+    const ms_mlp_params& o = next->offer;
+    const ms_mlp_params& a = next->acceptor;
+    if (o.n_groups != 1 || a.n_groups != 1 || o.hidden != 16 || a.hidden != 16 || !o.act_frag || !a.act_frag)
+        return fail(MS_EINVAL, "ms_env_step_act: one 16-wide net per role with act fragments");
+    if (o.in_dim != P.d_off || a.in_dim != P.d_acc || o.n_actions != P.C + 1 || a.n_actions != P.O + 1)
+        return fail(MS_EINVAL, "ms_env_step_act: net shapes do not match the env");
+    if (P.off_stride > 32 || P.acc_stride > 32 || o.n_actions > 16 || a.n_actions > 16 ||
+        !ms::env_step_act_supported(P, env->E))
+        return fail(MS_EINVAL, "ms_env_step_act: shape not supported (one k-step, <= 16 actions, a wave's rows)");
+    if (!next->off_action || !next->off_logprob || !next->acc_action || !next->acc_logprob || !next->common_row)
+        return fail(MS_EINVAL, "ms_env_step_act: NULL output / common row");
+    ms::FusedAct fa{o, a, next->common_row, next->seed, next->off_offset, next->acc_offset, next->offset_dev, next->off_action,
+                    next->off_logprob, next->acc_action, next->acc_logprob};
+    return env_step_impl(env, act, obs, rew, ev, &fa, stream);
+}
+
+int ms_env_step_act_supported(const ms_env* env) {
+    if (!env) return 0;
+    const ms::Params& P = env->P;
+    return !env->cfg.free_prices && P.off_stride <= 32 && P.acc_stride <= 32 && P.C + 1 <= 16 && P.O + 1 <= 16 &&
+           ms::env_step_act_supported(P, env->E);
+}
+
+static int env_step_impl(ms_env* env, const ms_actions* act, const ms_obs_out* obs, const ms_reward_out* rew,
+                         const ms_event_out* ev, const ms::FusedAct* fa, void* stream) {
     if (!env || !act) return fail(MS_EINVAL, "env/actions is NULL");
     if (!act->acceptor != !act->offer_core)
         return fail(MS_EINVAL, "acceptor and offer_core actions are given together (both NULL: hard-coded agents)");
@@ -282,7 +325,10 @@ int ms_env_step(ms_env* env, const ms_actions* act, const ms_obs_out* obs, const
         io.metrics_slots = ev->metrics_slots;
         if (io.metrics && io.metrics_slots < 1) return fail(MS_EINVAL, "ms_env_step: metrics_slots must be >= 1");
     }
-    HIP_TRY(ms::launch_env_step(env->P, env->E, env->recs, env->mt, env->liab, io, (hipStream_t)stream));
+    if (fa)
+        HIP_TRY(ms::launch_env_step_act(env->P, env->E, env->recs, env->mt, env->liab, io, *fa, (hipStream_t)stream));
+    else
+        HIP_TRY(ms::launch_env_step(env->P, env->E, env->recs, env->mt, env->liab, io, (hipStream_t)stream));
     env->round += 1;
     return MS_OK;
 }

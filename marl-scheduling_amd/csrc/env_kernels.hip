@@ -22,6 +22,9 @@
 #include <string.h>
 
 #include "ms_layout.h"
+#include "ms_act.h"  // the fused next-round acting (fused_act); it sets its own contraction, restored here:
+
+#pragma clang fp contract(off)  // the env round reproduces Python's float64 arithmetic (build.sh: -ffp-contract=off)
 
 namespace ms {
 
@@ -1612,6 +1615,183 @@ __device__ __forceinline__ void env_round(const Params& P, int64_t E, uint8_t* r
 #endif
 }
 
+// ---- the next round's acting of the wave's envs (ms_env_step_act): ActorCritic.act of the offer units and
+//      the compact acceptors (PPOmodules.py:53-63, SchedulingEnvironment.py:150-172) on the observations the
+//      round just built in its LDS, with the arithmetic and the Philox draws of k_act / k_act_common
+//      (ms_act.h), so the outputs equal ms_act_round_free(offer net, NULL, ...) on the emitted rows. One
+//      offer net and one acceptor net (n_groups 1), each one 32-input k-step and <= 16 actions
+//      (env_step_act_supported); item i of a net is row i (e * units + u), its uniform word (i >> 6) & 1 of
+//      the draw countered by row (i & ~64) + row_base, as in k_act_common's scan.
+template <int LPE, class SH>
+__device__ __forceinline__ void fused_act(const Params& P, int64_t E, const FusedAct& fa, int64_t slot) {
+    constexpr int EPW = kWave / LPE;  // envs per wave
+    extern __shared__ __align__(16) uint8_t smem_all[];
+    __shared__ float s_cum[16], s_lp[16];
+    __shared__ uint32_t s_tab[2];        // the common row's S (f32 bits) and last nonzero action
+    __shared__ uint32_t s_tmpl[8];
+    __shared__ int32_t s_list[kWave];    // listed (owner-row) acceptor items: lane of the scan
+    __shared__ float s_ulist[kWave];
+    Geom g;
+    if constexpr (SH::kStatic) {
+        constexpr Geom kg = make_geom(SH::kN, SH::kC, SH::kL, SH::kJ);
+        g = kg;
+    } else {
+        g = P;
+    }
+    wave_sync();  // the round's observation sources are complete in every group's LDS slice
+    const int lane = threadIdx.x, j = lane & 15, g4 = lane >> 4;
+    const int C = g.C, Ua = g.N * C, Uo = g.NL;
+    const int64_t e0 = slot * EPW;
+    const uint64_t dev_off = fa.offset_dev ? *fa.offset_dev : 0ull;
+    // weights: the act fragment blocks (ms_act_prepare), else derived from the f32 weights (bit-identical)
+    W1Split<1> wo, wa;
+    Head<1> ho, ha;
+    using FL = FragLayout<1, 1>;
+    if (const uint32_t* f = frag_groups<1, 1>(fa.off, false)) {
+        wo.load_frag(f + lane * FL::LW);
+        ho.load_frag(reinterpret_cast<const float*>(f + lane * FL::LW + 12));
+    } else {
+        wo.load(fa.off.w1, fa.off.in_dim, j, g4);
+        ho.load(fa.off, 0, j, g4);
+    }
+    if (const uint32_t* f = frag_groups<1, 1>(fa.acc, true)) {
+        wa.load_frag(f + lane * FL::LW);
+        ha.load_frag(reinterpret_cast<const float*>(f + lane * FL::LW + 12));
+        const uint32_t* tb = f + 64 * FL::LW;  // [16 running sums][16 log-probs][S][last nonzero]
+        if (lane < 34) {
+            const uint32_t v = tb[lane];
+            if (lane < 16)
+                s_cum[lane] = __uint_as_float(v);
+            else if (lane < 32)
+                s_lp[lane - 16] = __uint_as_float(v);
+            else
+                s_tab[lane - 32] = v;
+        }
+    } else {
+        wa.load(fa.acc.w1, fa.acc.in_dim, j, g4);
+        ha.load(fa.acc, 0, j, g4);
+        float S0;
+        int lnz0;
+        common_table<1, 1>(wa, ha, fa.common, g.acc_stride >> 2, s_tmpl, s_cum, s_lp, &S0, &lnz0, lane);
+        if (lane == 0) {
+            s_tab[0] = __float_as_uint(S0);
+            s_tab[1] = (uint32_t)lnz0;
+        }
+    }
+    wave_sync();
+    const float S = __uint_as_float(s_tab[0]);
+    const int last_nz = (int)s_tab[1];
+    const int Aa = fa.acc.n_actions, Ao = fa.off.n_actions;
+    const int nw = g.acc_stride >> 2, nwo = g.off_stride >> 2;
+    // ---- acceptors, one lane per item: rows equal to the common row sample from its table, the owners'
+    //      rows are listed for the MFMA tile
+    int n_list;
+    {
+        const int ge = lane / Ua, u = lane - ge * Ua, a = u / C, c = u - a * C;
+        const int64_t e = e0 + ge;
+        const bool in = lane < EPW * Ua && e < E;
+        const uint8_t* sl = smem_all + (size_t)(ge < EPW ? ge : 0) * g.s_total;
+        const int owner = in ? (int)reinterpret_cast<const int8_t*>(sl + g.s_rec + g.o_core_owner)[c] : 0;
+        const int64_t item = e * Ua + u;
+        uint32_t r0, r1;
+        philox2((uint32_t)(item & ~64ll) + (uint32_t)fa.acc.row_base, fa.acc_offset + dev_off, fa.seed, r0, r1);
+        const float uu = u24((item & 64) ? r1 : r0);
+        const bool common = in && owner != a + 1;
+        if (common) {
+            const float target = uu * S;
+            int cnt = 0;
+#pragma unroll
+            for (int step = 16; step >= 1; step >>= 1)
+                if (cnt + step <= 16 && s_cum[cnt + step - 1] <= target) cnt += step;
+            const int act = cnt >= Aa ? last_nz : cnt;
+            fa.acc_action[item] = (int8_t)act;
+            fa.acc_logprob[item] = s_lp[act];
+        }
+        const bool other = in && !common;
+        const uint64_t m = __ballot(other);
+        if (other) {
+            const int pos = __popcll(m & ((1ull << lane) - 1ull));
+            s_list[pos] = lane;
+            s_ulist[pos] = uu;
+        }
+        n_list = __popcll(m);
+    }
+    wave_sync();
+    for (int t0 = 0; t0 < n_list; t0 += 32) {
+        f4 acc[2];
+        int row[2];
+        float u2[2];
+#pragma unroll
+        for (int i = 0; i < 2; i++) {
+            const int k = t0 + 16 * i + j;
+            const bool v = k < n_list;
+            const int ln = s_list[v ? k : 0];
+            const int ge = ln / Ua, u = ln - ge * Ua, c = u - (u / C) * C;
+            const uint32_t* crow = reinterpret_cast<const uint32_t*>(smem_all + (size_t)ge * g.s_total + g.s_scratch) +
+                                   c * nw;
+            const int c0 = 2 * g4, c1 = 2 * g4 + 1;
+            const u4v x = bytes_to_bf16(crow[c0 < nw ? c0 : nw - 1], crow[c1 < nw ? c1 : nw - 1]);
+            acc[i] = (f4){0, 0, 0, 0};
+            acc[i] = mfma_bf16(wa.hi[0], x, acc[i]);
+            acc[i] = mfma_bf16(wa.mid[0], x, acc[i]);
+            acc[i] = mfma_bf16(wa.lo[0], x, acc[i]);
+            row[i] = v ? (int)((e0 + ge) * Ua + u) : -1;
+            u2[i] = v ? s_ulist[k] : 0.f;
+        }
+        int act[2];
+        float lp[2];
+        ha.run2(acc, Aa, g4, u2, act, lp);
+#pragma unroll
+        for (int i = 0; i < 2; i++)
+            if (row[i] >= 0 && g4 == 0) {
+                fa.acc_action[row[i]] = (int8_t)act[i];
+                fa.acc_logprob[row[i]] = lp[i];
+            }
+    }
+    // ---- offer units: their rows (the slot's template + pair) in 16-row tiles, two per step
+    const int pcol = (2 * C) >> 2, pshift = 8 * ((2 * C) & 3);
+    for (int t0 = 0; t0 < EPW * Uo; t0 += 32) {
+        f4 acc[2];
+        int row[2];
+        float u2[2];
+#pragma unroll
+        for (int i = 0; i < 2; i++) {
+            const int r = t0 + 16 * i + j;
+            const int ge = r / Uo, s = r - ge * Uo;
+            const int64_t e = e0 + ge;
+            const bool v = r < EPW * Uo && e < E;
+            const uint8_t* sc = smem_all + (size_t)(v ? ge : 0) * g.s_total + g.s_scratch;
+            const uint32_t* otmpl = reinterpret_cast<const uint32_t*>(sc + g.s_otmpl);
+            const uint16_t pair = reinterpret_cast<const uint16_t*>(sc + g.s_slotpair)[v ? s : 0];
+            uint32_t d[2];
+#pragma unroll
+            for (int h = 0; h < 2; h++) {
+                const int cc = 2 * g4 + h, w = cc < nwo ? cc : nwo - 1;
+                d[h] = otmpl[w] | (w == pcol ? (uint32_t)pair << pshift : 0u);
+            }
+            const u4v x = bytes_to_bf16(d[0], d[1]);
+            acc[i] = (f4){0, 0, 0, 0};
+            acc[i] = mfma_bf16(wo.hi[0], x, acc[i]);
+            acc[i] = mfma_bf16(wo.mid[0], x, acc[i]);
+            acc[i] = mfma_bf16(wo.lo[0], x, acc[i]);
+            const int64_t item = e * Uo + s;
+            uint32_t r0, r1;
+            philox2((uint32_t)(item & ~64ll) + (uint32_t)fa.off.row_base, fa.off_offset + dev_off, fa.seed, r0, r1);
+            u2[i] = u24((item & 64) ? r1 : r0);
+            row[i] = v ? (int)item : -1;
+        }
+        int act[2];
+        float lp[2];
+        ho.run2(acc, Ao, g4, u2, act, lp);
+#pragma unroll
+        for (int i = 0; i < 2; i++)
+            if (row[i] >= 0 && g4 == 0) {
+                fa.off_action[row[i]] = (int8_t)act[i];
+                fa.off_logprob[row[i]] = lp[i];
+            }
+    }
+}
+
 // One round for the 64 / LPE envs of wave slot blockIdx.x. (A persistent loop over several slots
 // per wave would let one slot's observation stores drain under the next slot's compute, but the
 // compiler then keeps the whole round's state live across iterations: 3x the VGPRs.)
@@ -1639,6 +1819,22 @@ __global__ void __launch_bounds__(64, 4) k_env_step(Params P, int64_t E, uint8_t
         g_wave_span[blockIdx.x % kProbeSlots][1] = __builtin_amdgcn_s_memrealtime();
     }
 #endif
+}
+
+// the round of k_env_step (compact acceptor observations) and then the next round's acting (fused_act)
+template <int LPE, class SH>
+__global__ void __launch_bounds__(64, 4) k_env_step_act(Params P, int64_t E, uint8_t* recs, uint32_t* mt, Liab* liab,
+                                                     StepIO io, FusedAct fa) {
+    if (io.span && threadIdx.x == 0) {
+        io.span[4 * blockIdx.x] = __builtin_amdgcn_s_memrealtime();
+        io.span[4 * blockIdx.x + 2] = __builtin_amdgcn_s_memtime();
+    }
+    env_round<LPE, false, true, SH>(P, E, recs, mt, liab, io, blockIdx.x);
+    fused_act<LPE, SH>(P, E, fa, blockIdx.x);
+    if (io.span && threadIdx.x == 0) {
+        io.span[4 * blockIdx.x + 3] = __builtin_amdgcn_s_memtime();
+        io.span[4 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime();
+    }
 }
 
 // Auctioneer.getAuctioneerAction (Auctioneer.py:95-102) on its own, as the driver calls it
@@ -1813,6 +2009,35 @@ hipError_t launch_env_step(const Params& P, int64_t E, uint8_t* recs, uint32_t* 
         case 16: return launch_step_t<16>(P, E, recs, mt, liab, io, s);
         case 32: return launch_step_t<32>(P, E, recs, mt, liab, io, s);
         default: return launch_step_t<64>(P, E, recs, mt, liab, io, s);
+    }
+}
+// ms_env_step_act: a wave's acceptor items one per lane and its offer rows in 16-row tiles (<= 64 each)
+bool env_step_act_supported(const Params& P, int64_t E) {
+    const int epw = kWave / lanes_per_env(P, E);
+    return epw * P.N * P.C <= kWave && epw * P.NL <= kWave && P.C <= 16;
+}
+template <int LPE, class SH>
+static hipError_t launch_step_act_sh(const Params& P, int64_t E, uint8_t* recs, uint32_t* mt, Liab* liab,
+                                     const StepIO& io, const FusedAct& fa, hipStream_t s) {
+    constexpr int G = kWave / LPE;
+    const int64_t blocks = (E + G - 1) / G;
+    const size_t lds = (size_t)P.s_total * G > 4 * kMtN ? (size_t)P.s_total * G : 4 * kMtN;
+    hipLaunchKernelGGL((k_env_step_act<LPE, SH>), dim3((unsigned)blocks), dim3(kWave), lds, s, P, E, recs, mt, liab, io,
+                       fa);
+    return hipGetLastError();
+}
+hipError_t launch_env_step_act(const Params& P, int64_t E, uint8_t* recs, uint32_t* mt, Liab* liab, const StepIO& io,
+                               const FusedAct& fa, hipStream_t s) {
+    if (!env_step_act_supported(P, E) || io.act_acc == nullptr || io.metrics != nullptr || io.obs_acc != nullptr)
+        return hipErrorInvalidValue;
+    switch (lanes_per_env(P, E)) {
+        case 16: return launch_step_act_sh<16, DynShape>(P, E, recs, mt, liab, io, fa, s);
+        case 32:
+#ifndef MS_NO_FIXED_SHAPES
+            if (is_shape<4, 4, 3, 1>(P)) return launch_step_act_sh<32, FixShape<4, 4, 3, 1>>(P, E, recs, mt, liab, io, fa, s);
+#endif
+            return launch_step_act_sh<32, DynShape>(P, E, recs, mt, liab, io, fa, s);
+        default: return launch_step_act_sh<64, DynShape>(P, E, recs, mt, liab, io, fa, s);
     }
 }
 hipError_t launch_env_auctioneer(const Params& P, int64_t E, uint8_t* recs, uint32_t* mt, int8_t* actions,

@@ -165,6 +165,18 @@ struct StepIO {
     int32_t metrics_slots;
 };
 
+// the fused next-round acting of ms_env_step_act (env_kernels.hip fused_act)
+struct FusedAct {
+    ms_mlp_params off, acc;
+    const int8_t* common;
+    uint64_t seed, off_offset, acc_offset;
+    const uint64_t* offset_dev;
+    int8_t* off_action;
+    float* off_logprob;
+    int8_t* acc_action;
+    float* acc_logprob;
+};
+
 // launch arguments of k_aggregate_obs (agg_kernels.hip): divided rows in, aggregated rows out
 struct AggArgs {
     const int8_t* acc;  // [E][N][C][acc_stride]

@@ -425,29 +425,6 @@ __global__ void __launch_bounds__(256) k_act(ActArgs a) {
     act_tiles<S1, NT, NT2, EXT_U>(a, blockIdx.x);
 }
 
-// The common row's sampling table (Head::table) into LDS: its dwords (zero past the row: they meet
-// zero weights, like k_act's clamped loads) through layer 1 and the head. One wave.
-template <int S1, int NT>
-__device__ __forceinline__ void common_table(const W1Split<S1>& w1, const Head<NT>& h1, const int8_t* common,
-                                             int stride4, uint32_t* tmpl, float* cum, float* lp, float* S, int* lnz,
-                                             int lane) {
-    const int j = lane & 15, g4 = lane >> 4;
-    const uint32_t* crow = reinterpret_cast<const uint32_t*>(common);
-    for (int d = lane; d < 8 * S1; d += 64) tmpl[d] = d < stride4 ? crow[d] : 0u;
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    f4 acc = {0, 0, 0, 0};
-#pragma unroll
-    for (int s = 0; s < S1; s++) {
-        const u4v x = bytes_to_bf16(tmpl[8 * s + 2 * g4], tmpl[8 * s + 2 * g4 + 1]);
-        acc = mfma_bf16(w1.hi[s], x, acc);
-        acc = mfma_bf16(w1.mid[s], x, acc);
-        acc = mfma_bf16(w1.lo[s], x, acc);
-    }
-    h1.table(acc, j, g4, cum, lp, S, lnz);
-}
-
 template <int S1, int NT, bool EXT_U, bool OWN>
 __device__ __forceinline__ void act_common_rows(const ActArgs& a, int block) {
     __shared__ int32_t s_list[4][kCommonSeg];

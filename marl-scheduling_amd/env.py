@@ -153,12 +153,14 @@ class BatchedEnv:
         return obs
 
     def step(self, acceptor, offer_core, offer_price=None, auctioneer=None, obs=None, rewards=None, events=None,
-             stream=None):
+             stream=None, next_act=None):
         """One round of SchedulingEnv.step (SchedulingEnvironment.py:32-83) for all replicas.
 
         acceptor [E,N,C] int8, offer_core [E,N,L] int8, offer_price [E,N,L] int8
         (free prices), auctioneer [E,C] int8 or None for the in-kernel
         HardcodedAuctioneerAcceptor. Returns (obs, rewards, events) dicts.
+        next_act (an abi.MsFusedAct): the next round's acting fused into the round (ms_env_step_act; fixed
+        prices, compact acceptor observations; see fused_act_supported).
         """
         for t in (acceptor, offer_core, offer_price, auctioneer):
             if t is not None:
@@ -187,9 +189,17 @@ class BatchedEnv:
                 assert m.dtype == torch.uint8 and m.is_contiguous() and m.shape[1:] == (self.E, abi.METRICS_BYTES)
             ev = abi.MsEventOut(ptr(events.get("accepted")), ptr(events.get("terminated")),
                                 ptr(events.get("launch_span")), ptr(m), 0 if m is None else m.shape[0])
-        check(lib.ms_env_step(self._h, ct.byref(a), ct.byref(o), ct.byref(r), ct.byref(ev) if ev else None,
-                              stream_ptr(stream)))
+        if next_act is not None:
+            check(lib.ms_env_step_act(self._h, ct.byref(a), ct.byref(o), ct.byref(r), ct.byref(ev) if ev else None,
+                                      ct.byref(next_act), stream_ptr(stream)))
+        else:
+            check(lib.ms_env_step(self._h, ct.byref(a), ct.byref(o), ct.byref(r), ct.byref(ev) if ev else None,
+                                  stream_ptr(stream)))
         return obs, rewards, events
+
+    def fused_act_supported(self) -> bool:
+        """Whether step(next_act=...) can run this env's rounds (ms_env_step_act_supported)."""
+        return bool(lib.ms_env_step_act_supported(self._h))
 
     def flags(self, stream=None) -> int:
         f = ct.c_uint32()

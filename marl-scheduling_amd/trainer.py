@@ -28,7 +28,7 @@ import numpy as np
 import torch
 
 from . import abi
-from ._lib import hip_capture
+from ._lib import hip_capture, ptr
 from .env import BatchedEnv
 from .ppo import (ActFrag, PPOGroup, PriceTable, act_round_free, discounted_returns, offer_act_free, reference_init_order,
                   reference_nets, unit_returns)
@@ -262,6 +262,13 @@ class Trainer:
         # update 10.06 -> 9.63 ms but the next rollout 14.50 -> 15.63 ms (every rollout launch
         # slower after a multi-stream update graph), so it is off by default
         self.update_streams = os.environ.get("MS_UPDATE_STREAMS", "0") == "1"
+        # fixed-price rounds with one net per role (cfg2): round t's env launch also samples round t + 1's
+        # actions from the observations it just built (ms_env_step_act), so a round is one launch
+        # (MS_ENV_FUSED_ACT=0: the act launch and the env launch of every round, for A/B measurements)
+        self.fused_step = (self.compact and not self.free and self.acc.group.policy.G == 1 and
+                           self.off.group.policy.G == 1 and self.acc_frag is not None and
+                           os.environ.get("MS_ENV_FUSED_ACT", "1") != "0" and
+                           all(env.fused_act_supported() for env, _, _ in self.env.parts))
         self.span_every = 0  # > 0: every span_every-th round's env launches record their span (bench)
         self.spans = None
         self.timings = dict(rollout=0.0, update=0.0)
@@ -329,6 +336,8 @@ class Trainer:
 
     def _act_part(self, t: int, k: int):
         """getActionForAllAgents of round t for replica part k (on stream k)."""
+        if self.fused_step and t > 0:
+            return  # sampled by round t - 1's env launch (_step_part)
         env, e0, e1 = self.env.parts[k]
         st = self.streams[k]
         E, N, C, L = e1 - e0, self.N, self.C, self.L
@@ -393,8 +402,18 @@ class Trainer:
         ev = dict(launch_span=self.spans[t, k]) if self.span_every and t % self.span_every == 0 else None
         if self.metric_bufs is not None:
             ev = dict(ev or {}, metrics=self.metric_bufs[k])
+        nxt = None
+        if self.fused_step and t + 1 < self.T:
+            # round t + 1's getActionForAllAgents (the fixed-price pair of _act_part) in this launch
+            seed, base, rb = self.seed * 7919, 8 * (t + 1), self.rank * self.E + e0
+            nxt = abi.MsFusedAct(self.off.group.policy_old.mlp_params(self.off_frag, rb * N * L),
+                                 self.acc.group.policy_old.mlp_params(self.acc_frag, rb * N * C), ptr(self.acc_common),
+                                 seed, base + 1, base + 3, ptr(self.rng_ctr), ptr(sl(self.off.actions[t + 1])),
+                                 ptr(sl(self.off.logprobs[t + 1])), ptr(sl(self.acc.actions[t + 1])),
+                                 ptr(sl(self.acc.logprobs[t + 1])))
         env.step(sl(self.acc.actions[t]).view(E, N, C), sl(self.off.actions[t]).view(E, N, L),
-                 sl(self.env_price).view(E, N, L) if self.free else None, obs=obs, rewards=rew, events=ev, stream=st)
+                 sl(self.env_price).view(E, N, L) if self.free else None, obs=obs, rewards=rew, events=ev, stream=st,
+                 next_act=nxt)
 
     def record_launch_spans(self, every: int):
         """Every `every`-th round's env launches record their span (first wave start, last wave end
