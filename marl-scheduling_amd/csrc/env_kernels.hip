@@ -1622,8 +1622,32 @@ __device__ __forceinline__ void env_round(const Params& P, int64_t E, uint8_t* r
 //      offer net and one acceptor net (n_groups 1), each one 32-input k-step and <= 16 actions
 //      (env_step_act_supported); item i of a net is row i (e * units + u), its uniform word (i >> 6) & 1 of
 //      the draw countered by row (i & ~64) + row_base, as in k_act_common's scan.
+// The fused acting's weights, issued at the start of the launch (their loads overlap the env round):
+// each lane's fragment of both nets (ms_act_prepare) and its dword of the acceptor's common-row table.
+struct FusedW {
+    W1Split<1> wo, wa;
+    Head<1> ho, ha;
+    uint32_t tab;   // table dword `lane` (< 34): 16 running sums, 16 log-probs, S, last nonzero action
+    bool frag;      // both fragment blocks present (else fused_act derives the weights)
+};
+__device__ __forceinline__ void fused_weights(const FusedAct& fa, FusedW& w) {
+    using FL = FragLayout<1, 1>;
+    const int lane = threadIdx.x;
+    const uint32_t* fo = frag_groups<1, 1>(fa.off, false);
+    const uint32_t* fc = frag_groups<1, 1>(fa.acc, true);
+    w.frag = fo && fc;
+    w.tab = 0;
+    if (w.frag) {
+        w.wo.load_frag(fo + lane * FL::LW);
+        w.ho.load_frag(reinterpret_cast<const float*>(fo + lane * FL::LW + 12));
+        w.wa.load_frag(fc + lane * FL::LW);
+        w.ha.load_frag(reinterpret_cast<const float*>(fc + lane * FL::LW + 12));
+        w.tab = fc[64 * FL::LW + (lane < 34 ? lane : 0)];
+    }
+}
+
 template <int LPE, class SH>
-__device__ __forceinline__ void fused_act(const Params& P, int64_t E, const FusedAct& fa, int64_t slot) {
+__device__ __forceinline__ void fused_act(const Params& P, int64_t E, const FusedAct& fa, FusedW& w, int64_t slot) {
     constexpr int EPW = kWave / LPE;  // envs per wave
     extern __shared__ __align__(16) uint8_t smem_all[];
     __shared__ float s_cum[16], s_lp[16];
@@ -1638,53 +1662,81 @@ __device__ __forceinline__ void fused_act(const Params& P, int64_t E, const Fuse
     } else {
         g = P;
     }
-    wave_sync();  // the round's observation sources are complete in every group's LDS slice
     const int lane = threadIdx.x, j = lane & 15, g4 = lane >> 4;
     const int C = g.C, Ua = g.N * C, Uo = g.NL;
     const int64_t e0 = slot * EPW;
     const uint64_t dev_off = fa.offset_dev ? *fa.offset_dev : 0ull;
-    // weights: the act fragment blocks (ms_act_prepare), else derived from the f32 weights (bit-identical)
-    W1Split<1> wo, wa;
-    Head<1> ho, ha;
-    using FL = FragLayout<1, 1>;
-    if (const uint32_t* f = frag_groups<1, 1>(fa.off, false)) {
-        wo.load_frag(f + lane * FL::LW);
-        ho.load_frag(reinterpret_cast<const float*>(f + lane * FL::LW + 12));
-    } else {
-        wo.load(fa.off.w1, fa.off.in_dim, j, g4);
-        ho.load(fa.off, 0, j, g4);
-    }
-    if (const uint32_t* f = frag_groups<1, 1>(fa.acc, true)) {
-        wa.load_frag(f + lane * FL::LW);
-        ha.load_frag(reinterpret_cast<const float*>(f + lane * FL::LW + 12));
-        const uint32_t* tb = f + 64 * FL::LW;  // [16 running sums][16 log-probs][S][last nonzero]
+    if (w.frag) {
         if (lane < 34) {
-            const uint32_t v = tb[lane];
             if (lane < 16)
-                s_cum[lane] = __uint_as_float(v);
+                s_cum[lane] = __uint_as_float(w.tab);
             else if (lane < 32)
-                s_lp[lane - 16] = __uint_as_float(v);
+                s_lp[lane - 16] = __uint_as_float(w.tab);
             else
-                s_tab[lane - 32] = v;
+                s_tab[lane - 32] = w.tab;
         }
-    } else {
-        wa.load(fa.acc.w1, fa.acc.in_dim, j, g4);
-        ha.load(fa.acc, 0, j, g4);
+    } else {  // derived from the f32 weights (bit-identical to the fragments)
+        w.wo.load(fa.off.w1, fa.off.in_dim, j, g4);
+        w.ho.load(fa.off, 0, j, g4);
+        w.wa.load(fa.acc.w1, fa.acc.in_dim, j, g4);
+        w.ha.load(fa.acc, 0, j, g4);
         float S0;
         int lnz0;
-        common_table<1, 1>(wa, ha, fa.common, g.acc_stride >> 2, s_tmpl, s_cum, s_lp, &S0, &lnz0, lane);
+        common_table<1, 1>(w.wa, w.ha, fa.common, g.acc_stride >> 2, s_tmpl, s_cum, s_lp, &S0, &lnz0, lane);
         if (lane == 0) {
             s_tab[0] = __float_as_uint(S0);
             s_tab[1] = (uint32_t)lnz0;
         }
     }
-    wave_sync();
-    const float S = __uint_as_float(s_tab[0]);
-    const int last_nz = (int)s_tab[1];
+    wave_sync();  // the table, and the round's observation sources in every group's LDS slice
     const int Aa = fa.acc.n_actions, Ao = fa.off.n_actions;
     const int nw = g.acc_stride >> 2, nwo = g.off_stride >> 2;
+    // ---- offer units: their rows (the slot's template + pair) in 16-row tiles, two per step
+    const int pcol = (2 * C) >> 2, pshift = 8 * ((2 * C) & 3);
+    for (int t0 = 0; t0 < EPW * Uo; t0 += 32) {
+        f4 acc[2];
+        int row[2];
+        float u2[2];
+#pragma unroll
+        for (int i = 0; i < 2; i++) {
+            const int r = t0 + 16 * i + j;
+            const int ge = r / Uo, s = r - ge * Uo;
+            const int64_t e = e0 + ge;
+            const bool v = r < EPW * Uo && e < E;
+            const uint8_t* sc = smem_all + (size_t)(v ? ge : 0) * g.s_total + g.s_scratch;
+            const uint32_t* otmpl = reinterpret_cast<const uint32_t*>(sc + g.s_otmpl);
+            const uint16_t pair = reinterpret_cast<const uint16_t*>(sc + g.s_slotpair)[v ? s : 0];
+            uint32_t d[2];
+#pragma unroll
+            for (int h = 0; h < 2; h++) {
+                const int cc = 2 * g4 + h, wd = cc < nwo ? cc : nwo - 1;
+                d[h] = otmpl[wd] | (wd == pcol ? (uint32_t)pair << pshift : 0u);
+            }
+            const u4v x = bytes_to_bf16(d[0], d[1]);
+            acc[i] = (f4){0, 0, 0, 0};
+            acc[i] = mfma_bf16(w.wo.hi[0], x, acc[i]);
+            acc[i] = mfma_bf16(w.wo.mid[0], x, acc[i]);
+            acc[i] = mfma_bf16(w.wo.lo[0], x, acc[i]);
+            const int64_t item = e * Uo + s;
+            uint32_t r0, r1;
+            philox2((uint32_t)(item & ~64ll) + (uint32_t)fa.off.row_base, fa.off_offset + dev_off, fa.seed, r0, r1);
+            u2[i] = u24((item & 64) ? r1 : r0);
+            row[i] = v ? (int)item : -1;
+        }
+        int act[2];
+        float lp[2];
+        w.ho.run2(acc, Ao, g4, u2, act, lp);
+#pragma unroll
+        for (int i = 0; i < 2; i++)
+            if (row[i] >= 0 && g4 == 0) {
+                fa.off_action[row[i]] = (int8_t)act[i];
+                fa.off_logprob[row[i]] = lp[i];
+            }
+    }
     // ---- acceptors, one lane per item: rows equal to the common row sample from its table, the owners'
     //      rows are listed for the MFMA tile
+    const float S = __uint_as_float(s_tab[0]);
+    const int last_nz = (int)s_tab[1];
     int n_list;
     {
         const int ge = lane / Ua, u = lane - ge * Ua, a = u / C, c = u - a * C;
@@ -1732,62 +1784,20 @@ __device__ __forceinline__ void fused_act(const Params& P, int64_t E, const Fuse
             const int c0 = 2 * g4, c1 = 2 * g4 + 1;
             const u4v x = bytes_to_bf16(crow[c0 < nw ? c0 : nw - 1], crow[c1 < nw ? c1 : nw - 1]);
             acc[i] = (f4){0, 0, 0, 0};
-            acc[i] = mfma_bf16(wa.hi[0], x, acc[i]);
-            acc[i] = mfma_bf16(wa.mid[0], x, acc[i]);
-            acc[i] = mfma_bf16(wa.lo[0], x, acc[i]);
+            acc[i] = mfma_bf16(w.wa.hi[0], x, acc[i]);
+            acc[i] = mfma_bf16(w.wa.mid[0], x, acc[i]);
+            acc[i] = mfma_bf16(w.wa.lo[0], x, acc[i]);
             row[i] = v ? (int)((e0 + ge) * Ua + u) : -1;
             u2[i] = v ? s_ulist[k] : 0.f;
         }
         int act[2];
         float lp[2];
-        ha.run2(acc, Aa, g4, u2, act, lp);
+        w.ha.run2(acc, Aa, g4, u2, act, lp);
 #pragma unroll
         for (int i = 0; i < 2; i++)
             if (row[i] >= 0 && g4 == 0) {
                 fa.acc_action[row[i]] = (int8_t)act[i];
                 fa.acc_logprob[row[i]] = lp[i];
-            }
-    }
-    // ---- offer units: their rows (the slot's template + pair) in 16-row tiles, two per step
-    const int pcol = (2 * C) >> 2, pshift = 8 * ((2 * C) & 3);
-    for (int t0 = 0; t0 < EPW * Uo; t0 += 32) {
-        f4 acc[2];
-        int row[2];
-        float u2[2];
-#pragma unroll
-        for (int i = 0; i < 2; i++) {
-            const int r = t0 + 16 * i + j;
-            const int ge = r / Uo, s = r - ge * Uo;
-            const int64_t e = e0 + ge;
-            const bool v = r < EPW * Uo && e < E;
-            const uint8_t* sc = smem_all + (size_t)(v ? ge : 0) * g.s_total + g.s_scratch;
-            const uint32_t* otmpl = reinterpret_cast<const uint32_t*>(sc + g.s_otmpl);
-            const uint16_t pair = reinterpret_cast<const uint16_t*>(sc + g.s_slotpair)[v ? s : 0];
-            uint32_t d[2];
-#pragma unroll
-            for (int h = 0; h < 2; h++) {
-                const int cc = 2 * g4 + h, w = cc < nwo ? cc : nwo - 1;
-                d[h] = otmpl[w] | (w == pcol ? (uint32_t)pair << pshift : 0u);
-            }
-            const u4v x = bytes_to_bf16(d[0], d[1]);
-            acc[i] = (f4){0, 0, 0, 0};
-            acc[i] = mfma_bf16(wo.hi[0], x, acc[i]);
-            acc[i] = mfma_bf16(wo.mid[0], x, acc[i]);
-            acc[i] = mfma_bf16(wo.lo[0], x, acc[i]);
-            const int64_t item = e * Uo + s;
-            uint32_t r0, r1;
-            philox2((uint32_t)(item & ~64ll) + (uint32_t)fa.off.row_base, fa.off_offset + dev_off, fa.seed, r0, r1);
-            u2[i] = u24((item & 64) ? r1 : r0);
-            row[i] = v ? (int)item : -1;
-        }
-        int act[2];
-        float lp[2];
-        ho.run2(acc, Ao, g4, u2, act, lp);
-#pragma unroll
-        for (int i = 0; i < 2; i++)
-            if (row[i] >= 0 && g4 == 0) {
-                fa.off_action[row[i]] = (int8_t)act[i];
-                fa.off_logprob[row[i]] = lp[i];
             }
     }
 }
@@ -1822,15 +1832,19 @@ __global__ void __launch_bounds__(64, 4) k_env_step(Params P, int64_t E, uint8_t
 }
 
 // the round of k_env_step (compact acceptor observations) and then the next round's acting (fused_act)
+// (two waves per SIMD: the launches it serves (cfg2, 4096 replicas) have no more, and the registers hold the
+// acting weights across the round)
 template <int LPE, class SH>
-__global__ void __launch_bounds__(64, 4) k_env_step_act(Params P, int64_t E, uint8_t* recs, uint32_t* mt, Liab* liab,
+__global__ void __launch_bounds__(64, 2) k_env_step_act(Params P, int64_t E, uint8_t* recs, uint32_t* mt, Liab* liab,
                                                      StepIO io, FusedAct fa) {
     if (io.span && threadIdx.x == 0) {
         io.span[4 * blockIdx.x] = __builtin_amdgcn_s_memrealtime();
         io.span[4 * blockIdx.x + 2] = __builtin_amdgcn_s_memtime();
     }
+    FusedW w;
+    fused_weights(fa, w);  // in flight during the round
     env_round<LPE, false, true, SH>(P, E, recs, mt, liab, io, blockIdx.x);
-    fused_act<LPE, SH>(P, E, fa, blockIdx.x);
+    fused_act<LPE, SH>(P, E, fa, w, blockIdx.x);
     if (io.span && threadIdx.x == 0) {
         io.span[4 * blockIdx.x + 3] = __builtin_amdgcn_s_memtime();
         io.span[4 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime();
