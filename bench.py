@@ -302,7 +302,14 @@ def bench_other(args):
         b_round = env_round_bytes(tr.env.shape, tr.cfg.new_jobs_per_round, tr.free, tr.compact)
         result["roofline"] = env_roofline(b_round, E, launch_us, tr.compact)
         result["roofline"]["clock_mhz"] = tr.launch_clock_mhz()
+        if getattr(tr, "fused_step", False):  # cfg2: the env launch also samples the next round's actions
+            result["roofline"]["kernel"] = "ms::k_env_step_act"
+            result["roofline"]["fused_next_act"] = (
+                "each launch span also holds round t+1's acting (offer + acceptor units from the observations "
+                "in its LDS); bytes are the env round's alone")
         result["act_roofline"] = act_roofline(tr, device)
+        if getattr(tr, "fused_step", False):
+            result["act_roofline"]["rollout_use"] = "round 0 only; rounds 1..T-1 act inside ms::k_env_step_act"
     if rank == 0:
         print(json.dumps(result))
     if world > 1:

@@ -1622,39 +1622,13 @@ __device__ __forceinline__ void env_round(const Params& P, int64_t E, uint8_t* r
 //      offer net and one acceptor net (n_groups 1), each one 32-input k-step and <= 16 actions
 //      (env_step_act_supported); item i of a net is row i (e * units + u), its uniform word (i >> 6) & 1 of
 //      the draw countered by row (i & ~64) + row_base, as in k_act_common's scan.
-// The fused acting's weights, issued at the start of the launch (their loads overlap the env round):
-// each lane's fragment of both nets (ms_act_prepare) and its dword of the acceptor's common-row table.
-struct FusedW {
-    W1Split<1> wo, wa;
-    Head<1> ho, ha;
-    uint32_t tab;   // table dword `lane` (< 34): 16 running sums, 16 log-probs, S, last nonzero action
-    bool frag;      // both fragment blocks present (else fused_act derives the weights)
-};
-__device__ __forceinline__ void fused_weights(const FusedAct& fa, FusedW& w) {
-    using FL = FragLayout<1, 1>;
-    const int lane = threadIdx.x;
-    const uint32_t* fo = frag_groups<1, 1>(fa.off, false);
-    const uint32_t* fc = frag_groups<1, 1>(fa.acc, true);
-    w.frag = fo && fc;
-    w.tab = 0;
-    if (w.frag) {
-        w.wo.load_frag(fo + lane * FL::LW);
-        w.ho.load_frag(reinterpret_cast<const float*>(fo + lane * FL::LW + 12));
-        w.wa.load_frag(fc + lane * FL::LW);
-        w.ha.load_frag(reinterpret_cast<const float*>(fc + lane * FL::LW + 12));
-        w.tab = fc[64 * FL::LW + (lane < 34 ? lane : 0)];
-    }
-}
-
 template <int LPE, class SH>
-__device__ __forceinline__ void fused_act(const Params& P, int64_t E, const FusedAct& fa, FusedW& w, int64_t slot) {
+__device__ __forceinline__ void fused_act(const Params& P, int64_t E, const FusedAct& fa, int64_t slot) {
     constexpr int EPW = kWave / LPE;  // envs per wave
     extern __shared__ __align__(16) uint8_t smem_all[];
     __shared__ float s_cum[16], s_lp[16];
-    __shared__ uint32_t s_tab[2];        // the common row's S (f32 bits) and last nonzero action
+    __shared__ uint32_t s_tab[2];  // the common row's S (f32 bits) and last nonzero action
     __shared__ uint32_t s_tmpl[8];
-    __shared__ int32_t s_list[kWave];    // listed (owner-row) acceptor items: lane of the scan
-    __shared__ float s_ulist[kWave];
     Geom g;
     if constexpr (SH::kStatic) {
         constexpr Geom kg = make_geom(SH::kN, SH::kC, SH::kL, SH::kJ);
@@ -1666,23 +1640,37 @@ __device__ __forceinline__ void fused_act(const Params& P, int64_t E, const Fuse
     const int C = g.C, Ua = g.N * C, Uo = g.NL;
     const int64_t e0 = slot * EPW;
     const uint64_t dev_off = fa.offset_dev ? *fa.offset_dev : 0ull;
-    if (w.frag) {
+    // weights: the act fragment blocks (ms_act_prepare), else derived from the f32 weights (bit-identical)
+    W1Split<1> wo, wa;
+    Head<1> ho, ha;
+    using FL = FragLayout<1, 1>;
+    const uint32_t* fo = frag_groups<1, 1>(fa.off, false);
+    const uint32_t* fc = frag_groups<1, 1>(fa.acc, true);
+    if (fo) {
+        wo.load_frag(fo + lane * FL::LW);
+        ho.load_frag(reinterpret_cast<const float*>(fo + lane * FL::LW + 12));
+    } else {
+        wo.load(fa.off.w1, fa.off.in_dim, j, g4);
+        ho.load(fa.off, 0, j, g4);
+    }
+    if (fc) {
+        wa.load_frag(fc + lane * FL::LW);
+        ha.load_frag(reinterpret_cast<const float*>(fc + lane * FL::LW + 12));
         if (lane < 34) {
+            const uint32_t v = fc[64 * FL::LW + lane];  // [16 running sums][16 log-probs][S][last nonzero]
             if (lane < 16)
-                s_cum[lane] = __uint_as_float(w.tab);
+                s_cum[lane] = __uint_as_float(v);
             else if (lane < 32)
-                s_lp[lane - 16] = __uint_as_float(w.tab);
+                s_lp[lane - 16] = __uint_as_float(v);
             else
-                s_tab[lane - 32] = w.tab;
+                s_tab[lane - 32] = v;
         }
-    } else {  // derived from the f32 weights (bit-identical to the fragments)
-        w.wo.load(fa.off.w1, fa.off.in_dim, j, g4);
-        w.ho.load(fa.off, 0, j, g4);
-        w.wa.load(fa.acc.w1, fa.acc.in_dim, j, g4);
-        w.ha.load(fa.acc, 0, j, g4);
+    } else {
+        wa.load(fa.acc.w1, fa.acc.in_dim, j, g4);
+        ha.load(fa.acc, 0, j, g4);
         float S0;
         int lnz0;
-        common_table<1, 1>(w.wa, w.ha, fa.common, g.acc_stride >> 2, s_tmpl, s_cum, s_lp, &S0, &lnz0, lane);
+        common_table<1, 1>(wa, ha, fa.common, g.acc_stride >> 2, s_tmpl, s_cum, s_lp, &S0, &lnz0, lane);
         if (lane == 0) {
             s_tab[0] = __float_as_uint(S0);
             s_tab[1] = (uint32_t)lnz0;
@@ -1691,12 +1679,17 @@ __device__ __forceinline__ void fused_act(const Params& P, int64_t E, const Fuse
     wave_sync();  // the table, and the round's observation sources in every group's LDS slice
     const int Aa = fa.acc.n_actions, Ao = fa.off.n_actions;
     const int nw = g.acc_stride >> 2, nwo = g.off_stride >> 2;
-    // ---- offer units: their rows (the slot's template + pair) in 16-row tiles, two per step
+    auto philox_u = [&](int64_t item, int64_t row_base, uint64_t off) {  // item i's uniform (k_act_common's rule)
+        uint32_t r0, r1;
+        philox2((uint32_t)(item & ~64ll) + (uint32_t)row_base, off + dev_off, fa.seed, r0, r1);
+        return u24((item & 64) ? r1 : r0);
+    };
+    // ---- the MFMA rows, all issued before either head runs (the three tiles' chains are independent):
+    //      offers: every slot's row (template + pair), 16-row tiles; acceptors: the row of each owned core,
+    //      which is the owner's acceptor row (item (owner - 1) * C + c); every other acceptor row is the
+    //      common row (sampled from its table below). EPW * C <= 16: one tile.
     const int pcol = (2 * C) >> 2, pshift = 8 * ((2 * C) & 3);
-    for (int t0 = 0; t0 < EPW * Uo; t0 += 32) {
-        f4 acc[2];
-        int row[2];
-        float u2[2];
+    auto offer_rows = [&](int t0, f4* acc, int* row, float* u2) {
 #pragma unroll
         for (int i = 0; i < 2; i++) {
             const int r = t0 + 16 * i + j;
@@ -1714,43 +1707,68 @@ __device__ __forceinline__ void fused_act(const Params& P, int64_t E, const Fuse
             }
             const u4v x = bytes_to_bf16(d[0], d[1]);
             acc[i] = (f4){0, 0, 0, 0};
-            acc[i] = mfma_bf16(w.wo.hi[0], x, acc[i]);
-            acc[i] = mfma_bf16(w.wo.mid[0], x, acc[i]);
-            acc[i] = mfma_bf16(w.wo.lo[0], x, acc[i]);
+            acc[i] = mfma_bf16(wo.hi[0], x, acc[i]);
+            acc[i] = mfma_bf16(wo.mid[0], x, acc[i]);
+            acc[i] = mfma_bf16(wo.lo[0], x, acc[i]);
             const int64_t item = e * Uo + s;
-            uint32_t r0, r1;
-            philox2((uint32_t)(item & ~64ll) + (uint32_t)fa.off.row_base, fa.off_offset + dev_off, fa.seed, r0, r1);
-            u2[i] = u24((item & 64) ? r1 : r0);
+            u2[i] = philox_u(item, fa.off.row_base, fa.off_offset);
             row[i] = v ? (int)item : -1;
         }
-        int act[2];
-        float lp[2];
-        w.ho.run2(acc, Ao, g4, u2, act, lp);
+    };
+    auto store = [&](int8_t* act_out, float* lp_out, const int* row, const int* act, const float* lp) {
 #pragma unroll
         for (int i = 0; i < 2; i++)
-            if (row[i] >= 0 && g4 == 0) {
-                fa.off_action[row[i]] = (int8_t)act[i];
-                fa.off_logprob[row[i]] = lp[i];
+            if (g4 == 0 && row[i] >= 0) {
+                act_out[row[i]] = (int8_t)act[i];
+                lp_out[row[i]] = lp[i];
             }
+    };
+    f4 acc_o[2], acc_a[2];
+    int row_o[2], row_a[2], act_o[2], act_a[2];
+    float u_o[2], u_a[2], lp_o[2], lp_a[2];
+    offer_rows(0, acc_o, row_o, u_o);
+    {
+        const int ge = j / C, c = j - ge * C;
+        const int64_t e = e0 + ge;
+        const uint8_t* sl = smem_all + (size_t)(ge < EPW ? ge : 0) * g.s_total;
+        const int owner = (int)reinterpret_cast<const int8_t*>(sl + g.s_rec + g.o_core_owner)[c];
+        const bool v = ge < EPW && e < E && owner > 0;
+        const uint32_t* crow = reinterpret_cast<const uint32_t*>(sl + g.s_scratch) + c * nw;
+        const int c0 = 2 * g4, c1 = 2 * g4 + 1;
+        const u4v x = bytes_to_bf16(crow[c0 < nw ? c0 : nw - 1], crow[c1 < nw ? c1 : nw - 1]);
+        acc_a[0] = (f4){0, 0, 0, 0};
+        acc_a[0] = mfma_bf16(wa.hi[0], x, acc_a[0]);
+        acc_a[0] = mfma_bf16(wa.mid[0], x, acc_a[0]);
+        acc_a[0] = mfma_bf16(wa.lo[0], x, acc_a[0]);
+        acc_a[1] = acc_a[0];  // (an empty partner tile: no row of it is written)
+        const int64_t item = e * Ua + (owner - 1) * C + c;
+        u_a[0] = philox_u(item, fa.acc.row_base, fa.acc_offset);
+        u_a[1] = 0.f;
+        row_a[0] = v ? (int)item : -1;
+        row_a[1] = -1;
     }
-    // ---- acceptors, one lane per item: rows equal to the common row sample from its table, the owners'
-    //      rows are listed for the MFMA tile
+    ho.run2(acc_o, Ao, g4, u_o, act_o, lp_o);
+    ha.run2(acc_a, Aa, g4, u_a, act_a, lp_a);
+    store(fa.off_action, fa.off_logprob, row_o, act_o, lp_o);
+    store(fa.acc_action, fa.acc_logprob, row_a, act_a, lp_a);
+    for (int t0 = 32; t0 < EPW * Uo; t0 += 32) {  // (LPE 16: four replicas' offers)
+        offer_rows(t0, acc_o, row_o, u_o);
+        ho.run2(acc_o, Ao, g4, u_o, act_o, lp_o);
+        store(fa.off_action, fa.off_logprob, row_o, act_o, lp_o);
+    }
+    // ---- acceptors whose row is the common row (a core the agent does not own): one lane per item, sampled
+    //      from the common row's table (k_act_common's scan)
     const float S = __uint_as_float(s_tab[0]);
     const int last_nz = (int)s_tab[1];
-    int n_list;
     {
         const int ge = lane / Ua, u = lane - ge * Ua, a = u / C, c = u - a * C;
         const int64_t e = e0 + ge;
-        const bool in = lane < EPW * Ua && e < E;
         const uint8_t* sl = smem_all + (size_t)(ge < EPW ? ge : 0) * g.s_total;
-        const int owner = in ? (int)reinterpret_cast<const int8_t*>(sl + g.s_rec + g.o_core_owner)[c] : 0;
-        const int64_t item = e * Ua + u;
-        uint32_t r0, r1;
-        philox2((uint32_t)(item & ~64ll) + (uint32_t)fa.acc.row_base, fa.acc_offset + dev_off, fa.seed, r0, r1);
-        const float uu = u24((item & 64) ? r1 : r0);
-        const bool common = in && owner != a + 1;
-        if (common) {
-            const float target = uu * S;
+        const bool in = lane < EPW * Ua && e < E;
+        const int owner = (int)reinterpret_cast<const int8_t*>(sl + g.s_rec + g.o_core_owner)[c];
+        if (in && owner != a + 1) {
+            const int64_t item = e * Ua + u;
+            const float target = philox_u(item, fa.acc.row_base, fa.acc_offset) * S;
             int cnt = 0;
 #pragma unroll
             for (int step = 16; step >= 1; step >>= 1)
@@ -1759,46 +1777,6 @@ __device__ __forceinline__ void fused_act(const Params& P, int64_t E, const Fuse
             fa.acc_action[item] = (int8_t)act;
             fa.acc_logprob[item] = s_lp[act];
         }
-        const bool other = in && !common;
-        const uint64_t m = __ballot(other);
-        if (other) {
-            const int pos = __popcll(m & ((1ull << lane) - 1ull));
-            s_list[pos] = lane;
-            s_ulist[pos] = uu;
-        }
-        n_list = __popcll(m);
-    }
-    wave_sync();
-    for (int t0 = 0; t0 < n_list; t0 += 32) {
-        f4 acc[2];
-        int row[2];
-        float u2[2];
-#pragma unroll
-        for (int i = 0; i < 2; i++) {
-            const int k = t0 + 16 * i + j;
-            const bool v = k < n_list;
-            const int ln = s_list[v ? k : 0];
-            const int ge = ln / Ua, u = ln - ge * Ua, c = u - (u / C) * C;
-            const uint32_t* crow = reinterpret_cast<const uint32_t*>(smem_all + (size_t)ge * g.s_total + g.s_scratch) +
-                                   c * nw;
-            const int c0 = 2 * g4, c1 = 2 * g4 + 1;
-            const u4v x = bytes_to_bf16(crow[c0 < nw ? c0 : nw - 1], crow[c1 < nw ? c1 : nw - 1]);
-            acc[i] = (f4){0, 0, 0, 0};
-            acc[i] = mfma_bf16(w.wa.hi[0], x, acc[i]);
-            acc[i] = mfma_bf16(w.wa.mid[0], x, acc[i]);
-            acc[i] = mfma_bf16(w.wa.lo[0], x, acc[i]);
-            row[i] = v ? (int)((e0 + ge) * Ua + u) : -1;
-            u2[i] = v ? s_ulist[k] : 0.f;
-        }
-        int act[2];
-        float lp[2];
-        w.ha.run2(acc, Aa, g4, u2, act, lp);
-#pragma unroll
-        for (int i = 0; i < 2; i++)
-            if (row[i] >= 0 && g4 == 0) {
-                fa.acc_action[row[i]] = (int8_t)act[i];
-                fa.acc_logprob[row[i]] = lp[i];
-            }
     }
 }
 
@@ -1832,19 +1810,15 @@ __global__ void __launch_bounds__(64, 4) k_env_step(Params P, int64_t E, uint8_t
 }
 
 // the round of k_env_step (compact acceptor observations) and then the next round's acting (fused_act)
-// (two waves per SIMD: the launches it serves (cfg2, 4096 replicas) have no more, and the registers hold the
-// acting weights across the round)
 template <int LPE, class SH>
-__global__ void __launch_bounds__(64, 2) k_env_step_act(Params P, int64_t E, uint8_t* recs, uint32_t* mt, Liab* liab,
+__global__ void __launch_bounds__(64, 4) k_env_step_act(Params P, int64_t E, uint8_t* recs, uint32_t* mt, Liab* liab,
                                                      StepIO io, FusedAct fa) {
     if (io.span && threadIdx.x == 0) {
         io.span[4 * blockIdx.x] = __builtin_amdgcn_s_memrealtime();
         io.span[4 * blockIdx.x + 2] = __builtin_amdgcn_s_memtime();
     }
-    FusedW w;
-    fused_weights(fa, w);  // in flight during the round
     env_round<LPE, false, true, SH>(P, E, recs, mt, liab, io, blockIdx.x);
-    fused_act<LPE, SH>(P, E, fa, w, blockIdx.x);
+    fused_act<LPE, SH>(P, E, fa, blockIdx.x);
     if (io.span && threadIdx.x == 0) {
         io.span[4 * blockIdx.x + 3] = __builtin_amdgcn_s_memtime();
         io.span[4 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime();
@@ -2025,10 +1999,11 @@ hipError_t launch_env_step(const Params& P, int64_t E, uint8_t* recs, uint32_t* 
         default: return launch_step_t<64>(P, E, recs, mt, liab, io, s);
     }
 }
-// ms_env_step_act: a wave's acceptor items one per lane and its offer rows in 16-row tiles (<= 64 each)
+// ms_env_step_act: a wave's acceptor items one per lane (<= 64), its offer rows in 16-row tiles (<= 64) and
+// its owned cores' rows in one
 bool env_step_act_supported(const Params& P, int64_t E) {
     const int epw = kWave / lanes_per_env(P, E);
-    return epw * P.N * P.C <= kWave && epw * P.NL <= kWave && P.C <= 16;
+    return epw * P.N * P.C <= kWave && epw * P.NL <= kWave && epw * P.C <= 16;
 }
 template <int LPE, class SH>
 static hipError_t launch_step_act_sh(const Params& P, int64_t E, uint8_t* recs, uint32_t* mt, Liab* liab,
