@@ -415,6 +415,28 @@ int ms_env_step_act(ms_env* env, const ms_actions* act, const ms_obs_out* obs, c
 /* 1 when ms_env_step_act can run this env's rounds (fixed prices, the shapes above), else 0. */
 int ms_env_step_act_supported(const ms_env* env);
 
+/* Per-round byte strides of ms_env_rollout_act's arrays: round t uses each array given to it
+ * advanced by t * stride bytes (0: the same array every round), and the acting after round t draws
+ * with off_offset / acc_offset + t * offset_step. */
+typedef struct ms_round_strides {
+    int64_t acceptor_action, offer_action;            /* ms_actions acceptor / offer_core */
+    int64_t core_rows, core_owner, offer_obs;         /* ms_obs_out */
+    int64_t offer_reward, acceptor_reward, agent_reward, auctioneer_reward;  /* ms_reward_out */
+    int64_t next_off_action, next_off_logprob, next_acc_action, next_acc_logprob;  /* ms_fused_act outputs */
+    uint64_t offset_step;
+} ms_round_strides;
+
+/* n_rounds consecutive ms_env_step_act calls in one launch (trainPPO.py:160-167's loop body for
+ * rounds t = 0 .. n_rounds - 1 of a fixed-price rollout, ring arrays advanced per round by `strides`):
+ * each wave steps its replicas and samples their next actions round after round, reading back what it
+ * wrote, with no launch between rounds. The acting after the last round runs only when
+ * act_after_last != 0. ev->launch_span (optional) records the whole launch ([waves][4]). Outputs
+ * are bit-identical to the n_rounds separate calls. Same requirements as ms_env_step_act, plus
+ * no accepted / terminated event records and no price / aggregated reward outputs. */
+int ms_env_rollout_act(ms_env* env, const ms_actions* act, const ms_obs_out* obs, const ms_reward_out* rew,
+                       const ms_event_out* ev, const ms_fused_act* next, const ms_round_strides* strides,
+                       int32_t n_rounds, int32_t act_after_last, void* stream);
+
 /* Discounted Monte-Carlo returns + per-sequence normalisation (PPOmodules.py:128-137):
  * rewards [T][M] (f32, as stored per round), for each sequence m:
  * G_t = r_t + gamma*G_{t+1} in float64, cast to f32, then

@@ -53,6 +53,9 @@ def _load():
                                        ct.POINTER(abi.MsRewardOut), ct.POINTER(abi.MsEventOut),
                                        ct.POINTER(abi.MsFusedAct), P]),
         "ms_env_step_act_supported": (ct.c_int, [P]),
+        "ms_env_rollout_act": (ct.c_int, [P, ct.POINTER(abi.MsActions), ct.POINTER(abi.MsObsOut),
+                                          ct.POINTER(abi.MsRewardOut), ct.POINTER(abi.MsEventOut),
+                                          ct.POINTER(abi.MsFusedAct), ct.POINTER(abi.MsRoundStrides), i32, i32, P]),
         "ms_env_round": (i64, [P]),
         "ms_env_flags": (ct.c_int, [P, ct.POINTER(u32), P]),
         "ms_env_randbelow": (ct.c_int, [P, i64, u32, ct.POINTER(u32), P]),
@@ -116,12 +119,14 @@ def _load():
     # ABI 14 added ms_bdqn_update*, 15 ms_bdqn_act_compact, 16 ms_mlp_params.row_base (a trailing field an
     # older library does not read: its acting draws are those of row_base 0). An older library (an A/B variant built
     # before them, tools/gpu_job.sh ab step) loads without them only when MARLSCHED_LENIENT_ABI=1 asks for it
-    lenient = os.environ.get("MARLSCHED_LENIENT_ABI") == "1" and version in (13, 14, 15)
+    lenient = os.environ.get("MARLSCHED_LENIENT_ABI") == "1" and version in (13, 14, 15, 16)
     if version != ABI_VERSION and not lenient:
         raise ImportError("libmarlsched.so ABI version mismatch (%d, want %d)" % (version, ABI_VERSION))
     for name, (res, args) in sig.items():
         if (version < 14 and name.startswith("ms_bdqn_update")) or (version < 15 and name == "ms_bdqn_act_compact") \
                 or (version < 16 and name.startswith("ms_env_step_act")):
+            continue
+        if lenient and not hasattr(L, name):  # an older build of this ABI (A/B variants)
             continue
         fn = getattr(L, name)
         fn.restype = res
@@ -134,7 +139,7 @@ lib = _load()
 # every entry point include/marlsched.h declares (checked by tests)
 EXPORTED = (
     "ms_last_error", "ms_abi_version", "ms_config_shape", "ms_env_create", "ms_env_destroy", "ms_env_shape",
-    "ms_env_reset", "ms_env_step", "ms_env_step_act", "ms_env_step_act_supported", "ms_env_round", "ms_env_flags", "ms_env_randbelow", "ms_env_auctioneer",
+    "ms_env_reset", "ms_env_step", "ms_env_step_act", "ms_env_step_act_supported", "ms_env_rollout_act", "ms_env_round", "ms_env_flags", "ms_env_randbelow", "ms_env_auctioneer",
     "ms_env_get_rng", "ms_env_set_rng", "ms_env_export",
     "ms_env_import", "ms_policy_act", "ms_policy_act_common", "ms_policy_act_compact",
     "ms_act_round_free", "ms_price_table_build", "ms_act_frag_bytes", "ms_act_prepare", "ms_offer_act_free", "ms_discounted_returns", "ms_unit_returns",

@@ -205,6 +205,13 @@ class MsFusedAct(ct.Structure):  # ms_fused_act (ABI 16)
                 ("acc_logprob", ct.c_void_p)]
 
 
+class MsRoundStrides(ct.Structure):  # ms_round_strides (ABI 16): bytes per round
+    _fields_ = [(n, ct.c_int64) for n in ("acceptor_action", "offer_action", "core_rows", "core_owner", "offer_obs",
+                                          "offer_reward", "acceptor_reward", "agent_reward", "auctioneer_reward",
+                                          "next_off_action", "next_off_logprob", "next_acc_action",
+                                          "next_acc_logprob")] + [("offset_step", ct.c_uint64)]
+
+
 class MsQnetParams(ct.Structure):
     _fields_ = [("w1", ct.c_void_p), ("b1", ct.c_void_p), ("w2", ct.c_void_p), ("b2", ct.c_void_p),
                 ("in_dim", ct.c_int32), ("hidden", ct.c_int32), ("n_actions", ct.c_int32), ("n_groups", ct.c_int32)]

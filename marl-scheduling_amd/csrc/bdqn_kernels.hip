@@ -138,7 +138,7 @@ __global__ void __launch_bounds__(256) k_bdqn_l1_cores(BdqnL1Compact p) {
     const int tid = threadIdx.x, lane = tid & 63;
     const int i = lane & 15, g4 = lane >> 4;
     const long long gw = (long long)blockIdx.x * 4 + (tid >> 6);
-    const int C = p.C, D = p.D, Dp = p.Dp;
+    const int C = p.C, Dp = p.Dp;
     const long long rtiles = (p.E + 15) / 16;
     const long long chunks = (rtiles + kL1TilesPerWave - 1) / kL1TilesPerWave;
     // wave -> (core, hidden tile, replica chunk); the 8 hidden tiles of a (core, chunk) are neighbours

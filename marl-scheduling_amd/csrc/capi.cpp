@@ -28,6 +28,8 @@ hipError_t launch_env_step(const Params&, int64_t, uint8_t*, uint32_t*, Liab*, c
 hipError_t launch_env_step_act(const Params&, int64_t, uint8_t*, uint32_t*, Liab*, const StepIO&, const FusedAct&,
                                hipStream_t);
 bool env_step_act_supported(const Params&, int64_t);
+hipError_t launch_env_rollout_act(const Params&, int64_t, uint8_t*, uint32_t*, Liab*, const StepIO&, const FusedAct&,
+                                  const RoundStride&, int, int, hipStream_t);
 hipError_t launch_env_randbelow(const Params&, uint8_t*, uint32_t*, int64_t, uint32_t, uint32_t*, hipStream_t);
 hipError_t launch_env_auctioneer(const Params&, int64_t, uint8_t*, uint32_t*, int8_t*, hipStream_t);
 hipError_t launch_policy_act(const ms_mlp_params*, const int8_t*, int, int64_t, int, int, const int8_t*, uint64_t,
@@ -243,37 +245,69 @@ int ms_env_reset(ms_env* env, const ms_obs_out* obs, void* stream) {
     return MS_OK;
 }
 
+struct RolloutArgs {
+    ms::RoundStride st;
+    int n_rounds, act_last;
+};
 static int env_step_impl(ms_env* env, const ms_actions* act, const ms_obs_out* obs, const ms_reward_out* rew,
-                         const ms_event_out* ev, const ms::FusedAct* fa, void* stream);
+                         const ms_event_out* ev, const ms::FusedAct* fa, const RolloutArgs* ro, void* stream);
 
 int ms_env_step(ms_env* env, const ms_actions* act, const ms_obs_out* obs, const ms_reward_out* rew,
                 const ms_event_out* ev, void* stream) {
-    return env_step_impl(env, act, obs, rew, ev, nullptr, stream);
+    return env_step_impl(env, act, obs, rew, ev, nullptr, nullptr, stream);
+}
+
+// the checks ms_env_step_act and ms_env_rollout_act share; fills fa
+static int fused_act_args(ms_env* env, const ms_actions* act, const ms_obs_out* obs, const ms_event_out* ev,
+                          const ms_fused_act* next, const char* who, ms::FusedAct* fa) {
+    if (!env || !next) return fail(MS_EINVAL, "env/next is NULL");
+    const ms::Params& P = env->P;
+    auto bad = [&](const char* why) { return fail(MS_EINVAL, "%s: %s", who, why); };
+    if (env->cfg.free_prices) return bad("fixed-price rounds only");
+    if (!obs || !obs->core_rows || !obs->core_owner || !obs->offer || obs->acceptor)
+        return bad("needs compact acceptor observations (core_rows, core_owner) and offer rows");
+    if (!act || !act->acceptor || (ev && ev->metrics)) return bad("the trainer's round only (actions given, no metrics)");
+    const ms_mlp_params& o = next->offer;
+    const ms_mlp_params& a = next->acceptor;
+    if (o.n_groups != 1 || a.n_groups != 1 || o.hidden != 16 || a.hidden != 16 || !o.act_frag || !a.act_frag)
+        return bad("one 16-wide net per role with act fragments");
+    if (o.in_dim != P.d_off || a.in_dim != P.d_acc || o.n_actions != P.C + 1 || a.n_actions != P.O + 1)
+        return bad("net shapes do not match the env");
+    if (P.off_stride > 32 || P.acc_stride > 32 || o.n_actions > 16 || a.n_actions > 16 ||
+        !ms::env_step_act_supported(P, env->E))
+        return bad("shape not supported (one k-step, <= 16 actions, a wave's rows)");
+    if (!next->off_action || !next->off_logprob || !next->acc_action || !next->acc_logprob || !next->common_row)
+        return bad("NULL output / common row");
+    *fa = ms::FusedAct{o, a, next->common_row, next->seed, next->off_offset, next->acc_offset, next->offset_dev,
+                       next->off_action, next->off_logprob, next->acc_action, next->acc_logprob};
+    return MS_OK;
 }
 
 int ms_env_step_act(ms_env* env, const ms_actions* act, const ms_obs_out* obs, const ms_reward_out* rew,
                     const ms_event_out* ev, const ms_fused_act* next, void* stream) {
-    if (!env || !next) return fail(MS_EINVAL, "env/next is NULL");
-    const ms::Params& P = env->P;
-    if (env->cfg.free_prices) return fail(MS_EINVAL, "ms_env_step_act: fixed-price rounds only");
-    if (!obs || !obs->core_rows || !obs->core_owner || !obs->offer || obs->acceptor)
-        return fail(MS_EINVAL, "ms_env_step_act: needs compact acceptor observations (core_rows, core_owner) and offer rows");
-    if (!act || !act->acceptor || (ev && ev->metrics))
-        return fail(MS_EINVAL, "ms_env_step_act: the trainer's round only (actions given, no metrics)");
-    const ms_mlp_params& o = next->offer;
-    const ms_mlp_params& a = next->acceptor;
-    if (o.n_groups != 1 || a.n_groups != 1 || o.hidden != 16 || a.hidden != 16 || !o.act_frag || !a.act_frag)
-        return fail(MS_EINVAL, "ms_env_step_act: one 16-wide net per role with act fragments");
-    if (o.in_dim != P.d_off || a.in_dim != P.d_acc || o.n_actions != P.C + 1 || a.n_actions != P.O + 1)
-        return fail(MS_EINVAL, "ms_env_step_act: net shapes do not match the env");
-    if (P.off_stride > 32 || P.acc_stride > 32 || o.n_actions > 16 || a.n_actions > 16 ||
-        !ms::env_step_act_supported(P, env->E))
-        return fail(MS_EINVAL, "ms_env_step_act: shape not supported (one k-step, <= 16 actions, a wave's rows)");
-    if (!next->off_action || !next->off_logprob || !next->acc_action || !next->acc_logprob || !next->common_row)
-        return fail(MS_EINVAL, "ms_env_step_act: NULL output / common row");
-    ms::FusedAct fa{o, a, next->common_row, next->seed, next->off_offset, next->acc_offset, next->offset_dev, next->off_action,
-                    next->off_logprob, next->acc_action, next->acc_logprob};
-    return env_step_impl(env, act, obs, rew, ev, &fa, stream);
+    ms::FusedAct fa;
+    const int rc = fused_act_args(env, act, obs, ev, next, "ms_env_step_act", &fa);
+    if (rc != MS_OK) return rc;
+    return env_step_impl(env, act, obs, rew, ev, &fa, nullptr, stream);
+}
+
+int ms_env_rollout_act(ms_env* env, const ms_actions* act, const ms_obs_out* obs, const ms_reward_out* rew,
+                       const ms_event_out* ev, const ms_fused_act* next, const ms_round_strides* strides,
+                       int32_t n_rounds, int32_t act_after_last, void* stream) {
+    ms::FusedAct fa;
+    const int rc = fused_act_args(env, act, obs, ev, next, "ms_env_rollout_act", &fa);
+    if (rc != MS_OK) return rc;
+    if (!strides || n_rounds < 1) return fail(MS_EINVAL, "ms_env_rollout_act: strides NULL or n_rounds < 1");
+    if (ev && (ev->accepted || ev->terminated))
+        return fail(MS_EINVAL, "ms_env_rollout_act: no accepted / terminated event records");
+    if (rew && (rew->price || rew->aggregated_offer || rew->aggregated_acceptor))
+        return fail(MS_EINVAL, "ms_env_rollout_act: no price / aggregated reward outputs");
+    const ms_round_strides& r = *strides;
+    RolloutArgs ro{{r.acceptor_action, r.offer_action, r.core_rows, r.core_owner, r.offer_obs, r.offer_reward,
+                    r.acceptor_reward, r.agent_reward, r.auctioneer_reward, r.next_off_action, r.next_off_logprob,
+                    r.next_acc_action, r.next_acc_logprob, r.offset_step},
+                   n_rounds, act_after_last ? 1 : 0};
+    return env_step_impl(env, act, obs, rew, ev, &fa, &ro, stream);
 }
 
 int ms_env_step_act_supported(const ms_env* env) {
@@ -284,7 +318,7 @@ int ms_env_step_act_supported(const ms_env* env) {
 }
 
 static int env_step_impl(ms_env* env, const ms_actions* act, const ms_obs_out* obs, const ms_reward_out* rew,
-                         const ms_event_out* ev, const ms::FusedAct* fa, void* stream) {
+                         const ms_event_out* ev, const ms::FusedAct* fa, const RolloutArgs* ro, void* stream) {
     if (!env || !act) return fail(MS_EINVAL, "env/actions is NULL");
     if (!act->acceptor != !act->offer_core)
         return fail(MS_EINVAL, "acceptor and offer_core actions are given together (both NULL: hard-coded agents)");
@@ -325,11 +359,14 @@ static int env_step_impl(ms_env* env, const ms_actions* act, const ms_obs_out* o
         io.metrics_slots = ev->metrics_slots;
         if (io.metrics && io.metrics_slots < 1) return fail(MS_EINVAL, "ms_env_step: metrics_slots must be >= 1");
     }
-    if (fa)
+    if (ro)
+        HIP_TRY(ms::launch_env_rollout_act(env->P, env->E, env->recs, env->mt, env->liab, io, *fa, ro->st, ro->n_rounds,
+                                           ro->act_last, (hipStream_t)stream));
+    else if (fa)
         HIP_TRY(ms::launch_env_step_act(env->P, env->E, env->recs, env->mt, env->liab, io, *fa, (hipStream_t)stream));
     else
         HIP_TRY(ms::launch_env_step(env->P, env->E, env->recs, env->mt, env->liab, io, (hipStream_t)stream));
-    env->round += 1;
+    env->round += ro ? ro->n_rounds : 1;
     return MS_OK;
 }
 

@@ -982,7 +982,7 @@ constexpr int kLiabPrefetch = 4;  // newest chain entries loaded ahead per core 
 // training loop's form: its act and gradient kernels read core rows + owners).
 template <int LPE, bool EXT, bool CMP, class SH>
 __device__ __forceinline__ void env_round(const Params& P, int64_t E, uint8_t* recs, uint32_t* mt, Liab* liab,
-                                          const StepIO& io, int64_t slot) {
+                                          const StepIO& io, int64_t slot, int lane_arg = -1) {
     extern __shared__ __align__(16) uint8_t smem_all[];
     // the shape: a compile-time constant for the BASELINE shapes (offsets fold into immediates,
     // loops over agents / cores / slots get constant trip counts), else the kernel arguments
@@ -993,7 +993,7 @@ __device__ __forceinline__ void env_round(const Params& P, int64_t E, uint8_t* r
     } else {
         g = P;
     }
-    const int lane = threadIdx.x;
+    const int lane = lane_arg >= 0 ? lane_arg : (int)threadIdx.x;  // (k_env_rollout_act: opaque per round)
     const Lanes<LPE> Lg(lane);
     const int gl = Lg.gl;
     const int64_t e_raw = slot * (kWave / LPE) + (lane / LPE);
@@ -1623,7 +1623,8 @@ __device__ __forceinline__ void env_round(const Params& P, int64_t E, uint8_t* r
 //      (env_step_act_supported); item i of a net is row i (e * units + u), its uniform word (i >> 6) & 1 of
 //      the draw countered by row (i & ~64) + row_base, as in k_act_common's scan.
 template <int LPE, class SH>
-__device__ __forceinline__ void fused_act(const Params& P, int64_t E, const FusedAct& fa, int64_t slot) {
+__device__ __forceinline__ void fused_act(const Params& P, int64_t E, const FusedAct& fa, int64_t slot,
+                                          int lane_arg = -1) {
     constexpr int EPW = kWave / LPE;  // envs per wave
     extern __shared__ __align__(16) uint8_t smem_all[];
     __shared__ float s_cum[16], s_lp[16];
@@ -1636,7 +1637,7 @@ __device__ __forceinline__ void fused_act(const Params& P, int64_t E, const Fuse
     } else {
         g = P;
     }
-    const int lane = threadIdx.x, j = lane & 15, g4 = lane >> 4;
+    const int lane = lane_arg >= 0 ? lane_arg : (int)threadIdx.x, j = lane & 15, g4 = lane >> 4;
     const int C = g.C, Ua = g.N * C, Uo = g.NL;
     const int64_t e0 = slot * EPW;
     const uint64_t dev_off = fa.offset_dev ? *fa.offset_dev : 0ull;
@@ -1822,6 +1823,75 @@ __global__ void __launch_bounds__(64, 4) k_env_step_act(Params P, int64_t E, uin
     if (io.span && threadIdx.x == 0) {
         io.span[4 * blockIdx.x + 3] = __builtin_amdgcn_s_memtime();
         io.span[4 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime();
+    }
+}
+
+template <class T>
+__device__ __forceinline__ T* advance(T* p, int64_t bytes) {
+    return p ? reinterpret_cast<T*>(reinterpret_cast<uintptr_t>(p) + bytes) : p;
+}
+// n_rounds rounds of k_env_step_act in one launch: each wave steps its replicas, then samples their next
+// actions, round after round; round t's arrays are the given ones advanced by t strides. A round reads what
+// the wave's lanes wrote in the round before (records, MT blocks, liabilities, actions): a workgroup-scope
+// fence (the wave is its workgroup) orders those writes before the next round's loads.
+// Every round re-reads its arguments from the kernel-argument segment through a pointer the compiler cannot
+// see through, and takes the lane index the same way: otherwise the loop-invariant argument loads and
+// lane arithmetic are hoisted out of the round loop and held across it (hundreds of spilled registers).
+struct RolloutArgs {
+    Params P;
+    int64_t E;
+    uint8_t* recs;
+    uint32_t* mt;
+    Liab* liab;
+    StepIO io;
+    FusedAct fa;
+    RoundStride st;
+    int n_rounds, act_last;
+};
+template <int LPE, class SH>
+__global__ void __launch_bounds__(64, 2) k_env_rollout_act(RolloutArgs A0) {
+    unsigned long long* span = A0.io.span;
+    if (span && threadIdx.x == 0) {
+        span[4 * blockIdx.x] = __builtin_amdgcn_s_memrealtime();
+        span[4 * blockIdx.x + 2] = __builtin_amdgcn_s_memtime();
+    }
+    const int n_rounds = A0.n_rounds;
+    for (int t = 0; t < n_rounds; t++) {
+        auto ka = __builtin_amdgcn_kernarg_segment_ptr();  // (constant address space)
+        asm volatile("" : "+s"(ka));
+        const RolloutArgs& A = *(const RolloutArgs*)ka;
+        int lane = threadIdx.x;
+        asm volatile("" : "+v"(lane));
+        const RoundStride& st = A.st;
+        StepIO io = A.io;
+        io.span = nullptr;
+        io.act_acc = advance(io.act_acc, t * st.act_acc);
+        io.act_off = advance(io.act_off, t * st.act_off);
+        io.obs_crow = advance(io.obs_crow, t * st.obs_crow);
+        io.obs_cown = advance(io.obs_cown, t * st.obs_cown);
+        io.obs_off = advance(io.obs_off, t * st.obs_off);
+        io.rew_offer = advance(io.rew_offer, t * st.rew_offer);
+        io.rew_acc = advance(io.rew_acc, t * st.rew_acc);
+        io.rew_agent = advance(io.rew_agent, t * st.rew_agent);
+        io.rew_auct = advance(io.rew_auct, t * st.rew_auct);
+        env_round<LPE, false, true, SH>(A.P, A.E, A.recs, A.mt, A.liab, io, blockIdx.x, lane);
+        if (t + 1 < n_rounds || A.act_last) {
+            FusedAct fa = A.fa;
+            fa.off_action = advance(fa.off_action, t * st.off_action);
+            fa.off_logprob = advance(fa.off_logprob, t * st.off_logprob);
+            fa.acc_action = advance(fa.acc_action, t * st.acc_action);
+            fa.acc_logprob = advance(fa.acc_logprob, t * st.acc_logprob);
+            fa.off_offset += (uint64_t)t * st.offset_step;
+            fa.acc_offset += (uint64_t)t * st.offset_step;
+            fused_act<LPE, SH>(A.P, A.E, fa, blockIdx.x, lane);
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        wave_sync();
+    }
+    if (span && threadIdx.x == 0) {
+        span[4 * blockIdx.x + 3] = __builtin_amdgcn_s_memtime();
+        span[4 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime();
     }
 }
 
@@ -2027,6 +2097,35 @@ hipError_t launch_env_step_act(const Params& P, int64_t E, uint8_t* recs, uint32
 #endif
             return launch_step_act_sh<32, DynShape>(P, E, recs, mt, liab, io, fa, s);
         default: return launch_step_act_sh<64, DynShape>(P, E, recs, mt, liab, io, fa, s);
+    }
+}
+template <int LPE, class SH>
+static hipError_t launch_rollout_act_sh(const Params& P, int64_t E, uint8_t* recs, uint32_t* mt, Liab* liab,
+                                        const StepIO& io, const FusedAct& fa, const RoundStride& st, int n_rounds,
+                                        int act_last, hipStream_t s) {
+    constexpr int G = kWave / LPE;
+    const int64_t blocks = (E + G - 1) / G;
+    const size_t lds = (size_t)P.s_total * G > 4 * kMtN ? (size_t)P.s_total * G : 4 * kMtN;
+    const RolloutArgs A{P, E, recs, mt, liab, io, fa, st, n_rounds, act_last};
+    hipLaunchKernelGGL((k_env_rollout_act<LPE, SH>), dim3((unsigned)blocks), dim3(kWave), lds, s, A);
+    return hipGetLastError();
+}
+hipError_t launch_env_rollout_act(const Params& P, int64_t E, uint8_t* recs, uint32_t* mt, Liab* liab,
+                                  const StepIO& io, const FusedAct& fa, const RoundStride& st, int n_rounds,
+                                  int act_last, hipStream_t s) {
+    if (!env_step_act_supported(P, E) || io.act_acc == nullptr || io.metrics != nullptr || io.obs_acc != nullptr ||
+        n_rounds < 1)
+        return hipErrorInvalidValue;
+    switch (lanes_per_env(P, E)) {
+        case 16: return launch_rollout_act_sh<16, DynShape>(P, E, recs, mt, liab, io, fa, st, n_rounds, act_last, s);
+        case 32:
+#ifndef MS_NO_FIXED_SHAPES
+            if (is_shape<4, 4, 3, 1>(P))
+                return launch_rollout_act_sh<32, FixShape<4, 4, 3, 1>>(P, E, recs, mt, liab, io, fa, st, n_rounds,
+                                                                       act_last, s);
+#endif
+            return launch_rollout_act_sh<32, DynShape>(P, E, recs, mt, liab, io, fa, st, n_rounds, act_last, s);
+        default: return launch_rollout_act_sh<64, DynShape>(P, E, recs, mt, liab, io, fa, st, n_rounds, act_last, s);
     }
 }
 hipError_t launch_env_auctioneer(const Params& P, int64_t E, uint8_t* recs, uint32_t* mt, int8_t* actions,

@@ -177,6 +177,13 @@ struct FusedAct {
     float* acc_logprob;
 };
 
+// per-round byte strides of k_env_rollout_act (ms_round_strides)
+struct RoundStride {
+    int64_t act_acc, act_off, obs_crow, obs_cown, obs_off, rew_offer, rew_acc, rew_agent, rew_auct;
+    int64_t off_action, off_logprob, acc_action, acc_logprob;
+    uint64_t offset_step;
+};
+
 // launch arguments of k_aggregate_obs (agg_kernels.hip): divided rows in, aggregated rows out
 struct AggArgs {
     const int8_t* acc;  // [E][N][C][acc_stride]

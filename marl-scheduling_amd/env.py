@@ -175,6 +175,28 @@ class BatchedEnv:
             assert auctioneer.numel() == self.E * self.C
         obs = self.obs_buffers() if obs is None else obs
         rewards = self.reward_buffers() if rewards is None else rewards
+        a, o, r, ev = self._step_structs(acceptor, offer_core, offer_price, auctioneer, obs, rewards, events)
+        if next_act is not None:
+            check(lib.ms_env_step_act(self._h, ct.byref(a), ct.byref(o), ct.byref(r), ct.byref(ev) if ev else None,
+                                      ct.byref(next_act), stream_ptr(stream)))
+        else:
+            check(lib.ms_env_step(self._h, ct.byref(a), ct.byref(o), ct.byref(r), ct.byref(ev) if ev else None,
+                                  stream_ptr(stream)))
+        return obs, rewards, events
+
+    def rollout_act(self, acceptor, offer_core, obs, rewards, next_act, strides, n_rounds, act_after_last=False,
+                    events=None, stream=None):
+        """n_rounds rounds of step(next_act=...) in one launch (ms_env_rollout_act): round t reads and
+        writes the given arrays advanced by t * strides (an abi.MsRoundStrides, bytes) and acts with the
+        Philox offsets + t * strides.offset_step. Bit-identical to the n_rounds step calls."""
+        for t in (acceptor, offer_core):
+            assert t.dtype == torch.int8 and t.device == self.device
+        a, o, r, ev = self._step_structs(acceptor, offer_core, None, None, obs, rewards, events)
+        check(lib.ms_env_rollout_act(self._h, ct.byref(a), ct.byref(o), ct.byref(r), ct.byref(ev) if ev else None,
+                                     ct.byref(next_act), ct.byref(strides), int(n_rounds), int(bool(act_after_last)),
+                                     stream_ptr(stream)))
+
+    def _step_structs(self, acceptor, offer_core, offer_price, auctioneer, obs, rewards, events):
         a = abi.MsActions(ptr(acceptor), ptr(offer_core), ptr(offer_price if self.free_prices else None),
                           ptr(auctioneer))
         o = abi.MsObsOut(ptr(obs.get("acceptor")), ptr(obs.get("offer")), ptr(obs.get("auctioneer")),
@@ -189,13 +211,7 @@ class BatchedEnv:
                 assert m.dtype == torch.uint8 and m.is_contiguous() and m.shape[1:] == (self.E, abi.METRICS_BYTES)
             ev = abi.MsEventOut(ptr(events.get("accepted")), ptr(events.get("terminated")),
                                 ptr(events.get("launch_span")), ptr(m), 0 if m is None else m.shape[0])
-        if next_act is not None:
-            check(lib.ms_env_step_act(self._h, ct.byref(a), ct.byref(o), ct.byref(r), ct.byref(ev) if ev else None,
-                                      ct.byref(next_act), stream_ptr(stream)))
-        else:
-            check(lib.ms_env_step(self._h, ct.byref(a), ct.byref(o), ct.byref(r), ct.byref(ev) if ev else None,
-                                  stream_ptr(stream)))
-        return obs, rewards, events
+        return a, o, r, ev
 
     def fused_act_supported(self) -> bool:
         """Whether step(next_act=...) can run this env's rounds (ms_env_step_act_supported)."""

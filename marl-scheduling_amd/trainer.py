@@ -267,8 +267,11 @@ class Trainer:
         # (MS_ENV_FUSED_ACT=0: the act launch and the env launch of every round, for A/B measurements)
         self.fused_step = (self.compact and not self.free and self.acc.group.policy.G == 1 and
                            self.off.group.policy.G == 1 and self.acc_frag is not None and
-                           os.environ.get("MS_ENV_FUSED_ACT", "1") != "0" and
+                           os.environ.get("MS_ENV_FUSED_ACT", "1") != "0" and self.metric_bufs is None and
                            all(env.fused_act_supported() for env, _, _ in self.env.parts))
+        # ... and the whole rollout's rounds are one launch (ms_env_rollout_act): each wave steps and acts
+        # for its replicas round after round (MS_ENV_ROLLOUT=0: one launch per round, for A/B measurements)
+        self.fused_rollout = self.fused_step and os.environ.get("MS_ENV_ROLLOUT", "1") != "0"
         self.span_every = 0  # > 0: every span_every-th round's env launches record their span (bench)
         self.spans = None
         self.timings = dict(rollout=0.0, update=0.0)
@@ -402,18 +405,41 @@ class Trainer:
         ev = dict(launch_span=self.spans[t, k]) if self.span_every and t % self.span_every == 0 else None
         if self.metric_bufs is not None:
             ev = dict(ev or {}, metrics=self.metric_bufs[k])
-        nxt = None
-        if self.fused_step and t + 1 < self.T:
-            # round t + 1's getActionForAllAgents (the fixed-price pair of _act_part) in this launch
-            seed, base, rb = self.seed * 7919, 8 * (t + 1), self.rank * self.E + e0
-            nxt = abi.MsFusedAct(self.off.group.policy_old.mlp_params(self.off_frag, rb * N * L),
-                                 self.acc.group.policy_old.mlp_params(self.acc_frag, rb * N * C), ptr(self.acc_common),
-                                 seed, base + 1, base + 3, ptr(self.rng_ctr), ptr(sl(self.off.actions[t + 1])),
-                                 ptr(sl(self.off.logprobs[t + 1])), ptr(sl(self.acc.actions[t + 1])),
-                                 ptr(sl(self.acc.logprobs[t + 1])))
+        nxt = self._fused_next(t + 1, k) if self.fused_step and t + 1 < self.T else None
         env.step(sl(self.acc.actions[t]).view(E, N, C), sl(self.off.actions[t]).view(E, N, L),
                  sl(self.env_price).view(E, N, L) if self.free else None, obs=obs, rewards=rew, events=ev, stream=st,
                  next_act=nxt)
+
+    def _fused_next(self, t: int, k: int):
+        """Round t's getActionForAllAgents (the fixed-price pair of _act_part) for replica part k, as the
+        acting fused into round t - 1's env launch."""
+        e0, e1 = self.env.parts[k][1:]
+        sl = lambda x: x[e0:e1]
+        N, C, L = self.N, self.C, self.L
+        seed, base, rb = self.seed * 7919, 8 * t, self.rank * self.E + e0
+        return abi.MsFusedAct(self.off.group.policy_old.mlp_params(self.off_frag, rb * N * L),
+                              self.acc.group.policy_old.mlp_params(self.acc_frag, rb * N * C), ptr(self.acc_common),
+                              seed, base + 1, base + 3, ptr(self.rng_ctr), ptr(sl(self.off.actions[t])),
+                              ptr(sl(self.off.logprobs[t])), ptr(sl(self.acc.actions[t])), ptr(sl(self.acc.logprobs[t])))
+
+    def _rollout_part(self, k: int):
+        """Rounds 0..T-1 of replica part k (env.step + saveRewards, and the acting of rounds 1..T-1) in
+        one launch (ms_env_rollout_act); round 0's acting ran before it (_act_part)."""
+        env, e0, e1 = self.env.parts[k]
+        E, N, C, L = e1 - e0, self.N, self.C, self.L
+        sl = lambda x: x[e0:e1]
+        obs = dict(self._acc_out(1, e0, e1), offer=sl(self.off_obs[1]))
+        rew = dict(offer=sl(self.off.rewards[0]).view(E, N, L), acceptor=sl(self.acc.rewards[0]).view(E, N, C),
+                   agent=sl(self.agent_reward), auctioneer=sl(self.auct_reward))
+        ev = dict(launch_span=self.spans[0, k]) if self.span_every else None
+        b = lambda x: x.stride(0) * x.element_size()  # bytes between ring slots t and t + 1
+        strides = abi.MsRoundStrides(b(self.acc.actions), b(self.off.actions), b(self.acc_rows), b(self.acc_owner),
+                                     b(self.off_obs), b(self.off.rewards), b(self.acc.rewards), 0, 0,
+                                     b(self.off.actions), b(self.off.logprobs), b(self.acc.actions),
+                                     b(self.acc.logprobs), 8)
+        env.rollout_act(sl(self.acc.actions[0]).view(E, N, C), sl(self.off.actions[0]).view(E, N, L), obs, rew,
+                        self._fused_next(1, k), strides, self.T, act_after_last=False, events=ev,
+                        stream=self.streams[k])
 
     def record_launch_spans(self, every: int):
         """Every `every`-th round's env launches record their span (first wave start, last wave end
@@ -425,7 +451,15 @@ class Trainer:
         self.spans = torch.zeros((self.T, len(self.env.parts), w, 4), dtype=torch.int64, device=self.device)
 
     def launch_spans_us(self):
-        """Durations (us) of the recorded env launches of the last rollout."""
+        """Durations (us) of the recorded env launches of the last rollout (fused_rollout: the one
+        launch of each part over T, per round)."""
+        if self.fused_rollout:
+            sp = self.spans[0].cpu().numpy()  # [parts][waves][4]
+            out = []
+            for w in sp:
+                w = w[w[:, 1] > 0]
+                out.append(float(w[:, 1].max() - w[:, 0].min()) / 100.0 / self.T)
+            return out
         sp = self.spans[:: self.span_every].cpu().numpy()  # [rounds][parts][waves][4]
         out = []
         for r in range(sp.shape[0]):
@@ -450,8 +484,13 @@ class Trainer:
         self._prepare_acting()
         for s in self.streams[1:]:  # fork: the side streams start after everything queued so far
             s.wait_stream(cur)
-        for t in range(self.T):
-            self.round(t)
+        if self.fused_rollout:
+            for k in range(len(self.env.parts)):
+                self._act_part(0, k)
+                self._rollout_part(k)
+        else:
+            for t in range(self.T):
+                self.round(t)
         for s in self.streams[1:]:  # join
             cur.wait_stream(s)
         self.rng_ctr.add_(8 * self.T)

@@ -65,24 +65,35 @@ def test_compact_trainer_equals_materialised_and_oracle(ms, name, E, T):
 @pytest.mark.parametrize("E,T", [(4096, 16), (96, 24), (1001, 12)])
 def test_fused_env_act_equals_two_launches(ms, monkeypatch, E, T):
     """cfg2 (fixed prices, one net per role): round t's env launch also samples round t + 1's actions from
-    the observations in its LDS (ms_env_step_act). Every ring equals the two-launch trainer's (the paired
-    act launch, then the env launch) bit for bit over two iterations: E = 4096 runs the fused
-    k_env_step_act<32, FixShape<4,4,3,1>>, E = 96 the LPE-16 generic one (four replicas per wave), E = 1001 a
-    partial last wave (one replica)."""
+    the observations in its LDS (ms_env_step_act), and by default the whole rollout is one launch
+    (ms_env_rollout_act: each wave loops over the rounds). Every ring of the one-launch rollout, of the
+    launch-per-round rollout and of the two-launch trainer (the paired act launch, then the env launch)
+    are equal bit for bit over two iterations: E = 4096 runs k_env_*_act<32, FixShape<4,4,3,1>>, E = 96
+    the LPE-16 generic one (four replicas per wave), E = 1001 a partial last wave (one replica)."""
     tr_mod = importlib.import_module("marl-scheduling_amd.trainer")
     mk = lambda: tr_mod.Trainer.from_named("cfg2", n_envs=E, update_step=T, seed=9, device="cuda:0")
-    fused = mk()
+    whole = mk()
+    monkeypatch.setenv("MS_ENV_ROLLOUT", "0")
+    per_round = mk()
     monkeypatch.setenv("MS_ENV_FUSED_ACT", "0")
     plain = mk()
-    assert fused.fused_step and not plain.fused_step
+    assert whole.fused_rollout and per_round.fused_step and not per_round.fused_rollout and not plain.fused_step
+    trs = (whole, per_round, plain)
     for it in range(2):
-        for t in (fused, plain):
+        for t in trs:
             t.rollout()
         torch.cuda.synchronize()
-        r0, r1 = _rings(fused), _rings(plain)
-        for k in r0:
-            assert torch.equal(r0[k], r1[k]), (it, k)
-        losses = [t.update() for t in (fused, plain)]
+        rings = [_rings(t) for t in trs]
+        for k in rings[0]:
+            for r in rings[1:]:
+                assert torch.equal(rings[0][k], r[k]), (it, k)
+        losses = [t.update() for t in trs]
         for k in losses[0]:
-            assert torch.equal(losses[0][k], losses[1][k]), (it, k)
-    assert fused.flags() == 0
+            for l in losses[1:]:
+                assert torch.equal(losses[0][k], l[k]), (it, k)
+    assert all(t.flags() == 0 for t in trs)
+    # the env state after the rollouts too (ms_env_export)
+    st = [t.env.parts[0][0].export_state() for t in trs]
+    for k in st[0]:
+        for o in st[1:]:
+            assert (st[0][k] == o[k]).all(), k
