@@ -303,13 +303,15 @@ def bench_other(args):
         result["roofline"] = env_roofline(b_round, E, launch_us, tr.compact)
         result["roofline"]["clock_mhz"] = tr.launch_clock_mhz()
         if getattr(tr, "fused_step", False):  # cfg2: the env launch also samples the next round's actions
-            result["roofline"]["kernel"] = "ms::k_env_step_act"
+            whole = getattr(tr, "fused_rollout", False)
+            result["roofline"]["kernel"] = "ms::k_env_rollout_act" if whole else "ms::k_env_step_act"
             result["roofline"]["fused_next_act"] = (
-                "each launch span also holds round t+1's acting (offer + acceptor units from the observations "
-                "in its LDS); bytes are the env round's alone")
+                "each round also holds round t+1's acting (offer + acceptor units from the observations in its "
+                "LDS); bytes are the env round's alone" +
+                ("; one launch runs all %d rounds: avg_launch_us = its span / %d" % (tr.T, tr.T) if whole else ""))
         result["act_roofline"] = act_roofline(tr, device)
         if getattr(tr, "fused_step", False):
-            result["act_roofline"]["rollout_use"] = "round 0 only; rounds 1..T-1 act inside ms::k_env_step_act"
+            result["act_roofline"]["rollout_use"] = "round 0 only; rounds 1..T-1 act inside the env launch"
     if rank == 0:
         print(json.dumps(result))
     if world > 1:
