@@ -110,9 +110,6 @@ __device__ __forceinline__ void act_tiles(const ActArgs& a, int block) {
     const int wv = gw - grp * a.waves_per_group;
     if (grp >= a.n1.n_groups) return;
     MS_APROBE_BEGIN
-#ifdef MS_XP_PRIO_OFF
-    __builtin_amdgcn_s_setprio(MS_XP_PRIO_OFF);
-#endif
     const int j = lane & 15, g4 = lane >> 4;
     constexpr int NP = NT2 > 0 ? NT2 : 1;
     constexpr int TW = PriceTW<NP>::v;
@@ -438,9 +435,6 @@ __device__ __forceinline__ void act_common_rows(const ActArgs& a, int block) {
     const int wv = gw - grp * a.waves_per_group;
     if (grp >= a.n1.n_groups) return;  // whole waves only: the kernel has no block barrier
     MS_APROBE_BEGIN
-#ifdef MS_XP_PRIO_ACC
-    __builtin_amdgcn_s_setprio(MS_XP_PRIO_ACC);
-#endif
     const int j = lane & 15, g4 = lane >> 4;
     const int A = a.n1.n_actions;
     const int stride4 = a.stride >> 2;
