@@ -23,6 +23,8 @@ import os
 import sys
 import time
 
+import numpy as np
+
 REPO = os.path.dirname(os.path.abspath(__file__))
 if REPO not in sys.path:
     sys.path.insert(0, REPO)
@@ -269,9 +271,15 @@ def bench_other(args):
     torch.cuda.synchronize(device)
     if hasattr(tr, "timings"):
         tr.timings = dict(rollout=0.0, update=0.0)
+    # every timed iteration's env launch spans (a device copy after it), as in main()
+    span_hist = None
+    if args.config != "cfg5":
+        span_hist = torch.zeros((args.steps,) + tuple(tr.spans.shape), dtype=tr.spans.dtype, device=device)
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    for i in range(args.steps):
         run()
+        if span_hist is not None:
+            span_hist[i].copy_(tr.spans)
     torch.cuda.synchronize(device)
     if world > 1:
         dist.barrier()
@@ -298,10 +306,12 @@ def bench_other(args):
     if args.config == "cfg5":
         result["roofline"] = bdqn_act_roofline(tr, device)
     else:
-        launch_us = tr.launch_spans_us()
+        per_iter_us = [tr.launch_spans_us(span_hist[i]) for i in range(args.steps)]
+        launch_us = [v for it in per_iter_us for v in it]
         b_round = env_round_bytes(tr.env.shape, tr.cfg.new_jobs_per_round, tr.free, tr.compact)
         result["roofline"] = env_roofline(b_round, E, launch_us, tr.compact)
-        result["roofline"]["clock_mhz"] = tr.launch_clock_mhz()
+        result["roofline"]["avg_launch_us_per_iteration"] = [sum(v) / len(v) for v in per_iter_us]
+        result["roofline"]["clock_mhz"] = median_clock(tr, span_hist)
         if getattr(tr, "fused_step", False):  # cfg2: the env launch also samples the next round's actions
             whole = getattr(tr, "fused_rollout", False)
             result["roofline"]["kernel"] = "ms::k_env_rollout_act" if whole else "ms::k_env_step_act"
@@ -414,9 +424,15 @@ def act_roofline(tr, device, reps: int = 20):
                              "after the timed region" % reps}
 
 
+def median_clock(tr, span_hist):
+    """The env waves' median shader clock (MHz) over the timed iterations' recorded launches."""
+    v = [c for c in (tr.launch_clock_mhz(h) for h in span_hist) if c is not None]
+    return float(np.median(v)) if v else None
+
+
 def env_roofline(b_round: int, envs: int, launch_us, compact: bool, variant_traffic: bool = True):
     """k_env_step's roofline entry: SURVEY 8(d) algorithmic bytes per env-round x replicas per launch
-    over the in-region launch span (tr.record_launch_spans)."""
+    over the in-region launch spans (tr.record_launch_spans), averaged over the timed iterations."""
     avg_s = sum(launch_us) / len(launch_us) / 1e6
     achieved = b_round * envs / avg_s / 1e9
     traffic = committed_traffic(b_round * envs, "compact" if compact else "") if variant_traffic else None
@@ -544,10 +560,14 @@ def step_kernel_line(E: int, device, world: int, rank: int):
         obs = env.compact_obs_buffers()
         rew = env.reward_buffers()
         env.reset(obs)
+        # every 10th round's launch span (first wave start -> last wave end) and its waves' shader
+        # clock, as the main line records them inside the rollout: the two lines compare on one box
+        spans = torch.zeros((STEP_RING // 10, E, 4), dtype=torch.int64, device=device)  # >= the launch's waves
 
         def body():
             for t in range(STEP_RING):
-                env.step(acc[t], off[t], price[t], obs=obs, rewards=rew)
+                ev = dict(launch_span=spans[t // 10]) if t % 10 == 0 else None
+                env.step(acc[t], off[t], price[t], obs=obs, rewards=rew, events=ev)
 
         for _ in range(STEP_WARMUP_ROUNDS // STEP_RING):
             body()
@@ -574,8 +594,18 @@ def step_kernel_line(E: int, device, world: int, rank: int):
             raise SystemExit("env error flags set in the step-kernel run: 0x%x" % env.flags())
         b_round = env_round_bytes(env.shape, cfg.new_jobs_per_round, True, True)
         us = sec / STEP_TIMED_ROUNDS * 1e6
+        sp = spans.cpu().numpy()
+        span_us, clk = [], []
+        for w in sp:
+            w = w[w[:, 1] > 0]
+            if len(w):
+                span_us.append(float(w[:, 1].max() - w[:, 0].min()) / 100.0)
+                ok = (w[:, 1] > w[:, 0]) & (w[:, 3] > w[:, 2])
+                clk.extend(((w[ok, 3] - w[ok, 2]) / (w[ok, 1] - w[ok, 0]) * 100.0).tolist())
         per_seed[str(seed)] = {"value": world * E * N * STEP_TIMED_ROUNDS / sec, "us_per_round": us,
-                               "frac": b_round * E / (us * 1e-6) / 1e9 / HBM_PEAK_GBS}
+                               "frac": b_round * E / (us * 1e-6) / 1e9 / HBM_PEAK_GBS,
+                               "launch_span_us": sum(span_us) / len(span_us) if span_us else None,
+                               "clock_mhz": float(np.median(clk)) if clk else None}
         del graph, env
     vals = [v["value"] for v in per_seed.values()]
     return {"metric": "agent-env-steps/s, env step kernel alone (SURVEY 8(d)(i))", "unit": "agent-env-steps/s",
@@ -584,7 +614,10 @@ def step_kernel_line(E: int, device, world: int, rank: int):
             "timed_rounds": STEP_TIMED_ROUNDS,
             "actions": "uniform, pre-sampled into a %d-round device ring" % STEP_RING,
             "timing": "HIP events on the launch stream around %d replays of a %d-round HIP graph"
-                      % (STEP_TIMED_ROUNDS // STEP_RING, STEP_RING)}
+                      % (STEP_TIMED_ROUNDS // STEP_RING, STEP_RING),
+            "launch_span": "launch_span_us: first wave start to last wave end of every 10th round's launch "
+                           "(the main line's roofline uses the same span inside the rollout); us_per_round also "
+                           "holds the gaps between launches"}
 
 
 def main():
@@ -641,16 +674,22 @@ def main():
         dist.barrier()
     torch.cuda.synchronize(device)
     tr.timings = dict(rollout=0.0, update=0.0)
+    # every timed iteration's spans, copied on the device after it (a ~2.6 MB copy per iteration): the
+    # policy changes as it trains and with it the env's work per round (more executions, spawns), so the
+    # span is averaged over all timed iterations, not read from the last one alone
+    span_hist = torch.zeros((args.steps,) + tuple(tr.spans.shape), dtype=tr.spans.dtype, device=device)
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    for i in range(args.steps):
         tr.iteration()
+        span_hist[i].copy_(tr.spans)
     torch.cuda.synchronize(device)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(device)
     elapsed = time.perf_counter() - t0
     timings = dict(tr.timings)
-    launch_us = tr.launch_spans_us()
+    per_iter_us = [tr.launch_spans_us(span_hist[i]) for i in range(args.steps)]
+    launch_us = [v for it in per_iter_us for v in it]
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=device)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -706,11 +745,13 @@ def main():
             "envs_per_launch": part_envs,
             "avg_launch_us": avg_step_s * 1e6,
             "launches_timed": len(launch_us),
-            # the env waves' shader clock over the same launches (s_memtime cycles / s_memrealtime ticks):
-            # the in-region span moves with it from box to box
-            "clock_mhz": tr.launch_clock_mhz(),
+            # per timed iteration: the policy trains, so the env's work per round drifts (from random init,
+            # the span grows over the first ~20 iterations: profiles/r5q)
+            "avg_launch_us_per_iteration": [sum(v) / len(v) for v in per_iter_us],
+            # the env waves' shader clock over the same launches (s_memtime cycles / s_memrealtime ticks)
+            "clock_mhz": median_clock(tr, span_hist),
             "launch_timing": "first-wave-start to last-wave-end span (s_memrealtime, 100 MHz) of every %d-th "
-                             "round's env launches in the last timed iteration (graph replay)" % SAMPLE_EVERY,
+                             "round's env launches in every timed iteration (graph replay), averaged" % SAMPLE_EVERY,
         },
         "breakdown_ms_per_step": {
             "rollout": timings["rollout"] / args.steps * 1e3,

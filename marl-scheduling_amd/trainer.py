@@ -450,17 +450,18 @@ class Trainer:
         w = self.env.parts[0][2] - self.env.parts[0][1]
         self.spans = torch.zeros((self.T, len(self.env.parts), w, 4), dtype=torch.int64, device=self.device)
 
-    def launch_spans_us(self):
+    def launch_spans_us(self, spans=None):
         """Durations (us) of the recorded env launches of the last rollout (fused_rollout: the one
-        launch of each part over T, per round)."""
+        launch of each part over T, per round), or of `spans` (a copy of self.spans)."""
+        spans = self.spans if spans is None else spans
         if self.fused_rollout:
-            sp = self.spans[0].cpu().numpy()  # [parts][waves][4]
+            sp = spans[0].cpu().numpy()  # [parts][waves][4]
             out = []
             for w in sp:
                 w = w[w[:, 1] > 0]
                 out.append(float(w[:, 1].max() - w[:, 0].min()) / 100.0 / self.T)
             return out
-        sp = self.spans[:: self.span_every].cpu().numpy()  # [rounds][parts][waves][4]
+        sp = spans[:: self.span_every].cpu().numpy()  # [rounds][parts][waves][4]
         out = []
         for r in range(sp.shape[0]):
             for k in range(sp.shape[1]):
@@ -469,9 +470,10 @@ class Trainer:
                 out.append(float(w[:, 1].max() - w[:, 0].min()) / 100.0)
         return out
 
-    def launch_clock_mhz(self):
+    def launch_clock_mhz(self, spans=None):
         """Median shader clock (MHz) of the recorded env launches' waves: shader cycles over 100 MHz ticks."""
-        sp = self.spans[:: self.span_every].cpu().numpy().reshape(-1, 4)
+        spans = self.spans if spans is None else spans
+        sp = spans[:: self.span_every].cpu().numpy().reshape(-1, 4)
         sp = sp[(sp[:, 1] > sp[:, 0]) & (sp[:, 3] > sp[:, 2])]
         if len(sp) == 0:
             return None
