@@ -758,13 +758,42 @@ __device__ void hardcoded_auctioneer(Rec& R, const Geom& P, const M128* s_mc, co
         s_auct[gl] = (int16_t)O;
     }
     // tie-break draws in core order on the env stream (Auctioneer.getAuctioneerAction
-    // Auctioneer.py:95-102), only for the cores with a candidate
+    // Auctioneer.py:95-102), only for the cores with a candidate. The draws run on the words the
+    // window already holds: each draw takes the first word from the stream position at which its
+    // _randbelow accepts (MtStream::randbelow's rule), the chain carried in registers, and each
+    // core lane reads its accepted word once at the end; a draw the window cannot finish and the
+    // ones after it go through MtStream::randbelow.
     const uint64_t need = L.ballot(gl < C && nt > 0);
     int my_pick = 0;
-    for (uint64_t m = need; m; m &= m - 1) {
-        const int c = __ffsll((unsigned long long)m) - 1;
-        const uint32_t pick = rs.randbelow(L.shfl((uint32_t)nt, c), L);
-        if (gl == c) my_pick = (int)pick;
+    if (need) {
+        if (rs.p >= rs.wend) rs.load(rs.p, 1, L);
+        const uint32_t tv = rs.word();
+        const int wpos = rs.wb + gl;
+        const bool live = wpos < rs.wend;
+        int p = rs.p, my_q = -1, my_sh = 0;
+        uint64_t rest = need;
+        for (uint64_t m = need; m; m &= m - 1) {
+            const int c = __ffsll((unsigned long long)m) - 1;
+            const uint32_t n = L.shfl((uint32_t)nt, c);
+            const int sh = __clz(n);  // 32 - n.bit_length()
+            const uint64_t acc = L.ballot(live && wpos >= p && (tv >> sh) < n);
+            if (!acc) break;
+            const int q = __ffsll((unsigned long long)acc) - 1;
+            if (gl == c) {
+                my_q = q;
+                my_sh = sh;
+            }
+            p = rs.wb + q + 1;
+            rest &= rest - 1;
+        }
+        const uint32_t w = L.shfl(tv, my_q < 0 ? 0 : my_q);
+        if (my_q >= 0) my_pick = (int)(w >> my_sh);
+        rs.p = p;
+        for (uint64_t m = rest; m; m &= m - 1) {
+            const int c = __ffsll((unsigned long long)m) - 1;
+            const uint32_t pick = rs.randbelow(L.shfl((uint32_t)nt, c), L);
+            if (gl == c) my_pick = (int)pick;
+        }
     }
     // the pick-th maximal candidate's position in the padded list
     if (gl < C && nt > 0) s_auct[gl] = (int16_t)kth_bit(ties, my_pick);
