@@ -274,12 +274,13 @@ def bench_other(args):
     # every timed iteration's env launch spans (a device copy after it), as in main()
     span_hist = None
     if args.config != "cfg5":
-        span_hist = torch.zeros((args.steps,) + tuple(tr.spans.shape), dtype=tr.spans.dtype, device=device)
+        sampled = tr.sampled_spans()
+        span_hist = torch.zeros((args.steps,) + tuple(sampled.shape), dtype=sampled.dtype, device=device)
     t0 = time.perf_counter()
     for i in range(args.steps):
         run()
         if span_hist is not None:
-            span_hist[i].copy_(tr.spans)
+            span_hist[i].copy_(sampled)
     torch.cuda.synchronize(device)
     if world > 1:
         dist.barrier()
@@ -674,14 +675,15 @@ def main():
         dist.barrier()
     torch.cuda.synchronize(device)
     tr.timings = dict(rollout=0.0, update=0.0)
-    # every timed iteration's spans, copied on the device after it (a ~2.6 MB copy per iteration): the
+    # every timed iteration's recorded spans, copied on the device after it (~5 MB, a few us): the
     # policy changes as it trains and with it the env's work per round (more executions, spawns), so the
     # span is averaged over all timed iterations, not read from the last one alone
-    span_hist = torch.zeros((args.steps,) + tuple(tr.spans.shape), dtype=tr.spans.dtype, device=device)
+    sampled = tr.sampled_spans()  # the recorded rounds only (~5 MB at cfg3: a few us per copy)
+    span_hist = torch.zeros((args.steps,) + tuple(sampled.shape), dtype=sampled.dtype, device=device)
     t0 = time.perf_counter()
     for i in range(args.steps):
         tr.iteration()
-        span_hist[i].copy_(tr.spans)
+        span_hist[i].copy_(sampled)
     torch.cuda.synchronize(device)
     if world > 1:
         dist.barrier()

@@ -402,7 +402,7 @@ class Trainer:
         rew = dict(offer=sl(self.off.rewards[t]).view(E, N, L), acceptor=sl(self.acc.rewards[t]).view(E, N, C),
                    agent=sl(self.agent_reward), auctioneer=sl(self.auct_reward),
                    price=sl(self.price.rewards[t]).view(E, N, L) if self.free else None)
-        ev = dict(launch_span=self.spans[t, k]) if self.span_every and t % self.span_every == 0 else None
+        ev = dict(launch_span=self.spans[t // self.span_every, k]) if self.span_every and t % self.span_every == 0 else None
         if self.metric_bufs is not None:
             ev = dict(ev or {}, metrics=self.metric_bufs[k])
         nxt = self._fused_next(t + 1, k) if self.fused_step and t + 1 < self.T else None
@@ -444,24 +444,27 @@ class Trainer:
     def record_launch_spans(self, every: int):
         """Every `every`-th round's env launches record their span (first wave start, last wave end
         on the 100 MHz s_memrealtime clock, and each wave's shader-clock cycles) into self.spans
-        [T][parts][waves][4]; read with launch_spans_us() / launch_clock_mhz(). Set before the first
+        [ceil(T / every)][parts][waves][4]; read with launch_spans_us() / launch_clock_mhz(). Set before the first
         rollout (the HIP graph captures it)."""
         self.span_every = int(every)
         w = self.env.parts[0][2] - self.env.parts[0][1]
-        self.spans = torch.zeros((self.T, len(self.env.parts), w, 4), dtype=torch.int64, device=self.device)
+        n = -(-self.T // self.span_every)  # row t // every holds round t's launches (t % every == 0)
+        self.spans = torch.zeros((n, len(self.env.parts), w, 4), dtype=torch.int64, device=self.device)
 
-    def launch_spans_us(self, spans=None):
+    def sampled_spans(self):
+        """The recorded rounds' spans ([ceil(T / span_every)][parts][waves][4], contiguous)."""
+        return self.spans
+
+    def launch_spans_us(self, sampled=None):
         """Durations (us) of the recorded env launches of the last rollout (fused_rollout: the one
-        launch of each part over T, per round), or of `spans` (a copy of self.spans)."""
-        spans = self.spans if spans is None else spans
+        launch of each part over T, per round), or of `sampled` (a copy of sampled_spans())."""
+        sp = (self.sampled_spans() if sampled is None else sampled).cpu().numpy()  # [rounds][parts][waves][4]
         if self.fused_rollout:
-            sp = spans[0].cpu().numpy()  # [parts][waves][4]
             out = []
-            for w in sp:
+            for w in sp[0]:  # [parts][waves][4]: round 0's slot holds the launch
                 w = w[w[:, 1] > 0]
                 out.append(float(w[:, 1].max() - w[:, 0].min()) / 100.0 / self.T)
             return out
-        sp = spans[:: self.span_every].cpu().numpy()  # [rounds][parts][waves][4]
         out = []
         for r in range(sp.shape[0]):
             for k in range(sp.shape[1]):
@@ -470,10 +473,9 @@ class Trainer:
                 out.append(float(w[:, 1].max() - w[:, 0].min()) / 100.0)
         return out
 
-    def launch_clock_mhz(self, spans=None):
+    def launch_clock_mhz(self, sampled=None):
         """Median shader clock (MHz) of the recorded env launches' waves: shader cycles over 100 MHz ticks."""
-        spans = self.spans if spans is None else spans
-        sp = spans[:: self.span_every].cpu().numpy().reshape(-1, 4)
+        sp = (self.sampled_spans() if sampled is None else sampled).cpu().numpy().reshape(-1, 4)
         sp = sp[(sp[:, 1] > sp[:, 0]) & (sp[:, 3] > sp[:, 2])]
         if len(sp) == 0:
             return None
@@ -482,7 +484,7 @@ class Trainer:
     def _rollout_body(self):
         cur = torch.cuda.current_stream(self.device)
         if self.span_every:
-            self.spans[:: self.span_every].zero_()
+            self.spans.zero_()
         self._prepare_acting()
         for s in self.streams[1:]:  # fork: the side streams start after everything queued so far
             s.wait_stream(cur)
