@@ -127,7 +127,7 @@ def test_two_rank_graphed_update_equals_eager(tmp_path):
             assert torch.equal(g[k], e[k]), (r, k)
 
 
-_UNION = dict(name="cfg3", E=64, T=12, iters=2, seed=3)
+_UNION = dict(E=64, T=12, iters=2, seed=3)
 
 
 def _ring_views(t):
@@ -141,7 +141,7 @@ def _ring_views(t):
     return out
 
 
-def _union_rank(rank, world, port, out_dir):
+def _union_rank(rank, world, port, out_dir, name):
     """One rank of a world-size-`world` run over E / world replicas (rank r = replicas
     [r E / world, (r + 1) E / world) of the union: env seeds env_seed(seed, r, E / world) = base + r E / world,
     Philox rows from replica_base r E / world), or the single process over all E (world 1)."""
@@ -152,7 +152,7 @@ def _union_rank(rank, world, port, out_dir):
         os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
         dist.init_process_group("gloo", rank=rank, world_size=world)
     tr = importlib.import_module("marl-scheduling_amd.trainer")
-    t = tr.Trainer.from_named(c["name"], n_envs=c["E"] // world, update_step=c["T"], seed=c["seed"], rank=rank,
+    t = tr.Trainer.from_named(name, n_envs=c["E"] // world, update_step=c["T"], seed=c["seed"], rank=rank,
                               world_size=world, use_graph=False)
     out = {}
     for it in range(c["iters"]):
@@ -166,13 +166,15 @@ def _union_rank(rank, world, port, out_dir):
             for k, v in u.group.policy.named_parameters():
                 out["it%d.w.%s.%s" % (it, u.name, k)] = v.detach().cpu().clone()
     out["flags"] = torch.tensor(t.flags())
+    out["fused"] = torch.tensor(int(t.fused_rollout))
     torch.save(out, os.path.join(out_dir, "union_w%d_r%d.pt" % (world, rank)))
     if world > 1:
         dist.destroy_process_group()
 
 
 @pytest.mark.gpu
-def test_two_rank_shards_equal_one_rank_on_the_union(tmp_path):
+@pytest.mark.parametrize("name", ["cfg3", "cfg2"])
+def test_two_rank_shards_equal_one_rank_on_the_union(tmp_path, name):
     """§8(e): 2 ranks x E/2 replicas == 1 rank x E replicas (SchedulingEnvironment.py:314-329, PPOmodules.py:548-597
     shared nets, gradient all-reduce mean). Replica e's env seed and Philox rows are functions of its
     global index, so every per-replica ring of iteration 1 (observations, actions, log-probs, rewards)
@@ -180,12 +182,14 @@ def test_two_rank_shards_equal_one_rank_on_the_union(tmp_path):
     and the weights after each iteration agree within 1e-5 (the all-reduce sums the two halves' f32
     gradients in another order than one rank's reduction). Iteration 2 acts on those weights: its
     actions, observations and rewards are compared bit for bit (a sampled action would flip only if a
-    uniform lay within ~1e-7 of a CDF boundary), its log-probs within 1e-5."""
-    mp.spawn(_union_rank, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True)
-    mp.spawn(_union_rank, args=(1, 0, str(tmp_path)), nprocs=1, join=True)
+    uniform lay within ~1e-7 of a CDF boundary), its log-probs within 1e-5. cfg2 runs the one-launch
+    rollout (ms_env_rollout_act), whose fused acting draws from each shard's global Philox rows."""
+    mp.spawn(_union_rank, args=(2, _free_port(), str(tmp_path), name), nprocs=2, join=True)
+    mp.spawn(_union_rank, args=(1, 0, str(tmp_path), name), nprocs=1, join=True)
     one = torch.load(tmp_path / "union_w1_r0.pt", weights_only=True)
     two = [torch.load(tmp_path / ("union_w2_r%d.pt" % r), weights_only=True) for r in range(2)]
     assert int(one.pop("flags")) == 0 and all(int(x.pop("flags")) == 0 for x in two)
+    assert all(int(x.pop("fused")) == (name == "cfg2") for x in [one] + two)
     h = _UNION["E"] // 2
     hp = importlib.import_module("marl-scheduling_amd.trainer").Hyper()
     bad = []
