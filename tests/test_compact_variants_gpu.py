@@ -62,13 +62,14 @@ def test_compact_trainer_equals_materialised_and_oracle(ms, name, E, T):
     assert all(t.flags() == 0 for t in trs)
 
 
-@pytest.mark.parametrize("E,T", [(4096, 16), (96, 24), (1001, 12)])
+@pytest.mark.parametrize("E,T", [(4096, 16), (4096, 200), (96, 24), (1001, 12)])
 def test_fused_env_act_equals_two_launches(ms, monkeypatch, E, T):
     """cfg2 (fixed prices, one net per role): round t's env launch also samples round t + 1's actions from
     the observations in its LDS (ms_env_step_act), and by default the whole rollout is one launch
     (ms_env_rollout_act: each wave loops over the rounds). Every ring of the one-launch rollout, of the
     launch-per-round rollout and of the two-launch trainer (the paired act launch, then the env launch)
-    are equal bit for bit over two iterations: E = 4096 runs k_env_*_act<32, FixShape<4,4,3,1>>, E = 96
+    are equal bit for bit over two iterations: E = 4096 runs k_env_*_act<32, FixShape<4,4,3,1>> (T = 200: the
+    BASELINE rollout length, every env crossing MT blocks inside the one launch), E = 96
     the LPE-16 generic one (four replicas per wave), E = 1001 a partial last wave (one replica)."""
     tr_mod = importlib.import_module("marl-scheduling_amd.trainer")
     mk = lambda: tr_mod.Trainer.from_named("cfg2", n_envs=E, update_step=T, seed=9, device="cuda:0")
