@@ -523,9 +523,10 @@ class PPOGroup:
 
     @torch.no_grad()
     def sync_old(self):
-        """policy_old.load_state_dict(policy.state_dict()) (PPOmodules.py:171)."""
-        for k in ACTOR_KEYS + CRITIC_KEYS:
-            getattr(self.policy_old, k).copy_(getattr(self.policy, k))
+        """policy_old.load_state_dict(policy.state_dict()) (PPOmodules.py:171): one multi-tensor copy
+        launch for all tensors instead of a copy node per tensor (update 8.63 -> 8.59 ms, profiles/r6e)."""
+        keys = ACTOR_KEYS + CRITIC_KEYS
+        torch._foreach_copy_([getattr(self.policy_old, k).data for k in keys], [getattr(self.policy, k).data for k in keys])
 
     def update(self, states, actions, old_logprobs, returns):
         """K epochs of full-batch clipped-surrogate PPO (PPOmodules.py:144-168).
