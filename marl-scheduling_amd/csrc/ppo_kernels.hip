@@ -1567,6 +1567,87 @@ __global__ void __launch_bounds__(256) k_key_gather(PpoArgs p) {
     }
 }
 
+// k_key_gather for [R][U] rollout rows (rus == 1, rrs == U, U <= 64): a wave stages 64 consecutive rows of
+// one array at a time in its LDS with coalesced 16-byte loads (the rows are contiguous), then each lane
+// (= row) picks its groups' units from there, so no load instruction strides across rows (the per-lane
+// loads of k_key_gather touch one 128-byte line per lane). Same outputs as k_key_gather.
+constexpr int kGatherWaves = 4;
+__global__ void __launch_bounds__(64 * kGatherWaves) k_key_gather_rows(PpoArgs p) {
+    extern __shared__ __align__(16) uint32_t s_stage[];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int U = (int)p.rrs, G = p.G, RL = (int)p.ret_ld;
+    const int pitch = U + 1;  // dwords per staged row (+1: the lanes of one read hit distinct banks)
+    uint32_t* st = s_stage + (size_t)wave * 64 * pitch;
+    const uint32_t kmask = p.D >= 4 ? 0xffffffffu : ((1u << (8 * p.D)) - 1u);
+    const long long n_chunks = (p.R + 63) >> 6;
+    // 64 rows x n dwords of src (row r0 + k at src + (r0 + k) * n) -> st[k * pitch + col]; rows past R read 0
+    auto stage = [&](const uint32_t* src, long long r0, int n) {
+        const int rows = (int)min(64ll, p.R - r0);
+        const int total = rows * n;  // dwords
+        const uint32_t* base = src + r0 * n;
+        const uint32_t mag = n > 1 ? 0xffffffffu / (uint32_t)n + 1u : 0u;  // d / n = umulhi(d, mag) for d < 2^12
+        for (int d0 = 4 * lane; d0 < total; d0 += 256) {
+            uint32_t v[4];
+            if (d0 + 3 < total && ((reinterpret_cast<uintptr_t>(base + d0) & 15) == 0)) {
+                const uint4 q = *reinterpret_cast<const uint4*>(base + d0);
+                v[0] = q.x, v[1] = q.y, v[2] = q.z, v[3] = q.w;
+            } else {
+#pragma unroll
+                for (int i = 0; i < 4; i++) v[i] = d0 + i < total ? base[d0 + i] : 0u;
+            }
+#pragma unroll
+            for (int i = 0; i < 4; i++) {
+                const int d = d0 + i;
+                if (d < total) {
+                    const int row = n > 1 ? (int)__umulhi((uint32_t)d, mag) : d;
+                    st[row * pitch + (d - row * n)] = v[i];
+                }
+            }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    };
+    auto done = [&]() {  // the staged values are read before the next stage overwrites them
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    };
+    for (long long ch = (long long)blockIdx.x * kGatherWaves + wave; ch < n_chunks;
+         ch += (long long)gridDim.x * kGatherWaves) {
+        const long long r0 = ch << 6, r = r0 + lane;
+        const bool in = r < p.R;
+        // dense indices (and marks) from the state words
+        stage(reinterpret_cast<const uint32_t*>(p.states), r0, U);
+        for (int g = 0; g < G; g++) {
+            const int u = p.unit_of_group[g];
+            uint32_t idx;
+            const bool ok = key_index(st[lane * pitch + u] & kmask, p.D, idx);
+            if (in) {
+                if (!ok) __hip_atomic_store(p.key_flag + g, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                uint8_t* mk = p.key_mark + (size_t)g * kKeyDense + idx;
+                if (*mk == 0) *mk = 1;
+                p.key_idx[(size_t)g * p.R + r] = idx;
+            }
+        }
+        done();
+        stage(reinterpret_cast<const uint32_t*>(p.old_lp), r0, U);
+        for (int g = 0; g < G; g++)
+            if (in) p.key_olp[(size_t)g * p.R + r] = __uint_as_float(st[lane * pitch + p.unit_of_group[g]]);
+        done();
+        // returns: p.ret may be a column offset into a wider [R][ret_ld] array (a later draw's groups),
+        // so only columns [0, G) of each row are ours: read per lane (64-byte lane stride at most)
+        for (int g = 0; g < G; g++)
+            if (in) p.key_ret[(size_t)g * p.R + r] = p.ret[(size_t)r * RL + g];
+        // actions: U bytes per row, staged as dwords (U % 4 == 0)
+        stage(reinterpret_cast<const uint32_t*>(p.actions), r0, U >> 2);
+        const uint8_t* sa = reinterpret_cast<const uint8_t*>(st);
+        for (int g = 0; g < G; g++)
+            if (in) p.key_act[(size_t)g * p.R + r] = (int8_t)sa[lane * pitch * 4 + p.unit_of_group[g]];
+        done();
+    }
+}
+
 // the row word of a dense index
 __device__ __forceinline__ uint32_t key_word_of(uint32_t idx, int D) {
     uint32_t w = 0;
@@ -1726,6 +1807,15 @@ static hipError_t launch_own(const PpoArgs& a, unsigned nb, hipStream_t st) {
     return launch_grad_cm<NQ, NT, kMaskRow>(a, nb, st);
 }
 
+// MS_KEY_GATHER_ROWS=0: the per-lane gather for every layout (A/B measurements)
+static bool gather_per_row() {
+    static const bool v = [] {
+        const char* e = getenv("MS_KEY_GATHER_ROWS");
+        return e && e[0] == '0';
+    }();
+    return v;
+}
+
 // the common-row path for inputs up to 128 bytes (its scan holds a row per lane in registers)
 template <int NQ, int NT>
 static hipError_t launch_grad_t(const PpoArgs& a0, hipStream_t st) {
@@ -1740,7 +1830,12 @@ static hipError_t launch_grad_t(const PpoArgs& a0, hipStream_t st) {
             if ((e = hipMemsetAsync(a.key_mark, 0, (size_t)a.G * kKeyDense, st)) != hipSuccess) return e;
             if ((e = hipMemsetAsync(a.key_flag, 0, a.G * sizeof(int32_t), st)) != hipSuccess) return e;
             const unsigned ib = (unsigned)std::min<long long>((a.R + 255) / 256, 16384);
-            hipLaunchKernelGGL(k_key_gather, dim3(ib), dim3(256), 0, st, a);
+            if (a.rus == 1 && a.rrs <= 64 && (a.rrs & 3) == 0 && !gather_per_row()) {
+                const size_t lds = (size_t)kGatherWaves * 64 * (a.rrs + 1) * 4;
+                hipLaunchKernelGGL(k_key_gather_rows, dim3(ib), dim3(64 * kGatherWaves), lds, st, a);
+            } else {
+                hipLaunchKernelGGL(k_key_gather, dim3(ib), dim3(256), 0, st, a);
+            }
             if ((e = hipGetLastError()) != hipSuccess) return e;
             hipLaunchKernelGGL(k_key_rank, dim3(a.G), dim3(1024), 0, st, a);
             if ((e = hipGetLastError()) != hipSuccess) return e;
