@@ -129,6 +129,7 @@ struct BoolC {
 // from the core owners of compact acceptor observations); keyed rows (the backward and the forward
 // of a group's distinct rows, k_key_scan sums the rows' loss derivatives in between)
 enum GradMode { kPlain = 0, kCommonRow = 1, kOwnerRow = 2, kKeyBack = 3, kKeyFwd = 4, kMaskRow = 5, kCommonFwd = 6 };
+constexpr int kX1 = 16;  // mode bit: the last action tile has exactly one action (k_ppo_grad)
 // kMaskRow: compact acceptor rows of many groups (the divided acceptors), the common rows already
 // summed by k_own_scan / k_own_common: each wave runs the tiles of the rows its group's own-row mask
 // lists, and one wave per group the common rows' virtual tile. kCommonFwd: the forward of the
@@ -154,8 +155,9 @@ __device__ unsigned long long g_grad_probe[kGradProbeWaves][4];
 template <int NT>
 constexpr bool grad_bf16h() { return MS_GRAD_BF16H && NT <= 2; }
 
-template <int NQ, int NT, int MODE>
+template <int NQ, int NT, int MODEX>
 struct GradLds {
+    static constexpr int MODE = MODEX & 15;  // (bit 4: kX1, see k_ppo_grad)
     static constexpr bool CM = MODE == kCommonRow || MODE == kOwnerRow;
     static constexpr bool ML = MODE == kMaskRow;
     static constexpr int S1 = (NQ + 1) / 2;           // 32-input k-steps of layer 1 (16*NQ inputs)
@@ -181,9 +183,14 @@ struct GradLds {
 
 // NQ = 16-wide input tiles with 16*NQ > D, NT = ceil(A/16) action tiles. A block owns 4 chunks
 // of one group and has L::WPB waves.
-template <int NQ, int NT, int MODE>
-__global__ void __launch_bounds__((64 * GradLds<NQ, NT, MODE>::WPB), ((NQ * NT >= 32) ? 1 : 2)) k_ppo_grad(PpoArgs p) {
-    using L = GradLds<NQ, NT, MODE>;
+template <int NQ, int NT, int MODEX>
+__global__ void __launch_bounds__((64 * GradLds<NQ, NT, MODEX>::WPB), ((NQ * NT >= 32) ? 1 : 2)) k_ppo_grad(PpoArgs p) {
+    using L = GradLds<NQ, NT, MODEX>;
+    constexpr int MODE = MODEX & 15;
+    // kX1: the last action tile holds one action (A = 16 (NT - 1) + 1, e.g. C + 1 = 17 or O + 1 = 49 at
+    // cfg4): its layer-3 row, backward term and weight gradient run on the VALU (4 FMAs per lane and a
+    // sum over the row's lane groups) instead of 12 f32 MFMAs on a tile of 15 padding actions
+    constexpr bool X1 = (MODEX & kX1) != 0;
     constexpr int TP = L::TP, TP2 = L::TP2, XPD = L::XPD, S1 = L::S1, W1B = L::W1B;
     constexpr int NTH = 64 * L::WPB, CPW = 4 / L::WPB;  // threads per block, chunks per wave
     // the wave index through readfirstlane: everything derived from it (chunk, tile range, row buffers)
@@ -324,6 +331,7 @@ __global__ void __launch_bounds__((64 * GradLds<NQ, NT, MODE>::WPB), ((NQ * NT >
 #pragma unroll
     for (int t = 0; t < NT; t++) gW3[t] = (f4){0, 0, 0, 0};
     float db2[4] = {0, 0, 0, 0}, cdb2[4] = {0, 0, 0, 0}, gC3[4] = {0, 0, 0, 0};
+    float gW3x[4] = {0, 0, 0, 0};  // (kX1) d W3[16 (NT - 1)][4 g4 + q] over this lane's rows
     float db3[NT][4];
 #pragma unroll
     for (int t = 0; t < NT; t++) db3[t][0] = db3[t][1] = db3[t][2] = db3[t][3] = 0.f;
@@ -401,7 +409,14 @@ __global__ void __launch_bounds__((64 * GradLds<NQ, NT, MODE>::WPB), ((NQ * NT >
 #pragma unroll
         for (int t = 0; t < NT; t++) {
             f4 zz = {0, 0, 0, 0};
-            if constexpr (HB) {
+            if (X1 && t == NT - 1) {
+                // action 16 t alone: W3[16 t] . h2 as this lane's 4 terms, summed over the row's lane groups
+                const f4 w3 = *reinterpret_cast<const f4*>(sW3 + (16 * t) * 16 + 4 * g4);
+                float pz = 0.f;
+#pragma unroll
+                for (int q = 0; q < 4; q++) pz = fmaf(w3[q], f.h2[q], pz);
+                zz[0] = xsum4g(pz);
+            } else if constexpr (HB) {
                 zz = mm3(4 + t, f.h2, zz);
             } else {
                 const f4 w3 = *reinterpret_cast<const f4*>(sW3 + (16 * t + j) * 16 + 4 * g4);
@@ -602,9 +617,15 @@ __global__ void __launch_bounds__((64 * GradLds<NQ, NT, MODE>::WPB), ((NQ * NT >
 
         // ---- backward through the hidden layers (same no-movement trick, transposed weights)
         f4 d2 = {0, 0, 0, 0};
+        float g16 = 0.f;  // (kX1) the single action's dz of row j, on every lane of the row
 #pragma unroll
         for (int t = 0; t < NT; t++) {
-            if constexpr (HB) {
+            if (X1 && t == NT - 1) {
+                g16 = __shfl(gz[t][0], j);  // lane (j, 0) holds action 16 t
+                const f4 w3 = *reinterpret_cast<const f4*>(sW3 + (16 * t) * 16 + 4 * g4);
+#pragma unroll
+                for (int q = 0; q < 4; q++) d2[q] = fmaf(w3[q], g16, d2[q]);
+            } else if constexpr (HB) {
                 d2 = mm3(4 + NT + t, gz[t], d2);
             } else {
 #pragma unroll
@@ -696,14 +717,14 @@ __global__ void __launch_bounds__((64 * GradLds<NQ, NT, MODE>::WPB), ((NQ * NT >
             const int fo = (4 * g4 + q) * TP + pr;
             T_h2[fo] = f.h2[q];
 #pragma unroll
-            for (int t = 0; t < NT; t++) T_gz[t * 16 * TP + fo] = gz[t][q];
+            for (int t = 0; t < (X1 ? NT - 1 : NT); t++) T_gz[t * 16 * TP + fo] = gz[t][q];
         }
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
         const f4 bh2 = *reinterpret_cast<const f4*>(T_h2 + rd);
         f4 agz[NT];
 #pragma unroll
-        for (int t = 0; t < NT; t++) agz[t] = *reinterpret_cast<const f4*>(T_gz + t * 16 * TP + rd);
+        for (int t = 0; t < (X1 ? NT - 1 : NT); t++) agz[t] = *reinterpret_cast<const f4*>(T_gz + t * 16 * TP + rd);
 #pragma unroll
         for (int s = 0; s < 4; s++) {
             gW2 = mfma4(ad2[s], bh1[s], gW2);
@@ -712,7 +733,11 @@ __global__ void __launch_bounds__((64 * GradLds<NQ, NT, MODE>::WPB), ((NQ * NT >
 #pragma unroll
         for (int s = 0; s < 4; s++)
 #pragma unroll
-            for (int t = 0; t < NT; t++) gW3[t] = mfma4(agz[t][s], bh2[s], gW3[t]);
+            for (int t = 0; t < (X1 ? NT - 1 : NT); t++) gW3[t] = mfma4(agz[t][s], bh2[s], gW3[t]);
+        if constexpr (X1) {
+#pragma unroll
+            for (int q = 0; q < 4; q++) gW3x[q] = fmaf(g16, f.h2[q], gW3x[q]);
+        }
         if (pair_done) {
             // dW1 / dC1 over the pair's 32 rows on the bf16 MFMA: A = d1 (e1) of rows 8*g4..+7 of
             // hidden unit j as three exact bf16 terms, B = the int8 inputs of those rows; output
@@ -1243,9 +1268,13 @@ __global__ void __launch_bounds__((64 * GradLds<NQ, NT, MODE>::WPB), ((NQ * NT >
             put(o.w2 + f * 16 + j, gW2[q]);
             put(o.cw2 + f * 16 + j, gC2[q]);
 #pragma unroll
-            for (int t = 0; t < NT; t++) {
+            for (int t = 0; t < (X1 ? NT - 1 : NT); t++) {
                 const int a = 16 * t + f;
                 if (a < A) put(o.w3 + a * 16 + j, gW3[t][q]);
+            }
+            if constexpr (X1) {  // row 16 (NT - 1) of dW3: unit f, summed over the 16 row lanes
+                const float v3 = xsum16(gW3x[q]);
+                if (j == 0) put(o.w3 + 16 * (NT - 1) * 16 + f, v3);
             }
             float v;
             v = xsum16(db2[q]);
@@ -1795,16 +1824,16 @@ __global__ void __launch_bounds__(1024) k_key_scan(PpoArgs p) {
 
 // compact rows of many groups: the common row's forward per group, the row scan over all groups,
 // the common sums per group, then the tiles of the marked rows (+ the virtual tile)
-template <int NQ, int NT>
+template <int NQ, int NT, int X = 0>
 static hipError_t launch_own(const PpoArgs& a, unsigned nb, hipStream_t st) {
     hipError_t e;
-    if ((e = launch_grad_cm<NQ, NT, kCommonFwd>(a, 1, st)) != hipSuccess) return e;
+    if ((e = launch_grad_cm<NQ, NT, kCommonFwd | X>(a, 1, st)) != hipSuccess) return e;
     const size_t lds = (size_t)a.A * 64 * (8 + 4) + 2 * 64 * 4;
     hipLaunchKernelGGL(k_own_scan, dim3((unsigned)a.own_nb, (unsigned)((a.G + 63) / 64)), dim3(256), lds, st, a);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     hipLaunchKernelGGL(k_own_common, dim3((unsigned)a.G), dim3(256), 0, st, a);
     if ((e = hipGetLastError()) != hipSuccess) return e;
-    return launch_grad_cm<NQ, NT, kMaskRow>(a, nb, st);
+    return launch_grad_cm<NQ, NT, kMaskRow | X>(a, nb, st);
 }
 
 // MS_KEY_GATHER_ROWS=0: the per-lane gather for every layout (A/B measurements)
@@ -1817,7 +1846,8 @@ static bool gather_per_row() {
 }
 
 // the common-row path for inputs up to 128 bytes (its scan holds a row per lane in registers)
-template <int NQ, int NT>
+// X = kX1: the tile path with a single-action last tile (A = 16 (NT - 1) + 1); the keyed passes never take it
+template <int NQ, int NT, int X = 0>
 static hipError_t launch_grad_t(const PpoArgs& a0, hipStream_t st) {
     PpoArgs a = a0;
     const unsigned nb = (unsigned)(a.n_chunks / 4);
@@ -1856,14 +1886,23 @@ static hipError_t launch_grad_t(const PpoArgs& a0, hipStream_t st) {
         if (a.common && a.stride >= 16) {
             using L = GradLds<NQ, NT, kCommonRow>;
             if (sizeof(float) * L::lds_floats <= 160 * 1024) {
-                if (a.owner && a.own_mask && a.G >= kOwnMinGroups) return launch_own<NQ, NT>(a, nb, st);
-                if (a.owner) return launch_grad_cm<NQ, NT, kOwnerRow>(a, nb, st);
-                return launch_grad_cm<NQ, NT, kCommonRow>(a, nb, st);
+                if (a.owner && a.own_mask && a.G >= kOwnMinGroups) return launch_own<NQ, NT, X>(a, nb, st);
+                if (a.owner) return launch_grad_cm<NQ, NT, kOwnerRow | X>(a, nb, st);
+                return launch_grad_cm<NQ, NT, kCommonRow | X>(a, nb, st);
             }
         }
     }
     if (a.owner) return hipErrorInvalidValue;  // compact rows need the common-row path
-    return launch_grad_cm<NQ, NT, kPlain>(a, nb, st);
+    return launch_grad_cm<NQ, NT, kPlain | X>(a, nb, st);
+}
+
+// MS_GRAD_X1=0: single-action last tiles on the MFMA like the others (A/B measurements)
+static bool grad_x1_enabled() {
+    static const bool v = [] {
+        const char* e = getenv("MS_GRAD_X1");
+        return !(e && e[0] == '0');
+    }();
+    return v;
 }
 
 // partial vectors per group that launch_ppo_grad writes (the keyed path adds its slot blocks)
@@ -1879,6 +1918,18 @@ hipError_t launch_ppo_grad(const PpoArgs& a, const GradOut& go, hipStream_t st) 
     if (nq <= Q && nt <= T) {            \
         e = launch_grad_t<Q, T>(a, st);  \
         goto reduce;                     \
+    }
+    // A = 16 (nt - 1) + 1 at the BASELINE shapes that have it (cfg4: offers C + 1 = 17 with 16 < D + 1 <= 64,
+    // divided acceptors O + 1 = 49 with 64 < D + 1 <= 128)
+    if (a.A % 16 == 1 && !keyed && grad_x1_enabled()) {
+        if (nt == 2 && nq > 2 && nq <= 4) {
+            e = launch_grad_t<4, 2, kX1>(a, st);
+            goto reduce;
+        }
+        if (nt == 4 && nq > 4 && nq <= 8) {
+            e = launch_grad_t<8, 4, kX1>(a, st);
+            goto reduce;
+        }
     }
     if (nt <= 1) {
         MS_PPO_CASE(1, 1) MS_PPO_CASE(2, 1) MS_PPO_CASE(4, 1) MS_PPO_CASE(8, 1) MS_PPO_CASE(16, 1)

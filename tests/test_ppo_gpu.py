@@ -191,8 +191,9 @@ def _rand_batch(G, T, E, U, D, stride, A, seed):
 @pytest.mark.parametrize("G,T,E,U,D,stride,A,K", [(8, 20, 37, 64, 51, 52, 25, 1), (8, 13, 11, 24, 18, 20, 9, 2),
                                                    (8, 9, 50, 24, 4, 4, 13, 1), (3, 7, 9, 3, 11, 12, 5, 2),
                                                    (2, 5, 16, 4, 195, 196, 97, 1), (2, 6, 21, 3, 16, 16, 5, 1),
-                                                   (1, 3, 333, 2, 99, 100, 49, 1)])
+                                                   (1, 3, 333, 2, 99, 100, 49, 1), (4, 8, 40, 6, 34, 36, 17, 2)])
 def test_fused_grad_matches_autograd(ms, G, T, E, U, D, stride, A, K):
+    """A = 17 / 49 with 16 < D + 1 <= 64 / 64 < D + 1 <= 128: the single-action last tile (kX1)."""
     ppo = _ppo(ms)
     torch.manual_seed(21)
     ref = ppo.PPOGroup(G, D, A, 0.003, 0.01, 0.9, 0.2, K, device="cuda")
