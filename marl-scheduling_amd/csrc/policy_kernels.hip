@@ -686,8 +686,10 @@ __global__ void __launch_bounds__(256) k_act_common(ActArgs a) {
 // first off_blocks blocks run the offer units (core + price chooser, k_act), the rest the acceptor
 // units on compact rows (k_act_common). The two workloads' waves share the CUs, so one's waits
 // hide under the other's work instead of each launch waiting out its own chain.
+// (four 4-wave blocks per CU; two for cfg4's acceptor half, whose 128-input rows and 64 action slots take
+// ~250 registers)
 template <int S1a, int NTa, int NT2a, int S1b, int NTb>
-__global__ void __launch_bounds__(256, 4) k_act_pair(ActArgs off, ActArgs acc, int off_blocks) {
+__global__ void __launch_bounds__(256, (S1b >= 4 ? 2 : 4)) k_act_pair(ActArgs off, ActArgs acc, int off_blocks) {
     if ((int)blockIdx.x < off_blocks)
         act_tiles<S1a, NTa, NT2a, false>(off, blockIdx.x);
     else
@@ -1070,9 +1072,19 @@ hipError_t launch_act_round(const ms_mlp_params* core, const ms_mlp_params* pric
     o.ptab = ptab;
     o.pdigit = pdigit;
     o.pkeys = pkeys;
+    const bool unpaired = env_int("MS_ACT_UNPAIRED", 0) != 0;
     const bool paired = (off_stride + 31) / 32 == 1 && core->n_actions <= 16 && price->n_actions <= 16 &&
-                        (acc_stride + 31) / 32 == 2 && acc->n_actions <= 32 && !env_int("MS_ACT_UNPAIRED", 0);
-    if (paired && (!act_tiles_fits(o) || !act_common_fits(c))) return hipErrorInvalidValue;
+                        (acc_stride + 31) / 32 == 2 && acc->n_actions <= 32 && !unpaired;
+    // cfg4's shapes (16 x 16 divided): 34-byte offer rows, 17 core actions, 99-byte acceptor rows, 49 actions
+    const bool paired4 = !paired && (off_stride + 31) / 32 == 2 && core->n_actions <= 32 && price->n_actions <= 16 &&
+                         (acc_stride + 31) / 32 == 4 && acc->n_actions <= 64 && !unpaired;
+    if ((paired || paired4) && (!act_tiles_fits(o) || !act_common_fits(c))) return hipErrorInvalidValue;
+    if (paired4) {
+        static const long long f4o = env_int("MS_ACT_PAIR4_WAVES", 2048), f4a = env_int("MS_ACT_PAIR4_COMMON_WAVES", 1024);
+        const unsigned ob = act_blocks(o, f4o), cb = act_common_blocks(c, f4a);
+        hipLaunchKernelGGL((k_act_pair<2, 2, 1, 4, 4>), dim3(ob + cb), dim3(256), 0, st, o, c, (int)ob);
+        return hipGetLastError();
+    }
     if (!paired) {
         hipError_t e = dispatch_act(o, st);
         return e != hipSuccess ? e : dispatch_act(c, st);
