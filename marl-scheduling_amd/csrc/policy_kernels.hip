@@ -1080,7 +1080,9 @@ hipError_t launch_act_round(const ms_mlp_params* core, const ms_mlp_params* pric
                          (acc_stride + 31) / 32 == 4 && acc->n_actions <= 64 && !unpaired;
     if ((paired || paired4) && (!act_tiles_fits(o) || !act_common_fits(c))) return hipErrorInvalidValue;
     if (paired4) {
-        static const long long f4o = env_int("MS_ACT_PAIR4_WAVES", 2048), f4a = env_int("MS_ACT_PAIR4_COMMON_WAVES", 1024);
+        // wave split swept at cfg4 (profiles/r6l, r6m): 1536 offer / 768 acceptor target waves 74.8 us per launch
+        // (2048 / 1024: 80.3, 1024 / 1024: 78.4, 3072 / 1536: 78.2, 4096 / 1024: 84.3; two launches: 102.4)
+        static const long long f4o = env_int("MS_ACT_PAIR4_WAVES", 1536), f4a = env_int("MS_ACT_PAIR4_COMMON_WAVES", 768);
         const unsigned ob = act_blocks(o, f4o), cb = act_common_blocks(c, f4a);
         hipLaunchKernelGGL((k_act_pair<2, 2, 1, 4, 4>), dim3(ob + cb), dim3(256), 0, st, o, c, (int)ob);
         return hipGetLastError();
