@@ -688,8 +688,11 @@ __global__ void __launch_bounds__(256) k_act_common(ActArgs a) {
 // hide under the other's work instead of each launch waiting out its own chain.
 // (four 4-wave blocks per CU; two for cfg4's acceptor half, whose 128-input rows and 64 action slots take
 // ~250 registers)
+#ifndef MS_ACT_PAIR_MINB
+#define MS_ACT_PAIR_MINB 4
+#endif
 template <int S1a, int NTa, int NT2a, int S1b, int NTb>
-__global__ void __launch_bounds__(256, (S1b >= 4 ? 2 : 4)) k_act_pair(ActArgs off, ActArgs acc, int off_blocks) {
+__global__ void __launch_bounds__(256, (S1b >= 4 ? 2 : MS_ACT_PAIR_MINB)) k_act_pair(ActArgs off, ActArgs acc, int off_blocks) {
     if ((int)blockIdx.x < off_blocks)
         act_tiles<S1a, NTa, NT2a, false>(off, blockIdx.x);
     else
