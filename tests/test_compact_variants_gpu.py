@@ -98,3 +98,31 @@ def test_fused_env_act_equals_two_launches(ms, monkeypatch, E, T):
     for k in st[0]:
         for o in st[1:]:
             assert (st[0][k] == o[k]).all(), k
+
+
+def test_rollout_act_rejects_unsupported_calls(ms):
+    """ms_env_rollout_act's argument checks (include/marlsched.h): n_rounds >= 1, no accepted /
+    terminated event records, a fixed-price env; each refusal is MS_EINVAL with a message, and the
+    env is left as it was (its round counter does not move)."""
+    lib_mod = importlib.import_module("marl-scheduling_amd._lib")
+    abi = importlib.import_module("marl-scheduling_amd.abi")
+    tr_mod = importlib.import_module("marl-scheduling_amd.trainer")
+    t = tr_mod.Trainer.from_named("cfg2", n_envs=96, update_step=8, seed=2, device="cuda:0")
+    assert t.fused_rollout
+    env, e0, e1 = t.env.parts[0]
+    E, N, C, L = e1 - e0, t.N, t.C, t.L
+    obs = dict(t._acc_out(1, e0, e1), offer=t.off_obs[1])
+    rew = dict(offer=t.off.rewards[0].view(E, N, L), acceptor=t.acc.rewards[0].view(E, N, C), agent=t.agent_reward,
+               auctioneer=t.auct_reward)
+    strides = abi.MsRoundStrides(*([0] * 13 + [8]))
+    nxt = t._fused_next(1, 0)
+    acc0, off0 = t.acc.actions[0].view(E, N, C), t.off.actions[0].view(E, N, L)
+    r0 = lib_mod.lib.ms_env_round(env._h)
+    with pytest.raises(lib_mod.MarlSchedError, match="n_rounds"):
+        env.rollout_act(acc0, off0, obs, rew, nxt, strides, 0)
+    acc_ev = torch.zeros((E, C, 16), dtype=torch.uint8, device="cuda:0")
+    with pytest.raises(lib_mod.MarlSchedError, match="event records"):
+        env.rollout_act(acc0, off0, obs, rew, nxt, strides, 1, events=dict(accepted=acc_ev))
+    assert lib_mod.lib.ms_env_round(env._h) == r0
+    free = tr_mod.Trainer.from_named("cfg3", n_envs=64, update_step=8, seed=2, device="cuda:0")
+    assert not free.fused_rollout and not free.env.parts[0][0].fused_act_supported()
