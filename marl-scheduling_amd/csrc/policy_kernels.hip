@@ -415,7 +415,10 @@ __device__ __forceinline__ void act_tiles(const ActArgs& a, int block) {
 // once (Head::table, the exact arithmetic of Head::run) and samples each row equal to it from its
 // own uniform with a handful of compares. The other rows are collected in LDS and run through the
 // MFMA tiles as in k_act. Outputs are bit-identical to k_act's.
-constexpr int kCommonSeg = 512;  // most rows per wave = capacity of the wave's LDS row list
+#ifndef MS_COMMON_SEG
+#define MS_COMMON_SEG 512
+#endif
+constexpr int kCommonSeg = MS_COMMON_SEG;  // most rows per wave = capacity of the wave's LDS row list
 
 template <int S1, int NT, int NT2, bool EXT_U>
 __global__ void __launch_bounds__(256) k_act(ActArgs a) {
