@@ -1605,14 +1605,15 @@ __global__ void __launch_bounds__(64 * kGatherWaves) k_key_gather_rows(PpoArgs p
     extern __shared__ __align__(16) uint32_t s_stage[];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int U = (int)p.rrs, G = p.G, RL = (int)p.ret_ld;
-    const int pitch = U + 1;  // dwords per staged row (+1: the lanes of one read hit distinct banks)
+    const int pitch = (U > RL ? U : RL) + 1;  // dwords per staged row (+1: the lanes of one read hit distinct banks)
     uint32_t* st = s_stage + (size_t)wave * 64 * pitch;
     const uint32_t kmask = p.D >= 4 ? 0xffffffffu : ((1u << (8 * p.D)) - 1u);
     const long long n_chunks = (p.R + 63) >> 6;
-    // 64 rows x n dwords of src (row r0 + k at src + (r0 + k) * n) -> st[k * pitch + col]; rows past R read 0
-    auto stage = [&](const uint32_t* src, long long r0, int n) {
+    // 64 rows x n dwords of src (row r0 + k at src + (r0 + k) * n) -> st[k * pitch + col]; rows past R are not
+    // read, and the last row only up to column `last` (an array may be a column window of a wider one)
+    auto stage = [&](const uint32_t* src, long long r0, int n, int last) {
         const int rows = (int)min(64ll, p.R - r0);
-        const int total = rows * n;  // dwords
+        const int total = (rows - 1) * n + last;  // dwords
         const uint32_t* base = src + r0 * n;
         const uint32_t mag = n > 1 ? 0xffffffffu / (uint32_t)n + 1u : 0u;  // d / n = umulhi(d, mag) for d < 2^12
         for (int d0 = 4 * lane; d0 < total; d0 += 256) {
@@ -1647,7 +1648,7 @@ __global__ void __launch_bounds__(64 * kGatherWaves) k_key_gather_rows(PpoArgs p
         const long long r0 = ch << 6, r = r0 + lane;
         const bool in = r < p.R;
         // dense indices (and marks) from the state words
-        stage(reinterpret_cast<const uint32_t*>(p.states), r0, U);
+        stage(reinterpret_cast<const uint32_t*>(p.states), r0, U, U);
         for (int g = 0; g < G; g++) {
             const int u = p.unit_of_group[g];
             uint32_t idx;
@@ -1660,16 +1661,18 @@ __global__ void __launch_bounds__(64 * kGatherWaves) k_key_gather_rows(PpoArgs p
             }
         }
         done();
-        stage(reinterpret_cast<const uint32_t*>(p.old_lp), r0, U);
+        stage(reinterpret_cast<const uint32_t*>(p.old_lp), r0, U, U);
         for (int g = 0; g < G; g++)
             if (in) p.key_olp[(size_t)g * p.R + r] = __uint_as_float(st[lane * pitch + p.unit_of_group[g]]);
         done();
-        // returns: p.ret may be a column offset into a wider [R][ret_ld] array (a later draw's groups),
-        // so only columns [0, G) of each row are ours: read per lane (64-byte lane stride at most)
+        // returns: p.ret may be a column window of a wider [R][ret_ld] array (a later draw's groups), so
+        // the last row is read only up to column G (the window's end in memory)
+        stage(reinterpret_cast<const uint32_t*>(p.ret), r0, RL, G);
         for (int g = 0; g < G; g++)
-            if (in) p.key_ret[(size_t)g * p.R + r] = p.ret[(size_t)r * RL + g];
+            if (in) p.key_ret[(size_t)g * p.R + r] = __uint_as_float(st[lane * pitch + g]);
+        done();
         // actions: U bytes per row, staged as dwords (U % 4 == 0)
-        stage(reinterpret_cast<const uint32_t*>(p.actions), r0, U >> 2);
+        stage(reinterpret_cast<const uint32_t*>(p.actions), r0, U >> 2, U >> 2);
         const uint8_t* sa = reinterpret_cast<const uint8_t*>(st);
         for (int g = 0; g < G; g++)
             if (in) p.key_act[(size_t)g * p.R + r] = (int8_t)sa[lane * pitch * 4 + p.unit_of_group[g]];
@@ -1860,8 +1863,9 @@ static hipError_t launch_grad_t(const PpoArgs& a0, hipStream_t st) {
             if ((e = hipMemsetAsync(a.key_mark, 0, (size_t)a.G * kKeyDense, st)) != hipSuccess) return e;
             if ((e = hipMemsetAsync(a.key_flag, 0, a.G * sizeof(int32_t), st)) != hipSuccess) return e;
             const unsigned ib = (unsigned)std::min<long long>((a.R + 255) / 256, 16384);
-            if (a.rus == 1 && a.rrs <= 64 && (a.rrs & 3) == 0 && !gather_per_row()) {
-                const size_t lds = (size_t)kGatherWaves * 64 * (a.rrs + 1) * 4;
+            if (a.rus == 1 && a.rrs <= 64 && (a.rrs & 3) == 0 && a.ret_ld <= 64 && a.ret_ld >= a.G &&
+                !gather_per_row()) {
+                const size_t lds = (size_t)kGatherWaves * 64 * (std::max<long long>(a.rrs, a.ret_ld) + 1) * 4;
                 hipLaunchKernelGGL(k_key_gather_rows, dim3(ib), dim3(64 * kGatherWaves), lds, st, a);
             } else {
                 hipLaunchKernelGGL(k_key_gather, dim3(ib), dim3(256), 0, st, a);
