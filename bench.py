@@ -54,6 +54,16 @@ def env_round_bytes(shape, k_new_jobs: int, free: bool, compact: bool = False) -
     return b_state + b_act + b_obs + b_rew
 
 
+def act_out_bytes(shape, free: bool) -> int:
+    """Bytes one replica's acting writes per round, the rollout buffers of selectAction (PPOmodules.py:114-125,
+    312-332): acceptor and core-chooser action (1 B) + log-prob (4 B) per unit, and with free prices the price
+    chooser's state (4 B), action (1 B), log-prob (4 B) and the env's price action (1 B) per offer unit. A fused
+    env + act launch (k_env_rollout_act_free) writes these beside the round's bytes and reads no observation
+    back: its roofline counts env_round_bytes + these."""
+    N, C, L = shape.n_agents, shape.n_cores, shape.collection_length
+    return 5 * N * C + 5 * N * L + (10 * N * L if free else 0)
+
+
 def cpu_baseline(seconds_budget: float = 20.0):
     """The CPU restatement timed on this host: oracle env step (C, OpenMP) + torch-CPU
     policy act / PPO update of the same cfg3 loop, on a bounded sample of replicas."""
@@ -200,7 +210,7 @@ ROLLOUT_STREAMS = 1   # replica parts on separate HIP streams in the rollout (Tr
 SAMPLE_EVERY = 8      # rounds between timed env launches
 
 
-def committed_traffic(alg_bytes_per_launch, variant=""):
+def committed_traffic(alg_bytes_per_launch, variant="", kernel="k_env_step"):
     """HBM bytes per k_env_step launch from the committed PMC passes of this workload
     (profiles/*/traffic.json, written by profiles/run_profile.sh: FETCH_SIZE doubled per the
     gfx950 correction + WRITE_SIZE, per launch): the most recent measurement by its ``measured_at``
@@ -215,7 +225,7 @@ def committed_traffic(alg_bytes_per_launch, variant=""):
         except (OSError, ValueError):
             continue
         # the passes of this workload's kernel variant (same algorithmic bytes per launch)
-        if (d.get("kernel") == "k_env_step" and d.get("bytes") and d.get("algorithmic_bytes") == alg_bytes_per_launch
+        if (d.get("kernel") == kernel and d.get("bytes") and d.get("algorithmic_bytes") == alg_bytes_per_launch
                 and d.get("variant", "") == variant):
             key = (d.get("measured_at", ""), p)
             if best is None or key > best[0]:
@@ -705,9 +715,15 @@ def main():
     value = agent_steps / elapsed
     avg_step_s = sum(launch_us) / len(launch_us) / 1e6
     part_envs = args.envs // args.rollout_streams
-    b_round = env_round_bytes(shape, tr.cfg.new_jobs_per_round, tr.free, tr.compact)
+    b_env = env_round_bytes(shape, tr.cfg.new_jobs_per_round, tr.free, tr.compact)
+    # the one-launch rollout (k_env_rollout_act_free, the default): one launch steps and acts for T rounds; its
+    # per-round span covers the env round and the next round's acting, so its bytes add the acting's outputs
+    fused = bool(getattr(tr, "fused_rollout_free", False))
+    kname = "k_env_rollout_act_free" if fused else "k_env_step"
+    b_act = act_out_bytes(shape, tr.free) if fused else 0
+    b_round = b_env + b_act
     achieved = b_round * part_envs / avg_step_s / 1e9
-    traffic = committed_traffic(b_round * part_envs, "compact" if tr.compact else "")
+    traffic = committed_traffic(b_round * part_envs, "compact" if tr.compact else "", kname)
     result = {
         "metric": METRIC,
         "value": value,
@@ -732,7 +748,7 @@ def main():
             "replicas_total": world * args.envs,
         },
         "roofline": {
-            "kernel": "ms::k_env_step",
+            "kernel": "ms::" + kname,
             "bound": "hbm",
             "achieved": achieved,
             "peak": HBM_PEAK_GBS,
@@ -741,8 +757,12 @@ def main():
             "traffic": traffic["bytes"] if traffic else None,
             "traffic_source": traffic["source"] if traffic else None,
             "bytes_per_env_round": b_round,
+            "env_bytes_per_env_round": b_env,
+            "act_bytes_per_env_round": b_act,
             "bytes_definition": "SURVEY.md 8(d) judge figure: state r+w, actions, observations delivered (1 B per "
-                                "element), rewards; liability entries left out (lower bound)",
+                                "element), rewards; liability entries left out (lower bound)" +
+                                ("; + the fused acting's outputs (bench.act_out_bytes: actions, log-probs, price "
+                                 "states written per unit)" if fused else ""),
             "acceptor_observations": "compact (owner row per core + owners)" if tr.compact else "materialised",
             "envs_per_launch": part_envs,
             "avg_launch_us": avg_step_s * 1e6,
@@ -752,8 +772,11 @@ def main():
             "avg_launch_us_per_iteration": [sum(v) / len(v) for v in per_iter_us],
             # the env waves' shader clock over the same launches (s_memtime cycles / s_memrealtime ticks)
             "clock_mhz": median_clock(tr, span_hist),
-            "launch_timing": "first-wave-start to last-wave-end span (s_memrealtime, 100 MHz) of every %d-th "
-                             "round's env launches in every timed iteration (graph replay), averaged" % SAMPLE_EVERY,
+            "launch_timing": ("first-wave-start to last-wave-end span (s_memrealtime, 100 MHz) of the one rollout "
+                              "launch of every timed iteration (graph replay) / its %d rounds: the env round + "
+                              "the next round's acting, per round" % tr.T) if fused else
+                             ("first-wave-start to last-wave-end span (s_memrealtime, 100 MHz) of every %d-th "
+                              "round's env launches in every timed iteration (graph replay), averaged" % SAMPLE_EVERY),
         },
         "breakdown_ms_per_step": {
             "rollout": timings["rollout"] / args.steps * 1e3,
@@ -763,6 +786,9 @@ def main():
         },
     }
     result["act_roofline"] = act_roofline(tr, device)
+    if fused:
+        result["act_roofline"]["rollout_use"] = ("round 0 only; rounds 1..T-1 act inside the rollout launch "
+                                                 "(k_env_rollout_act_free, one wave per agent)")
     if not args.no_step_kernel:
         del tr  # the trainer's rings are not needed by the step-kernel run
         torch.cuda.empty_cache()

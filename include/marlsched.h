@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define MS_ABI_VERSION 16
+#define MS_ABI_VERSION 17
 
 #define MS_MAX_KINDS 16
 #define MS_MAX_AGENTS 64
@@ -436,6 +436,58 @@ typedef struct ms_round_strides {
 int ms_env_rollout_act(ms_env* env, const ms_actions* act, const ms_obs_out* obs, const ms_reward_out* rew,
                        const ms_event_out* ev, const ms_fused_act* next, const ms_round_strides* strides,
                        int32_t n_rounds, int32_t act_after_last, void* stream);
+
+/* ABI 17: the locally shared free-price rollout (BASELINE cfg3; LocallySharedPPO + FreePriceOfferPPO, DESIGN
+ * §1) in one launch: every round's getActionForAllAgents (SchedulingEnvironment.py:150-172) fused after the env
+ * round that built its observations. A workgroup steps 4 * N replicas (16 lanes each) and then acts for them
+ * with one wave per agent: the agent's core chooser + price chooser (FreePriceOfferPPO.selectAction,
+ * PPOmodules.py:312-332) on its L offer rows of every replica and its acceptor net (LocallySharedPPO.selectAction,
+ * PPOmodules.py:532-543) on its C compact acceptor rows, from the rows still in the workgroup's LDS. Outputs are
+ * those of ms_act_round_free(core_chooser, price_chooser, ..., acceptor, ...) on the emitted observations, bit for
+ * bit: off_offset / acc_offset are that call's offsets, each net's row_base its Philox row base. */
+typedef struct ms_fused_act_free {
+    ms_mlp_params core_chooser;   /* N groups (one per agent, L units each); act_frag for off_obs_stride rows */
+    ms_mlp_params price_chooser;  /* N groups, 4 -> A with A <= 16 */
+    ms_mlp_params acceptor;       /* N groups (C units each); act_frag with the common row's table */
+    const int8_t* common_row;     /* [acc_obs_stride] the foreign acceptor row */
+    const ms_price_table* price_table; /* built for price_chooser's weights (ms_price_table_build) */
+    uint64_t seed, off_offset, acc_offset;
+    const uint64_t* offset_dev;   /* may be NULL */
+    int8_t* core_action;          /* [E][N*L] */
+    float* core_logprob;          /* [E][N*L] */
+    int8_t* price_state;          /* [E][N*L][4] */
+    int8_t* price_action;         /* [E][N*L] */
+    float* price_logprob;         /* [E][N*L] */
+    int8_t* env_price;            /* [E][N*L] the next round's offer_price actions (one buffer for every round) */
+    int8_t* acc_action;           /* [E][N*C] */
+    float* acc_logprob;           /* [E][N*C] */
+} ms_fused_act_free;
+
+/* Per-round byte strides of ms_env_rollout_act_free (as ms_round_strides, plus the price chooser's arrays). */
+typedef struct ms_round_strides_free {
+    int64_t acceptor_action, offer_action;                 /* ms_actions acceptor / offer_core (offer_price: 0) */
+    int64_t core_rows, core_owner, offer_obs;              /* ms_obs_out */
+    int64_t offer_reward, price_reward, acceptor_reward, agent_reward, auctioneer_reward; /* ms_reward_out */
+    int64_t next_core_action, next_core_logprob, next_price_state, next_price_action, next_price_logprob;
+    int64_t next_acc_action, next_acc_logprob;             /* ms_fused_act_free outputs */
+    uint64_t offset_step;
+} ms_round_strides_free;
+
+/* n_rounds rounds of a locally shared free-price rollout in one launch: round t steps the env with the
+ * actions act->acceptor / offer_core advanced by t strides and act->offer_price (the next->env_price buffer the
+ * acting refills), writes obs / rewards advanced by t strides, and then (t < n_rounds - 1, or act_after_last)
+ * samples round t + 1's actions into next's outputs advanced by t strides, with offsets + t * offset_step.
+ * Bit-identical to n_rounds pairs of ms_env_step + ms_act_round_free. Requires free prices, compact acceptor
+ * observations (core_rows, core_owner, offer), no events or metrics or aggregated rewards,
+ * ms_env_rollout_act_free_supported, N groups per net, act fragments for both nets and a price table.
+ * Every ring must hold n_rounds slots at its stride (the kernel does not see the sizes). MS_EINVAL otherwise. */
+int ms_env_rollout_act_free(ms_env* env, const ms_actions* act, const ms_obs_out* obs, const ms_reward_out* rew,
+                            const ms_event_out* ev, const ms_fused_act_free* next, const ms_round_strides_free* strides,
+                            int32_t n_rounds, int32_t act_after_last, void* stream);
+
+/* 1 when ms_env_rollout_act_free can run this env's rounds (free prices, N <= 8, max(N, C) <= 16, offer rows
+ * <= 32 bytes with <= 16 core actions, acceptor rows of 33..64 bytes with 17..32 actions), else 0. */
+int ms_env_rollout_act_free_supported(const ms_env* env);
 
 /* Discounted Monte-Carlo returns + per-sequence normalisation (PPOmodules.py:128-137):
  * rewards [T][M] (f32, as stored per round), for each sequence m:

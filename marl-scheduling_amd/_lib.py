@@ -27,7 +27,7 @@ class MarlSchedError(RuntimeError):
         self.code = code
 
 
-ABI_VERSION = 16  # include/marlsched.h MS_ABI_VERSION
+ABI_VERSION = 17  # include/marlsched.h MS_ABI_VERSION
 
 
 def _load():
@@ -56,6 +56,11 @@ def _load():
         "ms_env_rollout_act": (ct.c_int, [P, ct.POINTER(abi.MsActions), ct.POINTER(abi.MsObsOut),
                                           ct.POINTER(abi.MsRewardOut), ct.POINTER(abi.MsEventOut),
                                           ct.POINTER(abi.MsFusedAct), ct.POINTER(abi.MsRoundStrides), i32, i32, P]),
+        "ms_env_rollout_act_free": (ct.c_int, [P, ct.POINTER(abi.MsActions), ct.POINTER(abi.MsObsOut),
+                                               ct.POINTER(abi.MsRewardOut), ct.POINTER(abi.MsEventOut),
+                                               ct.POINTER(abi.MsFusedActFree), ct.POINTER(abi.MsRoundStridesFree), i32,
+                                               i32, P]),
+        "ms_env_rollout_act_free_supported": (ct.c_int, [P]),
         "ms_env_round": (i64, [P]),
         "ms_env_flags": (ct.c_int, [P, ct.POINTER(u32), P]),
         "ms_env_randbelow": (ct.c_int, [P, i64, u32, ct.POINTER(u32), P]),
@@ -117,14 +122,16 @@ def _load():
     L.ms_abi_version.restype = ct.c_int
     version = L.ms_abi_version()
     # ABI 14 added ms_bdqn_update*, 15 ms_bdqn_act_compact, 16 ms_mlp_params.row_base (a trailing field an
-    # older library does not read: its acting draws are those of row_base 0). An older library (an A/B variant built
+    # older library does not read: its acting draws are those of row_base 0) and ms_env_step_act /
+    # ms_env_rollout_act, 17 ms_env_rollout_act_free. An older library (an A/B variant built
     # before them, tools/gpu_job.sh ab step) loads without them only when MARLSCHED_LENIENT_ABI=1 asks for it
-    lenient = os.environ.get("MARLSCHED_LENIENT_ABI") == "1" and version in (13, 14, 15, 16)
+    lenient = os.environ.get("MARLSCHED_LENIENT_ABI") == "1" and version in (13, 14, 15, 16, 17)
     if version != ABI_VERSION and not lenient:
         raise ImportError("libmarlsched.so ABI version mismatch (%d, want %d)" % (version, ABI_VERSION))
     for name, (res, args) in sig.items():
         if (version < 14 and name.startswith("ms_bdqn_update")) or (version < 15 and name == "ms_bdqn_act_compact") \
-                or (version < 16 and name.startswith("ms_env_step_act")):
+                or (version < 16 and (name.startswith("ms_env_step_act") or name == "ms_env_rollout_act")) \
+                or (version < 17 and name.startswith("ms_env_rollout_act_free")):
             continue
         if lenient and not hasattr(L, name):  # an older build of this ABI (A/B variants)
             continue
@@ -135,11 +142,19 @@ def _load():
 
 
 lib = _load()
+ABI_LOADED = int(lib.ms_abi_version())  # < ABI_VERSION only for a lenient load of an older A/B variant
+
+
+def has(name: str) -> bool:
+    """Whether the loaded library exports `name` with its signature set (an older lenient variant may not)."""
+    return hasattr(lib, name) and getattr(lib, name).argtypes is not None
+
 
 # every entry point include/marlsched.h declares (checked by tests)
 EXPORTED = (
     "ms_last_error", "ms_abi_version", "ms_config_shape", "ms_env_create", "ms_env_destroy", "ms_env_shape",
-    "ms_env_reset", "ms_env_step", "ms_env_step_act", "ms_env_step_act_supported", "ms_env_rollout_act", "ms_env_round", "ms_env_flags", "ms_env_randbelow", "ms_env_auctioneer",
+    "ms_env_reset", "ms_env_step", "ms_env_step_act", "ms_env_step_act_supported", "ms_env_rollout_act",
+    "ms_env_rollout_act_free", "ms_env_rollout_act_free_supported", "ms_env_round", "ms_env_flags", "ms_env_randbelow", "ms_env_auctioneer",
     "ms_env_get_rng", "ms_env_set_rng", "ms_env_export",
     "ms_env_import", "ms_policy_act", "ms_policy_act_common", "ms_policy_act_compact",
     "ms_act_round_free", "ms_price_table_build", "ms_act_frag_bytes", "ms_act_prepare", "ms_offer_act_free", "ms_discounted_returns", "ms_unit_returns",

@@ -30,6 +30,9 @@ hipError_t launch_env_step_act(const Params&, int64_t, uint8_t*, uint32_t*, Liab
 bool env_step_act_supported(const Params&, int64_t);
 hipError_t launch_env_rollout_act(const Params&, int64_t, uint8_t*, uint32_t*, Liab*, const StepIO&, const FusedAct&,
                                   const RoundStride&, int, int, hipStream_t);
+hipError_t launch_env_rollout_act_free(const Params&, int64_t, uint8_t*, uint32_t*, Liab*, const StepIO&,
+                                       const FusedActFree&, const RoundStrideFree&, int, int, hipStream_t);
+bool env_rollout_free_supported(const Params&);
 hipError_t launch_env_randbelow(const Params&, uint8_t*, uint32_t*, int64_t, uint32_t, uint32_t*, hipStream_t);
 hipError_t launch_env_auctioneer(const Params&, int64_t, uint8_t*, uint32_t*, int8_t*, hipStream_t);
 hipError_t launch_policy_act(const ms_mlp_params*, const int8_t*, int, int64_t, int, int, const int8_t*, uint64_t,
@@ -251,6 +254,9 @@ struct RolloutArgs {
 };
 static int env_step_impl(ms_env* env, const ms_actions* act, const ms_obs_out* obs, const ms_reward_out* rew,
                          const ms_event_out* ev, const ms::FusedAct* fa, const RolloutArgs* ro, void* stream);
+static int fill_io(ms_env* env, const ms_actions* act, const ms_obs_out* obs, const ms_reward_out* rew,
+                   const ms_event_out* ev, ms::StepIO* out);
+static int check_mlp(const ms_mlp_params* p, int32_t obs_stride, int32_t n_units, int32_t units_per_group);
 
 int ms_env_step(ms_env* env, const ms_actions* act, const ms_obs_out* obs, const ms_reward_out* rew,
                 const ms_event_out* ev, void* stream) {
@@ -330,6 +336,23 @@ static int env_step_impl(ms_env* env, const ms_actions* act, const ms_obs_out* o
     if (__atomic_load_n(env->err_host, __ATOMIC_ACQUIRE))
         return fail(MS_EOVERFLOW, "an earlier round raised a per-env error flag (see ms_env_flags)");
     ms::StepIO io{};
+    const int rc = fill_io(env, act, obs, rew, ev, &io);
+    if (rc != MS_OK) return rc;
+    if (ro)
+        HIP_TRY(ms::launch_env_rollout_act(env->P, env->E, env->recs, env->mt, env->liab, io, *fa, ro->st, ro->n_rounds,
+                                           ro->act_last, (hipStream_t)stream));
+    else if (fa)
+        HIP_TRY(ms::launch_env_step_act(env->P, env->E, env->recs, env->mt, env->liab, io, *fa, (hipStream_t)stream));
+    else
+        HIP_TRY(ms::launch_env_step(env->P, env->E, env->recs, env->mt, env->liab, io, (hipStream_t)stream));
+    env->round += ro ? ro->n_rounds : 1;
+    return MS_OK;
+}
+
+// the launch's StepIO from the caller's structs
+static int fill_io(ms_env* env, const ms_actions* act, const ms_obs_out* obs, const ms_reward_out* rew,
+                   const ms_event_out* ev, ms::StepIO* out) {
+    ms::StepIO io{};
     io.err_word = env->err_host;
     io.act_acc = act->acceptor;
     io.act_off = act->offer_core;
@@ -359,14 +382,67 @@ static int env_step_impl(ms_env* env, const ms_actions* act, const ms_obs_out* o
         io.metrics_slots = ev->metrics_slots;
         if (io.metrics && io.metrics_slots < 1) return fail(MS_EINVAL, "ms_env_step: metrics_slots must be >= 1");
     }
-    if (ro)
-        HIP_TRY(ms::launch_env_rollout_act(env->P, env->E, env->recs, env->mt, env->liab, io, *fa, ro->st, ro->n_rounds,
-                                           ro->act_last, (hipStream_t)stream));
-    else if (fa)
-        HIP_TRY(ms::launch_env_step_act(env->P, env->E, env->recs, env->mt, env->liab, io, *fa, (hipStream_t)stream));
-    else
-        HIP_TRY(ms::launch_env_step(env->P, env->E, env->recs, env->mt, env->liab, io, (hipStream_t)stream));
-    env->round += ro ? ro->n_rounds : 1;
+    *out = io;
+    return MS_OK;
+}
+
+int ms_env_rollout_act_free_supported(const ms_env* env) {
+    return env && env->cfg.free_prices && ms::env_rollout_free_supported(env->P) ? 1 : 0;
+}
+
+int ms_env_rollout_act_free(ms_env* env, const ms_actions* act, const ms_obs_out* obs, const ms_reward_out* rew,
+                            const ms_event_out* ev, const ms_fused_act_free* next, const ms_round_strides_free* strides,
+                            int32_t n_rounds, int32_t act_after_last, void* stream) {
+    if (!env || !act || !next || !strides) return fail(MS_EINVAL, "env/act/next/strides is NULL");
+    const ms::Params& P = env->P;
+    auto bad = [&](const char* why) { return fail(MS_EINVAL, "ms_env_rollout_act_free: %s", why); };
+    if (!ms_env_rollout_act_free_supported(env))
+        return bad("free prices, N <= 8, max(N, C) <= 16, offer rows <= 32 B / <= 16 core actions, acceptor rows "
+                   "33..64 B / 17..32 actions only");
+    if (n_rounds < 1) return bad("n_rounds < 1");
+    if (!obs || !obs->core_rows || !obs->core_owner || !obs->offer || obs->acceptor || obs->auctioneer)
+        return bad("needs compact acceptor observations (core_rows, core_owner) and offer rows only");
+    if (!act->acceptor || !act->offer_core || act->offer_price != next->env_price || act->auctioneer)
+        return bad("actions: acceptor and offer_core given, offer_price = next->env_price, no auctioneer actions");
+    if (ev && (ev->accepted || ev->terminated || ev->metrics)) return bad("no event records or metrics");
+    if (rew && (rew->aggregated_offer || rew->aggregated_acceptor)) return bad("no aggregated reward outputs");
+    const ms_mlp_params& c = next->core_chooser;
+    const ms_mlp_params& p = next->price_chooser;
+    const ms_mlp_params& a = next->acceptor;
+    const int N = P.N, C = P.C, L = P.L;
+    int rc = check_mlp(&c, P.off_stride, N * L, L);
+    if (!rc) rc = check_mlp(&p, 4, N * L, L);
+    if (!rc) rc = check_mlp(&a, P.acc_stride, N * C, C);
+    if (rc) return rc;
+    if (c.in_dim != P.d_off || c.n_actions != C + 1 || a.in_dim != P.d_acc || a.n_actions != P.O + 1)
+        return bad("net shapes do not match the env");
+    if (p.in_dim != 4 || p.n_actions > 16) return bad("price chooser must be 4 -> A with A <= 16");
+    if (!c.act_frag || !a.act_frag) return bad("needs act fragments (ms_act_prepare) of both nets");
+    const ms_price_table* pt = next->price_table;
+    if (!pt || !pt->digit || !pt->table || pt->n_keys < 1 || (int64_t)pt->n_keys * 36 * 4 > 0x7fffffffLL)
+        return bad("needs a price table (digit, table, 1 <= n_keys)");
+    if (!next->common_row || !next->core_action || !next->core_logprob || !next->price_state || !next->price_action ||
+        !next->price_logprob || !next->env_price || !next->acc_action || !next->acc_logprob)
+        return bad("NULL output / common row");
+    if (env->E * N * L >= (1LL << 24) || env->E * N * C * 4 > 0x7fffffffLL || env->E * N * L * 4 > 0x7fffffffLL)
+        return bad("too many replicas for 32-bit row offsets");
+    if (__atomic_load_n(env->err_host, __ATOMIC_ACQUIRE))
+        return fail(MS_EOVERFLOW, "an earlier round raised a per-env error flag (see ms_env_flags)");
+    ms::StepIO io{};
+    rc = fill_io(env, act, obs, rew, ev, &io);
+    if (rc != MS_OK) return rc;
+    const ms::FusedActFree fa{c, p, a, next->common_row, pt->table, pt->digit, pt->n_keys, next->seed,
+                              next->off_offset, next->acc_offset, next->offset_dev, next->core_action,
+                              next->core_logprob, next->price_state, next->price_action, next->price_logprob,
+                              next->env_price, next->acc_action, next->acc_logprob};
+    const ms_round_strides_free& r = *strides;
+    const ms::RoundStrideFree st{r.acceptor_action, r.offer_action, r.core_rows, r.core_owner, r.offer_obs,
+                                 r.offer_reward, r.price_reward, r.acceptor_reward, r.agent_reward, r.auctioneer_reward,
+                                 r.next_core_action, r.next_core_logprob, r.next_price_state, r.next_price_action,
+                                 r.next_price_logprob, r.next_acc_action, r.next_acc_logprob, r.offset_step};
+    HIP_TRY(ms::launch_env_rollout_act_free(P, env->E, env->recs, env->mt, env->liab, io, fa, st, n_rounds,
+                                            act_after_last ? 1 : 0, (hipStream_t)stream));
+    env->round += n_rounds;
     return MS_OK;
 }
 

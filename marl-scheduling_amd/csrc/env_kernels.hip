@@ -45,6 +45,7 @@ __device__ __forceinline__ void wave_sync() {
 constexpr int kProbeSlots = 65536;
 __device__ unsigned long long g_phase_cycles[kProbeSlots][16];  // per block, summed on the host
 __device__ unsigned long long g_wave_span[kProbeSlots][2];      // last launch: s_memrealtime at entry / exit
+__device__ unsigned long long g_free_cycles[kProbeSlots][4];    // k_env_rollout_act_free: env, wait, act, wait
 #define MS_MARK(k)                                                     \
     do {                                                               \
         const uint64_t t_now = __builtin_amdgcn_s_memtime();          \
@@ -1011,8 +1012,11 @@ constexpr int kLiabPrefetch = 4;  // newest chain entries loaded ahead per core 
 // training loop's form: its act and gradient kernels read core rows + owners).
 template <int LPE, bool EXT, bool CMP, class SH>
 __device__ __forceinline__ void env_round(const Params& P, int64_t E, uint8_t* recs, uint32_t* mt, Liab* liab,
-                                          const StepIO& io, int64_t slot, int lane_arg = -1) {
-    extern __shared__ __align__(16) uint8_t smem_all[];
+                                          const StepIO& io, int64_t slot, int lane_arg = -1,
+                                          uint8_t* wave_lds = nullptr) {
+    // wave_lds: the wave's part of a multi-wave workgroup's LDS (k_env_rollout_act_free), else the block's
+    extern __shared__ __align__(16) uint8_t smem_dyn[];
+    uint8_t* const smem_all = wave_lds ? wave_lds : smem_dyn;
     // the shape: a compile-time constant for the BASELINE shapes (offsets fold into immediates,
     // loops over agents / cores / slots get constant trip counts), else the kernel arguments
     Geom g;
@@ -1924,6 +1928,455 @@ __global__ void __launch_bounds__(64, 2) k_env_rollout_act(RolloutArgs A0) {
     }
 }
 
+// ---- locally shared free-price rollouts (BASELINE cfg3; ms_env_rollout_act_free): the next round's
+//      getActionForAllAgents (SchedulingEnvironment.py:150-172) of a workgroup's replicas, one wave per agent,
+//      from the observations the workgroup's env round just built in its LDS: the agent's offer units
+//      (FreePriceOfferPPO.selectAction PPOmodules.py:312-332: core chooser, then the price chooser on
+//      [obs[2a:2a+2], obs[-2:]] or the dummy [-5] * 4) and its acceptors (LocallySharedPPO.selectAction
+//      PPOmodules.py:532-543, Agent.py:682-699) on the compact acceptor rows. The arithmetic and the Philox draws
+//      are k_act_pair's (act_tiles' core + price choosers with the price table, act_common_rows' compact
+//      acceptors), so the outputs equal ms_act_round_free's on the emitted observations bit for bit:
+//      a row's MFMA column, its four lanes' reductions and its draw depend on the row alone, not on the rows
+//      that share its tile.
+constexpr int kPriceTW1 = 36;  // floats per price-table entry of <= 16 actions (policy_kernels.hip PriceTW<1>)
+
+__device__ __forceinline__ uint32_t pick4u(const uint32_t (&v)[4], int k) {
+    return k == 0 ? v[0] : (k == 1 ? v[1] : (k == 2 ? v[2] : v[3]));
+}
+
+template <class SH>
+__device__ __forceinline__ void act_free(const Geom& g, int64_t E, const FusedActFree& fa, int64_t e0, int a, int lane,
+                                         uint8_t* lds, const FreeLds& fl) {
+    const int j = lane & 15, g4 = lane >> 4;
+    const int N = g.N, C = g.C, L = g.L, Uo = g.NL, Ua = N * C;
+    const int EW = kFreeEPW * N;  // the workgroup's replicas
+    const uint64_t dev_off = fa.offset_dev ? *fa.offset_dev : 0ull;
+    const int16_t* pdig = reinterpret_cast<const int16_t*>(lds + fl.pdig);
+    auto slice = [&](int k) -> const uint8_t* { return lds + k * g.s_total; };
+
+    // ---------------- the offer units: agent a's L slots of every replica, rows r = k * L + s
+    {
+        using FL = FragLayout<1, 1>;
+        constexpr int TW = kPriceTW1;
+        W1Split<1> w1;
+        Head<1> h1;
+        if (const uint32_t* fg = frag_groups<1, 1>(fa.core, false)) {
+            const uint32_t* lf = fg + (size_t)a * FL::GB + lane * FL::LW;
+            w1.load_frag(lf);
+            h1.load_frag(reinterpret_cast<const float*>(lf + 12));
+        } else {
+            w1.load(fa.core.w1 + (size_t)a * 16 * fa.core.in_dim, fa.core.in_dim, j, g4);
+            h1.load(fa.core, a, j, g4);
+        }
+        const int n_rows = EW * L, tiles = (n_rows + 15) >> 4;
+        const uint64_t off = fa.off_offset + dev_off;
+        const uint32_t rbase = (uint32_t)fa.core.row_base;
+        const long long rows_all = E * Uo;
+        const RawBuf ca_b(fa.core_action, rows_all), cl_b(fa.core_logprob, 4 * rows_all),
+            ps_b(fa.price_state, 4 * rows_all), pa_b(fa.price_action, rows_all), pl_b(fa.price_logprob, 4 * rows_all),
+            ep_b(fa.env_price, rows_all);
+        const RawBuf tab_b(fa.ptab + (size_t)a * fa.pkeys * TW, 4ll * fa.pkeys * TW);
+        const int nwo = g.off_stride >> 2, pcol = (2 * C) >> 2, pshift = 8 * ((2 * C) & 3);
+        const int A1 = fa.core.n_actions, A2 = fa.price.n_actions;
+        // the call row (e * N*L + a*L + s) of the agent's row r, -1 past the replicas; k, s: its replica in
+        // the workgroup and its slot (0 for rows past the end: their LDS reads stay in range)
+        auto row_of = [&](int r, int& k, int& s) -> int {
+            k = r / L;
+            s = r - k * L;
+            const bool v = r < n_rows && e0 + k < E;
+            const int row = (int)((e0 + k) * Uo) + a * L + s;
+            if (r >= n_rows) k = s = 0;
+            return v ? row : -1;
+        };
+        uint32_t rb0[4] = {0, 0, 0, 0}, rb1[4] = {0, 0, 0, 0};
+        // one tile pair up to the price chooser's input: the rows' core choices, the price inputs and their
+        // key digits (act_tiles: core2 + price_in2)
+        auto core_pair = [&](int tile, int (&cur)[2], int (&act)[2], float (&lp)[2], float (&u2)[2], int (&pin)[2],
+                             int (&dg)[2]) {
+            if ((tile & 3) == 0) {  // Philox for 4 tiles: lane (j, g4) draws row j of tile tile + g4
+                int k, s;
+                const int r = row_of(16 * (tile + g4) + j, k, s);
+                uint32_t r0, r1;
+                philox2((uint32_t)r + rbase, off, fa.seed, r0, r1);
+                rows_bcast(r1, rb1);
+                rows_bcast(r0, rb0);
+            }
+            const int kq = tile & 3;
+            int kk[2], ss[2];
+            f4 acc[2];
+            float u1[2];
+#pragma unroll
+            for (int i = 0; i < 2; i++) {
+                cur[i] = row_of(16 * (tile + i) + j, kk[i], ss[i]);
+                const uint8_t* sc = slice(kk[i]) + g.s_scratch;
+                const uint32_t* otmpl = reinterpret_cast<const uint32_t*>(sc + g.s_otmpl);
+                const uint32_t pr = reinterpret_cast<const uint16_t*>(sc + g.s_slotpair)[a * L + ss[i]];
+                uint32_t d[2];
+#pragma unroll
+                for (int h = 0; h < 2; h++) {
+                    const int cc = 2 * g4 + h, wd = cc < nwo ? cc : nwo - 1;
+                    d[h] = otmpl[wd] | (wd == pcol ? pr << pshift : 0u);
+                }
+                const u4v x = bytes_to_bf16(d[0], d[1]);
+                acc[i] = (f4){0, 0, 0, 0};
+                acc[i] = mfma_bf16(w1.hi[0], x, acc[i]);
+                acc[i] = mfma_bf16(w1.mid[0], x, acc[i]);
+                acc[i] = mfma_bf16(w1.lo[0], x, acc[i]);
+                u1[i] = u24(pick4u(rb0, kq + i));
+                u2[i] = u24(pick4u(rb1, kq + i));
+            }
+            h1.run2(acc, A1, g4, u1, act, lp);
+#pragma unroll
+            for (int i = 0; i < 2; i++) {
+                // byte kb of the row: the chosen core's (prio, rem) for g4 < 2, the slot's pair obs[-2:] for g4 >= 2
+                const int kb = g4 < 2 ? 2 * act[i] + g4 : 2 * C + (g4 - 2);
+                const int8_t* sc = reinterpret_cast<const int8_t*>(slice(kk[i]) + g.s_scratch);
+                const int byte = kb < 2 * C ? sc[g.s_otmpl + kb] : sc[g.s_slotpair + 2 * (a * L + ss[i]) + (kb - 2 * C)];
+                pin[i] = act[i] == 0 ? -5 : byte;
+                dg[i] = cur[i] >= 0 ? (int)pdig[g4 * 256 + pin[i] + 128] : 0;
+            }
+        };
+        // the price chooser's outputs of a pair (PPOmodules.py:316-332; env price -5 for core action 0)
+        auto price_out = [&](const int (&cur)[2], const int (&act)[2], const int (&pin)[2], const int (&pact)[2],
+                             const float (&plp)[2]) {
+#pragma unroll
+            for (int i = 0; i < 2; i++)
+                if (cur[i] >= 0) {
+                    const uint32_t pc = (uint32_t)cur[i];
+                    ps_b.st8(4 * pc + g4, pin[i]);
+                    if (g4 == 0) {
+                        pa_b.st8(pc, pact[i]);
+                        pl_b.stf(4 * pc, plp[i]);
+                        ep_b.st8(pc, act[i] == 0 ? -5 : pact[i]);
+                    }
+                }
+        };
+        bool any_miss = false;
+        for (int tile = 0; tile < tiles; tile += 2) {
+            int cur[2], act[2], pin[2], dg[2];
+            float lp[2], u2[2];
+            core_pair(tile, cur, act, lp, u2, pin, dg);
+            if (__ballot(dg[0] < 0 || dg[1] < 0) == 0ull) {
+                // every row of the pair is tabulated: sample from the table (act_tiles' arithmetic)
+                rows_sum2_i(dg[0], dg[1]);
+                float cum[2][4], S2[2];
+                int lnz[2], cnt[2], pact[2];
+                float plp[2];
+                uint32_t te[2];
+#pragma unroll
+                for (int i = 0; i < 2; i++) {
+                    te[i] = __umul24((uint32_t)dg[i], 4u * TW);
+                    const auto c4 = __builtin_amdgcn_raw_buffer_load_b128(tab_b.r, (int)(te[i] + 4 * (4 * g4)), 0, 0);
+#pragma unroll
+                    for (int q = 0; q < 4; q++) cum[i][q] = __uint_as_float(c4[q]);
+                    S2[i] = tab_b.ldf(te[i] + 4 * 32);
+                    lnz[i] = (int)tab_b.ld32(te[i] + 4 * 33);
+                }
+#pragma unroll
+                for (int i = 0; i < 2; i++) {
+                    const float target = u2[i] * S2[i];
+                    cnt[i] = 0;
+#pragma unroll
+                    for (int q = 0; q < 4; q++) cnt[i] += (cum[i][q] <= target) ? 1 : 0;
+                }
+                rows_sum2_i(cnt[0], cnt[1]);
+#pragma unroll
+                for (int i = 0; i < 2; i++) {
+                    pact[i] = cnt[i] >= A2 ? lnz[i] : cnt[i];
+                    plp[i] = tab_b.ldf(te[i] + 4 * (16 + pact[i]));
+                }
+                price_out(cur, act, pin, pact, plp);
+            } else {
+                any_miss = true;
+            }
+#pragma unroll
+            for (int i = 0; i < 2; i++)
+                if (cur[i] >= 0 && g4 == 0) {
+                    ca_b.st8((uint32_t)cur[i], act[i]);
+                    cl_b.stf(4 * (uint32_t)cur[i], lp[i]);
+                }
+        }
+        if (any_miss) {
+            // the pairs the table could not serve: the same pairs and draws again, the core chooser recomputed
+            // (bit-identical), then the price net itself (act_tiles' second loop)
+            Head<1> h2;
+            h2.load(fa.price, a, j, g4);
+            const float pw1 = fa.price.w1[((size_t)a * 16 + j) * 4 + g4];  // W1p[j][g4] (K = 4 inputs)
+            for (int tile = 0; tile < tiles; tile += 2) {
+                int cur[2], act[2], pin[2], dg[2];
+                float lp[2], u2[2];
+                core_pair(tile, cur, act, lp, u2, pin, dg);
+                if (__ballot(dg[0] < 0 || dg[1] < 0) == 0ull) continue;  // priced from the table above
+                int pact[2];
+                float plp[2];
+                f4 acc2[2];
+#pragma unroll
+                for (int i = 0; i < 2; i++) acc2[i] = mfma4(pw1, (float)pin[i], (f4){0, 0, 0, 0});
+                h2.run2(acc2, A2, g4, u2, pact, plp);
+                price_out(cur, act, pin, pact, plp);
+            }
+        }
+    }
+
+    // ---------------- the acceptors: agent a's C items of every replica, item m = k * C + c (group item
+    //                  i = e * C + c): the cores it does not own sample the common row's table, the owned ones
+    //                  are listed and run in 16-row MFMA tiles (act_common_rows with compact rows)
+    {
+        using FL = FragLayout<2, 2>;
+        const uint32_t* const fg = frag_groups<2, 2>(fa.acc, true);
+        const float* tab = reinterpret_cast<const float*>(lds + fl.tab) + a * kFreeTabDw;  // Head<2>::table
+        const float S = tab[64];
+        const int last_nz = __float_as_int(tab[65]);
+        int16_t* lm = reinterpret_cast<int16_t*>(lds + fl.list + a * kFreeListCap * 6);
+        float* lu = reinterpret_cast<float*>(lds + fl.list + a * kFreeListCap * 6 + 2 * kFreeListCap);
+        const int nw = g.acc_stride >> 2, Aa = fa.acc.n_actions;
+        const int n_items = EW * C;
+        const uint64_t off = fa.acc_offset + dev_off;
+        const uint32_t rbase = (uint32_t)fa.acc.row_base;
+        const long long rows_all = E * Ua;
+        const RawBuf aa_b(fa.acc_action, rows_all), al_b(fa.acc_logprob, 4 * rows_all);
+        // the listed rows [0, cnt) (cnt <= 32) as two 16-row tiles (a lone or partial tile: rows past cnt
+        // are computed on entry 0 and not written)
+        auto tiles2 = [&](int cnt) {
+            // the net's fragments only for the tiles (52 registers not held through the scan): loaded per call
+            // through a pointer the compiler cannot see through, so the loads are not hoisted out of the scan loop
+            W1Split<2> w1;
+            Head<2> h1;
+            if (fg) {
+                const uint32_t* lf = fg + (size_t)a * FL::GB + lane * FL::LW;
+                asm volatile("" : "+v"(lf));
+                w1.load_frag(lf);
+                h1.load_frag(reinterpret_cast<const float*>(lf + 24));
+            } else {
+                w1.load(fa.acc.w1 + (size_t)a * 16 * fa.acc.in_dim, fa.acc.in_dim, j, g4);
+                h1.load(fa.acc, a, j, g4);
+            }
+            f4 acc[2];
+            int row[2];
+            float uu[2];
+#pragma unroll
+            for (int i = 0; i < 2; i++) {
+                const int t = 16 * i + j;
+                const bool v = t < cnt;
+                const int mm = lm[v ? t : 0];
+                uu[i] = lu[v ? t : 0];
+                const int kk = mm / C, cc = mm - kk * C;
+                row[i] = v ? (int)((e0 + kk) * Ua) + a * C + cc : -1;
+                const uint32_t* crow = reinterpret_cast<const uint32_t*>(slice(kk) + g.s_scratch) + cc * nw;
+                acc[i] = (f4){0, 0, 0, 0};
+#pragma unroll
+                for (int s = 0; s < 2; s++) {
+                    const int c0 = 8 * s + 2 * g4, c1 = c0 + 1;
+                    const u4v x = bytes_to_bf16(crow[c0 < nw ? c0 : nw - 1], crow[c1 < nw ? c1 : nw - 1]);
+                    acc[i] = mfma_bf16(w1.hi[s], x, acc[i]);
+                    acc[i] = mfma_bf16(w1.mid[s], x, acc[i]);
+                    acc[i] = mfma_bf16(w1.lo[s], x, acc[i]);
+                }
+            }
+            int act[2];
+            float lp[2];
+            h1.run2(acc, Aa, g4, uu, act, lp);
+#pragma unroll
+            for (int i = 0; i < 2; i++)
+                if (row[i] >= 0 && g4 == 0) {
+                    aa_b.st8((uint32_t)row[i], act[i]);
+                    al_b.stf(4 * (uint32_t)row[i], lp[i]);
+                }
+        };
+        // item i's uniform: word (i >> 6) & 1 of the draw countered by the row of item i & ~64 (k_act_common's
+        // rule), so a lane's draw serves its item and the item 64 further when both are in this wave
+        const uint32_t i_base = (uint32_t)(e0 * C);
+        uint32_t last_ib = 0xffffffffu, wd0 = 0, wd1 = 0;
+        const uint64_t below = (1ull << lane) - 1ull;
+        int n_list = 0;
+        for (int m0 = 0; m0 < n_items; m0 += 64) {
+            const int m = m0 + lane;
+            const bool in = m < n_items;
+            const int k = in ? m / C : 0, c = in ? m - (m / C) * C : 0;
+            const bool valid = in && e0 + k < E;
+            const uint32_t i = i_base + (uint32_t)m, ib = i & ~64u;
+            const bool need = ib != last_ib;
+            if (__ballot(need)) {
+                const uint32_t eb = ib / (uint32_t)C;
+                uint32_t r0, r1;
+                philox2(eb * (uint32_t)Ua + (uint32_t)(a * C) + (ib - eb * (uint32_t)C) + rbase, off, fa.seed, r0, r1);
+                if (need) {
+                    last_ib = ib;
+                    wd0 = r0;
+                    wd1 = r1;
+                }
+            }
+            const float u = u24((i & 64u) ? wd1 : wd0);
+            const int own = reinterpret_cast<const int8_t*>(slice(k) + g.s_rec + g.o_core_owner)[c];
+            const bool owned = valid && own == a + 1;
+            if (valid && !owned) {
+                const float target = u * S;
+                int cnt = 0;
+#pragma unroll
+                for (int step = 32; step >= 1; step >>= 1)
+                    if (cnt + step <= 32 && tab[cnt + step - 1] <= target) cnt += step;
+                const int act = cnt >= Aa ? last_nz : cnt;
+                const uint32_t row = (uint32_t)((e0 + k) * Ua) + (uint32_t)(a * C + c);
+                aa_b.st8(row, act);
+                al_b.stf(4 * row, tab[32 + act]);
+            }
+            const uint64_t mo = __ballot(owned);
+            if (owned) {
+                const int p = n_list + __popcll(mo & below);
+                lm[p] = (int16_t)m;
+                lu[p] = u;
+            }
+            n_list += __popcll(mo);
+            wave_sync();
+            while (n_list >= 32) {
+                tiles2(32);
+                const int rest = n_list - 32;  // < 64: carried to the front of the list
+                int16_t vm = 0;
+                float vu = 0.f;
+                if (lane < rest) {
+                    vm = lm[32 + lane];
+                    vu = lu[32 + lane];
+                }
+                wave_sync();
+                if (lane < rest) {
+                    lm[lane] = vm;
+                    lu[lane] = vu;
+                }
+                wave_sync();
+                n_list = rest;
+            }
+        }
+        if (n_list > 0) tiles2(n_list);
+    }
+}
+
+struct RolloutFreeArgs {
+    Params P;
+    int64_t E;
+    uint8_t* recs;
+    uint32_t* mt;
+    Liab* liab;
+    StepIO io;
+    FusedActFree fa;
+    RoundStrideFree st;
+    int n_rounds, act_last;
+};
+// The locally shared free-price rollout in one launch: workgroup b holds replicas kFreeEPW * N * b .. in its LDS,
+// and wave w steps kFreeEPW of them (k_env_step's round, 16 lanes per replica) and then acts for agent w of all
+// of them (act_free), round after round, with a workgroup barrier between the phases: every agent's nets
+// act from registers and LDS on the rows the round just built, instead of an act launch re-reading them from
+// HBM. Round t's arrays are the given ones advanced by t strides. The round re-reads its arguments through
+// the opaque kernel-argument pointer (k_env_rollout_act). Two workgroups per CU: 4 waves per SIMD (<= 128 VGPRs).
+template <class SH>
+__global__ void __launch_bounds__(512, 4) k_env_rollout_act_free(RolloutFreeArgs A0) {
+    extern __shared__ __align__(16) uint8_t smem_free[];
+    Geom g;
+    if constexpr (SH::kStatic) {
+        constexpr Geom kg = make_geom(SH::kN, SH::kC, SH::kL, SH::kJ);
+        g = kg;
+    } else {
+        g = A0.P;
+    }
+    const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    const int lane0 = (int)threadIdx.x & 63;
+    const FreeLds fl = free_lds(g);
+    const int64_t wslot = (int64_t)blockIdx.x * g.N + wave;  // the wave's slot of kFreeEPW replicas
+    unsigned long long* span = A0.io.span;
+    if (span && lane0 == 0) {
+        span[4 * wslot] = __builtin_amdgcn_s_memrealtime();
+        span[4 * wslot + 2] = __builtin_amdgcn_s_memtime();
+    }
+    // once per launch (the acting nets do not change within a rollout): the price table's key digits, one copy
+    // per workgroup, and each agent's common-row sampling table (ms_act_prepare's, else computed here)
+    {
+        uint32_t* pd = reinterpret_cast<uint32_t*>(smem_free + fl.pdig);
+        const uint32_t* src = reinterpret_cast<const uint32_t*>(A0.fa.pdigit);
+        for (int k = (int)threadIdx.x; k < 512; k += (int)blockDim.x) pd[k] = src[k];
+        float* tab = reinterpret_cast<float*>(smem_free + fl.tab) + wave * kFreeTabDw;
+        if (const uint32_t* fg = frag_groups<2, 2>(A0.fa.acc, true)) {
+            using FL = FragLayout<2, 2>;
+            const uint32_t* tb = fg + (size_t)wave * FL::GB + 64 * FL::LW;
+            for (int k = lane0; k < kFreeTabDw; k += 64) reinterpret_cast<uint32_t*>(tab)[k] = tb[k];
+        } else {
+            const int j = lane0 & 15, g4 = lane0 >> 4;
+            W1Split<2> w1;
+            Head<2> h1;
+            w1.load(A0.fa.acc.w1 + (size_t)wave * 16 * A0.fa.acc.in_dim, A0.fa.acc.in_dim, j, g4);
+            h1.load(A0.fa.acc, wave, j, g4);
+            uint32_t* tmpl = reinterpret_cast<uint32_t*>(smem_free + fl.list + wave * kFreeListCap * 6);
+            int* lnz = reinterpret_cast<int*>(tab + 65);
+            common_table<2, 2>(w1, h1, A0.fa.common, g.acc_stride >> 2, tmpl, tab, tab + 32, tab + 64, lnz, lane0);
+        }
+    }
+    __syncthreads();
+#ifdef MS_PHASE_TIMING
+    // probe build: per wave, the shader cycles of the env rounds, the wait at the barrier after them, the acting,
+    // and the wait at the barrier after it (tools/env_phase_probe.py --free)
+    uint64_t f_prev = __builtin_amdgcn_s_memtime(), f_acc[4] = {0, 0, 0, 0};
+#define FREE_MARK(k)                                                   \
+    do {                                                               \
+        const uint64_t f_now = __builtin_amdgcn_s_memtime();          \
+        if ((k) >= 0) f_acc[(k) < 0 ? 0 : (k)] += f_now - f_prev;      \
+        f_prev = f_now;                                                \
+    } while (0)
+#else
+#define FREE_MARK(k) \
+    do {             \
+    } while (0)
+#endif
+    const int n_rounds = A0.n_rounds;
+    for (int t = 0; t < n_rounds; t++) {
+        auto ka = __builtin_amdgcn_kernarg_segment_ptr();  // (constant address space)
+        asm volatile("" : "+s"(ka));
+        const RolloutFreeArgs& A = *(const RolloutFreeArgs*)ka;
+        int lane = (int)threadIdx.x & 63;
+        asm volatile("" : "+v"(lane));
+        const RoundStrideFree& st = A.st;
+        StepIO io = A.io;
+        io.span = nullptr;
+        io.act_acc = advance(io.act_acc, t * st.act_acc);
+        io.act_off = advance(io.act_off, t * st.act_off);
+        io.obs_crow = advance(io.obs_crow, t * st.obs_crow);
+        io.obs_cown = advance(io.obs_cown, t * st.obs_cown);
+        io.obs_off = advance(io.obs_off, t * st.obs_off);
+        io.rew_offer = advance(io.rew_offer, t * st.rew_offer);
+        io.rew_price = advance(io.rew_price, t * st.rew_price);
+        io.rew_acc = advance(io.rew_acc, t * st.rew_acc);
+        io.rew_agent = advance(io.rew_agent, t * st.rew_agent);
+        io.rew_auct = advance(io.rew_auct, t * st.rew_auct);
+        FREE_MARK(-1);
+        env_round<kWave / kFreeEPW, false, true, SH>(A.P, A.E, A.recs, A.mt, A.liab, io, wslot, lane,
+                                                     smem_free + wave * kFreeEPW * g.s_total);
+        FREE_MARK(0);
+        if (t + 1 < n_rounds || A.act_last) {
+            __syncthreads();  // every replica's observation sources are in the LDS
+            FREE_MARK(1);
+            FusedActFree fa = A.fa;
+            fa.core_action = advance(fa.core_action, t * st.core_action);
+            fa.core_logprob = advance(fa.core_logprob, t * st.core_logprob);
+            fa.price_state = advance(fa.price_state, t * st.price_state);
+            fa.price_action = advance(fa.price_action, t * st.price_action);
+            fa.price_logprob = advance(fa.price_logprob, t * st.price_logprob);
+            fa.acc_action = advance(fa.acc_action, t * st.acc_action);
+            fa.acc_logprob = advance(fa.acc_logprob, t * st.acc_logprob);
+            fa.off_offset += (uint64_t)t * st.offset_step;
+            fa.acc_offset += (uint64_t)t * st.offset_step;
+            act_free<SH>(g, A.E, fa, (int64_t)blockIdx.x * kFreeEPW * g.N, wave, lane, smem_free, fl);
+            FREE_MARK(2);
+            __syncthreads();  // the actions are stored and the LDS is free for the next round
+            FREE_MARK(3);
+        }
+    }
+    if (span && lane0 == 0) {
+        span[4 * wslot + 3] = __builtin_amdgcn_s_memtime();
+        span[4 * wslot + 1] = __builtin_amdgcn_s_memrealtime();
+    }
+#ifdef MS_PHASE_TIMING
+    if (lane0 == 0)
+        for (int k = 0; k < 4; k++) g_free_cycles[wslot % kProbeSlots][k] += f_acc[k];
+#endif
+}
+
 // Auctioneer.getAuctioneerAction (Auctioneer.py:95-102) on its own, as the driver calls it
 // before env.step (trainPPO.py:162): writes actions [E][C] and advances the env stream by the
 // tie-break draws; a following ms_env_step with these actions then draws only the spawn.
@@ -2000,6 +2453,19 @@ extern "C" int ms_probe_phase_blocks(unsigned long long* out, int n_blocks) {
     if (n_blocks > ms::kProbeSlots) return -1;
     if (hipMemcpyFromSymbol(host, HIP_SYMBOL(ms::g_phase_cycles), sizeof(host)) != hipSuccess) return -1;
     memcpy(out, host, sizeof(unsigned long long) * 16 * n_blocks);
+    return 0;
+}
+// k_env_rollout_act_free's per-wave cycles (env rounds, barrier wait, acting, barrier wait) summed over the
+// launches since the last clear: out[4 * n_waves]
+extern "C" int ms_probe_free_cycles(unsigned long long* out, int n_waves, int clear) {
+    static unsigned long long host[ms::kProbeSlots][4];
+    if (n_waves > ms::kProbeSlots) return -1;
+    if (hipMemcpyFromSymbol(host, HIP_SYMBOL(ms::g_free_cycles), sizeof(host)) != hipSuccess) return -1;
+    memcpy(out, host, sizeof(unsigned long long) * 4 * n_waves);
+    if (clear) {
+        memset(host, 0, sizeof(host));
+        if (hipMemcpyToSymbol(HIP_SYMBOL(ms::g_free_cycles), host, sizeof(host)) != hipSuccess) return -1;
+    }
     return 0;
 }
 // entry / exit s_memrealtime (100 MHz) of every block of the last launch: out[2 * n_blocks]
@@ -2156,6 +2622,37 @@ hipError_t launch_env_rollout_act(const Params& P, int64_t E, uint8_t* recs, uin
             return launch_rollout_act_sh<32, DynShape>(P, E, recs, mt, liab, io, fa, st, n_rounds, act_last, s);
         default: return launch_rollout_act_sh<64, DynShape>(P, E, recs, mt, liab, io, fa, st, n_rounds, act_last, s);
     }
+}
+// ms_env_rollout_act_free: 16 lanes per replica (max(N, C) <= 16), one wave per agent (N <= 8: a 512-lane
+// workgroup), the core chooser one k-step with <= 16 actions, the acceptor two k-steps with 17..32 actions
+// (k_act_pair<1, 1, 1, 2, 2>'s shapes), the price chooser <= 16 actions, two workgroups' LDS per CU
+bool env_rollout_free_supported(const Params& P) {
+    return P.free_prices && P.N >= 1 && P.N <= 8 && P.C >= 1 && P.C <= 16 && P.off_stride <= 32 &&
+           P.C + 1 <= 16 && P.acc_stride > 32 && P.acc_stride <= 64 && P.O + 1 > 16 && P.O + 1 <= 32 &&
+           2 * (free_lds(P).total + 256) <= 160 * 1024;
+}
+template <class SH>
+static hipError_t launch_rollout_free_sh(const Params& P, int64_t E, uint8_t* recs, uint32_t* mt, Liab* liab,
+                                         const StepIO& io, const FusedActFree& fa, const RoundStrideFree& st,
+                                         int n_rounds, int act_last, hipStream_t s) {
+    const int64_t epb = (int64_t)kFreeEPW * P.N;
+    const int64_t blocks = (E + epb - 1) / epb;
+    const RolloutFreeArgs A{P, E, recs, mt, liab, io, fa, st, n_rounds, act_last};
+    hipLaunchKernelGGL((k_env_rollout_act_free<SH>), dim3((unsigned)blocks), dim3(64 * P.N), (size_t)free_lds(P).total, s,
+                       A);
+    return hipGetLastError();
+}
+hipError_t launch_env_rollout_act_free(const Params& P, int64_t E, uint8_t* recs, uint32_t* mt, Liab* liab,
+                                       const StepIO& io, const FusedActFree& fa, const RoundStrideFree& st,
+                                       int n_rounds, int act_last, hipStream_t s) {
+    if (!env_rollout_free_supported(P) || io.act_acc == nullptr || io.metrics != nullptr || io.obs_acc != nullptr ||
+        n_rounds < 1)
+        return hipErrorInvalidValue;
+#ifndef MS_NO_FIXED_SHAPES
+    if (is_shape<8, 8, 3, 1>(P))
+        return launch_rollout_free_sh<FixShape<8, 8, 3, 1>>(P, E, recs, mt, liab, io, fa, st, n_rounds, act_last, s);
+#endif
+    return launch_rollout_free_sh<DynShape>(P, E, recs, mt, liab, io, fa, st, n_rounds, act_last, s);
 }
 hipError_t launch_env_auctioneer(const Params& P, int64_t E, uint8_t* recs, uint32_t* mt, int8_t* actions,
                                  hipStream_t s) {

@@ -184,6 +184,51 @@ struct RoundStride {
     uint64_t offset_step;
 };
 
+// the fused next-round acting of a locally shared free-price rollout (ms_env_rollout_act_free,
+// env_kernels.hip act_free): one core chooser, price chooser and acceptor net per agent
+struct FusedActFree {
+    ms_mlp_params core, price, acc;
+    const int8_t* common;
+    const float* ptab;       // price table [N][pkeys][PriceTW] (ms_price_table)
+    const int16_t* pdigit;   // [4][256] key digit of byte value v at position p, -1: not tabulated
+    int32_t pkeys;
+    uint64_t seed, off_offset, acc_offset;
+    const uint64_t* offset_dev;
+    int8_t* core_action;     // [E][N*L]
+    float* core_logprob;
+    int8_t* price_state;     // [E][N*L][4]
+    int8_t* price_action;
+    float* price_logprob;
+    int8_t* env_price;       // [E][N*L]: the next round's offer_price actions (one buffer, every round)
+    int8_t* acc_action;      // [E][N*C]
+    float* acc_logprob;
+};
+
+// per-round byte strides of k_env_rollout_act_free (ms_round_strides_free)
+struct RoundStrideFree {
+    int64_t act_acc, act_off, obs_crow, obs_cown, obs_off, rew_offer, rew_price, rew_acc, rew_agent, rew_auct;
+    int64_t core_action, core_logprob, price_state, price_action, price_logprob, acc_action, acc_logprob;
+    uint64_t offset_step;
+};
+
+// The workgroup LDS of k_env_rollout_act_free: the env slices of its kFreeEPW * N replicas (wave w steps
+// replicas kFreeEPW * w ..), then the act area: the price table's key digits (one copy per workgroup) and per
+// wave (= agent) its acceptor net's common-row sampling table and its list of owned-core rows.
+constexpr int kFreeEPW = 4;        // replicas per wave (16 lanes each)
+constexpr int kFreeListCap = 96;   // < 32 carried + one 64-item step
+constexpr int kFreeTabDw = 68;     // [32 running sums][32 log-probs][S][last nonzero][2 pad] (Head<2>::table)
+struct FreeLds {
+    int32_t pdig, tab, list, total;
+};
+inline constexpr FreeLds free_lds(const Geom& g) {
+    FreeLds f{};
+    f.pdig = align16(kFreeEPW * g.N * g.s_total);
+    f.tab = f.pdig + 4 * 256 * 2;
+    f.list = f.tab + g.N * kFreeTabDw * 4;
+    f.total = f.list + g.N * kFreeListCap * 6;  // int16 item + f32 uniform per entry
+    return f;
+}
+
 // launch arguments of k_aggregate_obs (agg_kernels.hip): divided rows in, aggregated rows out
 struct AggArgs {
     const int8_t* acc;  // [E][N][C][acc_stride]

@@ -1098,7 +1098,7 @@ hipError_t launch_act_round(const ms_mlp_params* core, const ms_mlp_params* pric
         return e != hipSuccess ? e : dispatch_act(c, st);
     }
     // fewer, longer waves than either launch alone: the other half's waves fill the gaps
-    // (tools/sweep_act.sh: 2048 / 768 -> 2048 offer and 2048 acceptor waves at cfg3)
+    // (the tools/gpu_job.sh waves step; profiles/r4af: 2048 / 768 -> 2048 offer and 2048 acceptor waves at cfg3)
     static const long long t_off = env_int("MS_ACT_PAIR_WAVES", 2048), t_acc = env_int("MS_ACT_PAIR_COMMON_WAVES", 768);
     const unsigned ob = act_blocks(o, t_off), cb = act_common_blocks(c, t_acc);
     hipLaunchKernelGGL((k_act_pair<1, 1, 1, 2, 2>), dim3(ob + cb), dim3(256), 0, st, o, c, (int)ob);

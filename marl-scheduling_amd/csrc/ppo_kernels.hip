@@ -143,17 +143,8 @@ constexpr int kGradProbeWaves = 1 << 15;
 __device__ unsigned long long g_grad_probe[kGradProbeWaves][4];
 #endif
 
-// MS_GRAD_BF16H=1 (experiment build): the 16-wide weight x activation products of the
-// tile (layers 2-3 forward, their backward) as three-term bf16 on v_mfma_f32_16x16x32_bf16 instead of
-// four v_mfma_f32_16x16x4_f32 each: K = 32 holds two 16-wide terms side by side, so
-//   [Wh|Wh].[Xh;Xm] + [Wm|Wm].[Xh;Xm] + [Wh|Wl].[Xl;Xh]
-// = Wh Xh + Wh Xm + Wm Xh + Wm Xm + Wh Xl + Wl Xh (the three dropped products are below 2^-23 of the
-// leading one). The weights' fragments are split once per block into LDS; the activations per tile.
-#ifndef MS_GRAD_BF16H
-#define MS_GRAD_BF16H 0
-#endif
-template <int NT>
-constexpr bool grad_bf16h() { return MS_GRAD_BF16H && NT <= 2; }
+// (The 16-wide layers stay on the f32 MFMA: a three-term bf16 form of them measured slower, 2519 -> 2646 us
+// per offer-gradient call, profiles/r5m)
 
 template <int NQ, int NT, int MODEX>
 struct GradLds {
@@ -168,9 +159,7 @@ struct GradLds {
     static constexpr int NTR = NT + 1;               // 16-row transposes live at once (three phases per tile)
     // block: split W1 / C1 [2][3][16][W1B] bf16, then W2, C2, W3 and the biases (floats)
     static constexpr int w1s_floats = 2 * 3 * 16 * W1B / 2;
-    // (MS_GRAD_BF16H) split weight fragments [4 + 2 NT matrices][3 terms][64 lanes][4 dwords]
-    static constexpr int hb_floats = grad_bf16h<NT>() ? (4 + 2 * NT) * 3 * 64 * 4 : 0;
-    static constexpr int shared_floats = w1s_floats + 2 * 256 + 256 * NT + 16 * 5 + 16 * NT + 4 + hb_floats;
+    static constexpr int shared_floats = w1s_floats + 2 * 256 + 256 * NT + 16 * 5 + 16 * NT + 4;
     // per wave: d1 / e1 transposes over a tile pair, the per-tile transposes, 32 staged input rows
     // (common-row path: the common row's clamped logs, V, entropy, the list of the other rows,
     //  and the wave's int64 fixed-point sums of d min(surr)/d ratio * ratio per action [16*NT])
@@ -227,7 +216,6 @@ __global__ void __launch_bounds__((64 * GradLds<NQ, NT, MODEX>::WPB), ((NQ * NT 
     float* scb2 = scb1 + 16;            // 16
     float* sb3 = scb2 + 16;             // 16*NT
     float* scb3 = sb3 + 16 * NT;        // 1 (+3 pad)
-    u4v* sHB = reinterpret_cast<u4v*>(scb3 + 4);  // (MS_GRAD_BF16H) [matrix][term][lane] fragments
     float* sT = sm + L::shared_floats + wave * L::wave_floats;
     float* T_d1 = sT;                   // [16 features][TP2]: 32 rows of the tile pair
     float* T_e1 = sT + 16 * TP2;
@@ -277,53 +265,6 @@ __global__ void __launch_bounds__((64 * GradLds<NQ, NT, MODEX>::WPB), ((NQ * NT 
         if (tid == 0) scb3[0] = p.cb3[grp];
     }
     __syncthreads();
-    constexpr bool HB = grad_bf16h<NT>();
-    if constexpr (HB) {
-        // fragment of lane (i, g) for A[i][4g .. 4g+3] of matrix m: W2, C2, W2^T, C2^T, W3 tiles, W3^T tiles
-        for (int it = tid; it < (4 + 2 * NT) * 64; it += NTH) {
-            const int m = it >> 6, ln = it & 63, i = ln & 15, g = ln >> 4;
-            float h[4], md[4], lo[4];
-#pragma unroll
-            for (int e = 0; e < 4; e++) {
-                const int k = 4 * g + e;
-                float w;
-                if (m == 0) w = sW2[i * 16 + k];
-                else if (m == 1) w = sC2[i * 16 + k];
-                else if (m == 2) w = sW2[k * 16 + i];
-                else if (m == 3) w = sC2[k * 16 + i];
-                else if (m < 4 + NT) w = sW3[(16 * (m - 4) + i) * 16 + k];
-                else w = sW3[(16 * (m - 4 - NT) + k) * 16 + i];
-                h[e] = trunc_bf16(w);
-                const float r = w - h[e];
-                md[e] = trunc_bf16(r);
-                lo[e] = r - md[e];
-            }
-            const uint32_t h01 = pack_hi(h[0], h[1]), h23 = pack_hi(h[2], h[3]);
-            sHB[(m * 3 + 0) * 64 + ln] = (u4v){h01, h23, h01, h23};
-            sHB[(m * 3 + 1) * 64 + ln] = (u4v){pack_hi(md[0], md[1]), pack_hi(md[2], md[3]), pack_hi(md[0], md[1]),
-                                              pack_hi(md[2], md[3])};
-            sHB[(m * 3 + 2) * 64 + ln] = (u4v){h01, h23, pack_hi(lo[0], lo[1]), pack_hi(lo[2], lo[3])};
-        }
-        __syncthreads();
-    }
-    // acc + M . x for the 16 x 16 matrix m of sHB, x = this lane's 4 activations (column j, k 4 g4 + q)
-    auto mm3 = [&](int m, const float (&x)[4], f4 acc) {
-        float h[4], md[4], lo[4];
-#pragma unroll
-        for (int e = 0; e < 4; e++) {
-            h[e] = trunc_bf16(x[e]);
-            const float r = x[e] - h[e];
-            md[e] = trunc_bf16(r);
-            lo[e] = r - md[e];
-        }
-        const uint32_t h01 = pack_hi(h[0], h[1]), h23 = pack_hi(h[2], h[3]);
-        const u4v b1 = {h01, h23, pack_hi(md[0], md[1]), pack_hi(md[2], md[3])};
-        const u4v b3 = {pack_hi(lo[0], lo[1]), pack_hi(lo[2], lo[3]), h01, h23};
-        acc = mfma_bf16(sHB[(m * 3 + 0) * 64 + lane], b1, acc);
-        acc = mfma_bf16(sHB[(m * 3 + 1) * 64 + lane], b1, acc);
-        return mfma_bf16(sHB[(m * 3 + 2) * 64 + lane], b3, acc);
-    };
-
     f4 gW1[NQ], gC1[NQ], gW3[NT];
     f4 gW2 = {0, 0, 0, 0}, gC2 = {0, 0, 0, 0};
 #pragma unroll
@@ -387,10 +328,7 @@ __global__ void __launch_bounds__((64 * GradLds<NQ, NT, MODEX>::WPB), ((NQ * NT 
         }
         // layer 2: B operand = layer-1 output as is; A reads W2 with k permuted (k_true = 4*g4 + s)
         f4 a2 = {0, 0, 0, 0}, c2 = {0, 0, 0, 0};
-        if constexpr (HB) {
-            a2 = mm3(0, f.h1, a2);
-            c2 = mm3(1, f.hc1, c2);
-        } else {
+        {
             const f4 w2 = *reinterpret_cast<const f4*>(sW2 + j * 16 + 4 * g4);
             const f4 cw2 = *reinterpret_cast<const f4*>(sC2 + j * 16 + 4 * g4);
 #pragma unroll
@@ -416,8 +354,6 @@ __global__ void __launch_bounds__((64 * GradLds<NQ, NT, MODEX>::WPB), ((NQ * NT 
 #pragma unroll
                 for (int q = 0; q < 4; q++) pz = fmaf(w3[q], f.h2[q], pz);
                 zz[0] = xsum4g(pz);
-            } else if constexpr (HB) {
-                zz = mm3(4 + t, f.h2, zz);
             } else {
                 const f4 w3 = *reinterpret_cast<const f4*>(sW3 + (16 * t + j) * 16 + 4 * g4);
 #pragma unroll
@@ -625,8 +561,6 @@ __global__ void __launch_bounds__((64 * GradLds<NQ, NT, MODEX>::WPB), ((NQ * NT 
                 const f4 w3 = *reinterpret_cast<const f4*>(sW3 + (16 * t) * 16 + 4 * g4);
 #pragma unroll
                 for (int q = 0; q < 4; q++) d2[q] = fmaf(w3[q], g16, d2[q]);
-            } else if constexpr (HB) {
-                d2 = mm3(4 + NT + t, gz[t], d2);
             } else {
 #pragma unroll
                 for (int s = 0; s < 4; s++) d2 = mfma4(sW3[(16 * t + 4 * g4 + s) * 16 + j], gz[t][s], d2);
@@ -639,15 +573,10 @@ __global__ void __launch_bounds__((64 * GradLds<NQ, NT, MODEX>::WPB), ((NQ * NT 
             dc2[q] = sc3[4 * g4 + q] * g_v * (1.f - f.hc2[q] * f.hc2[q]);
         }
         f4 d1 = {0, 0, 0, 0}, e1 = {0, 0, 0, 0};
-        if constexpr (HB) {
-            d1 = mm3(2, dl2, d1);
-            e1 = mm3(3, dc2, e1);
-        } else {
 #pragma unroll
-            for (int s = 0; s < 4; s++) {
-                d1 = mfma4(sW2[(4 * g4 + s) * 16 + j], dl2[s], d1);
-                e1 = mfma4(sC2[(4 * g4 + s) * 16 + j], dc2[s], e1);
-            }
+        for (int s = 0; s < 4; s++) {
+            d1 = mfma4(sW2[(4 * g4 + s) * 16 + j], dl2[s], d1);
+            e1 = mfma4(sC2[(4 * g4 + s) * 16 + j], dc2[s], e1);
         }
         float dl1[4], dc1[4];
 #pragma unroll

@@ -15,7 +15,7 @@ import numpy as np
 import torch
 
 from . import abi
-from ._lib import check, drain_released, lib, ptr, release, stream_ptr
+from ._lib import check, drain_released, has, lib, ptr, release, stream_ptr
 
 
 class BatchedEnv:
@@ -184,17 +184,84 @@ class BatchedEnv:
                                   stream_ptr(stream)))
         return obs, rewards, events
 
+    @staticmethod
+    def check_rings(rings, n_rounds: int):
+        """The bounds contract of the one-launch rollouts (marlsched.h): each (tensor, stride, dtype) is a ring's
+        round-0 slot, read or written again at stride bytes for every later round, so its storage must hold
+        n_rounds slots (the kernel sees pointers only: a short ring would be an out-of-bounds GPU access)."""
+        for t, stride, dtype in rings:
+            if t is None:
+                continue
+            assert t.is_cuda and t.is_contiguous() and t.dtype == dtype, (t.shape, t.dtype, dtype)
+            st = t.untyped_storage()
+            end = st.data_ptr() + st.nbytes()
+            assert stride >= 0 and (stride == 0 or stride >= t.numel() * t.element_size()), "overlapping ring slots"
+            last = t.data_ptr() + (int(n_rounds) - 1) * int(stride) + t.numel() * t.element_size()
+            assert last <= end, "ring holds fewer than n_rounds slots at its stride"
+
+    def _ring_list(self, acceptor, offer_core, obs, rewards, strides, price=False):
+        i8, i32, f32 = torch.int8, torch.int32, torch.float32
+        rings = [(acceptor, strides.acceptor_action, i8), (offer_core, strides.offer_action, i8),
+                 (obs.get("core_rows"), strides.core_rows, i8), (obs.get("core_owner"), strides.core_owner, i8),
+                 (obs.get("offer"), strides.offer_obs, i8), (rewards.get("offer"), strides.offer_reward, f32),
+                 (rewards.get("acceptor"), strides.acceptor_reward, i32),
+                 (rewards.get("agent"), strides.agent_reward, i32),
+                 (rewards.get("auctioneer"), strides.auctioneer_reward, i32)]
+        if price:
+            rings.append((rewards.get("price"), strides.price_reward, f32))
+        return rings
+
     def rollout_act(self, acceptor, offer_core, obs, rewards, next_act, strides, n_rounds, act_after_last=False,
-                    events=None, stream=None):
+                    events=None, stream=None, next_out=None):
         """n_rounds rounds of step(next_act=...) in one launch (ms_env_rollout_act): round t reads and
         writes the given arrays advanced by t * strides (an abi.MsRoundStrides, bytes) and acts with the
-        Philox offsets + t * strides.offset_step. Bit-identical to the n_rounds step calls."""
+        Philox offsets + t * strides.offset_step. Bit-identical to the n_rounds step calls.
+        next_out: the tensors behind next_act's outputs, dict(off_action, off_logprob, acc_action, acc_logprob)
+        (round 0's slots), bounds-checked like the other rings when given."""
         for t in (acceptor, offer_core):
             assert t.dtype == torch.int8 and t.device == self.device
+        rings = self._ring_list(acceptor, offer_core, obs, rewards, strides)
+        if next_out is not None and (n_rounds > 1 or act_after_last):
+            n_act = n_rounds if act_after_last else n_rounds - 1
+            self.check_rings([(next_out["off_action"], strides.next_off_action, torch.int8),
+                              (next_out["off_logprob"], strides.next_off_logprob, torch.float32),
+                              (next_out["acc_action"], strides.next_acc_action, torch.int8),
+                              (next_out["acc_logprob"], strides.next_acc_logprob, torch.float32)], n_act)
+        self.check_rings(rings, n_rounds)
         a, o, r, ev = self._step_structs(acceptor, offer_core, None, None, obs, rewards, events)
         check(lib.ms_env_rollout_act(self._h, ct.byref(a), ct.byref(o), ct.byref(r), ct.byref(ev) if ev else None,
                                      ct.byref(next_act), ct.byref(strides), int(n_rounds), int(bool(act_after_last)),
                                      stream_ptr(stream)))
+
+    def rollout_act_free(self, acceptor, offer_core, obs, rewards, next_act, next_out, strides, n_rounds,
+                         act_after_last=False, events=None, stream=None):
+        """A locally shared free-price rollout of n_rounds rounds in one launch (ms_env_rollout_act_free; BASELINE
+        cfg3): round t steps the replicas with the actions advanced by t strides and next_out["env_price"] as the
+        offer prices, writes obs / rewards advanced by t strides, then samples round t + 1's actions into next_act's
+        outputs (an abi.MsFusedActFree; next_out: its tensors, round 0's slots) advanced by t strides. Bit-identical
+        to n_rounds pairs of step + act_round_free (SchedulingEnvironment.py:150-172, trainPPO.py:160-167)."""
+        i8, f32 = torch.int8, torch.float32
+        assert self.free_prices and next_out["env_price"].numel() == self.E * self.N * self.L
+        rings = self._ring_list(acceptor, offer_core, obs, rewards, strides, price=True)
+        rings.append((next_out["env_price"], 0, i8))
+        self.check_rings(rings, n_rounds)
+        if n_rounds > 1 or act_after_last:
+            n_act = n_rounds if act_after_last else n_rounds - 1
+            self.check_rings([(next_out["core_action"], strides.next_core_action, i8),
+                              (next_out["core_logprob"], strides.next_core_logprob, f32),
+                              (next_out["price_state"], strides.next_price_state, i8),
+                              (next_out["price_action"], strides.next_price_action, i8),
+                              (next_out["price_logprob"], strides.next_price_logprob, f32),
+                              (next_out["acc_action"], strides.next_acc_action, i8),
+                              (next_out["acc_logprob"], strides.next_acc_logprob, f32)], n_act)
+        a, o, r, ev = self._step_structs(acceptor, offer_core, next_out["env_price"], None, obs, rewards, events)
+        check(lib.ms_env_rollout_act_free(self._h, ct.byref(a), ct.byref(o), ct.byref(r),
+                                          ct.byref(ev) if ev else None, ct.byref(next_act), ct.byref(strides),
+                                          int(n_rounds), int(bool(act_after_last)), stream_ptr(stream)))
+
+    def rollout_free_supported(self) -> bool:
+        """Whether rollout_act_free can run this env's rounds (ms_env_rollout_act_free_supported)."""
+        return has("ms_env_rollout_act_free_supported") and bool(lib.ms_env_rollout_act_free_supported(self._h))
 
     def _step_structs(self, acceptor, offer_core, offer_price, auctioneer, obs, rewards, events):
         a = abi.MsActions(ptr(acceptor), ptr(offer_core), ptr(offer_price if self.free_prices else None),
@@ -214,8 +281,9 @@ class BatchedEnv:
         return a, o, r, ev
 
     def fused_act_supported(self) -> bool:
-        """Whether step(next_act=...) can run this env's rounds (ms_env_step_act_supported)."""
-        return bool(lib.ms_env_step_act_supported(self._h))
+        """Whether step(next_act=...) can run this env's rounds (ms_env_step_act_supported; False for an older
+        library without it)."""
+        return has("ms_env_step_act_supported") and bool(lib.ms_env_step_act_supported(self._h))
 
     def flags(self, stream=None) -> int:
         f = ct.c_uint32()

@@ -19,16 +19,18 @@ each optimizer step all-reduces one flattened gradient buffer (RCCL).
 """
 from __future__ import annotations
 
+import ctypes as ct
 import os
 import random
 import time
+import warnings
 from dataclasses import dataclass, field
 
 import numpy as np
 import torch
 
 from . import abi
-from ._lib import hip_capture, ptr
+from ._lib import ABI_LOADED, hip_capture, ptr
 from .env import BatchedEnv
 from .ppo import (ActFrag, PPOGroup, PriceTable, act_round_free, discounted_returns, offer_act_free, reference_init_order,
                   reference_nets, unit_returns)
@@ -205,6 +207,17 @@ class Trainer:
                                unit_major=self.price_unit_major)
         if world_size > 1:
             self._broadcast_params()
+        # A single net's item i takes word (i >> 6) & 1 of the draw countered by item i & ~64 (k_act_common's rule on
+        # the call's group item index e * S + s), so a shard or part draws what one call over all replicas would
+        # only when its first group item, (rank * E + e0) * S, is a multiple of 128. Otherwise the
+        # streams stay independent but a split run no longer reproduces the unsplit one: say so.
+        if world_size > 1 or rollout_streams > 1:
+            per_group = [("acceptor", self.acc.S)] + ([] if self.free else [("offer", self.off.S)])
+            for _, e0, _ in self.env.parts:
+                for name, S in per_group:
+                    if ((rank * self.E + e0) * S) % 128:
+                        warnings.warn("%s draws of replicas from %d differ from an unsplit run's: (rank * E + e0) * %d "
+                                      "is not a multiple of 128" % (name, rank * self.E + e0, S))
         # observation ring: slot t holds the state acted on at round t; slot T the next state. With
         # compact (and common_rows) the acceptor observations are kept as the env emits them
         # compactly: the owner row of every core + the owners (C rows per replica instead of N*C;
@@ -265,13 +278,21 @@ class Trainer:
         # fixed-price rounds with one net per role (cfg2): round t's env launch also samples round t + 1's
         # actions from the observations it just built (ms_env_step_act), so a round is one launch
         # (MS_ENV_FUSED_ACT=0: the act launch and the env launch of every round, for A/B measurements)
+        # (T > 1: the fused acting writes round t + 1's ring slots)
         self.fused_step = (self.compact and not self.free and self.acc.group.policy.G == 1 and
-                           self.off.group.policy.G == 1 and self.acc_frag is not None and
+                           self.off.group.policy.G == 1 and self.acc_frag is not None and self.T > 1 and
                            os.environ.get("MS_ENV_FUSED_ACT", "1") != "0" and self.metric_bufs is None and
                            all(env.fused_act_supported() for env, _, _ in self.env.parts))
         # ... and the whole rollout's rounds are one launch (ms_env_rollout_act): each wave steps and acts
         # for its replicas round after round (MS_ENV_ROLLOUT=0: one launch per round, for A/B measurements)
         self.fused_rollout = self.fused_step and os.environ.get("MS_ENV_ROLLOUT", "1") != "0"
+        # locally shared free-price rounds (cfg3): the whole rollout in one launch too (ms_env_rollout_act_free):
+        # a workgroup steps its replicas, then acts for them with one wave per agent, round after round
+        # (MS_ENV_ROLLOUT_FREE=0: an act launch and an env launch per round, for A/B measurements)
+        self.fused_rollout_free = (self.compact and self.free and arch == "local" and self.price_table is not None and
+                                   self.off_frag is not None and not self.price_unit_major and self.T > 1 and
+                                   self.metric_bufs is None and os.environ.get("MS_ENV_ROLLOUT_FREE", "1") != "0" and
+                                   all(env.rollout_free_supported() for env, _, _ in self.env.parts))
         self.span_every = 0  # > 0: every span_every-th round's env launches record their span (bench)
         self.spans = None
         self.timings = dict(rollout=0.0, update=0.0)
@@ -375,6 +396,15 @@ class Trainer:
                 offer_act_free(self.off.group.policy_old, self.price.group.policy_old, sl(self.off_obs[t]), C, seed,
                                base + 1, out, offset_dev=self.rng_ctr, stream=st, price_unit_stride=pus,
                                core_frag=self.off_frag, replica_base=rb)
+        elif self.compact and ABI_LOADED < 16:
+            # (an older A/B library: no fixed-price act_round_free; the two launches)
+            self.off.group.policy_old.act(sl(self.off_obs[t]), N * L, seed, base + 1, action=sl(self.off.actions[t]),
+                                          logprob=sl(self.off.logprobs[t]), offset_dev=self.rng_ctr, stream=st,
+                                          frag=self.off_frag, replica_base=rb)
+            self.acc.group.policy_old.act_compact(sl(self.acc_rows[t]), sl(self.acc_owner[t]), N * C, seed, base + 3,
+                                                  self.acc_common, action=sl(self.acc.actions[t]),
+                                                  logprob=sl(self.acc.logprobs[t]), stream=st, offset_dev=self.rng_ctr,
+                                                  frag=self.acc_frag, replica_base=rb)
         elif self.compact:
             # a fixed-price round: the offer units and the compact acceptors in one launch
             act_round_free(self.off.group.policy_old, None, sl(self.off_obs[t]), self.acc.group.policy_old,
@@ -441,6 +471,47 @@ class Trainer:
                         self._fused_next(1, k), strides, self.T, act_after_last=False, events=ev,
                         stream=self.streams[k])
 
+    def _fused_next_free(self, t: int, k: int):
+        """Round t's acting of a locally shared free-price round (act_round_free of _act_part) for replica part k,
+        fused into round t - 1 of the one-launch rollout: (abi.MsFusedActFree, its output tensors)."""
+        e0, e1 = self.env.parts[k][1:]
+        sl = lambda x: x[e0:e1]
+        N, C, L = self.N, self.C, self.L
+        seed, base, rb = self.seed * 7919, 8 * t, self.rank * self.E + e0
+        out = dict(core_action=sl(self.off.actions[t]), core_logprob=sl(self.off.logprobs[t]),
+                   price_state=sl(self.price_obs[t]), price_action=sl(self.price.actions[t]),
+                   price_logprob=sl(self.price.logprobs[t]), env_price=sl(self.env_price),
+                   acc_action=sl(self.acc.actions[t]), acc_logprob=sl(self.acc.logprobs[t]))
+        names = ("core_action", "core_logprob", "price_state", "price_action", "price_logprob", "env_price",
+                 "acc_action", "acc_logprob")
+        nxt = abi.MsFusedActFree(self.off.group.policy_old.mlp_params(self.off_frag, rb * N * L),
+                                 self.price.group.policy_old.mlp_params(),
+                                 self.acc.group.policy_old.mlp_params(self.acc_frag, rb * N * C), ptr(self.acc_common),
+                                 ct.addressof(self.price_table.struct), seed, base + 1, base + 3, ptr(self.rng_ctr),
+                                 *[ptr(out[n]) for n in names])
+        return nxt, out
+
+    def _rollout_part_free(self, k: int):
+        """Rounds 0..T-1 of replica part k of a locally shared free-price rollout (env.step + saveRewards, and the
+        acting of rounds 1..T-1) in one launch (ms_env_rollout_act_free); round 0's acting ran before it."""
+        env, e0, e1 = self.env.parts[k]
+        E, N, C, L = e1 - e0, self.N, self.C, self.L
+        sl = lambda x: x[e0:e1]
+        obs = dict(self._acc_out(1, e0, e1), offer=sl(self.off_obs[1]))
+        rew = dict(offer=sl(self.off.rewards[0]).view(E, N, L), acceptor=sl(self.acc.rewards[0]).view(E, N, C),
+                   agent=sl(self.agent_reward), auctioneer=sl(self.auct_reward),
+                   price=sl(self.price.rewards[0]).view(E, N, L))
+        ev = dict(launch_span=self.spans[0, k]) if self.span_every else None
+        b = lambda x: x.stride(0) * x.element_size()  # bytes between ring slots t and t + 1
+        strides = abi.MsRoundStridesFree(b(self.acc.actions), b(self.off.actions), b(self.acc_rows), b(self.acc_owner),
+                                         b(self.off_obs), b(self.off.rewards), b(self.price.rewards),
+                                         b(self.acc.rewards), 0, 0, b(self.off.actions), b(self.off.logprobs),
+                                         b(self.price_obs), b(self.price.actions), b(self.price.logprobs),
+                                         b(self.acc.actions), b(self.acc.logprobs), 8)
+        nxt, out = self._fused_next_free(1, k)
+        env.rollout_act_free(sl(self.acc.actions[0]).view(E, N, C), sl(self.off.actions[0]).view(E, N, L), obs, rew,
+                             nxt, out, strides, self.T, act_after_last=False, events=ev, stream=self.streams[k])
+
     def record_launch_spans(self, every: int):
         """Every `every`-th round's env launches record their span (first wave start, last wave end
         on the 100 MHz s_memrealtime clock, and each wave's shader-clock cycles) into self.spans
@@ -459,7 +530,7 @@ class Trainer:
         """Durations (us) of the recorded env launches of the last rollout (fused_rollout: the one
         launch of each part over T, per round), or of `sampled` (a copy of sampled_spans())."""
         sp = (self.sampled_spans() if sampled is None else sampled).cpu().numpy()  # [rounds][parts][waves][4]
-        if self.fused_rollout:
+        if self.fused_rollout or self.fused_rollout_free:
             out = []
             for w in sp[0]:  # [parts][waves][4]: round 0's slot holds the launch
                 w = w[w[:, 1] > 0]
@@ -488,10 +559,10 @@ class Trainer:
         self._prepare_acting()
         for s in self.streams[1:]:  # fork: the side streams start after everything queued so far
             s.wait_stream(cur)
-        if self.fused_rollout:
+        if self.fused_rollout or self.fused_rollout_free:
             for k in range(len(self.env.parts)):
                 self._act_part(0, k)
-                self._rollout_part(k)
+                (self._rollout_part_free if self.fused_rollout_free else self._rollout_part)(k)
         else:
             for t in range(self.T):
                 self.round(t)

@@ -88,3 +88,41 @@ def act_reference(flat: dict, obs: torch.Tensor, u: torch.Tensor):
     cdf = torch.cumsum(dist.probs, dim=-1)
     a = (u.unsqueeze(-1) >= cdf).sum(-1).clamp(max=probs.shape[-1] - 1)
     return a, dist.log_prob(a), dist.probs
+
+
+def grad_abs_bound(policy: RefActorCritic, states, actions, old_logprobs, rewards_norm, eps_clip: float):
+    """The per-element scale a summed gradient's rounding error is measured against: for every Linear layer
+    y = x W^T + b of the actor and the critic, sum over rows of |dL/dy_r| (x) |x_r| (weights) and of |dL/dy_r|
+    (biases), in the precision of `policy` (use float64). The gradient of PPOmodules.py:144-168's mean loss is
+    sum_r dL/dy_r (x) x_r: when its rows cancel, the sum is far smaller than these terms, and an f32 sum's error
+    is a fraction of the terms (~ log2(rows) * 2^-24 for a blocked sum), not of the sum. TEST INFRASTRUCTURE."""
+    seen = {}
+
+    def hook(name):
+        def f(mod, inp, out):
+            out.retain_grad()
+            seen[name] = (inp[0].detach(), out)
+        return f
+
+    layers = dict(w1=policy.actor[0], w2=policy.actor[2], w3=policy.actor[4], cw1=policy.critic[0],
+                  cw2=policy.critic[2], cw3=policy.critic[4])
+    handles = [lin.register_forward_hook(hook(k)) for k, lin in layers.items()]
+    try:
+        logprobs, values, entropy = policy.evaluate(states, actions)
+        ratios = torch.exp(logprobs - old_logprobs.detach())
+        adv = rewards_norm - values.detach()
+        s1 = ratios * adv
+        s2 = torch.clamp(ratios, 1 - eps_clip, 1 + eps_clip) * adv
+        loss = -torch.min(s1, s2) + 0.5 * nn.MSELoss()(values, rewards_norm) - 0.01 * entropy
+        policy.zero_grad()
+        loss.mean().backward()
+    finally:
+        for h in handles:
+            h.remove()
+    out = {}
+    for k, (x, y) in seen.items():
+        d = y.grad.detach().abs()
+        out[k] = d.T @ x.abs()
+        out[k.replace("w", "b")] = d.sum(0)
+    policy.zero_grad()
+    return out

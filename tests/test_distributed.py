@@ -166,14 +166,14 @@ def _union_rank(rank, world, port, out_dir, name):
             for k, v in u.group.policy.named_parameters():
                 out["it%d.w.%s.%s" % (it, u.name, k)] = v.detach().cpu().clone()
     out["flags"] = torch.tensor(t.flags())
-    out["fused"] = torch.tensor(int(t.fused_rollout))
+    out["fused"] = torch.tensor(int(t.fused_rollout or t.fused_rollout_free))
     torch.save(out, os.path.join(out_dir, "union_w%d_r%d.pt" % (world, rank)))
     if world > 1:
         dist.destroy_process_group()
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("name", ["cfg3", "cfg2"])
+@pytest.mark.parametrize("name", ["cfg3", "cfg2", "cfg4"])
 def test_two_rank_shards_equal_one_rank_on_the_union(tmp_path, name):
     """§8(e): 2 ranks x E/2 replicas == 1 rank x E replicas (SchedulingEnvironment.py:314-329, PPOmodules.py:548-597
     shared nets, gradient all-reduce mean). Replica e's env seed and Philox rows are functions of its
@@ -182,14 +182,15 @@ def test_two_rank_shards_equal_one_rank_on_the_union(tmp_path, name):
     and the weights after each iteration agree within 1e-5 (the all-reduce sums the two halves' f32
     gradients in another order than one rank's reduction). Iteration 2 acts on those weights: its
     actions, observations and rewards are compared bit for bit (a sampled action would flip only if a
-    uniform lay within ~1e-7 of a CDF boundary), its log-probs within 1e-5. cfg2 runs the one-launch
-    rollout (ms_env_rollout_act), whose fused acting draws from each shard's global Philox rows."""
+    uniform lay within ~1e-7 of a CDF boundary), its log-probs within 1e-5. cfg2 and cfg3 run the one-launch
+    rollouts (ms_env_rollout_act / ms_env_rollout_act_free), whose fused acting draws from each shard's global
+    Philox rows; cfg4 (divided: 256 acceptor nets, K = 3) has the largest all-reduce message (~5.3 MB)."""
     mp.spawn(_union_rank, args=(2, _free_port(), str(tmp_path), name), nprocs=2, join=True)
     mp.spawn(_union_rank, args=(1, 0, str(tmp_path), name), nprocs=1, join=True)
     one = torch.load(tmp_path / "union_w1_r0.pt", weights_only=True)
     two = [torch.load(tmp_path / ("union_w2_r%d.pt" % r), weights_only=True) for r in range(2)]
     assert int(one.pop("flags")) == 0 and all(int(x.pop("flags")) == 0 for x in two)
-    assert all(int(x.pop("fused")) == (name == "cfg2") for x in [one] + two)
+    assert all(int(x.pop("fused")) == (name in ("cfg2", "cfg3")) for x in [one] + two)
     h = _UNION["E"] // 2
     hp = importlib.import_module("marl-scheduling_amd.trainer").Hyper()
     bad = []

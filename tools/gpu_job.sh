@@ -16,6 +16,10 @@
 #   ab:<variant>:<n>[:<args>]  n alternating cfg3 bench lines of tools/_variants/<variant> and the
 #                       in-tree library (same box)                   -> ab_<variant>_{base,new}<i>.json
 #   waves:<off>:<acc>   cfg3 bench line with the paired act's wave split -> waves_<off>_<acc>.json
+#   envab:<VAR=v[+VAR=v]>:<n>[:<args>]  n alternating bench lines with those environment variables and without
+#                       (same box; args after ':', ',' for spaces)  -> envab_<i>_{with,without}.json
+#                       (the one-off A/B jobs of rounds 4-5, e.g. MS_UPDATE_STREAMS=1 at cfg4:
+#                        envab:MS_UPDATE_STREAMS=1:2:--config,cfg4,--steps,3,--no-cpu-baseline)
 # Example: bash tools/gpu_job.sh r5b gputest smoke bench cfgs profile
 set -uo pipefail
 TAG="$1"; shift
@@ -67,6 +71,13 @@ for step in "$@"; do
     waves)
       MS_ACT_PAIR_WAVES="$a1" MS_ACT_PAIR_COMMON_WAVES="$a2" timeout -k 10 300 python bench.py --no-cpu-baseline \
         --no-step-kernel --steps 6 > "$O/waves_${a1}_${a2}.json" 2> "$O/waves_${a1}_${a2}.err" || fail "$step" $? ;;
+    envab)
+      for i in $(seq 1 "${a2:-2}"); do
+        env ${a1//+/ } timeout -k 10 300 python bench.py ${a3//,/ } > "$O/envab_${i}_with.json" 2> "$O/envab_${i}_with.err" \
+          || fail "$step with $i" $?
+        timeout -k 10 300 python bench.py ${a3//,/ } > "$O/envab_${i}_without.json" 2> "$O/envab_${i}_without.err" \
+          || fail "$step without $i" $?
+      done ;;
     *)
       fail "$step (unknown step)" 2 ;;
   esac
