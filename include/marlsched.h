@@ -461,6 +461,10 @@ typedef struct ms_fused_act_free {
     int8_t* env_price;            /* [E][N*L] the next round's offer_price actions (one buffer for every round) */
     int8_t* acc_action;           /* [E][N*C] */
     float* acc_logprob;           /* [E][N*C] */
+    /* nonzero: leave the acceptor items of cores their agent does not own (the common row's, sampled from its
+     * table; the env reads only the owner's acceptor action, world.py:391-404) to ms_env_rollout_fill_common,
+     * which the caller runs later, e.g. on another stream beside other work; 0: the call runs it itself */
+    int32_t defer_common;
 } ms_fused_act_free;
 
 /* Per-round byte strides of ms_env_rollout_act_free (as ms_round_strides, plus the price chooser's arrays). */
@@ -484,6 +488,14 @@ typedef struct ms_round_strides_free {
 int ms_env_rollout_act_free(ms_env* env, const ms_actions* act, const ms_obs_out* obs, const ms_reward_out* rew,
                             const ms_event_out* ev, const ms_fused_act_free* next, const ms_round_strides_free* strides,
                             int32_t n_rounds, int32_t act_after_last, void* stream);
+
+/* The acceptor outputs of ms_env_rollout_act_free(..., next->defer_common = 1, ...) that the launch left: every
+ * acting round's items (e, a, c) with core_owner[e][c] != a + 1, with the same obs, next and strides as that call
+ * and next->offset_dev holding the value it held then (the Philox offsets of those rounds). On any stream ordered
+ * after the rollout launch and before the outputs are read. */
+int ms_env_rollout_fill_common(const ms_env* env, const ms_obs_out* obs, const ms_fused_act_free* next,
+                               const ms_round_strides_free* strides, int32_t n_rounds, int32_t act_after_last,
+                               void* stream);
 
 /* 1 when ms_env_rollout_act_free can run this env's rounds (free prices, N <= 8, max(N, C) <= 16, offer rows
  * <= 32 bytes with <= 16 core actions, acceptor rows of 33..64 bytes with 17..32 actions), else 0. */

@@ -61,6 +61,8 @@ def _load():
                                                ct.POINTER(abi.MsFusedActFree), ct.POINTER(abi.MsRoundStridesFree), i32,
                                                i32, P]),
         "ms_env_rollout_act_free_supported": (ct.c_int, [P]),
+        "ms_env_rollout_fill_common": (ct.c_int, [P, ct.POINTER(abi.MsObsOut), ct.POINTER(abi.MsFusedActFree),
+                                                  ct.POINTER(abi.MsRoundStridesFree), i32, i32, P]),
         "ms_env_round": (i64, [P]),
         "ms_env_flags": (ct.c_int, [P, ct.POINTER(u32), P]),
         "ms_env_randbelow": (ct.c_int, [P, i64, u32, ct.POINTER(u32), P]),
@@ -154,7 +156,7 @@ def has(name: str) -> bool:
 EXPORTED = (
     "ms_last_error", "ms_abi_version", "ms_config_shape", "ms_env_create", "ms_env_destroy", "ms_env_shape",
     "ms_env_reset", "ms_env_step", "ms_env_step_act", "ms_env_step_act_supported", "ms_env_rollout_act",
-    "ms_env_rollout_act_free", "ms_env_rollout_act_free_supported", "ms_env_round", "ms_env_flags", "ms_env_randbelow", "ms_env_auctioneer",
+    "ms_env_rollout_act_free", "ms_env_rollout_act_free_supported", "ms_env_rollout_fill_common", "ms_env_round", "ms_env_flags", "ms_env_randbelow", "ms_env_auctioneer",
     "ms_env_get_rng", "ms_env_set_rng", "ms_env_export",
     "ms_env_import", "ms_policy_act", "ms_policy_act_common", "ms_policy_act_compact",
     "ms_act_round_free", "ms_price_table_build", "ms_act_frag_bytes", "ms_act_prepare", "ms_offer_act_free", "ms_discounted_returns", "ms_unit_returns",

@@ -217,7 +217,7 @@ class MsFusedActFree(ct.Structure):  # ms_fused_act_free (ABI 17)
                 ("common_row", ct.c_void_p), ("price_table", ct.c_void_p), ("seed", ct.c_uint64),
                 ("off_offset", ct.c_uint64), ("acc_offset", ct.c_uint64), ("offset_dev", ct.c_void_p)] + [
         (n, ct.c_void_p) for n in ("core_action", "core_logprob", "price_state", "price_action", "price_logprob",
-                                   "env_price", "acc_action", "acc_logprob")]
+                                   "env_price", "acc_action", "acc_logprob")] + [("defer_common", ct.c_int32)]
 
 
 class MsRoundStridesFree(ct.Structure):  # ms_round_strides_free (ABI 17): bytes per round

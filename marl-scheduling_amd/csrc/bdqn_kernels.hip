@@ -240,6 +240,8 @@ __global__ void __launch_bounds__(256) k_bdqn_l1_gather(BdqnL1Compact p) {
 //      does not. Entry 0 is the common row itself (-1).
 __global__ void __launch_bounds__(256) k_bdqn_own_mask(BdqnAct p, unsigned long long* mask) {
     const long long e = (long long)blockIdx.x * 256 + threadIdx.x;
+    // k_bdqn_own_list's counter starts at zero (here, not a hipMemsetAsync: see k_key_clear)
+    if (e == 0) *const_cast<int32_t*>(p.n_owning) = 0;
     if (e >= p.rows / p.N) return;
     const int8_t* own = p.core_owner + (size_t)e * p.C;
     unsigned long long m = 0;
@@ -721,8 +723,7 @@ hipError_t launch_bdqn_act(const BdqnAct& p, hipStream_t st) {
     const unsigned blocks = (unsigned)((p.rows + (p.list ? 1 : 0) + rpb - 1) / rpb);
     if (p.list) {
         if (p.N > 64) return hipErrorInvalidValue;
-        hipError_t e = hipMemsetAsync(const_cast<int32_t*>(p.n_owning), 0, sizeof(int32_t), st);
-        if (e != hipSuccess) return e;
+        hipError_t e;
         const long long E = p.rows / p.N;
         hipLaunchKernelGGL(k_bdqn_own_mask, dim3((unsigned)((E + 255) / 256)), dim3(256), 0, st, p, p.own_mask);
         if ((e = hipGetLastError()) != hipSuccess) return e;

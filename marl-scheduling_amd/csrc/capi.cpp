@@ -33,6 +33,8 @@ hipError_t launch_env_rollout_act(const Params&, int64_t, uint8_t*, uint32_t*, L
 hipError_t launch_env_rollout_act_free(const Params&, int64_t, uint8_t*, uint32_t*, Liab*, const StepIO&,
                                        const FusedActFree&, const RoundStrideFree&, int, int, hipStream_t);
 bool env_rollout_free_supported(const Params&);
+hipError_t launch_env_fill_common(const Params&, int64_t, const StepIO&, const FusedActFree&, const RoundStrideFree&,
+                                  int, int, hipStream_t);
 hipError_t launch_env_randbelow(const Params&, uint8_t*, uint32_t*, int64_t, uint32_t, uint32_t*, hipStream_t);
 hipError_t launch_env_auctioneer(const Params&, int64_t, uint8_t*, uint32_t*, int8_t*, hipStream_t);
 hipError_t launch_policy_act(const ms_mlp_params*, const int8_t*, int, int64_t, int, int, const int8_t*, uint64_t,
@@ -386,6 +388,20 @@ static int fill_io(ms_env* env, const ms_actions* act, const ms_obs_out* obs, co
     return MS_OK;
 }
 
+static ms::FusedActFree free_act_args(const ms_fused_act_free& n) {
+    const ms_price_table* pt = n.price_table;
+    return ms::FusedActFree{n.core_chooser, n.price_chooser, n.acceptor, n.common_row,
+                            pt ? pt->table : nullptr, pt ? pt->digit : nullptr, pt ? pt->n_keys : 0, n.seed,
+                            n.off_offset, n.acc_offset, n.offset_dev, n.core_action, n.core_logprob, n.price_state,
+                            n.price_action, n.price_logprob, n.env_price, n.acc_action, n.acc_logprob};
+}
+static ms::RoundStrideFree free_strides(const ms_round_strides_free& r) {
+    return ms::RoundStrideFree{r.acceptor_action, r.offer_action, r.core_rows, r.core_owner, r.offer_obs,
+                               r.offer_reward, r.price_reward, r.acceptor_reward, r.agent_reward, r.auctioneer_reward,
+                               r.next_core_action, r.next_core_logprob, r.next_price_state, r.next_price_action,
+                               r.next_price_logprob, r.next_acc_action, r.next_acc_logprob, r.offset_step};
+}
+
 int ms_env_rollout_act_free_supported(const ms_env* env) {
     return env && env->cfg.free_prices && ms::env_rollout_free_supported(env->P) ? 1 : 0;
 }
@@ -424,25 +440,39 @@ int ms_env_rollout_act_free(ms_env* env, const ms_actions* act, const ms_obs_out
     if (!next->common_row || !next->core_action || !next->core_logprob || !next->price_state || !next->price_action ||
         !next->price_logprob || !next->env_price || !next->acc_action || !next->acc_logprob)
         return bad("NULL output / common row");
-    if (env->E * N * L >= (1LL << 24) || env->E * N * C * 4 > 0x7fffffffLL || env->E * N * L * 4 > 0x7fffffffLL)
+    if (env->E * N * L >= (1LL << 24) || env->E * N * C * 4 > 0x7fffffffLL || env->E * N * L * 4 > 0x7fffffffLL ||
+        env->E * (int64_t)(N * C) * (N * C) >= (1LL << 32))
         return bad("too many replicas for 32-bit row offsets");
     if (__atomic_load_n(env->err_host, __ATOMIC_ACQUIRE))
         return fail(MS_EOVERFLOW, "an earlier round raised a per-env error flag (see ms_env_flags)");
     ms::StepIO io{};
     rc = fill_io(env, act, obs, rew, ev, &io);
     if (rc != MS_OK) return rc;
-    const ms::FusedActFree fa{c, p, a, next->common_row, pt->table, pt->digit, pt->n_keys, next->seed,
-                              next->off_offset, next->acc_offset, next->offset_dev, next->core_action,
-                              next->core_logprob, next->price_state, next->price_action, next->price_logprob,
-                              next->env_price, next->acc_action, next->acc_logprob};
-    const ms_round_strides_free& r = *strides;
-    const ms::RoundStrideFree st{r.acceptor_action, r.offer_action, r.core_rows, r.core_owner, r.offer_obs,
-                                 r.offer_reward, r.price_reward, r.acceptor_reward, r.agent_reward, r.auctioneer_reward,
-                                 r.next_core_action, r.next_core_logprob, r.next_price_state, r.next_price_action,
-                                 r.next_price_logprob, r.next_acc_action, r.next_acc_logprob, r.offset_step};
+    const ms::FusedActFree fa = free_act_args(*next);
+    const ms::RoundStrideFree st = free_strides(*strides);
     HIP_TRY(ms::launch_env_rollout_act_free(P, env->E, env->recs, env->mt, env->liab, io, fa, st, n_rounds,
                                             act_after_last ? 1 : 0, (hipStream_t)stream));
+    if (!next->defer_common)
+        HIP_TRY(ms::launch_env_fill_common(P, env->E, io, fa, st, n_rounds, act_after_last ? 1 : 0, (hipStream_t)stream));
     env->round += n_rounds;
+    return MS_OK;
+}
+
+int ms_env_rollout_fill_common(const ms_env* env, const ms_obs_out* obs, const ms_fused_act_free* next,
+                               const ms_round_strides_free* strides, int32_t n_rounds, int32_t act_after_last,
+                               void* stream) {
+    if (!env || !obs || !next || !strides) return fail(MS_EINVAL, "env/obs/next/strides is NULL");
+    auto bad = [&](const char* why) { return fail(MS_EINVAL, "ms_env_rollout_fill_common: %s", why); };
+    if (!ms_env_rollout_act_free_supported(env)) return bad("not an env ms_env_rollout_act_free runs");
+    if (n_rounds < 1) return bad("n_rounds < 1");
+    if (!obs->core_owner || !next->acceptor.act_frag || !next->acc_action || !next->acc_logprob)
+        return bad("needs the owners, the acceptor's act fragments and its outputs");
+    if (next->acceptor.n_groups != env->P.N || next->acceptor.n_actions != env->P.O + 1)
+        return bad("acceptor net shape does not match the env");
+    ms::StepIO io{};
+    io.obs_cown = obs->core_owner;
+    HIP_TRY(ms::launch_env_fill_common(env->P, env->E, io, free_act_args(*next), free_strides(*strides), n_rounds,
+                                       act_after_last ? 1 : 0, (hipStream_t)stream));
     return MS_OK;
 }
 

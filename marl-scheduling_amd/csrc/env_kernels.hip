@@ -1944,6 +1944,10 @@ __device__ __forceinline__ uint32_t pick4u(const uint32_t (&v)[4], int k) {
     return k == 0 ? v[0] : (k == 1 ? v[1] : (k == 2 ? v[2] : v[3]));
 }
 
+// The acceptors of cores the agent does not own are left to k_acc_common_fill (after the launch, or later on
+// another stream): the env reads only the owner's acceptor action (world.py:391-404), so their sampling is off the
+// round's chain. (Sampling them here as well, k_act_common's table search per item: 50.2 us per round against
+// 47.4, profiles/r7g.)
 template <class SH>
 __device__ __forceinline__ void act_free(const Geom& g, int64_t E, const FusedActFree& fa, int64_t e0, int a, int lane,
                                          uint8_t* lds, const FreeLds& fl) {
@@ -2124,9 +2128,6 @@ __device__ __forceinline__ void act_free(const Geom& g, int64_t E, const FusedAc
     {
         using FL = FragLayout<2, 2>;
         const uint32_t* const fg = frag_groups<2, 2>(fa.acc, true);
-        const float* tab = reinterpret_cast<const float*>(lds + fl.tab) + a * kFreeTabDw;  // Head<2>::table
-        const float S = tab[64];
-        const int last_nz = __float_as_int(tab[65]);
         int16_t* lm = reinterpret_cast<int16_t*>(lds + fl.list + a * kFreeListCap * 6);
         float* lu = reinterpret_cast<float*>(lds + fl.list + a * kFreeListCap * 6 + 2 * kFreeListCap);
         const int nw = g.acc_stride >> 2, Aa = fa.acc.n_actions;
@@ -2195,7 +2196,10 @@ __device__ __forceinline__ void act_free(const Geom& g, int64_t E, const FusedAc
             const int k = in ? m / C : 0, c = in ? m - (m / C) * C : 0;
             const bool valid = in && e0 + k < E;
             const uint32_t i = i_base + (uint32_t)m, ib = i & ~64u;
-            const bool need = ib != last_ib;
+            const int own = reinterpret_cast<const int8_t*>(slice(k) + g.s_rec + g.o_core_owner)[c];
+            const bool owned = valid && own == a + 1;
+            // (only the owned items' uniforms: the common ones are sampled after the launch)
+            const bool need = owned && ib != last_ib;
             if (__ballot(need)) {
                 const uint32_t eb = ib / (uint32_t)C;
                 uint32_t r0, r1;
@@ -2207,19 +2211,6 @@ __device__ __forceinline__ void act_free(const Geom& g, int64_t E, const FusedAc
                 }
             }
             const float u = u24((i & 64u) ? wd1 : wd0);
-            const int own = reinterpret_cast<const int8_t*>(slice(k) + g.s_rec + g.o_core_owner)[c];
-            const bool owned = valid && own == a + 1;
-            if (valid && !owned) {
-                const float target = u * S;
-                int cnt = 0;
-#pragma unroll
-                for (int step = 32; step >= 1; step >>= 1)
-                    if (cnt + step <= 32 && tab[cnt + step - 1] <= target) cnt += step;
-                const int act = cnt >= Aa ? last_nz : cnt;
-                const uint32_t row = (uint32_t)((e0 + k) * Ua) + (uint32_t)(a * C + c);
-                aa_b.st8(row, act);
-                al_b.stf(4 * row, tab[32 + act]);
-            }
             const uint64_t mo = __ballot(owned);
             if (owned) {
                 const int p = n_list + __popcll(mo & below);
@@ -2250,6 +2241,73 @@ __device__ __forceinline__ void act_free(const Geom& g, int64_t E, const FusedAc
     }
 }
 
+// The acceptor items the one-launch rollout leaves (ms_env_rollout_act_free; k_env_rollout_act_free acts with
+// act_free<SH, false>): for every acting round t and every (replica e, agent a, core c) whose core a does not own,
+// k_act_common's sample from agent a's common-row table (Head::table, ms_act_prepare) with the item's uniform,
+// word (i >> 6) & 1 of the draw countered by the row of item i & ~64 (i = e * C + c): the outputs
+// ms_act_round_free writes for those items, bit for bit. One thread per item, lanes along the [E][N*C] rows
+// (coalesced byte / f32 stores), rounds on blockIdx.y; the N tables in LDS once per block.
+struct CommonFillArgs {
+    const int8_t* owner;     // round 0's owners [E][C] (the observation the acting of ring slot 1 read)
+    int8_t* action;          // round 0's outputs [E][N*C]
+    float* logprob;
+    int64_t owner_stride, action_stride, logprob_stride;  // bytes per round
+    const uint32_t* frag;    // the acceptor net's act fragment groups (frag_groups<2, 2>)
+    int E, N, C, A;
+    uint32_t row_base;
+    uint64_t seed, offset, offset_step;
+    const uint64_t* offset_dev;
+};
+constexpr int kFillPer = 8;  // items per thread of k_acc_common_fill: their owner loads in flight together
+__global__ void __launch_bounds__(256) k_acc_common_fill(CommonFillArgs p) {
+    __shared__ float tabs[8 * kFreeTabDw];
+    using FL = FragLayout<2, 2>;
+    const int t = blockIdx.y;
+    for (int k = threadIdx.x; k < p.N * kFreeTabDw; k += blockDim.x) {
+        const int a = k / kFreeTabDw;
+        tabs[k] = __uint_as_float(p.frag[(size_t)a * FL::GB + 64 * FL::LW + (k - a * kFreeTabDw)]);
+    }
+    const int C = p.C, U = p.N * C;
+    const int64_t n = (int64_t)p.E * U;
+    const uint32_t mag_u = magic_div((uint32_t)U), mag_c = magic_div((uint32_t)C);
+    const RawBuf own_b(advance(p.owner, t * p.owner_stride), (int64_t)p.E * C);
+    const RawBuf act_b(advance(p.action, t * p.action_stride), n), lp_b(advance(p.logprob, t * p.logprob_stride), 4 * n);
+    const uint64_t off = p.offset + (uint64_t)t * p.offset_step + (p.offset_dev ? *p.offset_dev : 0ull);
+    // item r = e * U + a * C + c (the [E][N*C] output row): block b takes kFillPer * 256 consecutive items
+    const uint32_t r0 = (uint32_t)blockIdx.x * (kFillPer * 256) + threadIdx.x;
+    int own[kFillPer];
+#pragma unroll
+    for (int k = 0; k < kFillPer; k++) {
+        const uint32_t r = r0 + 256 * k;
+        const uint32_t e = U == 1 ? r : __umulhi(r, mag_u);
+        const int u = (int)(r - e * (uint32_t)U);
+        const int c = u - small_div(u, C) * C;
+        own[k] = own_b.ld8s(e * (uint32_t)C + (uint32_t)c);  // (past the end: 0, the item is skipped below)
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < kFillPer; k++) {
+        const uint32_t r = r0 + 256 * k;
+        const uint32_t e = U == 1 ? r : __umulhi(r, mag_u);
+        const int u = (int)(r - e * (uint32_t)U);
+        const int a = small_div(u, C), c = u - a * C;
+        if ((int64_t)r >= n || own[k] == a + 1) continue;  // the owner's row: acted in the rollout launch
+        const uint32_t i = e * (uint32_t)C + (uint32_t)c, ib = i & ~64u;
+        const uint32_t eb = C == 1 ? ib : __umulhi(ib, mag_c);
+        uint32_t w0, w1;
+        philox2(eb * (uint32_t)U + (uint32_t)(a * C) + (ib - eb * (uint32_t)C) + p.row_base, off, p.seed, w0, w1);
+        const float* tab = tabs + a * kFreeTabDw;
+        const float target = u24((i & 64u) ? w1 : w0) * tab[64];
+        int cnt = 0;
+#pragma unroll
+        for (int step = 32; step >= 1; step >>= 1)
+            if (cnt + step <= 32 && tab[cnt + step - 1] <= target) cnt += step;
+        const int act = cnt >= p.A ? __float_as_int(tab[65]) : cnt;
+        act_b.st8(r, act);
+        lp_b.stf(4 * r, tab[32 + act]);
+    }
+}
+
 struct RolloutFreeArgs {
     Params P;
     int64_t E;
@@ -2260,6 +2318,7 @@ struct RolloutFreeArgs {
     FusedActFree fa;
     RoundStrideFree st;
     int n_rounds, act_last;
+    int prio;  // bit 0: the workgroup's waves 4.. at raised issue priority while acting, bit 1: during the env round
 };
 // The locally shared free-price rollout in one launch: workgroup b holds replicas kFreeEPW * N * b .. in its LDS,
 // and wave w steps kFreeEPW of them (k_env_step's round, 16 lanes per replica) and then acts for agent w of all
@@ -2287,26 +2346,11 @@ __global__ void __launch_bounds__(512, 4) k_env_rollout_act_free(RolloutFreeArgs
         span[4 * wslot + 2] = __builtin_amdgcn_s_memtime();
     }
     // once per launch (the acting nets do not change within a rollout): the price table's key digits, one copy
-    // per workgroup, and each agent's common-row sampling table (ms_act_prepare's, else computed here)
+    // per workgroup
     {
         uint32_t* pd = reinterpret_cast<uint32_t*>(smem_free + fl.pdig);
         const uint32_t* src = reinterpret_cast<const uint32_t*>(A0.fa.pdigit);
         for (int k = (int)threadIdx.x; k < 512; k += (int)blockDim.x) pd[k] = src[k];
-        float* tab = reinterpret_cast<float*>(smem_free + fl.tab) + wave * kFreeTabDw;
-        if (const uint32_t* fg = frag_groups<2, 2>(A0.fa.acc, true)) {
-            using FL = FragLayout<2, 2>;
-            const uint32_t* tb = fg + (size_t)wave * FL::GB + 64 * FL::LW;
-            for (int k = lane0; k < kFreeTabDw; k += 64) reinterpret_cast<uint32_t*>(tab)[k] = tb[k];
-        } else {
-            const int j = lane0 & 15, g4 = lane0 >> 4;
-            W1Split<2> w1;
-            Head<2> h1;
-            w1.load(A0.fa.acc.w1 + (size_t)wave * 16 * A0.fa.acc.in_dim, A0.fa.acc.in_dim, j, g4);
-            h1.load(A0.fa.acc, wave, j, g4);
-            uint32_t* tmpl = reinterpret_cast<uint32_t*>(smem_free + fl.list + wave * kFreeListCap * 6);
-            int* lnz = reinterpret_cast<int*>(tab + 65);
-            common_table<2, 2>(w1, h1, A0.fa.common, g.acc_stride >> 2, tmpl, tab, tab + 32, tab + 64, lnz, lane0);
-        }
     }
     __syncthreads();
 #ifdef MS_PHASE_TIMING
@@ -2345,8 +2389,13 @@ __global__ void __launch_bounds__(512, 4) k_env_rollout_act_free(RolloutFreeArgs
         io.rew_agent = advance(io.rew_agent, t * st.rew_agent);
         io.rew_auct = advance(io.rew_auct, t * st.rew_auct);
         FREE_MARK(-1);
+        // (the younger half of the workgroup's waves otherwise trails the older at every barrier: issue goes by
+        //  priority, then age)
+        const bool up = wave >= 4 && (A.prio & 2);
+        if (up) __builtin_amdgcn_s_setprio(1);
         env_round<kWave / kFreeEPW, false, true, SH>(A.P, A.E, A.recs, A.mt, A.liab, io, wslot, lane,
                                                      smem_free + wave * kFreeEPW * g.s_total);
+        if (up) __builtin_amdgcn_s_setprio(0);
         FREE_MARK(0);
         if (t + 1 < n_rounds || A.act_last) {
             __syncthreads();  // every replica's observation sources are in the LDS
@@ -2361,7 +2410,10 @@ __global__ void __launch_bounds__(512, 4) k_env_rollout_act_free(RolloutFreeArgs
             fa.acc_logprob = advance(fa.acc_logprob, t * st.acc_logprob);
             fa.off_offset += (uint64_t)t * st.offset_step;
             fa.acc_offset += (uint64_t)t * st.offset_step;
+            const bool up_act = wave >= 4 && (A.prio & 1);
+            if (up_act) __builtin_amdgcn_s_setprio(1);
             act_free<SH>(g, A.E, fa, (int64_t)blockIdx.x * kFreeEPW * g.N, wave, lane, smem_free, fl);
+            if (up_act) __builtin_amdgcn_s_setprio(0);
             FREE_MARK(2);
             __syncthreads();  // the actions are stored and the LDS is free for the next round
             FREE_MARK(3);
@@ -2637,9 +2689,28 @@ static hipError_t launch_rollout_free_sh(const Params& P, int64_t E, uint8_t* re
                                          int n_rounds, int act_last, hipStream_t s) {
     const int64_t epb = (int64_t)kFreeEPW * P.N;
     const int64_t blocks = (E + epb - 1) / epb;
-    const RolloutFreeArgs A{P, E, recs, mt, liab, io, fa, st, n_rounds, act_last};
+    static const int prio = [] {
+        const char* v = getenv("MS_FREE_PRIO");  // (measurement knob, tools/gpu_job.sh envab)
+        return v ? atoi(v) : 1;  // measured: 1 (acting) 49.6 -> 49.0 us per round, 3 (and env) 49.1 (profiles/r7c)
+    }();
+    const RolloutFreeArgs A{P, E, recs, mt, liab, io, fa, st, n_rounds, act_last, prio};
     hipLaunchKernelGGL((k_env_rollout_act_free<SH>), dim3((unsigned)blocks), dim3(64 * P.N), (size_t)free_lds(P).total, s,
                        A);
+    return hipGetLastError();
+}
+// the acceptor items of cores their agent does not own, every acting round of a k_env_rollout_act_free launch
+// with the same arguments (its outputs' other items are untouched)
+hipError_t launch_env_fill_common(const Params& P, int64_t E, const StepIO& io, const FusedActFree& fa,
+                                  const RoundStrideFree& st, int n_rounds, int act_last, hipStream_t s) {
+    const int n_acts = act_last ? n_rounds : n_rounds - 1;
+    if (!env_rollout_free_supported(P) || io.obs_cown == nullptr || fa.acc.act_frag == nullptr) return hipErrorInvalidValue;
+    if (n_acts < 1) return hipSuccess;
+    const CommonFillArgs c{io.obs_cown, fa.acc_action, fa.acc_logprob, st.obs_cown, st.acc_action, st.acc_logprob,
+                           static_cast<const uint32_t*>(fa.acc.act_frag) + 4, (int)E, P.N, P.C, fa.acc.n_actions,
+                           (uint32_t)fa.acc.row_base, fa.seed, fa.acc_offset, st.offset_step, fa.offset_dev};
+    const int64_t items = E * P.N * P.C;
+    const unsigned bx = (unsigned)((items + kFillPer * 256 - 1) / (kFillPer * 256));
+    hipLaunchKernelGGL(k_acc_common_fill, dim3(bx, (unsigned)n_acts), dim3(256), 0, s, c);
     return hipGetLastError();
 }
 hipError_t launch_env_rollout_act_free(const Params& P, int64_t E, uint8_t* recs, uint32_t* mt, Liab* liab,

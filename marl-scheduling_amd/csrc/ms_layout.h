@@ -213,18 +213,17 @@ struct RoundStrideFree {
 
 // The workgroup LDS of k_env_rollout_act_free: the env slices of its kFreeEPW * N replicas (wave w steps
 // replicas kFreeEPW * w ..), then the act area: the price table's key digits (one copy per workgroup) and per
-// wave (= agent) its acceptor net's common-row sampling table and its list of owned-core rows.
+// wave (= agent) its list of owned-core acceptor rows.
 constexpr int kFreeEPW = 4;        // replicas per wave (16 lanes each)
 constexpr int kFreeListCap = 96;   // < 32 carried + one 64-item step
 constexpr int kFreeTabDw = 68;     // [32 running sums][32 log-probs][S][last nonzero][2 pad] (Head<2>::table)
 struct FreeLds {
-    int32_t pdig, tab, list, total;
+    int32_t pdig, list, total;
 };
 inline constexpr FreeLds free_lds(const Geom& g) {
     FreeLds f{};
     f.pdig = align16(kFreeEPW * g.N * g.s_total);
-    f.tab = f.pdig + 4 * 256 * 2;
-    f.list = f.tab + g.N * kFreeTabDw * 4;
+    f.list = f.pdig + 4 * 256 * 2;
     f.total = f.list + g.N * kFreeListCap * 6;  // int16 item + f32 uniform per entry
     return f;
 }

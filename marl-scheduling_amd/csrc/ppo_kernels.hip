@@ -1480,6 +1480,16 @@ __device__ __forceinline__ bool key_index(uint32_t w, int D, uint32_t& idx) {
     return ok;
 }
 
+// the keyed passes' marks and flags to zero. A kernel, not hipMemsetAsync: in a replayed HIP graph the
+// captured memset of the marks was not reliably complete before k_key_gather read them (marks left from
+// the previous replay added ranks of no rows, which changed the backward's tile sums in the last bits;
+// the update-streams test caught it, profiles/r7k)
+__global__ void __launch_bounds__(256) k_key_clear(uint4* mark, size_t n16, int32_t* flag, int G) {
+    const size_t i0 = (size_t)blockIdx.x * 256 + threadIdx.x, step = (size_t)gridDim.x * 256;
+    for (size_t i = i0; i < n16; i += step) mark[i] = make_uint4(0u, 0u, 0u, 0u);
+    for (size_t i = i0; i < (size_t)G; i += step) flag[i] = 0;
+}
+
 // one pass over the rows: every group's (dense index, action, old log-prob, return) to contiguous
 // per-group arrays (so the scan reads whole lines instead of one unit's bytes of [R][U] rows), and
 // every row's dense index marked (a load first: the frequent rows' marks are set early; every writer
@@ -1789,8 +1799,13 @@ static hipError_t launch_grad_t(const PpoArgs& a0, hipStream_t st) {
             // keyed rows: mark -> rank -> forward of the ranks -> row scan -> backward of the ranks,
             // then the tile path for the groups the keyed passes could not take
             hipError_t e;
-            if ((e = hipMemsetAsync(a.key_mark, 0, (size_t)a.G * kKeyDense, st)) != hipSuccess) return e;
-            if ((e = hipMemsetAsync(a.key_flag, 0, a.G * sizeof(int32_t), st)) != hipSuccess) return e;
+            {
+                const size_t n16 = (size_t)a.G * kKeyDense / 16;
+                const unsigned cb = (unsigned)std::min<size_t>((n16 + 255) / 256, 4096);
+                hipLaunchKernelGGL(k_key_clear, dim3(cb), dim3(256), 0, st, reinterpret_cast<uint4*>(a.key_mark), n16,
+                                   a.key_flag, a.G);
+                if ((e = hipGetLastError()) != hipSuccess) return e;
+            }
             const unsigned ib = (unsigned)std::min<long long>((a.R + 255) / 256, 16384);
             if (a.rus == 1 && a.rrs <= 64 && (a.rrs & 3) == 0 && a.ret_ld <= 64 && a.ret_ld >= a.G &&
                 !gather_per_row()) {

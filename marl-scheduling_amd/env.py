@@ -259,6 +259,14 @@ class BatchedEnv:
                                           ct.byref(ev) if ev else None, ct.byref(next_act), ct.byref(strides),
                                           int(n_rounds), int(bool(act_after_last)), stream_ptr(stream)))
 
+    def fill_common(self, obs, next_act, strides, n_rounds, act_after_last=False, stream=None):
+        """The acceptor items of cores their agent does not own that rollout_act_free(next_act.defer_common = 1)
+        left (ms_env_rollout_fill_common): the same obs / strides / next_act as that call, with next_act.offset_dev
+        holding the offsets it held then."""
+        o = abi.MsObsOut(None, None, None, None, ptr(obs.get("core_owner")))
+        check(lib.ms_env_rollout_fill_common(self._h, ct.byref(o), ct.byref(next_act), ct.byref(strides), int(n_rounds),
+                                             int(bool(act_after_last)), stream_ptr(stream)))
+
     def rollout_free_supported(self) -> bool:
         """Whether rollout_act_free can run this env's rounds (ms_env_rollout_act_free_supported)."""
         return has("ms_env_rollout_act_free_supported") and bool(lib.ms_env_rollout_act_free_supported(self._h))

@@ -271,10 +271,11 @@ class Trainer:
         self.metric_slots = -(-T // self.ep_len) + 1
         self.metric_bufs = [env.metrics_buffer(self.metric_slots) for env, _, _ in self.env.parts] if metrics else None
         self.episode_log = []
-        # one rank: each unit type's update on its own stream (MS_UPDATE_STREAMS=1). Measured: the
-        # update 10.06 -> 9.63 ms but the next rollout 14.50 -> 15.63 ms (every rollout launch
-        # slower after a multi-stream update graph), so it is off by default
-        self.update_streams = os.environ.get("MS_UPDATE_STREAMS", "0") == "1"
+        # one rank: each unit type's update on its own stream (MS_UPDATE_STREAMS=0: one stream). Round 4: the
+        # update 10.06 -> 9.63 ms but the next rollout 14.50 -> 15.63 ms (every rollout launch slower after a
+        # multi-stream update graph), so it was off. Round 6, with cfg3's rollout one launch: update 8.50 -> 8.05 ms,
+        # rollout 9.99 -> 10.11 ms, iteration 18.50 -> 18.18 ms (profiles/r7b), so it is on
+        self.update_streams = os.environ.get("MS_UPDATE_STREAMS", "1") == "1"
         # fixed-price rounds with one net per role (cfg2): round t's env launch also samples round t + 1's
         # actions from the observations it just built (ms_env_step_act), so a round is one launch
         # (MS_ENV_FUSED_ACT=0: the act launch and the env launch of every round, for A/B measurements)
@@ -293,6 +294,14 @@ class Trainer:
                                    self.off_frag is not None and not self.price_unit_major and self.T > 1 and
                                    self.metric_bufs is None and os.environ.get("MS_ENV_ROLLOUT_FREE", "1") != "0" and
                                    all(env.rollout_free_supported() for env, _, _ in self.env.parts))
+        # ... and its acceptor items of cores their agent does not own (sampled from the common row's table; the env
+        # reads only the owner's acceptor action) are left to a second kernel (ms_env_rollout_fill_common) that
+        # iteration() runs inside the update, on the acceptor's stream beside the offer and price gradients
+        # (MS_DEFER_COMMON=0: at the end of the rollout). Offsets from a snapshot of rng_ctr taken by the rollout.
+        self.defer_common = (self.fused_rollout_free and self.update_streams and self.world_size == 1 and self.fused and
+                             os.environ.get("MS_DEFER_COMMON", "1") != "0")
+        self.rng_snap = torch.zeros(1, dtype=torch.int64, device=self.device)
+        self._fill_args = []
         self.span_every = 0  # > 0: every span_every-th round's env launches record their span (bench)
         self.spans = None
         self.timings = dict(rollout=0.0, update=0.0)
@@ -509,8 +518,18 @@ class Trainer:
                                          b(self.price_obs), b(self.price.actions), b(self.price.logprobs),
                                          b(self.acc.actions), b(self.acc.logprobs), 8)
         nxt, out = self._fused_next_free(1, k)
+        nxt.defer_common = int(self.defer_common)
         env.rollout_act_free(sl(self.acc.actions[0]).view(E, N, C), sl(self.off.actions[0]).view(E, N, L), obs, rew,
                              nxt, out, strides, self.T, act_after_last=False, events=ev, stream=self.streams[k])
+        if self.defer_common:  # the fill's arguments: the same call with the offsets of this rollout (snapshot)
+            fill = abi.MsFusedActFree.from_buffer_copy(nxt)
+            fill.offset_dev = ptr(self.rng_snap)
+            self._fill_args.append((env, obs, fill, strides))
+
+    def fill_common(self, stream=None):
+        """The deferred acceptor items of the last one-launch rollout (defer_common; idempotent)."""
+        for env, obs, fill, strides in self._fill_args:
+            env.fill_common(obs, fill, strides, self.T, act_after_last=False, stream=stream)
 
     def record_launch_spans(self, every: int):
         """Every `every`-th round's env launches record their span (first wave start, last wave end
@@ -557,6 +576,9 @@ class Trainer:
         if self.span_every:
             self.spans.zero_()
         self._prepare_acting()
+        self._fill_args = []
+        if self.defer_common:
+            self.rng_snap.copy_(self.rng_ctr)
         for s in self.streams[1:]:  # fork: the side streams start after everything queued so far
             s.wait_stream(cur)
         if self.fused_rollout or self.fused_rollout_free:
@@ -570,9 +592,11 @@ class Trainer:
             cur.wait_stream(s)
         self.rng_ctr.add_(8 * self.T)
 
-    def rollout(self):
+    def rollout(self, defer_common: bool = False):
         """UPDATE_STEP rounds. With use_graph the first rollout runs eagerly and is then
-        captured once into a HIP graph (every pointer is static); later rollouts replay it."""
+        captured once into a HIP graph (every pointer is static); later rollouts replay it.
+        defer_common (iteration()): leave the deferred acceptor items (self.defer_common) to the update, which
+        samples them on the acceptor's stream; otherwise the rings are complete when this returns."""
         if not self.use_graph:
             self._rollout_body()
         elif self.graph is None:
@@ -584,6 +608,8 @@ class Trainer:
             self.graph = g
         else:
             self.graph.replay()
+        if self.defer_common and not defer_common:
+            self.fill_common()
         self.rounds_done += self.T
 
     # ---- update
@@ -799,6 +825,8 @@ class Trainer:
             st.wait_stream(cur)
         for u, st in zip(units, self._unit_streams):
             with torch.cuda.stream(st):
+                if u is self.acc and self.defer_common:
+                    self.fill_common(stream=st)  # the rollout's deferred acceptor items, beside the other units
                 ls = []
                 for ep in self._epochs(u, all_sel[u.name], counts[u.name]):
                     ls.append(ep())
@@ -839,7 +867,7 @@ class Trainer:
         """One PPO iteration; device time of rollout / update accumulates in self.timings (s)."""
         ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
         ev[0].record()
-        self.rollout()
+        self.rollout(defer_common=True)
         ev[1].record()
         losses = self.update()
         ev[2].record()

@@ -17,8 +17,10 @@ pytestmark = pytest.mark.gpu
 
 
 def _rings(t):
-    out = {"acc_rows": t.acc_rows, "acc_owner": t.acc_owner, "off_obs": t.off_obs, "price_obs": t.price_obs,
-           "env_price": t.env_price, "agent_reward": t.agent_reward, "auct_reward": t.auct_reward}
+    out = {"acc_rows": t.acc_rows, "acc_owner": t.acc_owner, "off_obs": t.off_obs, "env_price": t.env_price,
+           "agent_reward": t.agent_reward, "auct_reward": t.auct_reward}
+    if t.price_obs is not None:
+        out["price_obs"] = t.price_obs
     for u in t.units():
         for k in ("actions", "logprobs", "rewards"):
             out["%s.%s" % (u.name, k)] = getattr(u, k)
@@ -160,3 +162,31 @@ def test_one_round_rollouts(ms, name):
         t.iteration()
     torch.cuda.synchronize()
     assert t.flags() == 0 and t.rounds_done == 2
+
+
+@pytest.mark.parametrize("name,E", [("cfg3", 2048), ("cfg2", 1024), ("cfg4", 256)])
+def test_update_streams_equal_one_stream(ms, monkeypatch, name, E):
+    """One rank updates each unit type on its own stream by default (Trainer.update_streams; the unit types are
+    independent nets, PPOmodules.py:548-597): every loss and weight equals the one-stream update's bit for bit,
+    over three iterations (each acting on the previous update's weights), graph-replayed. cfg3's trainer with
+    streams also defers the rollout's common acceptor items into the update (defer_common): every ring equals the
+    one-stream trainer's after each iteration."""
+    tr_mod = importlib.import_module("marl-scheduling_amd.trainer")
+    ppo = importlib.import_module("marl-scheduling_amd.ppo")
+    mk = lambda: tr_mod.Trainer.from_named(name, n_envs=E, update_step=12, seed=6, device="cuda:0")
+    streams = mk()
+    monkeypatch.setenv("MS_UPDATE_STREAMS", "0")
+    one = mk()
+    assert streams.update_streams and not one.update_streams
+    assert streams.defer_common == (name == "cfg3") and not one.defer_common
+    for it in range(3):
+        l0, l1 = streams.iteration(), one.iteration()
+        torch.cuda.synchronize()
+        for k in l0:
+            assert torch.equal(l0[k], l1[k]), (it, k)
+        r0, r1 = _rings(streams), _rings(one)
+        for k in r0:
+            assert torch.equal(r0[k], r1[k]), (it, k)
+    for u0, u1 in zip(streams.units(), one.units()):
+        for k in ppo.ACTOR_KEYS + ppo.CRITIC_KEYS:
+            assert torch.equal(getattr(u0.group.policy, k), getattr(u1.group.policy, k)), (u0.name, k)

@@ -17,7 +17,7 @@
 #                       in-tree library (same box)                   -> ab_<variant>_{base,new}<i>.json
 #   waves:<off>:<acc>   cfg3 bench line with the paired act's wave split -> waves_<off>_<acc>.json
 #   envab:<VAR=v[+VAR=v]>:<n>[:<args>]  n alternating bench lines with those environment variables and without
-#                       (same box; args after ':', ',' for spaces)  -> envab_<i>_{with,without}.json
+#                       (same box; args after ':', ',' for spaces)  -> envab_<vars>_<i>_{with,without}.json
 #                       (the one-off A/B jobs of rounds 4-5, e.g. MS_UPDATE_STREAMS=1 at cfg4:
 #                        envab:MS_UPDATE_STREAMS=1:2:--config,cfg4,--steps,3,--no-cpu-baseline)
 # Example: bash tools/gpu_job.sh r5b gputest smoke bench cfgs profile
@@ -72,10 +72,11 @@ for step in "$@"; do
       MS_ACT_PAIR_WAVES="$a1" MS_ACT_PAIR_COMMON_WAVES="$a2" timeout -k 10 300 python bench.py --no-cpu-baseline \
         --no-step-kernel --steps 6 > "$O/waves_${a1}_${a2}.json" 2> "$O/waves_${a1}_${a2}.err" || fail "$step" $? ;;
     envab)
+      n="envab_${a1//[^A-Za-z0-9]/_}"
       for i in $(seq 1 "${a2:-2}"); do
-        env ${a1//+/ } timeout -k 10 300 python bench.py ${a3//,/ } > "$O/envab_${i}_with.json" 2> "$O/envab_${i}_with.err" \
+        env ${a1//+/ } timeout -k 10 300 python bench.py ${a3//,/ } > "$O/${n}_${i}_with.json" 2> "$O/${n}_${i}_with.err" \
           || fail "$step with $i" $?
-        timeout -k 10 300 python bench.py ${a3//,/ } > "$O/envab_${i}_without.json" 2> "$O/envab_${i}_without.err" \
+        timeout -k 10 300 python bench.py ${a3//,/ } > "$O/${n}_${i}_without.json" 2> "$O/${n}_${i}_without.err" \
           || fail "$step without $i" $?
       done ;;
     *)
