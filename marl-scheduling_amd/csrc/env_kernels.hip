@@ -2308,6 +2308,123 @@ __global__ void __launch_bounds__(256) k_acc_common_fill(CommonFillArgs p) {
     }
 }
 
+// k_acc_common_fill for C % 4 == 0 (the shipped shapes): a thread takes 4 consecutive items (one replica, one
+// agent, cores c0..c0+3) of kFillRounds rounds, so the items' index math and Philox rows are computed once, the
+// owners come as one dword per round (all rounds' loads in flight together), and a quad none of whose cores its
+// agent owns is stored as one dword of actions and one 16-byte vector of log-probs (the per-item kernel: a byte
+// and a dword store per item, and the tables loaded once per round per block). PAIR (64 % C == 0): items i and
+// i ^ 64 take the two words of one draw, and i ^ 64 is the same agent's core c of replica e ^ (64 / C), so the
+// thread also takes that replica's quad and each draw is computed once (the Philox rounds are the kernel's
+// largest VALU cost: 32-bit multiplies at quarter rate). Same values bit for bit.
+constexpr int kFillRounds = 8;
+template <bool PAIR>
+__global__ void __launch_bounds__(256) k_acc_common_fill4(CommonFillArgs p, int n_acts, int fill_merge) {
+    __shared__ float tabs[8 * kFreeTabDw];
+    using FL = FragLayout<2, 2>;
+    for (int k = threadIdx.x; k < p.N * kFreeTabDw; k += blockDim.x) {
+        const int a = k / kFreeTabDw;
+        tabs[k] = __uint_as_float(p.frag[(size_t)a * FL::GB + 64 * FL::LW + (k - a * kFreeTabDw)]);
+    }
+    __syncthreads();
+    const int C = p.C, U = p.N * C, QR = U >> 2;  // quads per replica row
+    const uint32_t g = (uint32_t)blockIdx.x * 256 + threadIdx.x;
+    const uint32_t pr = __umulhi(g, magic_div((uint32_t)QR)), uq = g - pr * (uint32_t)QR;
+    const uint32_t S = PAIR ? 64u / (uint32_t)C : 1u;  // the partner replica's distance
+    const uint32_t e0 = PAIR ? (((pr & ~(S - 1u)) << 1) | (pr & (S - 1u))) : pr, e1 = e0 + S;
+    if (e0 >= (uint32_t)p.E) return;
+    const bool has1 = PAIR && e1 < (uint32_t)p.E;
+    const int u = 4 * (int)uq, a = small_div(u, C), c0 = u - a * C;
+    uint32_t row[4], hi = 0;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {  // item i = e * C + c: its uniform is word (i >> 6) & 1 of row(i & ~64)'s draw
+        if constexpr (PAIR) {      // (i & 64 == 0 for replica e0: row(i) is its own)
+            row[k] = e0 * (uint32_t)U + (uint32_t)(u + k) + p.row_base;
+        } else {
+            const uint32_t i = e0 * (uint32_t)C + (uint32_t)(c0 + k), ib = i & ~64u;
+            const uint32_t eb = C == 1 ? ib : __umulhi(ib, magic_div((uint32_t)C));
+            row[k] = eb * (uint32_t)U + (uint32_t)(a * C) + (ib - eb * (uint32_t)C) + p.row_base;
+            hi |= ((i >> 6) & 1u) << k;
+        }
+    }
+    const float* tab = tabs + a * kFreeTabDw;
+    const float tmax = tab[64];
+    const int t0 = (int)blockIdx.y * kFillRounds;
+    uint32_t own0[kFillRounds], own1[kFillRounds];
+#pragma unroll
+    for (int j = 0; j < kFillRounds; j++) {
+        const int8_t* ob = advance(p.owner, (int64_t)(t0 + j) * p.owner_stride);
+        own0[j] = t0 + j < n_acts ? *reinterpret_cast<const uint32_t*>(ob + (size_t)e0 * C + c0) : 0u;
+        own1[j] = has1 && t0 + j < n_acts ? *reinterpret_cast<const uint32_t*>(ob + (size_t)e1 * C + c0) : 0u;
+    }
+    const uint64_t off0 = p.offset + (p.offset_dev ? *p.offset_dev : 0ull);
+    const uint32_t mine = 0x01010101u * (uint32_t)(a + 1);
+    auto sample = [&](uint32_t w, uint32_t& acts, float& lp, int k) {
+        const float target = u24(w) * tmax;
+        int cnt = 0;
+#pragma unroll
+        for (int step = 32; step >= 1; step >>= 1)
+            if (cnt + step <= 32 && tab[cnt + step - 1] <= target) cnt += step;
+        const int act = cnt >= p.A ? __float_as_int(tab[65]) : cnt;
+        acts |= (uint32_t)(uint8_t)act << (8 * k);
+        lp = tab[32 + act];
+    };
+    auto store = [&](uint32_t e, int t, int owned, uint32_t acts, const float (&lps)[4]) {
+        const size_t r = (size_t)e * U + u;
+        int8_t* ad = advance(p.action, (int64_t)t * p.action_stride) + r;
+        float* ld = advance(p.logprob, (int64_t)t * p.logprob_stride) + r;
+        if (owned == 0 || fill_merge) {
+            uint32_t a4 = acts;
+            float4 l4 = make_float4(lps[0], lps[1], lps[2], lps[3]);
+            if (owned != 0) {  // merge the owned items the rollout wrote: whole quads, no partially written lines
+                const uint32_t old_a = *reinterpret_cast<const uint32_t*>(ad);
+                const float4 old_l = *reinterpret_cast<const float4*>(ld);
+                uint32_t m = 0;
+#pragma unroll
+                for (int k = 0; k < 4; k++) m |= ((owned >> k) & 1) ? 0xffu << (8 * k) : 0u;
+                a4 = (acts & ~m) | (old_a & m);
+                if (owned & 1) l4.x = old_l.x;
+                if (owned & 2) l4.y = old_l.y;
+                if (owned & 4) l4.z = old_l.z;
+                if (owned & 8) l4.w = old_l.w;
+            }
+            *reinterpret_cast<uint32_t*>(ad) = a4;
+            *reinterpret_cast<float4*>(ld) = l4;
+        } else {
+#pragma unroll
+            for (int k = 0; k < 4; k++)
+                if (!((owned >> k) & 1)) {
+                    ad[k] = (int8_t)(acts >> (8 * k));
+                    ld[k] = lps[k];
+                }
+        }
+    };
+#pragma unroll
+    for (int j = 0; j < kFillRounds; j++) {
+        const int t = t0 + j;
+        if (t >= n_acts) break;
+        const uint64_t off = off0 + (uint64_t)t * p.offset_step;
+        // byte k == 0: the agent owns core c0 + k (acted in the rollout launch); replica e1 absent: all owned
+        const uint32_t x0 = own0[j] ^ mine, x1 = has1 ? own1[j] ^ mine : 0u;
+        uint32_t acts0 = 0, acts1 = 0;
+        float lps0[4], lps1[4];
+        int owned0 = 0, owned1 = 0;
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const bool n0 = ((x0 >> (8 * k)) & 0xffu) != 0u, n1 = PAIR && ((x1 >> (8 * k)) & 0xffu) != 0u;
+            owned0 |= n0 ? 0 : 1 << k;
+            owned1 |= n1 ? 0 : 1 << k;
+            lps0[k] = lps1[k] = 0.f;
+            if (!n0 && !n1) continue;
+            uint32_t w0, w1;
+            philox2(row[k], off, p.seed, w0, w1);
+            if (n0) sample(PAIR ? w0 : (((hi >> k) & 1u) ? w1 : w0), acts0, lps0[k], k);
+            if (n1) sample(w1, acts1, lps1[k], k);
+        }
+        store(e0, t, owned0, acts0, lps0);
+        if (has1) store(e1, t, owned1, acts1, lps1);
+    }
+}
+
 struct RolloutFreeArgs {
     Params P;
     int64_t E;
@@ -2698,6 +2815,32 @@ static hipError_t launch_rollout_free_sh(const Params& P, int64_t E, uint8_t* re
                        A);
     return hipGetLastError();
 }
+// quads with owned items stored whole, merged with the values the rollout wrote: every line of the outputs is
+// written whole (the per-item stores left every line partial): 501 -> 425 us per 199-round fill (profiles/r7s).
+// MS_FILL_MERGE=0: the per-item stores (A/B measurements)
+static int fill_merge() {
+    static const int v = [] {
+        const char* e = getenv("MS_FILL_MERGE");
+        return e && e[0] == '0' ? 0 : 1;
+    }();
+    return v;
+}
+// MS_FILL_PAIR=0: the quad fill without the draw pairing (A/B measurements)
+static bool fill_pair_enabled() {
+    static const bool v = [] {
+        const char* e = getenv("MS_FILL_PAIR");
+        return !(e && e[0] == '0');
+    }();
+    return v;
+}
+// MS_FILL_QUAD=0: the per-item fill kernel (A/B measurements)
+static bool fill_quad_enabled() {
+    static const bool v = [] {
+        const char* e = getenv("MS_FILL_QUAD");
+        return !(e && e[0] == '0');
+    }();
+    return v;
+}
 // the acceptor items of cores their agent does not own, every acting round of a k_env_rollout_act_free launch
 // with the same arguments (its outputs' other items are untouched)
 hipError_t launch_env_fill_common(const Params& P, int64_t E, const StepIO& io, const FusedActFree& fa,
@@ -2709,6 +2852,24 @@ hipError_t launch_env_fill_common(const Params& P, int64_t E, const StepIO& io, 
                            static_cast<const uint32_t*>(fa.acc.act_frag) + 4, (int)E, P.N, P.C, fa.acc.n_actions,
                            (uint32_t)fa.acc.row_base, fa.seed, fa.acc_offset, st.offset_step, fa.offset_dev};
     const int64_t items = E * P.N * P.C;
+    // the quad kernel: C % 4 == 0 and every round's owners / actions 4-byte, log-probs 16-byte aligned
+    const bool quad = P.C % 4 == 0 && fill_quad_enabled() &&
+                      ((reinterpret_cast<uintptr_t>(c.owner) | (uintptr_t)c.owner_stride) & 3) == 0 &&
+                      ((reinterpret_cast<uintptr_t>(c.action) | (uintptr_t)c.action_stride) & 3) == 0 &&
+                      ((reinterpret_cast<uintptr_t>(c.logprob) | (uintptr_t)c.logprob_stride) & 15) == 0;
+    if (quad) {
+        const unsigned by = (unsigned)((n_acts + kFillRounds - 1) / kFillRounds);
+        const int64_t qr = (int64_t)P.N * P.C / 4;
+        if (64 % P.C == 0 && fill_pair_enabled()) {  // threads: quads of the replicas e with e & (64 / C) == 0
+            const int64_t S = 64 / P.C, pairs = (E + 2 * S - 1) / (2 * S) * S;
+            hipLaunchKernelGGL(k_acc_common_fill4<true>, dim3((unsigned)((pairs * qr + 255) / 256), by), dim3(256), 0, s,
+                               c, n_acts, fill_merge());
+        } else {
+            hipLaunchKernelGGL(k_acc_common_fill4<false>, dim3((unsigned)((E * qr + 255) / 256), by), dim3(256), 0, s, c,
+                               n_acts, fill_merge());
+        }
+        return hipGetLastError();
+    }
     const unsigned bx = (unsigned)((items + kFillPer * 256 - 1) / (kFillPer * 256));
     hipLaunchKernelGGL(k_acc_common_fill, dim3(bx, (unsigned)n_acts), dim3(256), 0, s, c);
     return hipGetLastError();

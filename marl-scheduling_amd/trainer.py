@@ -760,6 +760,8 @@ class Trainer:
         (several ranks only) and leaves the losses in out["losses"]."""
         T, E = self.T, self.E
         losses = {}
+        if self.defer_common:  # the rollout's deferred acceptor items (a trainer switched to several ranks)
+            self.fill_common()
         # Each unit type's draws update its nets in sequence (draw d trains on the weights draw d-1
         # left), but the unit types are independent nets: step s of the update = epoch k of draw d
         # of every unit type that has one, with ONE all-reduce of all their gradients (one
@@ -843,6 +845,8 @@ class Trainer:
         """The torch-autograd update (the numerical reference of the fused one)."""
         T = self.T
         losses = {}
+        if self.defer_common:
+            self.fill_common()
         for u in self.units():
             ls = []
             st_u = self.acceptor_rows(0, T) if (u is self.acc and self.compact) else self._states_of(u)

