@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define MS_ABI_VERSION 17
+#define MS_ABI_VERSION 18
 
 #define MS_MAX_KINDS 16
 #define MS_MAX_AGENTS 64
@@ -465,6 +465,11 @@ typedef struct ms_fused_act_free {
      * table; the env reads only the owner's acceptor action, world.py:391-404) to ms_env_rollout_fill_common,
      * which the caller runs later, e.g. on another stream beside other work; 0: the call runs it itself */
     int32_t defer_common;
+    /* (ABI 18; both NULL: the owned items go straight into acc_action / acc_logprob) [E][C] the owned acceptor
+     * items' outputs by core, item (e, owner - 1, c) at e * C + c: the rollout writes them here and the common fill
+     * then writes every item of acc_action / acc_logprob, whole lines instead of one item in eight per round */
+    int8_t* own_action;
+    float* own_logprob;
 } ms_fused_act_free;
 
 /* Per-round byte strides of ms_env_rollout_act_free (as ms_round_strides, plus the price chooser's arrays). */
@@ -475,6 +480,7 @@ typedef struct ms_round_strides_free {
     int64_t next_core_action, next_core_logprob, next_price_state, next_price_action, next_price_logprob;
     int64_t next_acc_action, next_acc_logprob;             /* ms_fused_act_free outputs */
     uint64_t offset_step;
+    int64_t next_own_action, next_own_logprob;             /* (ABI 18) ms_fused_act_free own_action / own_logprob */
 } ms_round_strides_free;
 
 /* n_rounds rounds of a locally shared free-price rollout in one launch: round t steps the env with the

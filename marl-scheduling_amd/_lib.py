@@ -27,7 +27,7 @@ class MarlSchedError(RuntimeError):
         self.code = code
 
 
-ABI_VERSION = 17  # include/marlsched.h MS_ABI_VERSION
+ABI_VERSION = 18  # include/marlsched.h MS_ABI_VERSION
 
 
 def _load():
@@ -125,9 +125,10 @@ def _load():
     version = L.ms_abi_version()
     # ABI 14 added ms_bdqn_update*, 15 ms_bdqn_act_compact, 16 ms_mlp_params.row_base (a trailing field an
     # older library does not read: its acting draws are those of row_base 0) and ms_env_step_act /
-    # ms_env_rollout_act, 17 ms_env_rollout_act_free. An older library (an A/B variant built
+    # ms_env_rollout_act, 17 ms_env_rollout_act_free, 18 its own_action / own_logprob (trailing fields a 17
+    # library does not read: it writes the owned items into the rings itself). An older library (an A/B variant built
     # before them, tools/gpu_job.sh ab step) loads without them only when MARLSCHED_LENIENT_ABI=1 asks for it
-    lenient = os.environ.get("MARLSCHED_LENIENT_ABI") == "1" and version in (13, 14, 15, 16, 17)
+    lenient = os.environ.get("MARLSCHED_LENIENT_ABI") == "1" and version in (13, 14, 15, 16, 17, 18)
     if version != ABI_VERSION and not lenient:
         raise ImportError("libmarlsched.so ABI version mismatch (%d, want %d)" % (version, ABI_VERSION))
     for name, (res, args) in sig.items():

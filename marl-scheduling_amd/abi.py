@@ -212,20 +212,23 @@ class MsRoundStrides(ct.Structure):  # ms_round_strides (ABI 16): bytes per roun
                                           "next_acc_logprob")] + [("offset_step", ct.c_uint64)]
 
 
-class MsFusedActFree(ct.Structure):  # ms_fused_act_free (ABI 17)
+class MsFusedActFree(ct.Structure):  # ms_fused_act_free (ABI 18: own_action / own_logprob)
     _fields_ = [("core_chooser", MsMlpParams), ("price_chooser", MsMlpParams), ("acceptor", MsMlpParams),
                 ("common_row", ct.c_void_p), ("price_table", ct.c_void_p), ("seed", ct.c_uint64),
                 ("off_offset", ct.c_uint64), ("acc_offset", ct.c_uint64), ("offset_dev", ct.c_void_p)] + [
         (n, ct.c_void_p) for n in ("core_action", "core_logprob", "price_state", "price_action", "price_logprob",
-                                   "env_price", "acc_action", "acc_logprob")] + [("defer_common", ct.c_int32)]
+                                   "env_price", "acc_action", "acc_logprob")] + [("defer_common", ct.c_int32),
+                                                                                ("own_action", ct.c_void_p),
+                                                                                ("own_logprob", ct.c_void_p)]
 
 
-class MsRoundStridesFree(ct.Structure):  # ms_round_strides_free (ABI 17): bytes per round
+class MsRoundStridesFree(ct.Structure):  # ms_round_strides_free (ABI 18): bytes per round
     _fields_ = [(n, ct.c_int64) for n in ("acceptor_action", "offer_action", "core_rows", "core_owner", "offer_obs",
                                           "offer_reward", "price_reward", "acceptor_reward", "agent_reward",
                                           "auctioneer_reward", "next_core_action", "next_core_logprob",
                                           "next_price_state", "next_price_action", "next_price_logprob",
-                                          "next_acc_action", "next_acc_logprob")] + [("offset_step", ct.c_uint64)]
+                                          "next_acc_action", "next_acc_logprob")] + [("offset_step", ct.c_uint64)] + [
+        ("next_own_action", ct.c_int64), ("next_own_logprob", ct.c_int64)]
 
 
 class MsQnetParams(ct.Structure):

@@ -393,13 +393,15 @@ static ms::FusedActFree free_act_args(const ms_fused_act_free& n) {
     return ms::FusedActFree{n.core_chooser, n.price_chooser, n.acceptor, n.common_row,
                             pt ? pt->table : nullptr, pt ? pt->digit : nullptr, pt ? pt->n_keys : 0, n.seed,
                             n.off_offset, n.acc_offset, n.offset_dev, n.core_action, n.core_logprob, n.price_state,
-                            n.price_action, n.price_logprob, n.env_price, n.acc_action, n.acc_logprob};
+                            n.price_action, n.price_logprob, n.env_price, n.acc_action, n.acc_logprob,
+                            n.own_action, n.own_logprob};
 }
 static ms::RoundStrideFree free_strides(const ms_round_strides_free& r) {
     return ms::RoundStrideFree{r.acceptor_action, r.offer_action, r.core_rows, r.core_owner, r.offer_obs,
                                r.offer_reward, r.price_reward, r.acceptor_reward, r.agent_reward, r.auctioneer_reward,
                                r.next_core_action, r.next_core_logprob, r.next_price_state, r.next_price_action,
-                               r.next_price_logprob, r.next_acc_action, r.next_acc_logprob, r.offset_step};
+                               r.next_price_logprob, r.next_acc_action, r.next_acc_logprob, r.offset_step,
+                               r.next_own_action, r.next_own_logprob};
 }
 
 int ms_env_rollout_act_free_supported(const ms_env* env) {
@@ -440,6 +442,7 @@ int ms_env_rollout_act_free(ms_env* env, const ms_actions* act, const ms_obs_out
     if (!next->common_row || !next->core_action || !next->core_logprob || !next->price_state || !next->price_action ||
         !next->price_logprob || !next->env_price || !next->acc_action || !next->acc_logprob)
         return bad("NULL output / common row");
+    if (!next->own_action != !next->own_logprob) return bad("own_action and own_logprob: both or neither");
     if (env->E * N * L >= (1LL << 24) || env->E * N * C * 4 > 0x7fffffffLL || env->E * N * L * 4 > 0x7fffffffLL ||
         env->E * (int64_t)(N * C) * (N * C) >= (1LL << 32))
         return bad("too many replicas for 32-bit row offsets");
@@ -467,6 +470,7 @@ int ms_env_rollout_fill_common(const ms_env* env, const ms_obs_out* obs, const m
     if (n_rounds < 1) return bad("n_rounds < 1");
     if (!obs->core_owner || !next->acceptor.act_frag || !next->acc_action || !next->acc_logprob)
         return bad("needs the owners, the acceptor's act fragments and its outputs");
+    if (!next->own_action != !next->own_logprob) return bad("own_action and own_logprob: both or neither");
     if (next->acceptor.n_groups != env->P.N || next->acceptor.n_actions != env->P.O + 1)
         return bad("acceptor net shape does not match the env");
     ms::StepIO io{};

@@ -1013,8 +1013,10 @@ constexpr int kLiabPrefetch = 4;  // newest chain entries loaded ahead per core 
 template <int LPE, bool EXT, bool CMP, class SH>
 __device__ __forceinline__ void env_round(const Params& P, int64_t E, uint8_t* recs, uint32_t* mt, Liab* liab,
                                           const StepIO& io, int64_t slot, int lane_arg = -1,
-                                          uint8_t* wave_lds = nullptr) {
-    // wave_lds: the wave's part of a multi-wave workgroup's LDS (k_env_rollout_act_free), else the block's
+                                          uint8_t* wave_lds = nullptr, const int8_t* acc_lds = nullptr) {
+    // wave_lds: the wave's part of a multi-wave workgroup's LDS (k_env_rollout_act_free), else the block's;
+    // acc_lds: the acceptor actions of the wave's replicas in the LDS ([kWave / LPE][N * C]; read instead of
+    // io.act_acc, which then serves the padding replicas only)
     extern __shared__ __align__(16) uint8_t smem_dyn[];
     uint8_t* const smem_all = wave_lds ? wave_lds : smem_dyn;
     // the shape: a compile-time constant for the BASELINE shapes (offsets fold into immediates,
@@ -1071,7 +1073,9 @@ __device__ __forceinline__ void env_round(const Params& P, int64_t E, uint8_t* r
         // the record and the dword-aligned action arrays: one batch of loads, then the LDS stores
         const uint32_t* src_rec = reinterpret_cast<const uint32_t*>(recs + e * (int64_t)g.rec_bytes);
         const int rec_dw = g.rec_bytes / 4;
-        const int8_t* a_src[4] = {io.act_acc ? io.act_acc + e * N * C : nullptr, io.act_off ? io.act_off + e * NL : nullptr,
+        const int8_t* a_src[4] = {acc_lds && active ? acc_lds + (lane / LPE) * N * C
+                                                    : (io.act_acc ? io.act_acc + e * N * C : nullptr),
+                                  io.act_off ? io.act_off + e * NL : nullptr,
                                   io.act_price ? io.act_price + e * NL : nullptr,
                                   io.act_auct ? io.act_auct + e * C : nullptr};
         int8_t* a_dst[4] = {a_acc, a_off, a_price, a_auct};
@@ -2136,6 +2140,7 @@ __device__ __forceinline__ void act_free(const Geom& g, int64_t E, const FusedAc
         const uint32_t rbase = (uint32_t)fa.acc.row_base;
         const long long rows_all = E * Ua;
         const RawBuf aa_b(fa.acc_action, rows_all), al_b(fa.acc_logprob, 4 * rows_all);
+        const RawBuf oa_b(fa.own_action, E * C), ol_b(fa.own_logprob, 4 * E * C);
         // the listed rows [0, cnt) (cnt <= 32) as two 16-row tiles (a lone or partial tile: rows past cnt
         // are computed on entry 0 and not written)
         auto tiles2 = [&](int cnt) {
@@ -2153,7 +2158,7 @@ __device__ __forceinline__ void act_free(const Geom& g, int64_t E, const FusedAc
                 h1.load(fa.acc, a, j, g4);
             }
             f4 acc[2];
-            int row[2];
+            int row[2], orow[2], lrow[2];
             float uu[2];
 #pragma unroll
             for (int i = 0; i < 2; i++) {
@@ -2163,6 +2168,8 @@ __device__ __forceinline__ void act_free(const Geom& g, int64_t E, const FusedAc
                 uu[i] = lu[v ? t : 0];
                 const int kk = mm / C, cc = mm - kk * C;
                 row[i] = v ? (int)((e0 + kk) * Ua) + a * C + cc : -1;
+                orow[i] = (int)(e0 * C) + mm;  // (e0 + kk) * C + cc
+                lrow[i] = fl.accx + kk * Ua + a * C + cc;
                 const uint32_t* crow = reinterpret_cast<const uint32_t*>(slice(kk) + g.s_scratch) + cc * nw;
                 acc[i] = (f4){0, 0, 0, 0};
 #pragma unroll
@@ -2180,8 +2187,16 @@ __device__ __forceinline__ void act_free(const Geom& g, int64_t E, const FusedAc
 #pragma unroll
             for (int i = 0; i < 2; i++)
                 if (row[i] >= 0 && g4 == 0) {
-                    aa_b.st8((uint32_t)row[i], act[i]);
-                    al_b.stf(4 * (uint32_t)row[i], lp[i]);
+                    if (fa.own_action) {
+                        // by core (the fill writes the rings' rows whole), and into the replica's LDS staging of
+                        // acceptor actions, where the next env round reads its owners' (StepIO::acc_in_lds)
+                        oa_b.st8((uint32_t)orow[i], act[i]);
+                        ol_b.stf(4 * (uint32_t)orow[i], lp[i]);
+                        reinterpret_cast<int8_t*>(lds)[lrow[i]] = (int8_t)act[i];
+                    } else {
+                        aa_b.st8((uint32_t)row[i], act[i]);
+                        al_b.stf(4 * (uint32_t)row[i], lp[i]);
+                    }
                 }
         };
         // item i's uniform: word (i >> 6) & 1 of the draw countered by the row of item i & ~64 (k_act_common's
@@ -2252,6 +2267,9 @@ struct CommonFillArgs {
     int8_t* action;          // round 0's outputs [E][N*C]
     float* logprob;
     int64_t owner_stride, action_stride, logprob_stride;  // bytes per round
+    const int8_t* own_action;  // round 0's owned items by core [E][C] (NULL: already in action / logprob)
+    const float* own_logprob;
+    int64_t own_action_stride, own_logprob_stride;
     const uint32_t* frag;    // the acceptor net's act fragment groups (frag_groups<2, 2>)
     int E, N, C, A;
     uint32_t row_base;
@@ -2291,7 +2309,15 @@ __global__ void __launch_bounds__(256) k_acc_common_fill(CommonFillArgs p) {
         const uint32_t e = U == 1 ? r : __umulhi(r, mag_u);
         const int u = (int)(r - e * (uint32_t)U);
         const int a = small_div(u, C), c = u - a * C;
-        if ((int64_t)r >= n || own[k] == a + 1) continue;  // the owner's row: acted in the rollout launch
+        if ((int64_t)r >= n) continue;
+        if (own[k] == a + 1) {  // the owner's row: acted in the rollout launch (by core: copied here)
+            if (p.own_action) {
+                const size_t oc = (size_t)e * C + c;
+                act_b.st8(r, advance(p.own_action, t * p.own_action_stride)[oc]);
+                lp_b.stf(4 * r, advance(p.own_logprob, t * p.own_logprob_stride)[oc]);
+            }
+            continue;
+        }
         const uint32_t i = e * (uint32_t)C + (uint32_t)c, ib = i & ~64u;
         const uint32_t eb = C == 1 ? ib : __umulhi(ib, mag_c);
         uint32_t w0, w1;
@@ -2358,26 +2384,22 @@ __global__ void __launch_bounds__(256) k_acc_common_fill4(CommonFillArgs p, int 
     }
     const uint64_t off0 = p.offset + (p.offset_dev ? *p.offset_dev : 0ull);
     const uint32_t mine = 0x01010101u * (uint32_t)(a + 1);
-    auto sample = [&](uint32_t w, uint32_t& acts, float& lp, int k) {
-        const float target = u24(w) * tmax;
-        int cnt = 0;
-#pragma unroll
-        for (int step = 32; step >= 1; step >>= 1)
-            if (cnt + step <= 32 && tab[cnt + step - 1] <= target) cnt += step;
-        const int act = cnt >= p.A ? __float_as_int(tab[65]) : cnt;
-        acts |= (uint32_t)(uint8_t)act << (8 * k);
-        lp = tab[32 + act];
-    };
     auto store = [&](uint32_t e, int t, int owned, uint32_t acts, const float (&lps)[4]) {
         const size_t r = (size_t)e * U + u;
         int8_t* ad = advance(p.action, (int64_t)t * p.action_stride) + r;
         float* ld = advance(p.logprob, (int64_t)t * p.logprob_stride) + r;
-        if (owned == 0 || fill_merge) {
+        if (owned == 0 || fill_merge || p.own_action) {
             uint32_t a4 = acts;
             float4 l4 = make_float4(lps[0], lps[1], lps[2], lps[3]);
             if (owned != 0) {  // merge the owned items the rollout wrote: whole quads, no partially written lines
-                const uint32_t old_a = *reinterpret_cast<const uint32_t*>(ad);
-                const float4 old_l = *reinterpret_cast<const float4*>(ld);
+                // (by core [E][C]: cores c0..c0 + 3 of replica e; else the rings' own quad)
+                const size_t oc = (size_t)e * C + c0;
+                const uint32_t old_a = p.own_action
+                                           ? *reinterpret_cast<const uint32_t*>(advance(p.own_action, (int64_t)t * p.own_action_stride) + oc)
+                                           : *reinterpret_cast<const uint32_t*>(ad);
+                const float4 old_l = p.own_action
+                                         ? *reinterpret_cast<const float4*>(advance(p.own_logprob, (int64_t)t * p.own_logprob_stride) + oc)
+                                         : *reinterpret_cast<const float4*>(ld);
                 uint32_t m = 0;
 #pragma unroll
                 for (int k = 0; k < 4; k++) m |= ((owned >> k) & 1) ? 0xffu << (8 * k) : 0u;
@@ -2405,20 +2427,50 @@ __global__ void __launch_bounds__(256) k_acc_common_fill4(CommonFillArgs p, int 
         const uint64_t off = off0 + (uint64_t)t * p.offset_step;
         // byte k == 0: the agent owns core c0 + k (acted in the rollout launch); replica e1 absent: all owned
         const uint32_t x0 = own0[j] ^ mine, x1 = has1 ? own1[j] ^ mine : 0u;
-        uint32_t acts0 = 0, acts1 = 0;
-        float lps0[4], lps1[4];
         int owned0 = 0, owned1 = 0;
 #pragma unroll
         for (int k = 0; k < 4; k++) {
-            const bool n0 = ((x0 >> (8 * k)) & 0xffu) != 0u, n1 = PAIR && ((x1 >> (8 * k)) & 0xffu) != 0u;
-            owned0 |= n0 ? 0 : 1 << k;
-            owned1 |= n1 ? 0 : 1 << k;
-            lps0[k] = lps1[k] = 0.f;
-            if (!n0 && !n1) continue;
+            owned0 |= ((x0 >> (8 * k)) & 0xffu) == 0u ? 1 << k : 0;
+            owned1 |= ((x1 >> (8 * k)) & 0xffu) == 0u ? 1 << k : 0;
+        }
+        // every item's draw and search, owned or not (the owned ones are replaced at the store), branch-free and
+        // in lockstep: the NI searches' dependent LDS reads of one step issue together instead of one search
+        // after the other behind the ownership branches (the kernel is bound by that latency, not by its stores)
+        constexpr int NI = PAIR ? 8 : 4;
+        float tg[NI];
+        int cnt[NI];
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
             uint32_t w0, w1;
             philox2(row[k], off, p.seed, w0, w1);
-            if (n0) sample(PAIR ? w0 : (((hi >> k) & 1u) ? w1 : w0), acts0, lps0[k], k);
-            if (n1) sample(w1, acts1, lps1[k], k);
+            tg[k] = u24(PAIR ? w0 : (((hi >> k) & 1u) ? w1 : w0)) * tmax;
+            if constexpr (PAIR) tg[4 + k] = u24(w1) * tmax;
+        }
+#pragma unroll
+        for (int i = 0; i < NI; i++) cnt[i] = 0;
+#pragma unroll
+        for (int step = 32; step >= 1; step >>= 1) {
+            float v[NI];
+#pragma unroll
+            for (int i = 0; i < NI; i++) v[i] = tab[min(cnt[i] + step, 32) - 1];
+#pragma unroll
+            for (int i = 0; i < NI; i++) cnt[i] = (cnt[i] + step <= 32 && v[i] <= tg[i]) ? cnt[i] + step : cnt[i];
+        }
+        const int lnz = __float_as_int(tab[65]);
+        uint32_t acts0 = 0, acts1 = 0;
+        float lps0[4], lps1[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const int a0 = cnt[k] >= p.A ? lnz : cnt[k];
+            acts0 |= (uint32_t)(uint8_t)a0 << (8 * k);
+            lps0[k] = tab[32 + a0];
+            if constexpr (PAIR) {
+                const int a1 = cnt[4 + k] >= p.A ? lnz : cnt[4 + k];
+                acts1 |= (uint32_t)(uint8_t)a1 << (8 * k);
+                lps1[k] = tab[32 + a1];
+            } else {
+                lps1[k] = 0.f;
+            }
         }
         store(e0, t, owned0, acts0, lps0);
         if (has1) store(e1, t, owned1, acts1, lps1);
@@ -2468,6 +2520,11 @@ __global__ void __launch_bounds__(512, 4) k_env_rollout_act_free(RolloutFreeArgs
         uint32_t* pd = reinterpret_cast<uint32_t*>(smem_free + fl.pdig);
         const uint32_t* src = reinterpret_cast<const uint32_t*>(A0.fa.pdigit);
         for (int k = (int)threadIdx.x; k < 512; k += (int)blockDim.x) pd[k] = src[k];
+        // (by-core mode) the acceptor actions the env rounds stage from the LDS: the acting writes the owners'
+        // items only, and the env checks every item's range (k_env_step: they are all sampled), so the others
+        // hold a valid action (0, "reject") instead of whatever the LDS held
+        uint32_t* ax = reinterpret_cast<uint32_t*>(smem_free + fl.accx);
+        for (int k = (int)threadIdx.x; k < (fl.total - fl.accx) / 4; k += (int)blockDim.x) ax[k] = 0u;
     }
     __syncthreads();
 #ifdef MS_PHASE_TIMING
@@ -2510,8 +2567,13 @@ __global__ void __launch_bounds__(512, 4) k_env_rollout_act_free(RolloutFreeArgs
         //  priority, then age)
         const bool up = wave >= 4 && (A.prio & 2);
         if (up) __builtin_amdgcn_s_setprio(1);
+        // rounds after the first (by-core mode): the owners' acceptor actions are where this launch's acting left
+        // them in the LDS (the rings' acceptor rows are written after the launch, by the fill)
+        const int8_t* acc_lds = t > 0 && A.fa.own_action
+                                    ? reinterpret_cast<const int8_t*>(smem_free + fl.accx) + wave * kFreeEPW * g.N * g.C
+                                    : nullptr;
         env_round<kWave / kFreeEPW, false, true, SH>(A.P, A.E, A.recs, A.mt, A.liab, io, wslot, lane,
-                                                     smem_free + wave * kFreeEPW * g.s_total);
+                                                     smem_free + wave * kFreeEPW * g.s_total, acc_lds);
         if (up) __builtin_amdgcn_s_setprio(0);
         FREE_MARK(0);
         if (t + 1 < n_rounds || A.act_last) {
@@ -2525,6 +2587,8 @@ __global__ void __launch_bounds__(512, 4) k_env_rollout_act_free(RolloutFreeArgs
             fa.price_logprob = advance(fa.price_logprob, t * st.price_logprob);
             fa.acc_action = advance(fa.acc_action, t * st.acc_action);
             fa.acc_logprob = advance(fa.acc_logprob, t * st.acc_logprob);
+            fa.own_action = advance(fa.own_action, t * st.own_action);
+            fa.own_logprob = advance(fa.own_logprob, t * st.own_logprob);
             fa.off_offset += (uint64_t)t * st.offset_step;
             fa.acc_offset += (uint64_t)t * st.offset_step;
             const bool up_act = wave >= 4 && (A.prio & 1);
@@ -2849,6 +2913,7 @@ hipError_t launch_env_fill_common(const Params& P, int64_t E, const StepIO& io, 
     if (!env_rollout_free_supported(P) || io.obs_cown == nullptr || fa.acc.act_frag == nullptr) return hipErrorInvalidValue;
     if (n_acts < 1) return hipSuccess;
     const CommonFillArgs c{io.obs_cown, fa.acc_action, fa.acc_logprob, st.obs_cown, st.acc_action, st.acc_logprob,
+                           fa.own_action, fa.own_logprob, st.own_action, st.own_logprob,
                            static_cast<const uint32_t*>(fa.acc.act_frag) + 4, (int)E, P.N, P.C, fa.acc.n_actions,
                            (uint32_t)fa.acc.row_base, fa.seed, fa.acc_offset, st.offset_step, fa.offset_dev};
     const int64_t items = E * P.N * P.C;
@@ -2856,7 +2921,9 @@ hipError_t launch_env_fill_common(const Params& P, int64_t E, const StepIO& io, 
     const bool quad = P.C % 4 == 0 && fill_quad_enabled() &&
                       ((reinterpret_cast<uintptr_t>(c.owner) | (uintptr_t)c.owner_stride) & 3) == 0 &&
                       ((reinterpret_cast<uintptr_t>(c.action) | (uintptr_t)c.action_stride) & 3) == 0 &&
-                      ((reinterpret_cast<uintptr_t>(c.logprob) | (uintptr_t)c.logprob_stride) & 15) == 0;
+                      ((reinterpret_cast<uintptr_t>(c.logprob) | (uintptr_t)c.logprob_stride) & 15) == 0 &&
+                      ((reinterpret_cast<uintptr_t>(c.own_action) | (uintptr_t)c.own_action_stride) & 3) == 0 &&
+                      ((reinterpret_cast<uintptr_t>(c.own_logprob) | (uintptr_t)c.own_logprob_stride) & 15) == 0;
     if (quad) {
         const unsigned by = (unsigned)((n_acts + kFillRounds - 1) / kFillRounds);
         const int64_t qr = (int64_t)P.N * P.C / 4;

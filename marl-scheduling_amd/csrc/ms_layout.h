@@ -202,6 +202,8 @@ struct FusedActFree {
     int8_t* env_price;       // [E][N*L]: the next round's offer_price actions (one buffer, every round)
     int8_t* acc_action;      // [E][N*C]
     float* acc_logprob;
+    int8_t* own_action;      // [E][C] the owned items by core (NULL: in acc_action / acc_logprob directly)
+    float* own_logprob;
 };
 
 // per-round byte strides of k_env_rollout_act_free (ms_round_strides_free)
@@ -209,6 +211,7 @@ struct RoundStrideFree {
     int64_t act_acc, act_off, obs_crow, obs_cown, obs_off, rew_offer, rew_price, rew_acc, rew_agent, rew_auct;
     int64_t core_action, core_logprob, price_state, price_action, price_logprob, acc_action, acc_logprob;
     uint64_t offset_step;
+    int64_t own_action, own_logprob;
 };
 
 // The workgroup LDS of k_env_rollout_act_free: the env slices of its kFreeEPW * N replicas (wave w steps
@@ -218,13 +221,16 @@ constexpr int kFreeEPW = 4;        // replicas per wave (16 lanes each)
 constexpr int kFreeListCap = 96;   // < 32 carried + one 64-item step
 constexpr int kFreeTabDw = 68;     // [32 running sums][32 log-probs][S][last nonzero][2 pad] (Head<2>::table)
 struct FreeLds {
-    int32_t pdig, list, total;
+    int32_t pdig, list, accx, total;
 };
 inline constexpr FreeLds free_lds(const Geom& g) {
     FreeLds f{};
     f.pdig = align16(kFreeEPW * g.N * g.s_total);
     f.list = f.pdig + 4 * 256 * 2;
-    f.total = f.list + g.N * kFreeListCap * 6;  // int16 item + f32 uniform per entry
+    f.accx = align16(f.list + g.N * kFreeListCap * 6);  // int16 item + f32 uniform per entry
+    // (by-core mode) the replicas' acceptor actions [kFreeEPW * N][N * C]: the acting writes its owned items, the
+    // next env round stages its owners' from here (outside the wave slots the MT refill may overwrite)
+    f.total = f.accx + align4(kFreeEPW * g.N * g.N * g.C);
     return f;
 }
 

@@ -254,6 +254,11 @@ class BatchedEnv:
                               (next_out["price_logprob"], strides.next_price_logprob, f32),
                               (next_out["acc_action"], strides.next_acc_action, i8),
                               (next_out["acc_logprob"], strides.next_acc_logprob, f32)], n_act)
+            if next_out.get("own_action") is not None:  # the owned items by core [E][C] (ABI 18)
+                assert next_out["own_action"].numel() == self.E * self.C
+                self.check_rings([(next_out["own_action"], strides.next_own_action, i8),
+                                  (next_out["own_logprob"], strides.next_own_logprob, f32)], n_act)
+        assert bool(next_act.own_action) == (next_out.get("own_action") is not None)
         a, o, r, ev = self._step_structs(acceptor, offer_core, next_out["env_price"], None, obs, rewards, events)
         check(lib.ms_env_rollout_act_free(self._h, ct.byref(a), ct.byref(o), ct.byref(r),
                                           ct.byref(ev) if ev else None, ct.byref(next_act), ct.byref(strides),

@@ -295,12 +295,19 @@ class Trainer:
                                    self.metric_bufs is None and os.environ.get("MS_ENV_ROLLOUT_FREE", "1") != "0" and
                                    all(env.rollout_free_supported() for env, _, _ in self.env.parts))
         # ... and its acceptor items of cores their agent does not own (sampled from the common row's table; the env
-        # reads only the owner's acceptor action) are left to a second kernel (ms_env_rollout_fill_common) that
-        # iteration() runs inside the update, on the acceptor's stream beside the offer and price gradients
-        # (MS_DEFER_COMMON=0: at the end of the rollout). Offsets from a snapshot of rng_ctr taken by the rollout.
+        # reads only the owner's acceptor action) are left to a second kernel (ms_env_rollout_fill_common) after the
+        # launch. MS_DEFER_COMMON=1: iteration() runs it inside the update instead, on the acceptor's stream beside
+        # the offer and price gradients (offsets from a snapshot of rng_ctr taken by the rollout); measured even
+        # (17.84-17.92 ms per iteration either way, profiles/r7: the update is as throughput-bound as the rollout)
         self.defer_common = (self.fused_rollout_free and self.update_streams and self.world_size == 1 and self.fused and
-                             os.environ.get("MS_DEFER_COMMON", "1") != "0")
+                             os.environ.get("MS_DEFER_COMMON", "0") == "1")
         self.rng_snap = torch.zeros(1, dtype=torch.int64, device=self.device)
+        # the rollout's owned acceptor items by core ([T][E][C]; ABI 18): the fill then writes the acceptor rings'
+        # rows whole (MS_FILL_OWN=0: the rollout writes them into the rings, one item in eight of a line)
+        self.acc_own = None
+        if self.fused_rollout_free and ABI_LOADED >= 18 and os.environ.get("MS_FILL_OWN", "1") != "0":
+            self.acc_own = (torch.zeros((T, self.E, C), dtype=torch.int8, device=dev),
+                            torch.zeros((T, self.E, C), dtype=torch.float32, device=dev))
         self._fill_args = []
         self.span_every = 0  # > 0: every span_every-th round's env launches record their span (bench)
         self.spans = None
@@ -498,6 +505,9 @@ class Trainer:
                                  self.acc.group.policy_old.mlp_params(self.acc_frag, rb * N * C), ptr(self.acc_common),
                                  ct.addressof(self.price_table.struct), seed, base + 1, base + 3, ptr(self.rng_ctr),
                                  *[ptr(out[n]) for n in names])
+        if self.acc_own is not None:
+            out.update(own_action=sl(self.acc_own[0][t]), own_logprob=sl(self.acc_own[1][t]))
+            nxt.own_action, nxt.own_logprob = ptr(out["own_action"]), ptr(out["own_logprob"])
         return nxt, out
 
     def _rollout_part_free(self, k: int):
@@ -517,6 +527,8 @@ class Trainer:
                                          b(self.acc.rewards), 0, 0, b(self.off.actions), b(self.off.logprobs),
                                          b(self.price_obs), b(self.price.actions), b(self.price.logprobs),
                                          b(self.acc.actions), b(self.acc.logprobs), 8)
+        if self.acc_own is not None:
+            strides.next_own_action, strides.next_own_logprob = b(self.acc_own[0]), b(self.acc_own[1])
         nxt, out = self._fused_next_free(1, k)
         nxt.defer_common = int(self.defer_common)
         env.rollout_act_free(sl(self.acc.actions[0]).view(E, N, C), sl(self.off.actions[0]).view(E, N, L), obs, rew,

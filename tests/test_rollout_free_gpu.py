@@ -58,14 +58,17 @@ def _compare(trs, iters=2):
         assert (st[0][k] == st[1][k]).all(), k
 
 
-@pytest.mark.parametrize("E,T", [(16384, 200), (2048, 16), (1001, 12)])
-def test_cfg3_one_launch_rollout_equals_two_launches(ms, monkeypatch, E, T):
+@pytest.mark.parametrize("E,T,own", [(16384, 200, "1"), (2048, 16, "1"), (2048, 16, "0"), (1001, 12, "1")])
+def test_cfg3_one_launch_rollout_equals_two_launches(ms, monkeypatch, E, T, own):
     """cfg3 at the BASELINE size (E 16384, UPDATE_STEP 200: every replica crosses MT blocks inside the launch),
     at E 2048 and at E 1001 (a last workgroup of 9 replicas: 4 N = 32 per workgroup), the FixShape<8,8,3,1>
-    kernel: equal to the act launch + env launch per round, bit for bit."""
+    kernel: equal to the act launch + env launch per round, bit for bit. own "1": the owned acceptor items go
+    through the by-core buffers (ABI 18) and the fill writes whole rows; "0": straight into the rings."""
     tr_mod = importlib.import_module("marl-scheduling_amd.trainer")
+    monkeypatch.setenv("MS_FILL_OWN", own)
     trs = _trainers(monkeypatch, lambda: tr_mod.Trainer.from_named("cfg3", n_envs=E, update_step=T, seed=11,
                                                                     device="cuda:0"))
+    assert (trs[0].acc_own is not None) == (own == "1")
     _compare(trs)
 
 
@@ -169,11 +172,12 @@ def test_update_streams_equal_one_stream(ms, monkeypatch, name, E):
     """One rank updates each unit type on its own stream by default (Trainer.update_streams; the unit types are
     independent nets, PPOmodules.py:548-597): every loss and weight equals the one-stream update's bit for bit,
     over three iterations (each acting on the previous update's weights), graph-replayed. cfg3's trainer with
-    streams also defers the rollout's common acceptor items into the update (defer_common): every ring equals the
+    streams also defers (MS_DEFER_COMMON=1) the rollout's common acceptor items into the update: every ring equals the
     one-stream trainer's after each iteration."""
     tr_mod = importlib.import_module("marl-scheduling_amd.trainer")
     ppo = importlib.import_module("marl-scheduling_amd.ppo")
     mk = lambda: tr_mod.Trainer.from_named(name, n_envs=E, update_step=12, seed=6, device="cuda:0")
+    monkeypatch.setenv("MS_DEFER_COMMON", "1")
     streams = mk()
     monkeypatch.setenv("MS_UPDATE_STREAMS", "0")
     one = mk()
