@@ -45,7 +45,7 @@ __device__ __forceinline__ void wave_sync() {
 constexpr int kProbeSlots = 65536;
 __device__ unsigned long long g_phase_cycles[kProbeSlots][16];  // per block, summed on the host
 __device__ unsigned long long g_wave_span[kProbeSlots][2];      // last launch: s_memrealtime at entry / exit
-__device__ unsigned long long g_free_cycles[kProbeSlots][4];    // k_env_rollout_act_free: env, wait, act, wait
+__device__ unsigned long long g_free_cycles[kProbeSlots][5];    // k_env_rollout_act_free: env, wait, offers, acceptors, wait
 #define MS_MARK(k)                                                     \
     do {                                                               \
         const uint64_t t_now = __builtin_amdgcn_s_memtime();          \
@@ -1952,10 +1952,26 @@ __device__ __forceinline__ uint32_t pick4u(const uint32_t (&v)[4], int k) {
 // another stream): the env reads only the owner's acceptor action (world.py:391-404), so their sampling is off the
 // round's chain. (Sampling them here as well, k_act_common's table search per item: 50.2 us per round against
 // 47.4, profiles/r7g.)
-template <class SH>
+template <class SH, int PART = 3>  // PART bit 0: the offer units, bit 1: the acceptors (the probe build times them apart)
 __device__ __forceinline__ void act_free(const Geom& g, int64_t E, const FusedActFree& fa, int64_t e0, int a, int lane,
-                                         uint8_t* lds, const FreeLds& fl) {
+                                         uint8_t* lds, const FreeLds& fl, bool pace_on = false) {
     const int j = lane & 15, g4 = lane >> 4;
+    // pace_on: waves a and a ^ 4 share a SIMD, where issue goes to the older wave first, so one of them finishes
+    // its acting well before the other and waits at the round's barrier. After each step (a tile pair, a 64-item
+    // scan) a wave counts it in the LDS and raises its issue priority while it is behind its partner.
+    const int partner = a ^ 4;
+    const bool pacing = pace_on && partner < g.N;
+    auto pace = [&]() {
+        if (!pacing) return;
+        volatile int* pg = reinterpret_cast<volatile int*>(lds + fl.pace);
+        const int mine = pg[a] + 1;
+        pg[a] = mine;
+        const int other = __builtin_amdgcn_readfirstlane(pg[partner]);
+        if (other > __builtin_amdgcn_readfirstlane(mine))
+            __builtin_amdgcn_s_setprio(1);
+        else
+            __builtin_amdgcn_s_setprio(0);
+    };
     const int N = g.N, C = g.C, L = g.L, Uo = g.NL, Ua = N * C;
     const int EW = kFreeEPW * N;  // the workgroup's replicas
     const uint64_t dev_off = fa.offset_dev ? *fa.offset_dev : 0ull;
@@ -1963,7 +1979,7 @@ __device__ __forceinline__ void act_free(const Geom& g, int64_t E, const FusedAc
     auto slice = [&](int k) -> const uint8_t* { return lds + k * g.s_total; };
 
     // ---------------- the offer units: agent a's L slots of every replica, rows r = k * L + s
-    {
+    if constexpr ((PART & 1) != 0) {
         using FL = FragLayout<1, 1>;
         constexpr int TW = kPriceTW1;
         W1Split<1> w1;
@@ -2103,6 +2119,7 @@ __device__ __forceinline__ void act_free(const Geom& g, int64_t E, const FusedAc
                     ca_b.st8((uint32_t)cur[i], act[i]);
                     cl_b.stf(4 * (uint32_t)cur[i], lp[i]);
                 }
+            pace();
         }
         if (any_miss) {
             // the pairs the table could not serve: the same pairs and draws again, the core chooser recomputed
@@ -2129,7 +2146,7 @@ __device__ __forceinline__ void act_free(const Geom& g, int64_t E, const FusedAc
     // ---------------- the acceptors: agent a's C items of every replica, item m = k * C + c (group item
     //                  i = e * C + c): the cores it does not own sample the common row's table, the owned ones
     //                  are listed and run in 16-row MFMA tiles (act_common_rows with compact rows)
-    {
+    if constexpr ((PART & 2) != 0) {
         using FL = FragLayout<2, 2>;
         const uint32_t* const fg = frag_groups<2, 2>(fa.acc, true);
         int16_t* lm = reinterpret_cast<int16_t*>(lds + fl.list + a * kFreeListCap * 6);
@@ -2233,6 +2250,7 @@ __device__ __forceinline__ void act_free(const Geom& g, int64_t E, const FusedAc
                 lu[p] = u;
             }
             n_list += __popcll(mo);
+            pace();
             wave_sync();
             while (n_list >= 32) {
                 tiles2(32);
@@ -2487,7 +2505,8 @@ struct RolloutFreeArgs {
     FusedActFree fa;
     RoundStrideFree st;
     int n_rounds, act_last;
-    int prio;  // bit 0: the workgroup's waves 4.. at raised issue priority while acting, bit 1: during the env round
+    int prio;  // bit 0: the workgroup's waves 4.. at raised issue priority while acting, bit 1: during the env round,
+               // bit 2: the acting's waves paced against their SIMD partners (act_free pace_on)
 };
 // The locally shared free-price rollout in one launch: workgroup b holds replicas kFreeEPW * N * b .. in its LDS,
 // and wave w steps kFreeEPW of them (k_env_step's round, 16 lanes per replica) and then acts for agent w of all
@@ -2524,13 +2543,13 @@ __global__ void __launch_bounds__(512, 4) k_env_rollout_act_free(RolloutFreeArgs
         // items only, and the env checks every item's range (k_env_step: they are all sampled), so the others
         // hold a valid action (0, "reject") instead of whatever the LDS held
         uint32_t* ax = reinterpret_cast<uint32_t*>(smem_free + fl.accx);
-        for (int k = (int)threadIdx.x; k < (fl.total - fl.accx) / 4; k += (int)blockDim.x) ax[k] = 0u;
+        for (int k = (int)threadIdx.x; k < (fl.total - fl.accx) / 4; k += (int)blockDim.x) ax[k] = 0u;  // (+ pace)
     }
     __syncthreads();
 #ifdef MS_PHASE_TIMING
     // probe build: per wave, the shader cycles of the env rounds, the wait at the barrier after them, the acting,
     // and the wait at the barrier after it (tools/env_phase_probe.py --free)
-    uint64_t f_prev = __builtin_amdgcn_s_memtime(), f_acc[4] = {0, 0, 0, 0};
+    uint64_t f_prev = __builtin_amdgcn_s_memtime(), f_acc[5] = {0, 0, 0, 0, 0};
 #define FREE_MARK(k)                                                   \
     do {                                                               \
         const uint64_t f_now = __builtin_amdgcn_s_memtime();          \
@@ -2593,11 +2612,18 @@ __global__ void __launch_bounds__(512, 4) k_env_rollout_act_free(RolloutFreeArgs
             fa.acc_offset += (uint64_t)t * st.offset_step;
             const bool up_act = wave >= 4 && (A.prio & 1);
             if (up_act) __builtin_amdgcn_s_setprio(1);
-            act_free<SH>(g, A.E, fa, (int64_t)blockIdx.x * kFreeEPW * g.N, wave, lane, smem_free, fl);
-            if (up_act) __builtin_amdgcn_s_setprio(0);
+            const bool pace_on = (A.prio & 4) != 0;
+#ifdef MS_PHASE_TIMING
+            act_free<SH, 1>(g, A.E, fa, (int64_t)blockIdx.x * kFreeEPW * g.N, wave, lane, smem_free, fl, pace_on);
             FREE_MARK(2);
-            __syncthreads();  // the actions are stored and the LDS is free for the next round
+            act_free<SH, 2>(g, A.E, fa, (int64_t)blockIdx.x * kFreeEPW * g.N, wave, lane, smem_free, fl, pace_on);
+#else
+            act_free<SH>(g, A.E, fa, (int64_t)blockIdx.x * kFreeEPW * g.N, wave, lane, smem_free, fl, pace_on);
+#endif
+            if (up_act || pace_on) __builtin_amdgcn_s_setprio(0);
             FREE_MARK(3);
+            __syncthreads();  // the actions are stored and the LDS is free for the next round
+            FREE_MARK(4);
         }
     }
     if (span && lane0 == 0) {
@@ -2606,7 +2632,7 @@ __global__ void __launch_bounds__(512, 4) k_env_rollout_act_free(RolloutFreeArgs
     }
 #ifdef MS_PHASE_TIMING
     if (lane0 == 0)
-        for (int k = 0; k < 4; k++) g_free_cycles[wslot % kProbeSlots][k] += f_acc[k];
+        for (int k = 0; k < 5; k++) g_free_cycles[wslot % kProbeSlots][k] += f_acc[k];
 #endif
 }
 
@@ -2691,10 +2717,10 @@ extern "C" int ms_probe_phase_blocks(unsigned long long* out, int n_blocks) {
 // k_env_rollout_act_free's per-wave cycles (env rounds, barrier wait, acting, barrier wait) summed over the
 // launches since the last clear: out[4 * n_waves]
 extern "C" int ms_probe_free_cycles(unsigned long long* out, int n_waves, int clear) {
-    static unsigned long long host[ms::kProbeSlots][4];
+    static unsigned long long host[ms::kProbeSlots][5];
     if (n_waves > ms::kProbeSlots) return -1;
     if (hipMemcpyFromSymbol(host, HIP_SYMBOL(ms::g_free_cycles), sizeof(host)) != hipSuccess) return -1;
-    memcpy(out, host, sizeof(unsigned long long) * 4 * n_waves);
+    memcpy(out, host, sizeof(unsigned long long) * 5 * n_waves);
     if (clear) {
         memset(host, 0, sizeof(host));
         if (hipMemcpyToSymbol(HIP_SYMBOL(ms::g_free_cycles), host, sizeof(host)) != hipSuccess) return -1;
@@ -2872,7 +2898,9 @@ static hipError_t launch_rollout_free_sh(const Params& P, int64_t E, uint8_t* re
     const int64_t blocks = (E + epb - 1) / epb;
     static const int prio = [] {
         const char* v = getenv("MS_FREE_PRIO");  // (measurement knob, tools/gpu_job.sh envab)
-        return v ? atoi(v) : 1;  // measured: 1 (acting) 49.6 -> 49.0 us per round, 3 (and env) 49.1 (profiles/r7c)
+        // measured: 1 (acting) 49.6 -> 49.0 us per round, 3 (and env) 49.1 (profiles/r7c); 4 (paced acting)
+        // 47.07 -> 46.66 us against 1 over three A/B pairs, wait after acting 9.0k -> 4.5k cycles (profiles/r7)
+        return v ? atoi(v) : 4;
     }();
     const RolloutFreeArgs A{P, E, recs, mt, liab, io, fa, st, n_rounds, act_last, prio};
     hipLaunchKernelGGL((k_env_rollout_act_free<SH>), dim3((unsigned)blocks), dim3(64 * P.N), (size_t)free_lds(P).total, s,

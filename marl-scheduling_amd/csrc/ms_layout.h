@@ -221,7 +221,7 @@ constexpr int kFreeEPW = 4;        // replicas per wave (16 lanes each)
 constexpr int kFreeListCap = 96;   // < 32 carried + one 64-item step
 constexpr int kFreeTabDw = 68;     // [32 running sums][32 log-probs][S][last nonzero][2 pad] (Head<2>::table)
 struct FreeLds {
-    int32_t pdig, list, accx, total;
+    int32_t pdig, list, accx, pace, total;
 };
 inline constexpr FreeLds free_lds(const Geom& g) {
     FreeLds f{};
@@ -230,7 +230,8 @@ inline constexpr FreeLds free_lds(const Geom& g) {
     f.accx = align16(f.list + g.N * kFreeListCap * 6);  // int16 item + f32 uniform per entry
     // (by-core mode) the replicas' acceptor actions [kFreeEPW * N][N * C]: the acting writes its owned items, the
     // next env round stages its owners' from here (outside the wave slots the MT refill may overwrite)
-    f.total = f.accx + align4(kFreeEPW * g.N * g.N * g.C);
+    f.pace = f.accx + align4(kFreeEPW * g.N * g.N * g.C);
+    f.total = f.pace + 4 * 8;  // (MS_FREE_PRIO bit 2) each wave's count of acting steps done
     return f;
 }
 

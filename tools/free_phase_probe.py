@@ -2,8 +2,9 @@
 
 Loads the probe build (tools/_probe/libmarlsched_probe.so from tools/build_phase_probe.sh, -DMS_PHASE_TIMING)
 in place of the product library, runs cfg3 PPO iterations (one rollout launch each), and prints per wave and
-round the shader cycles of its four phases: the env round (k_env_step's round of its 4 replicas), the wait at
-the workgroup barrier after it, its agent's acting, and the wait at the barrier after that. Large waits mean
+round the shader cycles of its five phases: the env round (k_env_step's round of its 4 replicas), the wait at
+the workgroup barrier after it, its agent's offer units, its agent's acceptors, and the wait at the barrier after
+that. Large waits mean
 the workgroup's waves are unbalanced (the slowest wave of a phase holds the other seven)."""
 import ctypes as ct
 import importlib
@@ -27,8 +28,8 @@ def main(E=16384, iters=3, T=200):
     tr = tr_mod.Trainer.from_named("cfg3", n_envs=E, update_step=T, seed=0, device="cuda:0")
     assert tr.fused_rollout_free
     waves = E // 4
-    buf = (ct.c_ulonglong * (4 * waves))()
-    names = ("env round", "wait after env", "acting", "wait after acting")
+    buf = (ct.c_ulonglong * (5 * waves))()
+    names = ("env round", "wait after env", "offer units", "acceptors", "wait after acting")
     for it in range(iters):
         tr.rollout()
         torch.cuda.synchronize()
@@ -37,7 +38,7 @@ def main(E=16384, iters=3, T=200):
         torch.cuda.synchronize()
         if it == 0:
             continue  # the first rollout runs eagerly before its graph capture: two launches' worth
-        c = np.frombuffer(buf, dtype=np.uint64).reshape(waves, 4).astype(np.float64) / T
+        c = np.frombuffer(buf, dtype=np.uint64).reshape(waves, 5).astype(np.float64) / T
         tot = c.sum(1)
         print("iteration %d: cycles per wave per round (mean / p10 / p50 / p90 over %d waves)" % (it, waves))
         for k, n in enumerate(names):
@@ -47,8 +48,9 @@ def main(E=16384, iters=3, T=200):
                                                                  100 * v.mean() / tot.mean()))
         print("  %-18s %8.0f" % ("total", tot.mean()))
         # per agent (wave index within the workgroup) acting cycles
-        ag = c[:, 2].reshape(-1, 8).mean(0)
-        print("  acting by agent:   " + " ".join("%.0f" % x for x in ag))
+        for k, n in ((2, "offers"), (3, "acceptors")):
+            ag = c[:, k].reshape(-1, 8).mean(0)
+            print("  %-10s by agent: " % n + " ".join("%.0f" % x for x in ag))
     print("clock: the bench's clock_mhz converts cycles to us")
 
 
