@@ -350,6 +350,13 @@ def unit_returns(rewards_teu: torch.Tensor, unit_of_group: torch.Tensor, gamma: 
     return out
 
 
+def combine_losses(terms):
+    """PPO.update's loss (PPOmodules.py:157-159) per group from ms_ppo_grad's [..., 3] terms (mean -min(surr),
+    mean (V - G)^2, mean entropy): -min + 0.5 * mse - 0.01 * entropy, the same f32 operations for one epoch's
+    [G][3] or several epochs' stacked [n][G][3]."""
+    return terms[..., 0] + 0.5 * terms[..., 1] - 0.01 * terms[..., 2]
+
+
 class HipAdam:
     """torch.optim.Adam (defaults betas (0.9, 0.999), eps 1e-8, no weight decay) over the
     parameters of one PPOGroup as one ``ms_adam_step`` launch per step: tensor i of
@@ -612,10 +619,21 @@ class PPOGroup:
         # alive until its last launch (a caller's temporaries would otherwise be freed and reused)
         keep = (states_i8, actions_i8, old_logprobs, returns_teg, unit_of_group, common_row, core_owner, ws, loss_buf)
 
-        def run():
+        def launch(out=None):
+            """The gradient; the loss terms [G][3] into out (a caller's [G][3] float32 tensor, e.g. one epoch's
+            slot of a [n][G][3] buffer whose losses are combined at once) or into this epoch's own buffer."""
             assert keep
+            g = grads
+            if out is not None:
+                assert out.shape == loss_buf.shape and out.dtype == torch.float32 and out.is_contiguous()
+                g = abi.MsPpoGrads.from_buffer_copy(grads)
+                g.loss = ptr(out)
             check(lib.ms_ppo_grad(ct.byref(a), ct.byref(c), ct.byref(batch), ct.c_float(self.eps_clip), ptr(ws),
-                                  ws_bytes, ct.byref(grads), stream_ptr(stream)))
-            return loss_buf[:, 0] + 0.5 * loss_buf[:, 1] - 0.01 * loss_buf[:, 2]
+                                  ws_bytes, ct.byref(g), stream_ptr(stream)))
+            return loss_buf if out is None else out
 
+        def run():
+            return combine_losses(launch())
+
+        run.launch = launch
         return run

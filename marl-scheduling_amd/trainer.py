@@ -32,8 +32,8 @@ import torch
 from . import abi
 from ._lib import ABI_LOADED, hip_capture, ptr
 from .env import BatchedEnv
-from .ppo import (ActFrag, PPOGroup, PriceTable, act_round_free, discounted_returns, offer_act_free, reference_init_order,
-                  reference_nets, unit_returns)
+from .ppo import (ActFrag, PPOGroup, PriceTable, act_round_free, combine_losses, discounted_returns, offer_act_free,
+                  reference_init_order, reference_nets, unit_returns)
 
 
 @dataclass
@@ -205,6 +205,8 @@ class Trainer:
             self.price = _Unit("price", self.E, T, N * L, (N * L) // go, 4, 4, s.price_actions,
                                mk(go, 4, s.price_actions, hp.offer_gamma, k_off, nets["price"]), dev, torch.float32,
                                unit_major=self.price_unit_major)
+        if self.free and os.environ.get("MS_PRICE_KEYED", "1") == "0":
+            self.price.group.row_keys = 1  # the price chooser's gradient on the tile path (A/B measurements)
         if world_size > 1:
             self._broadcast_params()
         # A single net's item i takes word (i >> 6) & 1 of the draw countered by item i & ~64 (k_act_common's rule on
@@ -794,18 +796,21 @@ class Trainer:
                 seq += [ep] * u.group.K
                 col += n
             steps[u.name] = (u, seq, [])
+        # each unit type's loss terms of every (draw, epoch) into one [n][G][3] buffer, combined once at the end
+        terms = {name: torch.empty((len(seq), u.group.policy.G, 3), dtype=torch.float32, device=self.device)
+                 for name, (u, seq, _) in steps.items()}
         for s in range(max(len(v[1]) for v in steps.values())):
             live = [(u, seq, ls) for u, seq, ls in steps.values() if s < len(seq)]
             for u, seq, ls in live:
-                ls.append(seq[s]())
+                ls.append(seq[s].launch(terms[u.name][s]))
             if self.world_size > 1:
                 yield [p for u, _, _ in live for p in u.group.policy.parameters()]
             for u, _, _ in live:
                 u.group.hip_optimizer.step()
         for u, _, ls in steps.values():
-            u.group.last_losses = ls
+            losses[u.name] = combine_losses(terms[u.name])
+            u.group.last_losses = list(losses[u.name].unbind(0))
             u.group.sync_old()
-            losses[u.name] = torch.stack(ls)
         self._carry_last_observation()
         out["losses"] = losses
 
@@ -841,13 +846,15 @@ class Trainer:
             with torch.cuda.stream(st):
                 if u is self.acc and self.defer_common:
                     self.fill_common(stream=st)  # the rollout's deferred acceptor items, beside the other units
-                ls = []
-                for ep in self._epochs(u, all_sel[u.name], counts[u.name]):
-                    ls.append(ep())
+                seq = self._epochs(u, all_sel[u.name], counts[u.name])
+                # every (draw, epoch)'s loss terms into one buffer, combined at once (not four small kernels each)
+                terms = torch.empty((len(seq), u.group.policy.G, 3), dtype=torch.float32, device=self.device)
+                for i, ep in enumerate(seq):
+                    ep.launch(terms[i])
                     u.group.hip_optimizer.step(st)
-                u.group.last_losses = ls
+                losses[u.name] = combine_losses(terms)
+                u.group.last_losses = list(losses[u.name].unbind(0))
                 u.group.sync_old()
-                losses[u.name] = torch.stack(ls)
         for st in self._unit_streams:
             cur.wait_stream(st)
         self._carry_last_observation()
