@@ -2363,7 +2363,7 @@ __global__ void __launch_bounds__(256) k_acc_common_fill(CommonFillArgs p) {
 constexpr int kFillRounds = 8;
 template <bool PAIR>
 __global__ void __launch_bounds__(256) k_acc_common_fill4(CommonFillArgs p, int n_acts, int fill_merge) {
-    __shared__ float tabs[8 * kFreeTabDw];
+    __shared__ __align__(16) float tabs[8 * kFreeTabDw];
     using FL = FragLayout<2, 2>;
     for (int k = threadIdx.x; k < p.N * kFreeTabDw; k += blockDim.x) {
         const int a = k / kFreeTabDw;
@@ -2392,6 +2392,9 @@ __global__ void __launch_bounds__(256) k_acc_common_fill4(CommonFillArgs p, int 
     }
     const float* tab = tabs + a * kFreeTabDw;
     const float tmax = tab[64];
+    float bm[3];  // the maxima of the first three blocks of 8 running sums
+#pragma unroll
+    for (int b = 0; b < 3; b++) bm[b] = tab[8 * b + 7];
     const int t0 = (int)blockIdx.y * kFillRounds;
     uint32_t own0[kFillRounds], own1[kFillRounds];
 #pragma unroll
@@ -2464,15 +2467,27 @@ __global__ void __launch_bounds__(256) k_acc_common_fill4(CommonFillArgs p, int 
             tg[k] = u24(PAIR ? w0 : (((hi >> k) & 1u) ? w1 : w0)) * tmax;
             if constexpr (PAIR) tg[4 + k] = u24(w1) * tmax;
         }
+        // the count of running sums <= target (the binary search's result: the sums are non-decreasing) in two
+        // levels: the block of 8 from the 4 block maxima held in registers, then that block's 8 sums (two 16-byte
+        // LDS reads, every item's issued together) -- instead of 6 dependent LDS reads per item
 #pragma unroll
-        for (int i = 0; i < NI; i++) cnt[i] = 0;
+        for (int i = 0; i < NI; i++) {
+            int nb = 0;
 #pragma unroll
-        for (int step = 32; step >= 1; step >>= 1) {
-            float v[NI];
+            for (int b = 0; b < 3; b++) nb += bm[b] <= tg[i] ? 1 : 0;
+            cnt[i] = nb;  // block 0..3 (block 3 also when all of its sums are <= target: its count is then 8)
+        }
+        float4 blo[NI], bhi[NI];
 #pragma unroll
-            for (int i = 0; i < NI; i++) v[i] = tab[min(cnt[i] + step, 32) - 1];
+        for (int i = 0; i < NI; i++) {
+            blo[i] = *reinterpret_cast<const float4*>(tab + 8 * cnt[i]);
+            bhi[i] = *reinterpret_cast<const float4*>(tab + 8 * cnt[i] + 4);
+        }
 #pragma unroll
-            for (int i = 0; i < NI; i++) cnt[i] = (cnt[i] + step <= 32 && v[i] <= tg[i]) ? cnt[i] + step : cnt[i];
+        for (int i = 0; i < NI; i++) {
+            const float t = tg[i];
+            cnt[i] = 8 * cnt[i] + (blo[i].x <= t) + (blo[i].y <= t) + (blo[i].z <= t) + (blo[i].w <= t) + (bhi[i].x <= t) +
+                     (bhi[i].y <= t) + (bhi[i].z <= t) + (bhi[i].w <= t);
         }
         const int lnz = __float_as_int(tab[65]);
         uint32_t acts0 = 0, acts1 = 0;
