@@ -2362,7 +2362,7 @@ __global__ void __launch_bounds__(256) k_acc_common_fill(CommonFillArgs p) {
 // largest VALU cost: 32-bit multiplies at quarter rate). Same values bit for bit.
 constexpr int kFillRounds = 8;
 template <bool PAIR>
-__global__ void __launch_bounds__(256) k_acc_common_fill4(CommonFillArgs p, int n_acts, int fill_merge) {
+__global__ void __launch_bounds__(256) k_acc_common_fill4(CommonFillArgs p, int n_acts, int merge) {  // merge: fill_merge()
     __shared__ __align__(16) float tabs[8 * kFreeTabDw];
     using FL = FragLayout<2, 2>;
     for (int k = threadIdx.x; k < p.N * kFreeTabDw; k += blockDim.x) {
@@ -2409,7 +2409,7 @@ __global__ void __launch_bounds__(256) k_acc_common_fill4(CommonFillArgs p, int 
         const size_t r = (size_t)e * U + u;
         int8_t* ad = advance(p.action, (int64_t)t * p.action_stride) + r;
         float* ld = advance(p.logprob, (int64_t)t * p.logprob_stride) + r;
-        if (owned == 0 || fill_merge || p.own_action) {
+        if (owned == 0 || merge || p.own_action) {
             uint32_t a4 = acts;
             float4 l4 = make_float4(lps[0], lps[1], lps[2], lps[3]);
             if (owned != 0) {  // merge the owned items the rollout wrote: whole quads, no partially written lines
